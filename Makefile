@@ -1,0 +1,43 @@
+# Builds the MI355X backend (libtts_hip.so, gfx950) and the CPU oracle (liboracle.so, tests only).
+# No cmake: plain hipcc / gcc.  `make -j8`.
+
+HIPCC ?= /opt/rocm/bin/hipcc
+CC ?= gcc
+ARCH ?= gfx950
+
+PKG := tts.cpp_amd
+SRC := $(PKG)/csrc
+OUT := $(PKG)/lib
+OBJ := build/obj
+
+# -ffp-contract=off: every a*b+c in the parity-relevant kernels rounds twice, as ggml's scalar C does
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+            -Wno-unused-variable -Wno-unused-but-set-variable -Wno-unused-value -Wno-unused-result -Iinclude -munsafe-fp-atomics
+CXXFLAGS := -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include
+
+HIP_SRCS := $(wildcard $(SRC)/*.hip)
+CPP_SRCS := $(wildcard $(SRC)/*.cpp)
+HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJ)/%.hip.o,$(HIP_SRCS))
+CPP_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.cpp.o,$(CPP_SRCS))
+
+all: $(OUT)/libtts_hip.so oracle/_build/liboracle.so
+
+$(OBJ)/%.hip.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/tts_hip.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/%.cpp.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/tts_hip.h include/tts_runners.h
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(CXXFLAGS) -x c++ -c $< -o $@
+
+$(OUT)/libtts_hip.so: $(HIP_OBJS) $(CPP_OBJS)
+	@mkdir -p $(OUT)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -lpthread
+
+oracle/_build/liboracle.so: oracle/ggml_ref.c oracle/ggml_ref.h include/tts_hip.h
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build $(OUT) oracle/_build
+
+.PHONY: all clean

@@ -1,0 +1,214 @@
+/*
+ * tts_hip.h — C-ABI of the MI355X (gfx950) compute backend for TTS.cpp's decode path.
+ *
+ * This is the drop-in boundary.  TTS.cpp builds ggml graphs (e.g. build_parler_graph,
+ * /root/reference/src/models/parler/model.cpp:520-614) and hands them to a ggml backend through
+ * ggml_backend_sched (/root/reference/src/tts_model.cpp:53-67).  A ggml backend is a vtable
+ * (ggml_backend_i / ggml_backend_buffer_i / ggml_backend_device_i, fork `ggml/` submodule,
+ * .gitmodules:1-4, absent here).  Every entry point below is what that vtable needs underneath:
+ *
+ *   tts_hip_backend_init        <- ggml_backend_dev_init / ggml_backend_metal_init()
+ *                                  (selection sites: src/tts_model.cpp:40,56,134;
+ *                                   src/models/parler/model.cpp:327,345; src/decoder/dac_model.cpp:128 ...)
+ *   tts_hip_buffer_alloc/free   <- ggml_backend_buffer_type_i::alloc_buffer / buffer_i::free_buffer
+ *                                  (callers: src/tts_model.cpp:150, src/models/parler/model.cpp:377)
+ *   tts_hip_tensor_set          <- ggml_backend_tensor_set (src/tts_model.cpp:157-164)
+ *   tts_hip_tensor_get          <- ggml_backend_tensor_get_async (src/tts_model.cpp:25-36); it
+ *                                  synchronises the compute stream first, because no caller in
+ *                                  the reference ever calls ggml_backend_synchronize.
+ *   tts_hip_memset              <- ggml_backend_buffer_clear (src/models/parler/model.cpp:383)
+ *   tts_hip_supports_op         <- ggml_backend_device_i::supports_op
+ *   tts_hip_graph_compute       <- ggml_backend_i::graph_compute
+ *                                  (reached from ggml_backend_sched_graph_compute_async,
+ *                                   src/models/parler/model.cpp:645)
+ *   tts_hip_synchronize         <- ggml_backend_i::synchronize
+ *
+ * Tensors cross the boundary as `tts_tensor`, a plain C mirror of the ggml_tensor fields a backend
+ * reads (type, ne, nb, op, op_params, src, data).  Type ids use ggml's numbering so the ggml
+ * adapter maps them 1:1.  No torch or HIP types appear in any signature.
+ *
+ * Errors: every int-returning entry point returns TTS_STATUS_* (0 = success), mirroring
+ * ggml_status; allocation failure returns NULL (reference checks NULL, model.cpp:377-380).
+ */
+#ifndef TTS_HIP_H
+#define TTS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TTS_MAX_DIMS 4
+#define TTS_MAX_SRC 4
+#define TTS_MAX_OP_PARAMS 16
+#define TTS_MAX_NAME 48
+
+/* ggml_type numbering (ggml.h of the fork's early-2025 base). */
+enum tts_type {
+    TTS_TYPE_F32 = 0,
+    TTS_TYPE_F16 = 1,
+    TTS_TYPE_Q4_0 = 2,
+    TTS_TYPE_Q4_1 = 3,
+    TTS_TYPE_Q5_0 = 6,
+    TTS_TYPE_Q5_1 = 7,
+    TTS_TYPE_Q8_0 = 8,
+    TTS_TYPE_Q8_1 = 9,
+    TTS_TYPE_Q4_K = 12,
+    TTS_TYPE_Q6_K = 14,
+    TTS_TYPE_Q8_K = 15,
+    TTS_TYPE_I8 = 24,
+    TTS_TYPE_I16 = 25,
+    TTS_TYPE_I32 = 26,
+    TTS_TYPE_COUNT = 40
+};
+
+/* Ops the TTS.cpp graphs emit.  Names follow ggml_op; numbering is our own
+ * (the adapter maps ggml_op -> tts_op by name). */
+enum tts_op {
+    TTS_OP_NONE = 0,
+    TTS_OP_DUP,
+    TTS_OP_ADD,
+    TTS_OP_SUB,
+    TTS_OP_MUL,
+    TTS_OP_DIV,
+    TTS_OP_SQR,
+    TTS_OP_SQRT,
+    TTS_OP_SIN,
+    TTS_OP_COS,
+    TTS_OP_SUM_ROWS,
+    TTS_OP_REPEAT,
+    TTS_OP_CONCAT,
+    TTS_OP_NORM,
+    TTS_OP_RMS_NORM,
+    TTS_OP_MUL_MAT,
+    TTS_OP_SCALE,
+    TTS_OP_CPY,
+    TTS_OP_CONT,
+    TTS_OP_RESHAPE,
+    TTS_OP_VIEW,
+    TTS_OP_PERMUTE,
+    TTS_OP_TRANSPOSE,
+    TTS_OP_GET_ROWS,
+    TTS_OP_SOFT_MAX,
+    TTS_OP_ROPE,
+    TTS_OP_CLAMP,
+    TTS_OP_CONV_TRANSPOSE_1D,
+    TTS_OP_IM2COL,
+    TTS_OP_UPSCALE,
+    TTS_OP_PAD,
+    TTS_OP_LEAKY_RELU,
+    TTS_OP_UNARY,
+    TTS_OP_CUMSUM, /* fork op */
+    TTS_OP_MOD,    /* fork op */
+    TTS_OP_ROUND,  /* fork op */
+    TTS_OP_STFT,   /* fork op */
+    TTS_OP_ISTFT,  /* fork op */
+    TTS_OP_COUNT
+};
+
+enum tts_unary_op {
+    TTS_UNARY_ABS = 0,
+    TTS_UNARY_NEG,
+    TTS_UNARY_TANH,
+    TTS_UNARY_RELU,
+    TTS_UNARY_SIGMOID,
+    TTS_UNARY_GELU,
+    TTS_UNARY_SILU,
+    TTS_UNARY_EXP,
+    TTS_UNARY_COUNT
+};
+
+enum tts_status {
+    TTS_STATUS_SUCCESS = 0,
+    TTS_STATUS_FAILED = -1,
+    TTS_STATUS_ALLOC_FAILED = -2,
+    TTS_STATUS_UNSUPPORTED = -3,
+    TTS_STATUS_BAD_ARG = -4,
+    TTS_STATUS_NO_DEVICE = -5
+};
+
+/* Plain mirror of the ggml_tensor fields a backend reads.  `data` is a device pointer for
+ * tensors handed to tts_hip_* (a host pointer for the CPU oracle in oracle/).  op_params hold
+ * int32 and float (bit-cast) parameters exactly where ggml_set_op_params puts them. */
+typedef struct tts_tensor {
+    int32_t type;
+    int32_t op;
+    int64_t ne[TTS_MAX_DIMS];
+    size_t nb[TTS_MAX_DIMS];
+    int32_t op_params[TTS_MAX_OP_PARAMS];
+    struct tts_tensor * src[TTS_MAX_SRC];
+    struct tts_tensor * view_src;
+    size_t view_offs;
+    void * data;
+    int32_t flags;
+    int32_t pad_;
+    char name[TTS_MAX_NAME];
+} tts_tensor;
+
+/* ---- type traits (host, no device needed) ---- */
+size_t tts_type_size(int type);       /* bytes per block */
+int64_t tts_blck_size(int type);      /* elements per block */
+size_t tts_row_size(int type, int64_t ne0);
+const char * tts_type_name(int type);
+const char * tts_op_name(int op);
+
+/* ---- device / backend (ggml_backend_i + ggml_backend_buffer_i underneath) ---- */
+typedef struct tts_hip_backend * tts_hip_backend_t;
+
+int tts_hip_device_count(void);
+tts_hip_backend_t tts_hip_backend_init(int device); /* NULL if no device */
+void tts_hip_backend_free(tts_hip_backend_t backend);
+const char * tts_hip_backend_name(tts_hip_backend_t backend);
+
+void * tts_hip_buffer_alloc(tts_hip_backend_t backend, size_t size); /* 256-B aligned device memory */
+void tts_hip_buffer_free(tts_hip_backend_t backend, void * ptr);
+size_t tts_hip_buffer_alignment(void);
+
+int tts_hip_tensor_set(tts_hip_backend_t backend, void * dst_dev, const void * src_host, size_t size);
+int tts_hip_tensor_get(tts_hip_backend_t backend, void * dst_host, const void * src_dev, size_t size);
+int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size);
+int tts_hip_memset(tts_hip_backend_t backend, void * dst_dev, int value, size_t size);
+int tts_hip_synchronize(tts_hip_backend_t backend);
+
+int tts_hip_supports_op(const tts_tensor * node);
+int tts_hip_graph_compute(tts_hip_backend_t backend, tts_tensor * const * nodes, int n_nodes);
+
+/* Backend options (env-free knobs used by the bench / tests). */
+enum tts_hip_option {
+    TTS_HIP_OPT_FUSION = 0,      /* 1 = pattern fusion in graph_compute (default 1) */
+    TTS_HIP_OPT_PROFILE_GEMV = 1 /* 1 = time quantized GEMV launches with HIP events */
+};
+int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
+/* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for
+ * weight type `type` (-1 = all types). */
+int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t * launches, double * bytes, int reset);
+
+/* Raw kernel entry points for micro-benchmarks (device pointers, current backend stream).
+ * y[M][N] = W[N][K] . x[M][K]; W is `type` (Q4_K / Q8_0 / F16 / F32) row-major, N rows of K. */
+int tts_hip_gemv(tts_hip_backend_t backend, int type, const void * w, const float * x, float * y,
+                 int64_t K, int64_t N, int64_t M);
+
+/* ---- generic backend vtable: lets the same C++ runners target the HIP backend or the CPU oracle
+ * (the latter lives in oracle/ and is only linked by tests and bench.py's cpu_baseline leg). ---- */
+typedef struct tts_backend_iface {
+    void * ctx;
+    const char * name;
+    void * (*alloc)(void * ctx, size_t size);
+    void (*free)(void * ctx, void * ptr);
+    int (*set)(void * ctx, void * dst, const void * src, size_t size);
+    int (*get)(void * ctx, void * dst, const void * src, size_t size);
+    int (*memset)(void * ctx, void * dst, int value, size_t size);
+    int (*compute)(void * ctx, tts_tensor * const * nodes, int n_nodes);
+    int (*synchronize)(void * ctx);
+} tts_backend_iface;
+
+/* Fills `out` with the HIP backend's vtable. */
+int tts_hip_backend_iface(tts_hip_backend_t backend, tts_backend_iface * out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TTS_HIP_H */

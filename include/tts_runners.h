@@ -1,0 +1,67 @@
+/*
+ * tts_runners.h — C-ABI of the host-side runners that drive the backend with TTS.cpp's graphs.
+ *
+ * The runners mirror the reference's runner interface (parler_tts_runner::decode /
+ * generate_from_batch, /root/reference/src/models/parler/model.cpp:648-693, 762-792) over a
+ * tts_backend_iface, so the same graphs run on the HIP backend (product) or on the CPU oracle
+ * (tests and bench cpu_baseline only).  Weights are deterministic synthetic tensors of the exact
+ * shapes/types of the named config (no checkpoints offline: BASELINE.md §3).
+ */
+#ifndef TTS_RUNNERS_H
+#define TTS_RUNNERS_H
+
+#include "tts_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Parler-TTS decoder config (defaults = Parler-TTS mini v1, src/models/parler/model.h:67-81). */
+typedef struct tts_parler_config {
+    int32_t n_layers;        /* 24 */
+    int32_t hidden_size;     /* 1024 */
+    int32_t n_attn_heads;    /* 16 */
+    int32_t ffn_size;        /* 4096 */
+    int32_t n_output_heads;  /* 9 codebooks */
+    int32_t output_vocab;    /* 1088 */
+    int32_t audio_vocab;     /* 1024 */
+    int32_t max_ctx;         /* 4096 (KV capacity) */
+    int32_t n_encode;        /* 3 ("female voice" T5 tokens) */
+    int32_t prompt_vocab;    /* 32128 (T5) */
+    int32_t max_positions;   /* 4102 */
+    int32_t weight_type;     /* TTS_TYPE_Q4_K for config 3 */
+    int32_t head_type;       /* TTS_TYPE_F32 (heads unquantized by default) */
+    int32_t use_cross_attn;  /* 1 */
+    int32_t batch;           /* independent prompts stepped in lockstep (1 = reference graph) */
+    int32_t eos_token;       /* 1024 */
+    int32_t bos_token;       /* 1025 */
+    uint64_t seed;           /* synthetic weight seed base (0x5EED) */
+    uint64_t arena_bytes;    /* compute arena (0 = default 256 MiB) */
+} tts_parler_config;
+
+typedef struct tts_parler tts_parler;
+
+void tts_parler_default_config(tts_parler_config * cfg);
+tts_parler * tts_parler_create(const tts_backend_iface * be, const tts_parler_config * cfg);
+void tts_parler_free(tts_parler * p);
+/* Resets positions / EOS state (KV contents become unreachable). */
+void tts_parler_reset(tts_parler * p);
+/* Text-prompt pass: tokens [batch][n] (parler batch_from_sentence path). */
+int tts_parler_prefill(tts_parler * p, const int32_t * tokens, int32_t n);
+/* One AR decode step: audio tokens [batch][n_output_heads] -> logits [batch][n_output_heads][vocab]. */
+int tts_parler_decode(tts_parler * p, const int32_t * audio_tokens, float * logits);
+/* Greedy generation loop (generate_from_batch with sampler::max): runs n_steps AR steps after the
+ * current position and writes sampled tokens [batch][n_steps][n_output_heads]. */
+int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out);
+int32_t tts_parler_position(const tts_parler * p);
+/* Nodes in the last step graph and bytes of the compute arena it used. */
+int32_t tts_parler_last_graph_nodes(const tts_parler * p);
+uint64_t tts_parler_weight_bytes(const tts_parler * p);
+/* Debug: copy a named node of the last graph to host (returns bytes, 0 if not found). */
+uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,879 @@
+/*
+ * oracle/ggml_ref.c — TEST INFRASTRUCTURE ONLY (see ggml_ref.h header for pinning status).
+ *
+ * Restatement of ggml-cpu scalar semantics for the ops emitted by TTS.cpp graph builders:
+ *   Parler step   /root/reference/src/models/parler/model.cpp:387-614
+ *   DAC / codec   /root/reference/src/decoder/dac_model.cpp:100-170,
+ *                 /root/reference/src/decoder/general_neural_audio_codec.cpp:133-172
+ *   helpers       /root/reference/src/util.cpp:86-217
+ * The op arithmetic itself is in the unvendored ggml fork (upstream ggml-cpu, early-2025 base);
+ * each function below names the upstream routine it restates.
+ */
+#define _GNU_SOURCE
+#include "ggml_ref.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MIN(a, b) ((a) < (b) ? (a) : (b))
+#define MAX(a, b) ((a) > (b) ? (a) : (b))
+
+typedef double ggml_float;
+
+/* ------------------------------------------------------------------------------------------ */
+/* fp16 <-> fp32: ggml_compute_fp16_to_fp32 / ggml_compute_fp32_to_fp16 (ggml-impl.h, the     */
+/* FP16 library's bit-exact scalar algorithm; identical to F16C _cvtss_sh RNE results).       */
+
+static inline float bits_to_f32(uint32_t w) {
+    float f;
+    memcpy(&f, &w, 4);
+    return f;
+}
+static inline uint32_t f32_to_bits(float f) {
+    uint32_t w;
+    memcpy(&w, &f, 4);
+    return w;
+}
+
+float ref_fp16_to_fp32(ref_fp16_t h) {
+    const uint32_t w = (uint32_t)h << 16;
+    const uint32_t sign = w & 0x80000000u;
+    const uint32_t two_w = w + w;
+    const uint32_t exp_offset = 0xE0u << 23;
+    const float exp_scale = 0x1.0p-112f;
+    const float normalized = bits_to_f32((two_w >> 4) + exp_offset) * exp_scale;
+    const uint32_t magic_mask = 126u << 23;
+    const float magic_bias = 0.5f;
+    const float denormalized = bits_to_f32((two_w >> 17) | magic_mask) - magic_bias;
+    const uint32_t denorm_cutoff = 1u << 27;
+    const uint32_t result = sign | (two_w < denorm_cutoff ? f32_to_bits(denormalized) : f32_to_bits(normalized));
+    return bits_to_f32(result);
+}
+
+ref_fp16_t ref_fp32_to_fp16(float f) {
+    const float scale_to_inf = 0x1.0p+112f;
+    const float scale_to_zero = 0x1.0p-110f;
+    float base = (fabsf(f) * scale_to_inf) * scale_to_zero;
+    const uint32_t w = f32_to_bits(f);
+    const uint32_t shl1_w = w + w;
+    const uint32_t sign = w & 0x80000000u;
+    uint32_t bias = shl1_w & 0xFF000000u;
+    if (bias < 0x71000000u) bias = 0x71000000u;
+    base = bits_to_f32((bias >> 1) + 0x07800000u) + base;
+    const uint32_t bits = f32_to_bits(base);
+    const uint32_t exp_bits = (bits >> 13) & 0x00007C00u;
+    const uint32_t mantissa_bits = bits & 0x00000FFFu;
+    const uint32_t nonsign = exp_bits + mantissa_bits;
+    return (ref_fp16_t)((sign >> 16) | (shl1_w > 0xFF000000u ? 0x7E00u : nonsign));
+}
+
+/* nearest_int (ggml-quants.c): round-to-nearest-even via the 1.5*2^23 magic constant. */
+int ref_nearest_int(float fval) {
+    float val = fval + 12582912.f;
+    int i;
+    memcpy(&i, &val, sizeof(int));
+    return (i & 0x007fffff) - 0x00400000;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* K-quants: get_scale_min_k4, dequantize_row_q4_K, quantize_row_q8_K_ref,                     */
+/* ggml_vec_dot_q4_K_q8_K (generic).                                                           */
+
+void ref_get_scale_min_k4(int j, const uint8_t * q, uint8_t * d, uint8_t * m) {
+    if (j < 4) {
+        *d = q[j] & 63;
+        *m = q[j + 4] & 63;
+    } else {
+        *d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        *m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+void ref_dequantize_row_q4_K(const ref_block_q4_K * x, float * y, int64_t k) {
+    const int64_t nb = k / QK_K;
+    for (int64_t i = 0; i < nb; i++) {
+        const uint8_t * q = x[i].qs;
+        const float d = ref_fp16_to_fp32(x[i].d);
+        const float mn = ref_fp16_to_fp32(x[i].dmin);
+        int is = 0;
+        uint8_t sc, m;
+        for (int j = 0; j < QK_K; j += 64) {
+            ref_get_scale_min_k4(is + 0, x[i].scales, &sc, &m);
+            const float d1 = d * sc;
+            const float m1 = mn * m;
+            ref_get_scale_min_k4(is + 1, x[i].scales, &sc, &m);
+            const float d2 = d * sc;
+            const float m2 = mn * m;
+            for (int l = 0; l < 32; ++l) *y++ = d1 * (q[l] & 0xF) - m1;
+            for (int l = 0; l < 32; ++l) *y++ = d2 * (q[l] >> 4) - m2;
+            q += 32;
+            is += 2;
+        }
+    }
+}
+
+void ref_dequantize_row_q8_0(const ref_block_q8_0 * x, float * y, int64_t k) {
+    const int64_t nb = k / QK8_0;
+    for (int64_t i = 0; i < nb; i++) {
+        const float d = ref_fp16_to_fp32(x[i].d);
+        for (int j = 0; j < QK8_0; ++j) y[i * QK8_0 + j] = x[i].qs[j] * d;
+    }
+}
+
+void ref_quantize_row_q8_K(const float * x, ref_block_q8_K * y, int64_t k) {
+    const int64_t nb = k / QK_K;
+    for (int64_t i = 0; i < nb; i++) {
+        float max = 0;
+        float amax = 0;
+        for (int j = 0; j < QK_K; ++j) {
+            float ax = fabsf(x[j]);
+            if (ax > amax) {
+                amax = ax;
+                max = x[j];
+            }
+        }
+        if (!amax) {
+            y[i].d = 0;
+            memset(y[i].qs, 0, QK_K);
+            memset(y[i].bsums, 0, sizeof(y[i].bsums));
+            x += QK_K;
+            continue;
+        }
+        const float iscale = -127.f / max;
+        for (int j = 0; j < QK_K; ++j) {
+            int v = ref_nearest_int(iscale * x[j]);
+            y[i].qs[j] = (int8_t)MIN(127, v);
+        }
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ++ii) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = (int16_t)sum;
+        }
+        y[i].d = 1 / iscale;
+        x += QK_K;
+    }
+}
+
+/* quantize_row_q8_0_ref */
+void ref_quantize_row_q8_0(const float * x, ref_block_q8_0 * y, int64_t k) {
+    const int64_t nb = k / QK8_0;
+    for (int64_t i = 0; i < nb; i++) {
+        float amax = 0.0f;
+        for (int j = 0; j < QK8_0; j++) amax = MAX(amax, fabsf(x[i * QK8_0 + j]));
+        const float d = amax / ((1 << 7) - 1);
+        const float id = d ? 1.0f / d : 0.0f;
+        y[i].d = ref_fp32_to_fp16(d);
+        for (int j = 0; j < QK8_0; ++j) {
+            const float x0 = x[i * QK8_0 + j] * id;
+            y[i].qs[j] = (int8_t)roundf(x0);
+        }
+    }
+}
+
+void ref_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy) {
+    const ref_block_q4_K * x = (const ref_block_q4_K *)vx;
+    const ref_block_q8_K * y = (const ref_block_q8_K *)vy;
+    const int nb = n / QK_K;
+    static const uint32_t kmask1 = 0x3f3f3f3f;
+    static const uint32_t kmask2 = 0x0f0f0f0f;
+    static const uint32_t kmask3 = 0x03030303;
+    uint32_t utmp[4];
+    const uint8_t * scales = (const uint8_t *)&utmp[0];
+    const uint8_t * mins = (const uint8_t *)&utmp[2];
+    int8_t aux8[QK_K];
+    int16_t aux16[8];
+    float sums[8];
+    int32_t aux32[8];
+    memset(sums, 0, 8 * sizeof(float));
+    float sumf = 0;
+    for (int i = 0; i < nb; ++i) {
+        const uint8_t * q4 = x[i].qs;
+        const int8_t * q8 = y[i].qs;
+        memset(aux32, 0, 8 * sizeof(int32_t));
+        int8_t * a = aux8;
+        for (int j = 0; j < QK_K / 64; ++j) {
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] & 0xF);
+            a += 32;
+            for (int l = 0; l < 32; ++l) a[l] = (int8_t)(q4[l] >> 4);
+            a += 32;
+            q4 += 32;
+        }
+        memcpy(utmp, x[i].scales, 12);
+        utmp[3] = ((utmp[2] >> 4) & kmask2) | (((utmp[1] >> 6) & kmask3) << 4);
+        const uint32_t uaux = utmp[1] & kmask1;
+        utmp[1] = (utmp[2] & kmask2) | (((utmp[0] >> 6) & kmask3) << 4);
+        utmp[2] = uaux;
+        utmp[0] &= kmask1;
+        int sumi = 0;
+        for (int j = 0; j < QK_K / 16; ++j) sumi += y[i].bsums[j] * mins[j / 2];
+        a = aux8;
+        int is = 0;
+        for (int j = 0; j < QK_K / 32; ++j) {
+            int32_t scale = scales[is++];
+            for (int r = 0; r < 4; ++r) {
+                for (int l = 0; l < 8; ++l) aux16[l] = q8[l] * a[l];
+                for (int l = 0; l < 8; ++l) aux32[l] += scale * aux16[l];
+                q8 += 8;
+                a += 8;
+            }
+        }
+        const float d = ref_fp16_to_fp32(x[i].d) * y[i].d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+        const float dmin = ref_fp16_to_fp32(x[i].dmin) * y[i].d;
+        sumf -= dmin * sumi;
+    }
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    *s = sumf;
+}
+
+void ref_vec_dot_q8_0_q8_0(int n, float * s, const void * vx, const void * vy) {
+    const ref_block_q8_0 * x = (const ref_block_q8_0 *)vx;
+    const ref_block_q8_0 * y = (const ref_block_q8_0 *)vy;
+    const int nb = n / QK8_0;
+    float sumf = 0;
+    for (int ib = 0; ib < nb; ++ib) {
+        int sumi = 0;
+        for (int j = 0; j < QK8_0; j++) sumi += x[ib].qs[j] * y[ib].qs[j];
+        sumf += sumi * (ref_fp16_to_fp32(x[ib].d) * ref_fp16_to_fp32(y[ib].d));
+    }
+    *s = sumf;
+}
+
+void ref_vec_dot_f16(int n, float * s, const ref_fp16_t * x, const ref_fp16_t * y) {
+    ggml_float sumf = 0.0;
+    for (int i = 0; i < n; ++i) sumf += (ggml_float)(ref_fp16_to_fp32(x[i]) * ref_fp16_to_fp32(y[i]));
+    *s = (float)sumf;
+}
+
+void ref_vec_dot_f32(int n, float * s, const float * x, const float * y) {
+    ggml_float sumf = 0.0;
+    for (int i = 0; i < n; ++i) sumf += (ggml_float)(x[i] * y[i]);
+    *s = (float)sumf;
+}
+
+/* ggml_gelu_f32 + GGML_GELU_FP16 table lookup (ggml_vec_gelu_f32). */
+#define GELU_COEF_A 0.044715f
+#define SQRT_2_OVER_PI 0.79788456080286535587989211986876f
+
+float ref_gelu_f32(float x) {
+    return 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+}
+
+static ref_fp16_t g_gelu_table[1 << 16];
+static pthread_once_t g_gelu_once = PTHREAD_ONCE_INIT;
+static void gelu_table_init(void) {
+    for (int i = 0; i < (1 << 16); ++i) {
+        float f = ref_fp16_to_fp32((ref_fp16_t)i);
+        g_gelu_table[i] = ref_fp32_to_fp16(ref_gelu_f32(f));
+    }
+}
+
+float ref_gelu_table(float x) {
+    pthread_once(&g_gelu_once, gelu_table_init);
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    ref_fp16_t t = ref_fp32_to_fp16(x);
+    return ref_fp16_to_fp32(g_gelu_table[t]);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* type traits                                                                                */
+
+static size_t ref_type_size(int type) {
+    switch (type) {
+        case TTS_TYPE_F32: return 4;
+        case TTS_TYPE_F16: return 2;
+        case TTS_TYPE_Q4_K: return sizeof(ref_block_q4_K);
+        case TTS_TYPE_Q8_0: return sizeof(ref_block_q8_0);
+        case TTS_TYPE_Q8_K: return sizeof(ref_block_q8_K);
+        case TTS_TYPE_I32: return 4;
+        case TTS_TYPE_I16: return 2;
+        case TTS_TYPE_I8: return 1;
+        default: return 0;
+    }
+}
+static int64_t ref_blck_size(int type) {
+    switch (type) {
+        case TTS_TYPE_Q4_K: case TTS_TYPE_Q8_K: return QK_K;
+        case TTS_TYPE_Q8_0: return QK8_0;
+        default: return 1;
+    }
+}
+static size_t ref_row_size(int type, int64_t ne) { return ref_type_size(type) * (ne / ref_blck_size(type)); }
+
+/* ------------------------------------------------------------------------------------------ */
+/* ref_gemv: ggml_compute_forward_mul_mat for a 2-D weight and M activation columns           */
+
+typedef struct {
+    int type;
+    const void * w;
+    const float * x;
+    float * y;
+    int64_t K, N, M;
+    const void * xq; /* quantized activations, one row per column */
+    size_t xq_row;
+    int ith, nth;
+} gemv_job;
+
+static void gemv_rows(const gemv_job * j) {
+    const size_t wrow = ref_row_size(j->type, j->K);
+    const int64_t dr = (j->N + j->nth - 1) / j->nth;
+    const int64_t r0 = dr * j->ith, r1 = MIN(r0 + dr, j->N);
+    for (int64_t m = 0; m < j->M; ++m) {
+        for (int64_t n = r0; n < r1; ++n) {
+            const char * wr = (const char *)j->w + n * wrow;
+            float s = 0;
+            switch (j->type) {
+                case TTS_TYPE_Q4_K:
+                    ref_vec_dot_q4_K_q8_K((int)j->K, &s, wr, (const char *)j->xq + m * j->xq_row);
+                    break;
+                case TTS_TYPE_Q8_0:
+                    ref_vec_dot_q8_0_q8_0((int)j->K, &s, wr, (const char *)j->xq + m * j->xq_row);
+                    break;
+                case TTS_TYPE_F16:
+                    ref_vec_dot_f16((int)j->K, &s, (const ref_fp16_t *)wr,
+                                    (const ref_fp16_t *)((const char *)j->xq + m * j->xq_row));
+                    break;
+                default:
+                    ref_vec_dot_f32((int)j->K, &s, (const float *)wr, j->x + m * j->K);
+                    break;
+            }
+            j->y[m * j->N + n] = s;
+        }
+    }
+}
+
+static void * gemv_thread(void * p) {
+    gemv_rows((const gemv_job *)p);
+    return NULL;
+}
+
+/* convert activation rows to the weight type's vec_dot_type (from_float) */
+static void * quantize_activations(int type, const float * x, int64_t K, int64_t M, size_t * row) {
+    int vtype = type == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : type == TTS_TYPE_Q8_0 ? TTS_TYPE_Q8_0
+              : type == TTS_TYPE_F16 ? TTS_TYPE_F16 : TTS_TYPE_F32;
+    *row = ref_row_size(vtype, K);
+    if (vtype == TTS_TYPE_F32) return NULL;
+    char * q = (char *)malloc(*row * M);
+    for (int64_t m = 0; m < M; ++m) {
+        const float * xr = x + m * K;
+        char * qr = q + m * *row;
+        if (vtype == TTS_TYPE_Q8_K) ref_quantize_row_q8_K(xr, (ref_block_q8_K *)qr, K);
+        else if (vtype == TTS_TYPE_Q8_0) ref_quantize_row_q8_0(xr, (ref_block_q8_0 *)qr, K);
+        else for (int64_t k = 0; k < K; ++k) ((ref_fp16_t *)qr)[k] = ref_fp32_to_fp16(xr[k]);
+    }
+    return q;
+}
+
+void ref_gemv(int type, const void * w, const float * x, float * y, int64_t K, int64_t N, int64_t M, int n_threads) {
+    size_t row = 0;
+    void * xq = quantize_activations(type, x, K, M, &row);
+    if (n_threads < 1) n_threads = 1;
+    gemv_job jobs[256];
+    pthread_t th[256];
+    if (n_threads > 256) n_threads = 256;
+    for (int t = 0; t < n_threads; ++t) {
+        jobs[t] = (gemv_job){type, w, x, y, K, N, M, xq, row, t, n_threads};
+    }
+    for (int t = 1; t < n_threads; ++t) pthread_create(&th[t], NULL, gemv_thread, &jobs[t]);
+    gemv_rows(&jobs[0]);
+    for (int t = 1; t < n_threads; ++t) pthread_join(th[t], NULL);
+    free(xq);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Graph interpreter: ggml_compute_forward_* restatements over tts_tensor.                    */
+
+#define PF(t, i0, i1, i2, i3) ((float *)((char *)(t)->data + (i0) * (t)->nb[0] + (i1) * (t)->nb[1] + (i2) * (t)->nb[2] + (i3) * (t)->nb[3]))
+
+static inline float get_op_f(const tts_tensor * t, int i) {
+    float f;
+    memcpy(&f, &t->op_params[i], 4);
+    return f;
+}
+
+static int64_t nelements(const tts_tensor * t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+static int64_t nrows(const tts_tensor * t) { return t->ne[1] * t->ne[2] * t->ne[3]; }
+
+static inline float load_elem(const tts_tensor * t, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
+    const char * p = (const char *)t->data + i0 * t->nb[0] + i1 * t->nb[1] + i2 * t->nb[2] + i3 * t->nb[3];
+    switch (t->type) {
+        case TTS_TYPE_F16: return ref_fp16_to_fp32(*(const ref_fp16_t *)p);
+        case TTS_TYPE_I32: return (float)*(const int32_t *)p;
+        default: return *(const float *)p;
+    }
+}
+static inline void store_elem(const tts_tensor * t, int64_t i0, int64_t i1, int64_t i2, int64_t i3, float v) {
+    char * p = (char *)t->data + i0 * t->nb[0] + i1 * t->nb[1] + i2 * t->nb[2] + i3 * t->nb[3];
+    switch (t->type) {
+        case TTS_TYPE_F16: *(ref_fp16_t *)p = ref_fp32_to_fp16(v); break;
+        case TTS_TYPE_I32: *(int32_t *)p = (int32_t)v; break;
+        default: *(float *)p = v; break;
+    }
+}
+
+static void unravel(int64_t k, const int64_t * ne, int64_t * i) {
+    i[0] = k % ne[0]; k /= ne[0];
+    i[1] = k % ne[1]; k /= ne[1];
+    i[2] = k % ne[2]; k /= ne[2];
+    i[3] = k;
+}
+
+/* ggml_compute_forward_dup: element k of src (flattened, i0 fastest) -> element k of dst. */
+static void op_dup(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * src = dst->src[0];
+    const int64_t n = nelements(dst);
+    const int64_t dr = (n + nth - 1) / nth;
+    const int64_t k0 = dr * ith, k1 = MIN(k0 + dr, n);
+    int64_t is[4], id[4];
+    if (src->type == dst->type && src->type == TTS_TYPE_I32) {
+        for (int64_t k = k0; k < k1; ++k) {
+            unravel(k, src->ne, is);
+            unravel(k, dst->ne, id);
+            *(int32_t *)((char *)dst->data + id[0] * dst->nb[0] + id[1] * dst->nb[1] + id[2] * dst->nb[2] + id[3] * dst->nb[3]) =
+                *(const int32_t *)((const char *)src->data + is[0] * src->nb[0] + is[1] * src->nb[1] + is[2] * src->nb[2] + is[3] * src->nb[3]);
+        }
+        return;
+    }
+    for (int64_t k = k0; k < k1; ++k) {
+        unravel(k, src->ne, is);
+        unravel(k, dst->ne, id);
+        store_elem(dst, id[0], id[1], id[2], id[3], load_elem(src, is[0], is[1], is[2], is[3]));
+    }
+}
+
+/* ggml_compute_forward_cpy: cpy(a, b) writes a into b; dst is a view of b. */
+static void op_cpy(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * src = dst->src[0];
+    const int64_t n = nelements(src);
+    const int64_t dr = (n + nth - 1) / nth;
+    const int64_t k0 = dr * ith, k1 = MIN(k0 + dr, n);
+    int64_t is[4], id[4];
+    for (int64_t k = k0; k < k1; ++k) {
+        unravel(k, src->ne, is);
+        unravel(k, dst->ne, id);
+        store_elem(dst, id[0], id[1], id[2], id[3], load_elem(src, is[0], is[1], is[2], is[3]));
+    }
+}
+
+/* ggml_compute_forward_{add,sub,mul,div}_f32 with ggml_can_repeat broadcasting of src1. */
+static void op_binary(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    const int64_t nr = nrows(dst);
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        const int64_t j3 = i3 % b->ne[3], j2 = i2 % b->ne[2], j1 = i1 % b->ne[1];
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0) {
+            const float x = load_elem(a, i0, i1, i2, i3);
+            const float y = load_elem(b, i0 % b->ne[0], j1, j2, j3);
+            float v;
+            switch (dst->op) {
+                case TTS_OP_ADD: v = x + y; break;
+                case TTS_OP_SUB: v = x - y; break;
+                case TTS_OP_MUL: v = x * y; break;
+                default: v = x / y; break;
+            }
+            store_elem(dst, i0, i1, i2, i3, v);
+        }
+    }
+}
+
+/* ggml_vec_*_f32 unary maps (ggml-cpu vec.h); LEAKY_RELU / CLAMP / SCALE / fork ROUND, MOD. */
+static float unary_apply(const tts_tensor * dst, float x) {
+    switch (dst->op) {
+        case TTS_OP_SQR: return x * x;
+        case TTS_OP_SQRT: return sqrtf(x);
+        case TTS_OP_SIN: return sinf(x);
+        case TTS_OP_COS: return cosf(x);
+        case TTS_OP_SCALE: return x * get_op_f(dst, 0);
+        case TTS_OP_CLAMP: return MAX(MIN(x, get_op_f(dst, 1)), get_op_f(dst, 0));
+        case TTS_OP_LEAKY_RELU: {
+            const float ns = get_op_f(dst, 0);
+            return ((x > 0.f) ? x : 0.f) + ns * ((x < 0.0f) ? x : 0.f);
+        }
+        case TTS_OP_ROUND: return roundf(x);
+        case TTS_OP_MOD: return fmodf(x, get_op_f(dst, 0));
+        case TTS_OP_UNARY:
+            switch (dst->op_params[0]) {
+                case TTS_UNARY_ABS: return fabsf(x);
+                case TTS_UNARY_NEG: return -x;
+                case TTS_UNARY_TANH: return tanhf(x);
+                case TTS_UNARY_RELU: return (x > 0.f) ? x : 0.f;
+                case TTS_UNARY_SIGMOID: return 1.f / (1.f + expf(-x));
+                case TTS_UNARY_GELU: return ref_gelu_table(x);
+                case TTS_UNARY_SILU: return x / (1.0f + expf(-x));
+                case TTS_UNARY_EXP: return expf(x);
+            }
+    }
+    return x;
+}
+
+static void op_unary(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const int64_t nr = nrows(dst);
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0) {
+            store_elem(dst, i0, i1, i2, i3, unary_apply(dst, load_elem(a, i0, i1, i2, i3)));
+        }
+    }
+}
+
+/* ggml_compute_forward_norm_f32 / rms_norm_f32: double accumulation, then float scale. */
+static void op_norm(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const float eps = get_op_f(dst, 0);
+    const int64_t ne00 = a->ne[0];
+    for (int64_t i3 = 0; i3 < a->ne[3]; i3++) {
+        for (int64_t i2 = 0; i2 < a->ne[2]; i2++) {
+            for (int64_t i1 = ith; i1 < a->ne[1]; i1 += nth) {
+                const float * x = PF(a, 0, i1, i2, i3);
+                float * y = PF(dst, 0, i1, i2, i3);
+                if (dst->op == TTS_OP_NORM) {
+                    ggml_float sum = 0.0;
+                    for (int64_t i = 0; i < ne00; i++) sum += (ggml_float)x[i];
+                    const float mean = (float)(sum / ne00);
+                    ggml_float sum2 = 0.0;
+                    for (int64_t i = 0; i < ne00; i++) {
+                        const float v = x[i] - mean;
+                        y[i] = v;
+                        sum2 += (ggml_float)(v * v);
+                    }
+                    const float variance = (float)(sum2 / ne00);
+                    const float scale = 1.0f / sqrtf(variance + eps);
+                    for (int64_t i = 0; i < ne00; i++) y[i] *= scale;
+                } else {
+                    ggml_float sum = 0.0;
+                    for (int64_t i = 0; i < ne00; i++) sum += (ggml_float)(x[i] * x[i]);
+                    const float mean = (float)(sum / ne00);
+                    memmove(y, x, ne00 * sizeof(float));
+                    const float scale = 1.0f / sqrtf(mean + eps);
+                    for (int64_t i = 0; i < ne00; i++) y[i] *= scale;
+                }
+            }
+        }
+    }
+}
+
+/* ggml_compute_forward_soft_max_f32: wp = x*scale + slope*mask (mask row = i1 % ne01, row
+ * stride ne00), max, expf, double sum, scale by 1/sum. */
+static void op_soft_max(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * mask = dst->src[1];
+    const float scale = get_op_f(dst, 0);
+    const int64_t nc = a->ne[0];
+    const int64_t ne01 = a->ne[1];
+    const int64_t nr = nrows(a);
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    float * wp = (float *)malloc(nc * sizeof(float));
+    for (int64_t i1 = r0; i1 < r1; i1++) {
+        const float * sp = (const float *)((const char *)a->data + i1 * a->nb[1]);
+        float * dp = (float *)((char *)dst->data + i1 * dst->nb[1]);
+        for (int64_t i = 0; i < nc; ++i) wp[i] = sp[i] * scale;
+        if (mask) {
+            const int64_t mr = i1 % ne01;
+            for (int64_t i = 0; i < nc; ++i) {
+                float mv = mask->type == TTS_TYPE_F16 ? ref_fp16_to_fp32(((const ref_fp16_t *)mask->data)[mr * nc + i])
+                                                      : ((const float *)mask->data)[mr * nc + i];
+                wp[i] += 1.0f * mv;
+            }
+        }
+        float max = -INFINITY;
+        for (int64_t i = 0; i < nc; ++i) max = MAX(max, wp[i]);
+        ggml_float sum = 0.0;
+        for (int64_t i = 0; i < nc; ++i) {
+            const float val = expf(wp[i] - max);
+            sum += (ggml_float)val;
+            dp[i] = val;
+        }
+        sum = 1.0 / sum;
+        const float s = (float)sum;
+        for (int64_t i = 0; i < nc; ++i) dp[i] *= s;
+    }
+    free(wp);
+}
+
+/* ggml_compute_forward_mul_mat: src0 [K,N,ne02,ne03] x src1 [K,M,ne12,ne13] -> [N,M,ne12,ne13];
+ * src1 rows converted to vec_dot_type first; broadcast r2 = ne12/ne02, r3 = ne13/ne03. */
+static void op_mul_mat(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * s0 = dst->src[0];
+    const tts_tensor * s1 = dst->src[1];
+    const int64_t K = s0->ne[0];
+    const int64_t r2 = s1->ne[2] / s0->ne[2], r3 = s1->ne[3] / s0->ne[3];
+    int vtype = s0->type == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : s0->type == TTS_TYPE_Q8_0 ? TTS_TYPE_Q8_0
+              : s0->type == TTS_TYPE_F16 ? TTS_TYPE_F16 : TTS_TYPE_F32;
+    const size_t qrow = ref_row_size(vtype, K);
+    float * xr = (float *)malloc(K * sizeof(float));
+    char * xq = (char *)malloc(qrow);
+    const int64_t nout = dst->ne[1] * dst->ne[2] * dst->ne[3];
+    const int64_t dr = (nout + nth - 1) / nth;
+    const int64_t c0 = dr * ith, c1 = MIN(c0 + dr, nout);
+    for (int64_t c = c0; c < c1; ++c) {
+        const int64_t i13 = c / (dst->ne[1] * dst->ne[2]);
+        const int64_t i12 = (c - i13 * dst->ne[1] * dst->ne[2]) / dst->ne[1];
+        const int64_t i11 = c - i13 * dst->ne[1] * dst->ne[2] - i12 * dst->ne[1];
+        for (int64_t k = 0; k < K; ++k) xr[k] = load_elem(s1, k, i11, i12, i13);
+        if (vtype == TTS_TYPE_Q8_K) ref_quantize_row_q8_K(xr, (ref_block_q8_K *)xq, K);
+        else if (vtype == TTS_TYPE_Q8_0) ref_quantize_row_q8_0(xr, (ref_block_q8_0 *)xq, K);
+        else if (vtype == TTS_TYPE_F16) for (int64_t k = 0; k < K; ++k) ((ref_fp16_t *)xq)[k] = ref_fp32_to_fp16(xr[k]);
+        const int64_t i02 = i12 / r2, i03 = i13 / r3;
+        for (int64_t i01 = 0; i01 < s0->ne[1]; ++i01) {
+            const char * wr = (const char *)s0->data + i01 * s0->nb[1] + i02 * s0->nb[2] + i03 * s0->nb[3];
+            float s = 0;
+            switch (s0->type) {
+                case TTS_TYPE_Q4_K: ref_vec_dot_q4_K_q8_K((int)K, &s, wr, xq); break;
+                case TTS_TYPE_Q8_0: ref_vec_dot_q8_0_q8_0((int)K, &s, wr, xq); break;
+                case TTS_TYPE_F16: ref_vec_dot_f16((int)K, &s, (const ref_fp16_t *)wr, (const ref_fp16_t *)xq); break;
+                default: {
+                    /* src0 rows may be strided in ne0 only if nb[0]==4 (ggml requires it) */
+                    ggml_float sum = 0.0;
+                    const float * w = (const float *)wr;
+                    for (int64_t k = 0; k < K; ++k) sum += (ggml_float)(w[k] * xr[k]);
+                    s = (float)sum;
+                } break;
+            }
+            *PF(dst, i01, i11, i12, i13) = s;
+        }
+    }
+    free(xr);
+    free(xq);
+}
+
+/* ggml_compute_forward_get_rows (f32 / f16 / q4_K / q8_0 source; I32 index). */
+static void op_get_rows(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * s0 = dst->src[0];
+    const tts_tensor * s1 = dst->src[1];
+    const int64_t nc = s0->ne[0];
+    const int64_t nr = s1->ne[0] * s1->ne[1] * s1->ne[2];
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    for (int64_t i = r0; i < r1; ++i) {
+        const int64_t i12 = i / (s1->ne[1] * s1->ne[0]);
+        const int64_t i11 = (i - i12 * s1->ne[1] * s1->ne[0]) / s1->ne[0];
+        const int64_t i10 = i - i12 * s1->ne[1] * s1->ne[0] - i11 * s1->ne[0];
+        const int64_t i01 = *(const int32_t *)((const char *)s1->data + i10 * s1->nb[0] + i11 * s1->nb[1] + i12 * s1->nb[2]);
+        const char * src = (const char *)s0->data + i01 * s0->nb[1] + i11 * s0->nb[2] + i12 * s0->nb[3];
+        float * out = (float *)((char *)dst->data + i10 * dst->nb[1] + i11 * dst->nb[2] + i12 * dst->nb[3]);
+        switch (s0->type) {
+            case TTS_TYPE_Q4_K: ref_dequantize_row_q4_K((const ref_block_q4_K *)src, out, nc); break;
+            case TTS_TYPE_Q8_0: ref_dequantize_row_q8_0((const ref_block_q8_0 *)src, out, nc); break;
+            case TTS_TYPE_F16: for (int64_t k = 0; k < nc; ++k) out[k] = ref_fp16_to_fp32(((const ref_fp16_t *)src)[k]); break;
+            default: memcpy(out, src, nc * sizeof(float)); break;
+        }
+    }
+}
+
+/* ggml_compute_forward_concat (any dim). */
+static void op_concat(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    const int dim = dst->op_params[0];
+    int64_t o[4] = {0, 0, 0, 0};
+    o[dim] = a->ne[dim];
+    const int64_t nr = nrows(dst);
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0) {
+            float v;
+            if (i0 < a->ne[0] && i1 < a->ne[1] && i2 < a->ne[2] && i3 < a->ne[3]) v = load_elem(a, i0, i1, i2, i3);
+            else v = load_elem(b, i0 - o[0], i1 - o[1], i2 - o[2], i3 - o[3]);
+            store_elem(dst, i0, i1, i2, i3, v);
+        }
+    }
+}
+
+/* ggml_compute_forward_sum_rows_f32 (ggml_vec_sum_f32: double accumulation). */
+static void op_sum_rows(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const int64_t nr = nrows(a);
+    for (int64_t r = ith; r < nr; r += nth) {
+        const int64_t i3 = r / (a->ne[2] * a->ne[1]);
+        const int64_t i2 = (r - i3 * a->ne[2] * a->ne[1]) / a->ne[1];
+        const int64_t i1 = r - i3 * a->ne[2] * a->ne[1] - i2 * a->ne[1];
+        ggml_float s = 0.0;
+        for (int64_t i0 = 0; i0 < a->ne[0]; ++i0) s += (ggml_float)load_elem(a, i0, i1, i2, i3);
+        *PF(dst, 0, i1, i2, i3) = (float)s;
+    }
+}
+
+/* ggml_compute_forward_repeat_f32: dst[i] = src[i mod ne_src]. */
+static void op_repeat(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const int64_t nr = nrows(dst);
+    for (int64_t r = ith; r < nr; r += nth) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0)
+            store_elem(dst, i0, i1, i2, i3, load_elem(a, i0 % a->ne[0], i1 % a->ne[1], i2 % a->ne[2], i3 % a->ne[3]));
+    }
+}
+
+/* ggml_compute_forward_rope_f32, NEOX and NORM modes, optional freq_factors (src[2]), no YaRN.
+ * op_params: [1]=n_dims [2]=mode [4]=n_ctx_orig [5]=freq_base [6]=freq_scale [7]=ext_factor
+ *            [8]=attn_factor */
+static void op_rope(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * pos = dst->src[1];
+    const tts_tensor * ff = dst->src[2];
+    const int n_dims = dst->op_params[1];
+    const int mode = dst->op_params[2];
+    const float freq_base = get_op_f(dst, 5);
+    const float freq_scale = get_op_f(dst, 6);
+    const float attn_factor = get_op_f(dst, 8);
+    const int is_neox = mode & 2;
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    float * cache = (float *)malloc(a->ne[0] * sizeof(float));
+    for (int64_t i3 = 0; i3 < a->ne[3]; i3++) {
+        for (int64_t i2 = 0; i2 < a->ne[2]; i2++) {
+            const int64_t p = ((const int32_t *)pos->data)[i2];
+            float theta = (float)p;
+            for (int64_t i0 = 0; i0 < a->ne[0]; i0 += 2) {
+                const float f = ff ? ((const float *)ff->data)[i0 / 2] : 1.0f;
+                const float th = freq_scale * (theta / f);
+                cache[i0 + 0] = cosf(th) * attn_factor;
+                cache[i0 + 1] = sinf(th) * attn_factor;
+                theta *= theta_scale;
+            }
+            for (int64_t i1 = ith; i1 < a->ne[1]; i1 += nth) {
+                for (int64_t i0 = 0; i0 < n_dims; i0 += 2) {
+                    const float c = cache[i0], s = cache[i0 + 1];
+                    if (is_neox) {
+                        const int64_t ic = i0 / 2;
+                        const float x0 = *PF(a, ic, i1, i2, i3);
+                        const float x1 = *PF(a, ic + n_dims / 2, i1, i2, i3);
+                        *PF(dst, ic, i1, i2, i3) = x0 * c - x1 * s;
+                        *PF(dst, ic + n_dims / 2, i1, i2, i3) = x0 * s + x1 * c;
+                    } else {
+                        const float x0 = *PF(a, i0, i1, i2, i3);
+                        const float x1 = *PF(a, i0 + 1, i1, i2, i3);
+                        *PF(dst, i0, i1, i2, i3) = x0 * c - x1 * s;
+                        *PF(dst, i0 + 1, i1, i2, i3) = x0 * s + x1 * c;
+                    }
+                }
+                for (int64_t i0 = n_dims; i0 < a->ne[0]; i0++) *PF(dst, i0, i1, i2, i3) = *PF(a, i0, i1, i2, i3);
+            }
+        }
+    }
+    free(cache);
+}
+
+static int is_view_op(int op) {
+    return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
+}
+
+static int compute_node_mt(tts_tensor * node, int ith, int nth) {
+    switch (node->op) {
+        case TTS_OP_NONE: case TTS_OP_VIEW: case TTS_OP_RESHAPE: case TTS_OP_PERMUTE: case TTS_OP_TRANSPOSE:
+            return 0;
+        case TTS_OP_DUP: case TTS_OP_CONT: op_dup(node, ith, nth); return 0;
+        case TTS_OP_CPY: op_cpy(node, ith, nth); return 0;
+        case TTS_OP_ADD: case TTS_OP_SUB: case TTS_OP_MUL: case TTS_OP_DIV: op_binary(node, ith, nth); return 0;
+        case TTS_OP_SQR: case TTS_OP_SQRT: case TTS_OP_SIN: case TTS_OP_COS: case TTS_OP_SCALE: case TTS_OP_CLAMP:
+        case TTS_OP_LEAKY_RELU: case TTS_OP_ROUND: case TTS_OP_MOD: case TTS_OP_UNARY:
+            op_unary(node, ith, nth); return 0;
+        case TTS_OP_NORM: case TTS_OP_RMS_NORM: op_norm(node, ith, nth); return 0;
+        case TTS_OP_SOFT_MAX: op_soft_max(node, ith, nth); return 0;
+        case TTS_OP_MUL_MAT: op_mul_mat(node, ith, nth); return 0;
+        case TTS_OP_GET_ROWS: op_get_rows(node, ith, nth); return 0;
+        case TTS_OP_CONCAT: op_concat(node, ith, nth); return 0;
+        case TTS_OP_SUM_ROWS: op_sum_rows(node, ith, nth); return 0;
+        case TTS_OP_REPEAT: op_repeat(node, ith, nth); return 0;
+        case TTS_OP_ROPE: op_rope(node, ith, nth); return 0;
+        default: return TTS_STATUS_UNSUPPORTED;
+    }
+}
+
+int oracle_compute_node(tts_tensor * node) { return compute_node_mt(node, 0, 1); }
+
+/* ---- threaded graph execution: one barrier per node, as ggml_graph_compute does ---- */
+typedef struct {
+    tts_tensor * const * nodes;
+    int n_nodes;
+    int nth;
+    pthread_barrier_t barrier;
+    int status;
+} graph_state;
+
+typedef struct {
+    graph_state * g;
+    int ith;
+} graph_worker;
+
+static void * graph_thread(void * p) {
+    graph_worker * w = (graph_worker *)p;
+    graph_state * g = w->g;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        tts_tensor * node = g->nodes[i];
+        if (is_view_op(node->op)) continue;
+        int st = compute_node_mt(node, w->ith, g->nth);
+        if (st != 0 && w->ith == 0) g->status = st;
+        pthread_barrier_wait(&g->barrier);
+    }
+    return NULL;
+}
+
+int oracle_graph_compute(tts_tensor * const * nodes, int n_nodes, int n_threads) {
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    graph_state g;
+    g.nodes = nodes;
+    g.n_nodes = n_nodes;
+    g.nth = n_threads;
+    g.status = 0;
+    pthread_barrier_init(&g.barrier, NULL, (unsigned)n_threads);
+    graph_worker w[256];
+    pthread_t th[256];
+    for (int t = 0; t < n_threads; ++t) w[t] = (graph_worker){&g, t};
+    for (int t = 1; t < n_threads; ++t) pthread_create(&th[t], NULL, graph_thread, &w[t]);
+    graph_thread(&w[0]);
+    for (int t = 1; t < n_threads; ++t) pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&g.barrier);
+    return g.status;
+}
+
+/* ---- backend vtable over host memory ---- */
+static int g_oracle_threads = 1;
+static void * ob_alloc(void * ctx, size_t size) {
+    (void)ctx;
+    void * p = NULL;
+    if (posix_memalign(&p, 256, size ? size : 256) != 0) return NULL;
+    memset(p, 0, size);
+    return p;
+}
+static void ob_free(void * ctx, void * p) { (void)ctx; free(p); }
+static int ob_set(void * ctx, void * dst, const void * src, size_t n) { (void)ctx; memcpy(dst, src, n); return 0; }
+static int ob_get(void * ctx, void * dst, const void * src, size_t n) { (void)ctx; memcpy(dst, src, n); return 0; }
+static int ob_memset(void * ctx, void * dst, int v, size_t n) { (void)ctx; memset(dst, v, n); return 0; }
+static int ob_compute(void * ctx, tts_tensor * const * nodes, int n) { (void)ctx; return oracle_graph_compute(nodes, n, g_oracle_threads); }
+static int ob_sync(void * ctx) { (void)ctx; return 0; }
+
+int oracle_backend_iface(tts_backend_iface * out, int n_threads) {
+    g_oracle_threads = n_threads < 1 ? 1 : n_threads;
+    out->ctx = NULL;
+    out->name = "oracle-cpu";
+    out->alloc = ob_alloc;
+    out->free = ob_free;
+    out->set = ob_set;
+    out->get = ob_get;
+    out->memset = ob_memset;
+    out->compute = ob_compute;
+    out->synchronize = ob_sync;
+    return 0;
+}

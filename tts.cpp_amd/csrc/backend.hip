@@ -1,0 +1,345 @@
+// HIP backend: the C-ABI of include/tts_hip.h.  One backend = one device + one HIP stream
+// (one per runner, as TTS.cpp's server runs one runner per worker thread:
+// /root/reference/examples/server/server.cpp:316-321).
+#include <cmath>
+#include <cstring>
+
+#include "hip_internal.h"
+
+using namespace tts;
+
+namespace tts {
+int launch_fused(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes, int i, int * consumed);
+}
+
+// GGML_GELU_FP16 table: fp16(ggml_gelu_f32(fp16_to_fp32(i))) for every fp16 bit pattern,
+// computed on the host with the same f32 expression ggml uses (no contraction; see Makefile).
+static void build_gelu_table(uint16_t * t) {
+    const float GELU_COEF_A = 0.044715f;
+    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    for (int i = 0; i < 65536; ++i) {
+        const float x = fp16_to_fp32_host((uint16_t)i);
+        const float g = 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+        t[i] = fp32_to_fp16_host(g);
+    }
+}
+
+static const size_t kScratchBytes = 64u << 20;
+
+extern "C" {
+
+int tts_hip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+tts_hip_backend_t tts_hip_backend_init(int device) {
+    int n = tts_hip_device_count();
+    if (device < 0 || device >= n) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    auto * be = new tts_hip_backend();
+    be->device = device;
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    TTS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    snprintf(be->name, sizeof(be->name), "HIP%d(%s)", device, prop.gcnArchName);
+    TTS_HIP_CHECK(hipMalloc((void **)&be->scratch, kScratchBytes));
+    be->scratch_size = kScratchBytes;
+    std::vector<uint16_t> tab(65536);
+    build_gelu_table(tab.data());
+    TTS_HIP_CHECK(hipMalloc((void **)&be->gelu_table, 65536 * sizeof(uint16_t)));
+    TTS_HIP_CHECK(hipMemcpy(be->gelu_table, tab.data(), 65536 * sizeof(uint16_t), hipMemcpyHostToDevice));
+    return be;
+}
+
+void tts_hip_backend_free(tts_hip_backend_t be) {
+    if (!be) return;
+    hipSetDevice(be->device);
+    hipStreamSynchronize(be->stream);
+    for (auto & p : be->ev_pending) {
+        hipEventDestroy(p.first);
+        hipEventDestroy(p.second);
+    }
+    for (auto e : be->ev_free) hipEventDestroy(e);
+    hipFree(be->scratch);
+    hipFree(be->gelu_table);
+    hipStreamDestroy(be->stream);
+    delete be;
+}
+
+const char * tts_hip_backend_name(tts_hip_backend_t be) { return be ? be->name : "HIP(null)"; }
+
+size_t tts_hip_buffer_alignment(void) { return 256; }
+
+void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {
+    if (!be) return nullptr;
+    hipSetDevice(be->device);
+    void * p = nullptr;
+    if (hipMalloc(&p, size ? size : 256) != hipSuccess) return nullptr;
+    return p;
+}
+
+void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
+    if (!be || !ptr) return;
+    hipSetDevice(be->device);
+    hipStreamSynchronize(be->stream);
+    hipFree(ptr);
+}
+
+int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
+    if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    return 0;
+}
+
+int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    // The reference reads the host copy right after get_tensor_async with no synchronize
+    // (src/tts_model.cpp:25-36), so this call completes the stream first.
+    if (hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToHost, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    return 0;
+}
+
+int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToDevice, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+
+int tts_hip_memset(tts_hip_backend_t be, void * dst, int value, size_t size) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return hipMemsetAsync(dst, value, size, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+
+int tts_hip_synchronize(tts_hip_backend_t be) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return hipStreamSynchronize(be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+
+static bool is_f32(const tts_tensor * t) { return t && t->type == TTS_TYPE_F32; }
+
+int tts_hip_supports_op(const tts_tensor * n) {
+    if (!n) return 0;
+    // a buffer-less host leaf (util.cpp:86-94 reciprocal trick) cannot be read by the device;
+    // the adapter flags such sources with flags bit 1 (host data).
+    for (int i = 0; i < TTS_MAX_SRC; ++i)
+        if (n->src[i] && (n->src[i]->flags & 2)) return 0;
+    switch (n->op) {
+        case TTS_OP_NONE: case TTS_OP_VIEW: case TTS_OP_RESHAPE: case TTS_OP_PERMUTE: case TTS_OP_TRANSPOSE:
+            return 1;
+        case TTS_OP_DUP: case TTS_OP_CONT: case TTS_OP_CPY:
+            return (n->type == TTS_TYPE_F32 || n->type == TTS_TYPE_F16 || n->type == TTS_TYPE_I32) &&
+                   (n->src[0]->type == TTS_TYPE_F32 || n->src[0]->type == TTS_TYPE_F16 || n->src[0]->type == TTS_TYPE_I32);
+        case TTS_OP_ADD: case TTS_OP_SUB: case TTS_OP_MUL: case TTS_OP_DIV:
+        case TTS_OP_SQR: case TTS_OP_SQRT: case TTS_OP_SIN: case TTS_OP_COS: case TTS_OP_SCALE: case TTS_OP_CLAMP:
+        case TTS_OP_LEAKY_RELU: case TTS_OP_ROUND: case TTS_OP_MOD: case TTS_OP_UNARY: case TTS_OP_CONCAT:
+        case TTS_OP_REPEAT: case TTS_OP_SUM_ROWS:
+            return 1;
+        case TTS_OP_NORM: case TTS_OP_RMS_NORM:
+            return is_f32(n->src[0]) && n->src[0]->nb[0] == 4;
+        case TTS_OP_SOFT_MAX:
+            return is_f32(n->src[0]);
+        case TTS_OP_ROPE:
+            return is_f32(n->src[0]);
+        case TTS_OP_GET_ROWS:
+            return n->src[1]->type == TTS_TYPE_I32 &&
+                   (n->src[0]->type == TTS_TYPE_F32 || n->src[0]->type == TTS_TYPE_F16 || n->src[0]->type == TTS_TYPE_Q4_K ||
+                    n->src[0]->type == TTS_TYPE_Q8_0);
+        case TTS_OP_MUL_MAT: {
+            const tts_tensor * a = n->src[0];
+            const tts_tensor * b = n->src[1];
+            if (!is_f32(b)) return 0;
+            if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) return 1;
+            if (a->type == TTS_TYPE_Q4_K) return a->ne[0] % 256 == 0;
+            if (a->type == TTS_TYPE_Q8_0) return a->ne[0] % 32 == 0;
+            return 0;
+        }
+        default:
+            return 0;
+    }
+}
+
+}  // extern "C"
+
+static bool rows_contig_f32(const tts_tensor * t) { return t->type == TTS_TYPE_F32 && t->nb[0] == 4; }
+
+// MUL_MAT with a 2-D weight matrix and a column set whose rows are contiguous: the decode GEMV.
+static bool is_gemv(const tts_tensor * n) {
+    const tts_tensor * a = n->src[0];
+    const tts_tensor * b = n->src[1];
+    if (a->ne[2] != 1 || a->ne[3] != 1) return false;
+    if (!rows_contig_f32(b)) return false;
+    // columns must be evenly strided (b viewed as [K, M] with stride nb[1])
+    if (b->ne[2] * b->ne[3] != 1 && !(b->nb[2] == b->nb[1] * (size_t)b->ne[1] && b->nb[3] == b->nb[2] * (size_t)b->ne[2]))
+        return false;
+    if (n->nb[0] != 4 || (n->ne[2] * n->ne[3] != 1 && !(n->nb[2] == n->nb[1] * (size_t)n->ne[1]))) return false;
+    if (a->nb[0] != tts_type_size(a->type)) return false;
+    if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) {
+        // worthwhile only for weight-shaped operands with K multiple of 4
+        if (a->ne[0] % 4 != 0 || (b->nb[1] % 16) != 0) return false;
+    }
+    if ((b->nb[1] % 4) != 0) return false;
+    return true;
+}
+
+static int compute_mul_mat(tts_hip_backend * be, const tts_tensor * n) {
+    const tts_tensor * a = n->src[0];
+    const tts_tensor * b = n->src[1];
+    if (!is_gemv(n)) {
+        if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) return launch_op(be, n);
+        return TTS_STATUS_UNSUPPORTED;
+    }
+    const int64_t K = a->ne[0], N = a->ne[1];
+    const int64_t M = b->ne[1] * b->ne[2] * b->ne[3];
+    const int64_t xcs = (int64_t)(b->nb[1] / 4);
+    const int64_t ycs = (int64_t)(n->nb[1] / 4);
+    const int64_t wrb = (int64_t)a->nb[1];
+    ActQuant & aq = be->aq;
+    if (a->type != TTS_TYPE_F32) {
+        const int vt = a->type == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : a->type;
+        const bool hit = aq.src == b->data && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
+        if (!hit) {
+            if (act_quant_bytes(a->type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+            launch_quantize_act(be, a->type, (const float *)b->data, xcs, K, M, aq);
+            aq.src = b->data;
+            aq.graph_epoch = be->graph_epoch;
+        }
+    } else {
+        aq.vtype = TTS_TYPE_F32;
+        aq.src = nullptr;
+    }
+    launch_gemv(be, a->type, a->data, wrb, (const float *)b->data, xcs, &aq, (float *)n->data, ycs, K, N, M);
+    return 0;
+}
+
+static bool is_view_op(int op) {
+    return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
+}
+
+extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    be->graph_epoch++;
+    for (int i = 0; i < n_nodes; ++i) {
+        tts_tensor * n = nodes[i];
+        if (is_view_op(n->op)) continue;
+        if (be->fusion) {
+            int consumed = 0;
+            int st = launch_fused(be, nodes, n_nodes, i, &consumed);
+            if (st != 0) return st;
+            if (consumed > 0) {
+                i += consumed - 1;
+                continue;
+            }
+        }
+        int st;
+        if (n->op == TTS_OP_MUL_MAT) st = compute_mul_mat(be, n);
+        else st = launch_op(be, n);
+        if (st != 0) {
+            fprintf(stderr, "tts_hip_graph_compute: node %d (%s, %s) failed: %d\n", i, n->name, tts_op_name(n->op), st);
+            return st;
+        }
+        // any write into a buffer that the cached activation quantization was built from
+        // invalidates it (the cache is keyed by src pointer within this graph)
+        if (be->aq.src && n->data == be->aq.src) be->aq.src = nullptr;
+    }
+    return 0;
+}
+
+extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    switch (option) {
+        case TTS_HIP_OPT_FUSION: be->fusion = value != 0; return 0;
+        case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
+        default: return TTS_STATUS_BAD_ARG;
+    }
+}
+
+extern "C" int tts_hip_gemv_stats(tts_hip_backend_t be, int type, double * ms, int64_t * launches, double * bytes, int reset) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+    for (size_t i = 0; i < be->ev_pending.size(); ++i) {
+        float t = 0;
+        TTS_HIP_CHECK(hipEventElapsedTime(&t, be->ev_pending[i].first, be->ev_pending[i].second));
+        const int ty = be->ev_type[i];
+        be->gemv_ms[ty] += t;
+        be->gemv_launches[ty] += 1;
+        be->gemv_bytes[ty] += be->ev_bytes[i];
+        be->ev_free.push_back(be->ev_pending[i].first);
+        be->ev_free.push_back(be->ev_pending[i].second);
+    }
+    be->ev_pending.clear();
+    be->ev_bytes.clear();
+    be->ev_type.clear();
+    double a = 0, c = 0;
+    int64_t b = 0;
+    for (int ty = 0; ty < TTS_TYPE_COUNT; ++ty) {
+        if (type >= 0 && ty != type) continue;
+        a += be->gemv_ms[ty];
+        b += be->gemv_launches[ty];
+        c += be->gemv_bytes[ty];
+    }
+    if (ms) *ms = a;
+    if (launches) *launches = b;
+    if (bytes) *bytes = c;
+    if (reset) {
+        for (int ty = 0; ty < TTS_TYPE_COUNT; ++ty) {
+            be->gemv_ms[ty] = 0;
+            be->gemv_launches[ty] = 0;
+            be->gemv_bytes[ty] = 0;
+        }
+    }
+    return 0;
+}
+
+extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
+                            int64_t M) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    if (type == TTS_TYPE_Q4_K && K % 256) return TTS_STATUS_BAD_ARG;
+    if (type == TTS_TYPE_Q8_0 && K % 32) return TTS_STATUS_BAD_ARG;
+    if (type != TTS_TYPE_Q4_K && type != TTS_TYPE_Q8_0 && type != TTS_TYPE_F16 && type != TTS_TYPE_F32) return TTS_STATUS_UNSUPPORTED;
+    if ((type == TTS_TYPE_F32 || type == TTS_TYPE_F16) && K % 4) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    ActQuant aq;
+    if (type != TTS_TYPE_F32) {
+        if (act_quant_bytes(type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+        launch_quantize_act(be, type, x, K, K, M, aq);
+    } else {
+        aq.vtype = TTS_TYPE_F32;
+    }
+    be->aq.src = nullptr;  // scratch overwritten
+    launch_gemv(be, type, w, (int64_t)tts_row_size(type, K), x, K, &aq, y, N, K, N, M);
+    return 0;
+}
+
+// ---- generic vtable over this backend ----
+static void * hb_alloc(void * c, size_t n) { return tts_hip_buffer_alloc((tts_hip_backend_t)c, n); }
+static void hb_free(void * c, void * p) { tts_hip_buffer_free((tts_hip_backend_t)c, p); }
+static int hb_set(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_set((tts_hip_backend_t)c, d, s, n); }
+static int hb_get(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_get((tts_hip_backend_t)c, d, s, n); }
+static int hb_memset(void * c, void * d, int v, size_t n) { return tts_hip_memset((tts_hip_backend_t)c, d, v, n); }
+static int hb_compute(void * c, tts_tensor * const * nodes, int n) { return tts_hip_graph_compute((tts_hip_backend_t)c, nodes, n); }
+static int hb_sync(void * c) { return tts_hip_synchronize((tts_hip_backend_t)c); }
+
+extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * out) {
+    if (!be || !out) return TTS_STATUS_BAD_ARG;
+    out->ctx = be;
+    out->name = be->name;
+    out->alloc = hb_alloc;
+    out->free = hb_free;
+    out->set = hb_set;
+    out->get = hb_get;
+    out->memset = hb_memset;
+    out->compute = hb_compute;
+    out->synchronize = hb_sync;
+    return 0;
+}

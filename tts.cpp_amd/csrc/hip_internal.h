@@ -1,0 +1,95 @@
+// Internal HIP backend state and kernel launchers (not part of the C-ABI).
+#pragma once
+
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "common.h"
+
+#define TTS_HIP_CHECK(expr)                                                                          \
+    do {                                                                                             \
+        hipError_t err_ = (expr);                                                                    \
+        if (err_ != hipSuccess) {                                                                    \
+            fprintf(stderr, "%s:%d: HIP error %s: %s\n", __FILE__, __LINE__, #expr, hipGetErrorString(err_)); \
+            abort();                                                                                 \
+        }                                                                                            \
+    } while (0)
+
+namespace tts {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Tensor view handed to kernels by value: data pointer, shape and byte strides (ggml ne/nb).
+struct TD {
+    char * data;
+    int64_t ne[4];
+    int64_t nb[4];
+    int32_t type;
+    int32_t pad;
+};
+
+inline TD make_td(const tts_tensor * t) {
+    TD d;
+    d.data = (char *)t->data;
+    for (int i = 0; i < 4; ++i) {
+        d.ne[i] = t->ne[i];
+        d.nb[i] = (int64_t)t->nb[i];
+    }
+    d.type = t->type;
+    d.pad = 0;
+    return d;
+}
+
+// Device scratch for quantized activations (Q8_K / Q8_0 / F16 copies of a mul_mat src1).
+struct ActQuant {
+    const void * src = nullptr;  // src1 data pointer the cache entry was built from
+    int64_t K = 0, M = 0;
+    int vtype = -1;
+    int64_t graph_epoch = -1;
+    int8_t * qs = nullptr;      // [M][K] int8 (Q8_K / Q8_0) or fp16 [M][K] (F16)
+    float * d = nullptr;        // [M][K/256] (Q8_K) or [M][K/32] (Q8_0: fp16-rounded d as float)
+    int32_t * bsums = nullptr;  // [M][K/16] (Q8_K)
+};
+
+}  // namespace tts
+
+struct tts_hip_backend {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    char name[64] = {0};
+    // scratch arena for activation quantization
+    char * scratch = nullptr;
+    size_t scratch_size = 0;
+    tts::ActQuant aq;
+    int64_t graph_epoch = 0;
+    uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
+    bool fusion = true;
+    bool profile_gemv = false;
+    double gemv_ms[TTS_TYPE_COUNT] = {0};
+    int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
+    double gemv_bytes[TTS_TYPE_COUNT] = {0};
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending;
+    std::vector<double> ev_bytes;
+    std::vector<int> ev_type;
+    std::vector<hipEvent_t> ev_free;
+};
+
+namespace tts {
+
+// ---- launchers (k_gemv.hip) ----
+// Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
+void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
+// y[m*ycs + n] = dot(W row n, x column m)
+void launch_gemv(tts_hip_backend * be, int wtype, const void * w, int64_t w_row_bytes, const float * x, int64_t xcs,
+                 const ActQuant * aq, float * y, int64_t ycs, int64_t K, int64_t N, int64_t M);
+size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
+
+// ---- launchers (k_ops.hip) ----
+int launch_op(tts_hip_backend * be, const tts_tensor * node);
+
+}  // namespace tts

@@ -1,0 +1,476 @@
+// Generic strided op kernels for the ggml ops TTS.cpp graphs emit.  Every kernel
+// takes ggml-style (ne, nb) views so that VIEW / PERMUTE / TRANSPOSE nodes stay metadata-only,
+// exactly as in ggml.  Reductions that ggml-cpu performs in double (NORM, RMS_NORM, SUM_ROWS,
+// SOFT_MAX's denominator, f32 dot products) are done in f64 here as well, which keeps results
+// within an ulp of the CPU oracle.  Fused fast paths live in k_fused.hip.
+#include "hip_internal.h"
+
+namespace tts {
+
+__device__ __forceinline__ float td_load(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
+    const char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
+    if (t.type == TTS_TYPE_F16) return __half2float(*(const __half *)p);
+    if (t.type == TTS_TYPE_I32) return (float)*(const int32_t *)p;
+    return *(const float *)p;
+}
+__device__ __forceinline__ void td_store(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3, float v) {
+    char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
+    if (t.type == TTS_TYPE_F16) *(__half *)p = __float2half_rn(v);
+    else if (t.type == TTS_TYPE_I32) *(int32_t *)p = (int32_t)v;
+    else *(float *)p = v;
+}
+__device__ __forceinline__ void unravel(int64_t k, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
+    i0 = k % ne[0];
+    k /= ne[0];
+    i1 = k % ne[1];
+    k /= ne[1];
+    i2 = k % ne[2];
+    i3 = k / ne[2];
+}
+
+// ---- copies: element k of src (flattened, i0 fastest) -> element k of dst (ggml dup/cpy) ----
+__global__ void k_cpy(TD dst, TD src, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a0, a1, a2, a3, b0, b1, b2, b3;
+        unravel(k, src.ne, a0, a1, a2, a3);
+        unravel(k, dst.ne, b0, b1, b2, b3);
+        if (src.type == TTS_TYPE_I32 && dst.type == TTS_TYPE_I32) {
+            *(int32_t *)(dst.data + b0 * dst.nb[0] + b1 * dst.nb[1] + b2 * dst.nb[2] + b3 * dst.nb[3]) =
+                *(const int32_t *)(src.data + a0 * src.nb[0] + a1 * src.nb[1] + a2 * src.nb[2] + a3 * src.nb[3]);
+        } else {
+            td_store(dst, b0, b1, b2, b3, td_load(src, a0, a1, a2, a3));
+        }
+    }
+}
+
+// ---- binary with broadcast of src1 (ggml_can_repeat) ----
+template <int OP>
+__global__ void k_binary(TD dst, TD a, TD b, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unravel(k, dst.ne, i0, i1, i2, i3);
+        const float x = td_load(a, i0, i1, i2, i3);
+        const float y = td_load(b, i0 % b.ne[0], i1 % b.ne[1], i2 % b.ne[2], i3 % b.ne[3]);
+        float v;
+        if (OP == TTS_OP_ADD) v = __fadd_rn(x, y);
+        else if (OP == TTS_OP_SUB) v = __fsub_rn(x, y);
+        else if (OP == TTS_OP_MUL) v = __fmul_rn(x, y);
+        else v = __fdiv_rn(x, y);
+        td_store(dst, i0, i1, i2, i3, v);
+    }
+}
+
+// Contiguous fast path: dst, a contiguous f32; b contiguous f32 broadcast over rows.
+template <int OP>
+__global__ void k_binary_cont(float * __restrict__ dst, const float * __restrict__ a, const float * __restrict__ b,
+                              int64_t n, int64_t nb_el) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const float x = a[k];
+        const float y = b[k % nb_el];
+        float v;
+        if (OP == TTS_OP_ADD) v = __fadd_rn(x, y);
+        else if (OP == TTS_OP_SUB) v = __fsub_rn(x, y);
+        else if (OP == TTS_OP_MUL) v = __fmul_rn(x, y);
+        else v = __fdiv_rn(x, y);
+        dst[k] = v;
+    }
+}
+
+// ---- unary maps ----
+struct UnaryParams {
+    int op;
+    int uop;
+    float p0, p1;
+    const uint16_t * gelu_table;
+};
+
+__device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
+    switch (P.op) {
+        case TTS_OP_SQR: return __fmul_rn(x, x);
+        case TTS_OP_SQRT: return __fsqrt_rn(x);
+        case TTS_OP_SIN: return sinf(x);
+        case TTS_OP_COS: return cosf(x);
+        case TTS_OP_SCALE: return __fmul_rn(x, P.p0);
+        case TTS_OP_CLAMP: return fmaxf(fminf(x, P.p1), P.p0);
+        case TTS_OP_LEAKY_RELU: return __fadd_rn((x > 0.f) ? x : 0.f, __fmul_rn(P.p0, (x < 0.f) ? x : 0.f));
+        case TTS_OP_ROUND: return roundf(x);
+        case TTS_OP_MOD: return fmodf(x, P.p0);
+        default: break;
+    }
+    switch (P.uop) {
+        case TTS_UNARY_ABS: return fabsf(x);
+        case TTS_UNARY_NEG: return -x;
+        case TTS_UNARY_TANH: return tanhf(x);
+        case TTS_UNARY_RELU: return x > 0.f ? x : 0.f;
+        case TTS_UNARY_SIGMOID: return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x)));
+        case TTS_UNARY_GELU: {
+            if (x <= -10.0f) return 0.0f;
+            if (x >= 10.0f) return x;
+            const uint16_t h = __half_as_ushort(__float2half_rn(x));
+            return __half2float(__ushort_as_half(P.gelu_table[h]));
+        }
+        case TTS_UNARY_SILU: return __fdiv_rn(x, __fadd_rn(1.0f, expf(-x)));
+        case TTS_UNARY_EXP: return expf(x);
+    }
+    return x;
+}
+
+__global__ void k_unary(TD dst, TD a, int64_t n, UnaryParams P) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unravel(k, dst.ne, i0, i1, i2, i3);
+        td_store(dst, i0, i1, i2, i3, unary_apply(P, td_load(a, i0, i1, i2, i3)));
+    }
+}
+
+__global__ void k_unary_cont(float * __restrict__ dst, const float * __restrict__ a, int64_t n, UnaryParams P) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+        dst[k] = unary_apply(P, a[k]);
+}
+
+// ---- block reductions in double ----
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T * sh) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    T r = 0;
+    for (int i = 0; i < nw; ++i) r += sh[i];
+    return r;
+}
+__device__ __forceinline__ float block_max(float v, float * sh) {
+    for (int off = 32; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    float r = sh[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, sh[i]);
+    return r;
+}
+
+// ---- NORM / RMS_NORM (ggml_compute_forward_norm_f32 / rms_norm_f32), one block per row ----
+template <bool RMS>
+__global__ __launch_bounds__(256) void k_norm(TD dst, TD a, float eps) {
+    __shared__ double shd[8];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % a.ne[1], i2 = (r / a.ne[1]) % a.ne[2], i3 = r / (a.ne[1] * a.ne[2]);
+    const float * x = (const float *)(a.data + i1 * a.nb[1] + i2 * a.nb[2] + i3 * a.nb[3]);
+    float * y = (float *)(dst.data + i1 * dst.nb[1] + i2 * dst.nb[2] + i3 * dst.nb[3]);
+    const int64_t n = a.ne[0];
+    if (!RMS) {
+        double s = 0.0;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double)x[i];
+        s = block_sum<double>(s, shd);
+        const float mean = (float)(s / (double)n);
+        double s2 = 0.0;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+            const float v = __fsub_rn(x[i], mean);
+            s2 += (double)__fmul_rn(v, v);
+        }
+        s2 = block_sum<double>(s2, shd);
+        const float variance = (float)(s2 / (double)n);
+        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(variance, eps)));
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) y[i] = __fmul_rn(__fsub_rn(x[i], mean), scale);
+    } else {
+        double s = 0.0;
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double)__fmul_rn(x[i], x[i]);
+        s = block_sum<double>(s, shd);
+        const float mean = (float)(s / (double)n);
+        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(mean, eps)));
+        for (int64_t i = threadIdx.x; i < n; i += blockDim.x) y[i] = __fmul_rn(x[i], scale);
+    }
+}
+
+// ---- SOFT_MAX ext (scale, optional mask row i1 % ne01 with row stride ne00) ----
+__global__ __launch_bounds__(256) void k_soft_max(TD dst, TD a, const char * mask, int mask_f16, float scale) {
+    __shared__ double shd[8];
+    __shared__ float shf[8];
+    const int64_t r = blockIdx.x;
+    const int64_t nc = a.ne[0];
+    const float * sp = (const float *)(a.data + r * a.nb[1]);
+    float * dp = (float *)(dst.data + r * dst.nb[1]);
+    const int64_t mr = r % a.ne[1];
+    float mx = -INFINITY;
+    for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        float w = __fmul_rn(sp[i], scale);
+        if (mask) {
+            const float mv = mask_f16 ? __half2float(((const __half *)mask)[mr * nc + i]) : ((const float *)mask)[mr * nc + i];
+            w = __fadd_rn(w, __fmul_rn(1.0f, mv));
+        }
+        dp[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = block_max(mx, shf);
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
+        const float v = expf(__fsub_rn(dp[i], mx));
+        dp[i] = v;
+        s += (double)v;
+    }
+    s = block_sum<double>(s, shd);
+    const float inv = (float)(1.0 / s);
+    for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) dp[i] = __fmul_rn(dp[i], inv);
+}
+
+// ---- GET_ROWS (f32 / f16 / q4_K / q8_0 source, i32 index) ----
+__global__ void k_get_rows(TD dst, TD s0, TD s1) {
+    const int64_t i = blockIdx.x;  // index into flattened s1
+    const int64_t i10 = i % s1.ne[0], i11 = (i / s1.ne[0]) % s1.ne[1], i12 = i / (s1.ne[0] * s1.ne[1]);
+    const int64_t i01 = *(const int32_t *)(s1.data + i10 * s1.nb[0] + i11 * s1.nb[1] + i12 * s1.nb[2]);
+    const char * src = s0.data + i01 * s0.nb[1] + i11 * s0.nb[2] + i12 * s0.nb[3];
+    float * out = (float *)(dst.data + i10 * dst.nb[1] + i11 * dst.nb[2] + i12 * dst.nb[3]);
+    const int64_t nc = s0.ne[0];
+    for (int64_t k = threadIdx.x; k < nc; k += blockDim.x) {
+        float v;
+        if (s0.type == TTS_TYPE_F32) v = ((const float *)src)[k];
+        else if (s0.type == TTS_TYPE_F16) v = __half2float(((const __half *)src)[k]);
+        else if (s0.type == TTS_TYPE_Q8_0) {
+            const block_q8_0 * b = (const block_q8_0 *)src + k / QK8_0;
+            v = __fmul_rn((float)b->qs[k % QK8_0], __half2float(__ushort_as_half(b->d)));
+        } else {  // Q4_K: dequantize_row_q4_K
+            const block_q4_K * b = (const block_q4_K *)src + k / QK_K;
+            const int e = (int)(k % QK_K);
+            const int j64 = e / 64, w = e % 64, hi = w >= 32, l = w % 32;
+            const int sb = 2 * j64 + hi;
+            const uint8_t * q = b->scales;
+            int sc, mn;
+            if (sb < 4) {
+                sc = q[sb] & 63;
+                mn = q[sb + 4] & 63;
+            } else {
+                sc = (q[sb + 4] & 0xF) | ((q[sb - 4] >> 6) << 4);
+                mn = (q[sb + 4] >> 4) | ((q[sb] >> 6) << 4);
+            }
+            const float d = __half2float(__ushort_as_half(b->d));
+            const float dm = __half2float(__ushort_as_half(b->dmin));
+            const uint8_t qb = b->qs[32 * j64 + l];
+            const int qv = hi ? (qb >> 4) : (qb & 0xF);
+            v = __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
+        }
+        out[k] = v;
+    }
+}
+
+// ---- CONCAT / REPEAT / SUM_ROWS ----
+__global__ void k_concat(TD dst, TD a, TD b, int dim, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i[4];
+        unravel(k, dst.ne, i[0], i[1], i[2], i[3]);
+        float v;
+        if (i[0] < a.ne[0] && i[1] < a.ne[1] && i[2] < a.ne[2] && i[3] < a.ne[3]) v = td_load(a, i[0], i[1], i[2], i[3]);
+        else {
+            i[dim] -= a.ne[dim];
+            v = td_load(b, i[0], i[1], i[2], i[3]);
+            i[dim] += a.ne[dim];
+        }
+        td_store(dst, i[0], i[1], i[2], i[3], v);
+    }
+}
+
+__global__ void k_repeat(TD dst, TD a, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unravel(k, dst.ne, i0, i1, i2, i3);
+        td_store(dst, i0, i1, i2, i3, td_load(a, i0 % a.ne[0], i1 % a.ne[1], i2 % a.ne[2], i3 % a.ne[3]));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sum_rows(TD dst, TD a) {
+    __shared__ double shd[8];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % a.ne[1], i2 = (r / a.ne[1]) % a.ne[2], i3 = r / (a.ne[1] * a.ne[2]);
+    double s = 0.0;
+    for (int64_t i = threadIdx.x; i < a.ne[0]; i += blockDim.x) s += (double)td_load(a, i, i1, i2, i3);
+    s = block_sum<double>(s, shd);
+    if (threadIdx.x == 0) td_store(dst, 0, i1, i2, i3, (float)s);
+}
+
+// ---- ROPE (NORM / NEOX, optional freq factors; theta by repeated multiply as ggml_rope_cache_init) ----
+__global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int n_dims, int neox, float theta_scale,
+                       float freq_scale, float attn_factor) {
+    const int64_t i1 = blockIdx.x, i2 = blockIdx.y, i3 = blockIdx.z;
+    const int64_t p = pos[i2];
+    for (int64_t i0 = 2 * threadIdx.x; i0 < a.ne[0]; i0 += 2 * blockDim.x) {
+        if (i0 < n_dims) {
+            float theta = (float)p;
+            for (int64_t k = 0; k < i0 / 2; ++k) theta = __fmul_rn(theta, theta_scale);
+            const float f = ff ? ff[i0 / 2] : 1.0f;
+            const float th = __fmul_rn(freq_scale, __fdiv_rn(theta, f));
+            const float c = __fmul_rn(cosf(th), attn_factor), s = __fmul_rn(sinf(th), attn_factor);
+            int64_t j0, j1;
+            if (neox) {
+                j0 = i0 / 2;
+                j1 = i0 / 2 + n_dims / 2;
+            } else {
+                j0 = i0;
+                j1 = i0 + 1;
+            }
+            const float x0 = td_load(a, j0, i1, i2, i3), x1 = td_load(a, j1, i1, i2, i3);
+            td_store(dst, j0, i1, i2, i3, __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s)));
+            td_store(dst, j1, i1, i2, i3, __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c)));
+        } else {
+            td_store(dst, i0, i1, i2, i3, td_load(a, i0, i1, i2, i3));
+            if (i0 + 1 < a.ne[0]) td_store(dst, i0 + 1, i1, i2, i3, td_load(a, i0 + 1, i1, i2, i3));
+        }
+    }
+}
+
+// ---- generic f32 x f32 MUL_MAT (attention products): one wave per output, f64 accumulation ----
+__global__ __launch_bounds__(256) void k_mul_mat_f32(TD dst, TD s0, TD s1, int64_t nout) {
+    const int lane = threadIdx.x & 63;
+    const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (o >= nout) return;
+    const int64_t i01 = o % dst.ne[0];
+    int64_t rest = o / dst.ne[0];
+    const int64_t i11 = rest % dst.ne[1];
+    rest /= dst.ne[1];
+    const int64_t i12 = rest % dst.ne[2];
+    const int64_t i13 = rest / dst.ne[2];
+    const int64_t i02 = i12 / (s1.ne[2] / s0.ne[2]), i03 = i13 / (s1.ne[3] / s0.ne[3]);
+    const char * a = s0.data + i01 * s0.nb[1] + i02 * s0.nb[2] + i03 * s0.nb[3];
+    const char * b = s1.data + i11 * s1.nb[1] + i12 * s1.nb[2] + i13 * s1.nb[3];
+    double acc = 0.0;
+    const int64_t K = s0.ne[0];
+    for (int64_t k = lane; k < K; k += 64) {
+        const float x = s0.type == TTS_TYPE_F16 ? __half2float(*(const __half *)(a + k * s0.nb[0])) : *(const float *)(a + k * s0.nb[0]);
+        const float y = *(const float *)(b + k * s1.nb[0]);
+        acc += (double)__fmul_rn(x, y);
+    }
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) *(float *)(dst.data + i01 * dst.nb[0] + i11 * dst.nb[1] + i12 * dst.nb[2] + i13 * dst.nb[3]) = (float)acc;
+}
+
+// ------------------------------------------------------------------------------------------
+
+static inline float op_f(const tts_tensor * t, int i) {
+    float f;
+    memcpy(&f, &t->op_params[i], 4);
+    return f;
+}
+static inline int64_t nel(const tts_tensor * t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+static inline bool is_cont(const tts_tensor * t) {
+    size_t es = tts_type_size(t->type);
+    return t->nb[0] == es && t->nb[1] == t->nb[0] * t->ne[0] && t->nb[2] == t->nb[1] * t->ne[1] && t->nb[3] == t->nb[2] * t->ne[2];
+}
+static inline unsigned grid_for(int64_t n, int bs = 256) {
+    int64_t g = (n + bs - 1) / bs;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+
+int launch_op(tts_hip_backend * be, const tts_tensor * node) {
+    hipStream_t st = be->stream;
+    const tts_tensor * s0 = node->src[0];
+    const tts_tensor * s1 = node->src[1];
+    TD d = make_td(node);
+    switch (node->op) {
+        case TTS_OP_DUP:
+        case TTS_OP_CONT:
+        case TTS_OP_CPY: {
+            const int64_t n = nel(s0);
+            if (n == 0) return 0;
+            if (is_cont(s0) && is_cont(node) && s0->type == node->type) {
+                TTS_HIP_CHECK(hipMemcpyAsync(node->data, s0->data, n * tts_type_size(s0->type), hipMemcpyDeviceToDevice, st));
+                return 0;
+            }
+            hipLaunchKernelGGL(k_cpy, dim3(grid_for(n)), dim3(256), 0, st, d, make_td(s0), n);
+        } break;
+        case TTS_OP_ADD:
+        case TTS_OP_SUB:
+        case TTS_OP_MUL:
+        case TTS_OP_DIV: {
+            const int64_t n = nel(node);
+            if (n == 0) return 0;
+            const bool fast = is_cont(node) && is_cont(s0) && is_cont(s1) && node->type == TTS_TYPE_F32 &&
+                              s0->type == TTS_TYPE_F32 && s1->type == TTS_TYPE_F32 && s1->ne[0] == s0->ne[0] &&
+                              (n % nel(s1)) == 0 &&
+                              (s1->ne[1] == s0->ne[1] || s1->ne[1] == 1) && s1->ne[2] == 1 && s1->ne[3] == 1;
+            const dim3 g(grid_for(n)), b(256);
+            if (fast) {
+                const int64_t nb_el = nel(s1);
+                switch (node->op) {
+                    case TTS_OP_ADD: hipLaunchKernelGGL(k_binary_cont<TTS_OP_ADD>, g, b, 0, st, (float *)node->data, (const float *)s0->data, (const float *)s1->data, n, nb_el); break;
+                    case TTS_OP_SUB: hipLaunchKernelGGL(k_binary_cont<TTS_OP_SUB>, g, b, 0, st, (float *)node->data, (const float *)s0->data, (const float *)s1->data, n, nb_el); break;
+                    case TTS_OP_MUL: hipLaunchKernelGGL(k_binary_cont<TTS_OP_MUL>, g, b, 0, st, (float *)node->data, (const float *)s0->data, (const float *)s1->data, n, nb_el); break;
+                    default: hipLaunchKernelGGL(k_binary_cont<TTS_OP_DIV>, g, b, 0, st, (float *)node->data, (const float *)s0->data, (const float *)s1->data, n, nb_el); break;
+                }
+            } else {
+                TD a = make_td(s0), bb = make_td(s1);
+                switch (node->op) {
+                    case TTS_OP_ADD: hipLaunchKernelGGL(k_binary<TTS_OP_ADD>, g, b, 0, st, d, a, bb, n); break;
+                    case TTS_OP_SUB: hipLaunchKernelGGL(k_binary<TTS_OP_SUB>, g, b, 0, st, d, a, bb, n); break;
+                    case TTS_OP_MUL: hipLaunchKernelGGL(k_binary<TTS_OP_MUL>, g, b, 0, st, d, a, bb, n); break;
+                    default: hipLaunchKernelGGL(k_binary<TTS_OP_DIV>, g, b, 0, st, d, a, bb, n); break;
+                }
+            }
+        } break;
+        case TTS_OP_SQR: case TTS_OP_SQRT: case TTS_OP_SIN: case TTS_OP_COS: case TTS_OP_SCALE: case TTS_OP_CLAMP:
+        case TTS_OP_LEAKY_RELU: case TTS_OP_ROUND: case TTS_OP_MOD: case TTS_OP_UNARY: {
+            const int64_t n = nel(node);
+            if (n == 0) return 0;
+            UnaryParams P;
+            P.op = node->op;
+            P.uop = node->op == TTS_OP_UNARY ? node->op_params[0] : -1;
+            P.p0 = op_f(node, 0);
+            P.p1 = op_f(node, 1);
+            P.gelu_table = be->gelu_table;
+            if (is_cont(node) && is_cont(s0) && node->type == TTS_TYPE_F32 && s0->type == TTS_TYPE_F32)
+                hipLaunchKernelGGL(k_unary_cont, dim3(grid_for(n)), dim3(256), 0, st, (float *)node->data, (const float *)s0->data, n, P);
+            else
+                hipLaunchKernelGGL(k_unary, dim3(grid_for(n)), dim3(256), 0, st, d, make_td(s0), n, P);
+        } break;
+        case TTS_OP_NORM:
+        case TTS_OP_RMS_NORM: {
+            const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
+            if (node->op == TTS_OP_NORM) hipLaunchKernelGGL(k_norm<false>, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), op_f(node, 0));
+            else hipLaunchKernelGGL(k_norm<true>, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), op_f(node, 0));
+        } break;
+        case TTS_OP_SOFT_MAX: {
+            const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
+            const tts_tensor * m = node->src[1];
+            hipLaunchKernelGGL(k_soft_max, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), m ? (const char *)m->data : nullptr,
+                               m ? (m->type == TTS_TYPE_F16) : 0, op_f(node, 0));
+        } break;
+        case TTS_OP_GET_ROWS: {
+            const int64_t nr = s1->ne[0] * s1->ne[1] * s1->ne[2];
+            hipLaunchKernelGGL(k_get_rows, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), make_td(s1));
+        } break;
+        case TTS_OP_CONCAT: {
+            const int64_t n = nel(node);
+            hipLaunchKernelGGL(k_concat, dim3(grid_for(n)), dim3(256), 0, st, d, make_td(s0), make_td(s1), node->op_params[0], n);
+        } break;
+        case TTS_OP_REPEAT: {
+            const int64_t n = nel(node);
+            hipLaunchKernelGGL(k_repeat, dim3(grid_for(n)), dim3(256), 0, st, d, make_td(s0), n);
+        } break;
+        case TTS_OP_SUM_ROWS: {
+            const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
+            hipLaunchKernelGGL(k_sum_rows, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0));
+        } break;
+        case TTS_OP_ROPE: {
+            const int n_dims = node->op_params[1];
+            const int mode = node->op_params[2];
+            const float freq_base = op_f(node, 5), freq_scale = op_f(node, 6), attn_factor = op_f(node, 8);
+            const float theta_scale = powf(freq_base, -2.0f / n_dims);
+            const tts_tensor * ff = node->src[2];
+            dim3 grid((unsigned)s0->ne[1], (unsigned)s0->ne[2], (unsigned)s0->ne[3]);
+            hipLaunchKernelGGL(k_rope, grid, dim3(64), 0, st, d, make_td(s0), (const int32_t *)s1->data,
+                               ff ? (const float *)ff->data : nullptr, n_dims, (mode & 2) ? 1 : 0, theta_scale, freq_scale, attn_factor);
+        } break;
+        case TTS_OP_MUL_MAT: {
+            // generic float path (quantized weights go through launch_gemv in backend.hip)
+            const int64_t nout = nel(node);
+            hipLaunchKernelGGL(k_mul_mat_f32, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
+        } break;
+        default:
+            return TTS_STATUS_UNSUPPORTED;
+    }
+    TTS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace tts

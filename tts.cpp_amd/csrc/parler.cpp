@@ -1,0 +1,531 @@
+// Parler-TTS decoder runner: builds the same per-step graph as
+// parler_tts_runner::build_parler_graph (/root/reference/src/models/parler/model.cpp:520-614),
+// stores K/V like parler_build_kv_store (:420-439), precomputes cross K/V like
+// prep_cross_key_values (:110-173) and samples greedily like sampler::max
+// (/root/reference/src/sampler.cpp:185-204) inside the generate_from_batch loop (:762-792).
+//
+// Extension (batch > 1): B independent prompts stepped in lockstep share every weight GEMV
+// (M = B columns) while each keeps its own KV cache (attention gets a 4th "sequence" dim).
+// With batch == 1 the node list is exactly the reference's.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/tts_runners.h"
+#include "graph.h"
+#include "synth.h"
+
+using namespace tts;
+
+struct parler_layer {
+    tts_tensor *q, *k, *v, *o, *sa_norm, *sa_norm_b;
+    tts_tensor *aq, *ak, *av, *ao, *a_norm, *a_norm_b;
+    tts_tensor *cross_k, *cross_v;
+    tts_tensor *fc1, *fc2, *f_norm, *f_norm_b;
+};
+
+struct tts_parler {
+    tts_parler_config cfg;
+    tts_backend_iface be;
+    tg::context wctx;
+    void * wbuf = nullptr;
+    size_t wbytes = 0;
+    void * kvbuf = nullptr;
+    size_t kvbytes = 0;
+    std::vector<tts_tensor *> embds, heads;
+    std::vector<parler_layer> layers;
+    tts_tensor *pos_embd = nullptr, *prompt_embd = nullptr, *text_encoding = nullptr, *norm = nullptr, *norm_b = nullptr;
+    std::vector<tts_tensor *> k_l, v_l;
+    char * arena = nullptr;
+    size_t arena_size = 0;
+    tg::context gctx;
+    tts_tensor * res = nullptr;
+    tts_tensor *in_tokens = nullptr, *in_positions = nullptr, *in_mask = nullptr, *in_mask_cross = nullptr;
+    int32_t position = 0;
+    int32_t current_step = 0;
+    int32_t last_nodes = 0;
+    std::vector<std::vector<int32_t>> output_tokens;  // per sequence, flat [steps][heads]
+    std::vector<std::vector<char>> eos_seen;
+    uint64_t tensor_index = 0;
+};
+
+extern "C" void tts_parler_default_config(tts_parler_config * c) {
+    c->n_layers = 24;
+    c->hidden_size = 1024;
+    c->n_attn_heads = 16;
+    c->ffn_size = 4096;
+    c->n_output_heads = 9;
+    c->output_vocab = 1088;
+    c->audio_vocab = 1024;
+    c->max_ctx = 4096;
+    c->n_encode = 3;
+    c->prompt_vocab = 32128;
+    c->max_positions = 4102;
+    c->weight_type = TTS_TYPE_Q4_K;
+    c->head_type = TTS_TYPE_F32;
+    c->use_cross_attn = 1;
+    c->batch = 1;
+    c->eos_token = 1024;
+    c->bos_token = 1025;
+    c->seed = 0x5EED;
+    c->arena_bytes = 0;
+}
+
+// ---- weights ----
+struct wspec {
+    tts_tensor * t;
+    int kind;  // 0 = matrix (synth_fill), 1 = norm weight (~1), 2 = bias (~0), 3 = embedding f32
+    uint64_t seed;
+};
+
+static tts_tensor * wnew(tts_parler * p, std::vector<wspec> & specs, int type, int64_t ne0, int64_t ne1, int kind,
+                         const std::string & name) {
+    tts_tensor * t = ne1 > 1 ? tg::new_tensor_2d(p->wctx, type, ne0, ne1) : tg::new_tensor_1d(p->wctx, type, ne0);
+    tg::set_name(t, name);
+    t->flags |= tg::TG_FLAG_PERSIST;
+    specs.push_back({t, kind, p->cfg.seed ^ (p->tensor_index++)});
+    return t;
+}
+
+static bool upload_weights(tts_parler * p, std::vector<wspec> & specs) {
+    size_t total = 0;
+    for (auto & s : specs) total += (tg::nbytes(s.t) + 255) & ~(size_t)255;
+    p->wbuf = p->be.alloc(p->be.ctx, total);
+    if (!p->wbuf) return false;
+    p->wbytes = total;
+    size_t off = 0;
+    std::vector<char> host;
+    for (auto & s : specs) {
+        tts_tensor * t = s.t;
+        const size_t nb = tg::nbytes(t);
+        t->data = (char *)p->wbuf + off;
+        off += (nb + 255) & ~(size_t)255;
+        host.resize(nb);
+        const int64_t K = t->ne[0], rows = tg::nelements(t) / t->ne[0];
+        const int kind = (t->type == TTS_TYPE_F32) ? s.kind : 0;
+        const float std = s.kind == 3 ? 0.25f : 0.02f;
+        switch (kind) {
+            case 1:synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.1f, 1.0f); break;
+            case 2: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.02f, 0.0f); break;
+            case 3: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.5f, 0.0f); break;
+            default: synth_fill(t->type, host.data(), rows, K, s.seed, std); break;
+        }
+        if (p->be.set(p->be.ctx, t->data, host.data(), nb) != 0) return false;
+    }
+    return true;
+}
+
+static tts_tensor * layer_norm(tg::context & c, tts_tensor * x, tts_tensor * w, tts_tensor * b) {
+    // parler_build_layer_norm (model.cpp:412-418): eps 1e-5, norm -> mul -> add
+    x = tg::norm(c, x, 0.00001f);
+    x = tg::mul(c, x, w);
+    return tg::add(c, x, b);
+}
+
+static bool run_graph(tts_parler * p, tg::context & c) {
+    if (!tg::alloc_graph(c, p->arena, p->arena_size)) {
+        fprintf(stderr, "parler: compute arena too small (%zu needed)\n", c.arena_used);
+        return false;
+    }
+    return true;
+}
+
+// prep_cross_key_values: per layer cross_k = cont(permute(reshape(K . text_encoding))) [hd, n_enc, H],
+// cross_v = cont_3d(transpose(V . text_encoding), n_enc, hd, H) (model.cpp:146-156).
+static bool prep_cross_key_values(tts_parler * p) {
+    const auto & cf = p->cfg;
+    const int hd = cf.hidden_size / cf.n_attn_heads;
+    tg::context & c = p->gctx;
+    c.reset();
+    for (int l = 0; l < cf.n_layers; ++l) {
+        parler_layer & L = p->layers[l];
+        tts_tensor * Kc = tg::mul_mat(c, L.ak, p->text_encoding);
+        tts_tensor * Vc = tg::mul_mat(c, L.av, p->text_encoding);
+        Kc = tg::reshape_3d(c, Kc, hd, cf.n_attn_heads, cf.n_encode);
+        Vc = tg::transpose(c, Vc);
+        tts_tensor * k = tg::cont(c, tg::permute(c, Kc, 0, 2, 1, 3));
+        tts_tensor * v = tg::cont_3d(c, Vc, cf.n_encode, hd, cf.n_attn_heads);
+        if (cf.batch > 1) {
+            tts_tensor * shape = tg::new_tensor_4d(c, TTS_TYPE_F32, cf.n_encode, hd, cf.n_attn_heads, cf.batch);
+            shape->data = L.cross_v->data;  // metadata only (repeat reads shape->ne)
+            v = tg::repeat(c, v, shape);
+        }
+        tg::build_forward_expand(c, tg::cpy(c, k, L.cross_k));
+        tg::build_forward_expand(c, tg::cpy(c, v, L.cross_v));
+    }
+    if (!run_graph(p, c)) return false;
+    if (p->be.compute(p->be.ctx, c.nodes.data(), (int)c.nodes.size()) != 0) return false;
+    return p->be.synchronize(p->be.ctx) == 0;
+}
+
+extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tts_parler_config * cfg) {
+    auto * p = new tts_parler();
+    p->cfg = *cfg;
+    p->be = *be;
+    const auto & cf = p->cfg;
+    const int64_t H = cf.hidden_size;
+    const int hd = cf.hidden_size / cf.n_attn_heads;
+    const int B = cf.batch < 1 ? 1 : cf.batch;
+    p->cfg.batch = B;
+    std::vector<wspec> specs;
+    // decoder.embed_tokens.{i} (Q4_K when quantized), decoder.lm_heads.{i}.weight.head (F32)
+    for (int i = 0; i < cf.n_output_heads; ++i)
+        p->embds.push_back(wnew(p, specs, cf.weight_type, H, cf.output_vocab, 3, "embd_" + std::to_string(i)));
+    for (int i = 0; i < cf.n_output_heads; ++i)
+        p->heads.push_back(wnew(p, specs, cf.head_type, H, cf.output_vocab, 0, "head_" + std::to_string(i)));
+    p->pos_embd = wnew(p, specs, TTS_TYPE_F32, H, cf.max_positions, 3, "positional_embed");
+    p->prompt_embd = wnew(p, specs, TTS_TYPE_F32, H, cf.prompt_vocab, 3, "embed_prompts");
+    p->text_encoding = wnew(p, specs, TTS_TYPE_F32, H, cf.n_encode, 3, "text_encoding");
+    p->norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, "layer_norm.weight");
+    p->norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, "layer_norm.bias");
+    p->layers.resize(cf.n_layers);
+    for (int l = 0; l < cf.n_layers; ++l) {
+        parler_layer & L = p->layers[l];
+        const std::string pre = "layers." + std::to_string(l);
+        L.q = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.q_proj");
+        L.k = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.k_proj");
+        L.v = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.v_proj");
+        L.o = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.out_proj");
+        L.sa_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".self_attn_layer_norm.weight");
+        L.sa_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".self_attn_layer_norm.bias");
+        L.aq = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.q_proj");
+        // encoder_attn k/v stay F32 (quantize_impl.cpp: quantize_cross_attn_kv off by default)
+        L.ak = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.k_proj");
+        L.av = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.v_proj");
+        L.ao = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.out_proj");
+        L.a_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".encoder_attn_layer_norm.weight");
+        L.a_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".encoder_attn_layer_norm.bias");
+        L.fc1 = wnew(p, specs, cf.weight_type, H, cf.ffn_size, 0, pre + ".fc1");
+        L.fc2 = wnew(p, specs, cf.weight_type, cf.ffn_size, H, 0, pre + ".fc2");
+        L.f_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".final_layer_norm.weight");
+        L.f_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".final_layer_norm.bias");
+    }
+    if (!upload_weights(p, specs)) {
+        fprintf(stderr, "parler: weight allocation/upload failed\n");
+        delete p;
+        return nullptr;
+    }
+    // cross K/V + KV caches in one persistent buffer
+    const size_t ck = (size_t)hd * cf.n_encode * cf.n_attn_heads * 4;
+    const size_t cv = ck * (size_t)B;
+    const size_t kvl = (size_t)H * cf.max_ctx * 4 * (size_t)B;
+    p->kvbytes = (size_t)cf.n_layers * (((ck + 255) & ~(size_t)255) + ((cv + 255) & ~(size_t)255) + 2 * kvl);
+    p->kvbuf = p->be.alloc(p->be.ctx, p->kvbytes);
+    if (!p->kvbuf) {
+        delete p;
+        return nullptr;
+    }
+    p->be.memset(p->be.ctx, p->kvbuf, 0, p->kvbytes);  // ggml_backend_buffer_clear(buf, 0)
+    char * kp = (char *)p->kvbuf;
+    for (int l = 0; l < cf.n_layers; ++l) {
+        parler_layer & L = p->layers[l];
+        L.cross_k = tg::new_tensor_3d(p->wctx, TTS_TYPE_F32, hd, cf.n_encode, cf.n_attn_heads);
+        L.cross_k->data = kp;
+        kp += (ck + 255) & ~(size_t)255;
+        if (B > 1) L.cross_v = tg::new_tensor_4d(p->wctx, TTS_TYPE_F32, cf.n_encode, hd, cf.n_attn_heads, B);
+        else L.cross_v = tg::new_tensor_3d(p->wctx, TTS_TYPE_F32, cf.n_encode, hd, cf.n_attn_heads);
+        L.cross_v->data = kp;
+        kp += (cv + 255) & ~(size_t)255;
+        // parler_kv_cache_init: 1-D F32 [hidden*max_ctx] per layer (x B sequences)
+        tts_tensor * k = tg::new_tensor_1d(p->wctx, TTS_TYPE_F32, H * cf.max_ctx * B);
+        k->data = kp;
+        kp += kvl;
+        tts_tensor * v = tg::new_tensor_1d(p->wctx, TTS_TYPE_F32, H * cf.max_ctx * B);
+        v->data = kp;
+        kp += kvl;
+        tg::set_name(k, "cache_k_l" + std::to_string(l));
+        tg::set_name(v, "cache_v_l" + std::to_string(l));
+        p->k_l.push_back(k);
+        p->v_l.push_back(v);
+    }
+    p->arena_size = cf.arena_bytes ? cf.arena_bytes : (256ull << 20);
+    p->arena = (char *)p->be.alloc(p->be.ctx, p->arena_size);
+    if (!p->arena) {
+        delete p;
+        return nullptr;
+    }
+    if (cf.use_cross_attn && !prep_cross_key_values(p)) {
+        fprintf(stderr, "parler: cross K/V precompute failed\n");
+        delete p;
+        return nullptr;
+    }
+    tts_parler_reset(p);
+    return p;
+}
+
+extern "C" void tts_parler_free(tts_parler * p) {
+    if (!p) return;
+    if (p->arena) p->be.free(p->be.ctx, p->arena);
+    if (p->kvbuf) p->be.free(p->be.ctx, p->kvbuf);
+    if (p->wbuf) p->be.free(p->be.ctx, p->wbuf);
+    delete p;
+}
+
+extern "C" void tts_parler_reset(tts_parler * p) {
+    p->position = 0;
+    p->current_step = 0;
+    p->output_tokens.assign(p->cfg.batch, {});
+    p->eos_seen.assign(p->cfg.batch, std::vector<char>(p->cfg.n_output_heads, 0));
+}
+
+// build_parler_graph for n tokens per sequence (n = 1 in audio generation).
+static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
+    const auto & cf = p->cfg;
+    const int B = cf.batch;
+    const int64_t H = cf.hidden_size;
+    const int hd = cf.hidden_size / cf.n_attn_heads;
+    const int nh = cf.n_attn_heads;
+    const int64_t full = p->position + n;
+    const size_t S = (size_t)H * cf.max_ctx * 4;  // per-sequence cache stride
+    tg::context & c = p->gctx;
+    c.reset();
+
+    // parler_build_inp_embd (model.cpp:387-410)
+    p->in_positions = tg::new_tensor_1d(c, TTS_TYPE_I32, n);
+    tg::set_input(p->in_positions);
+    tts_tensor * inp = nullptr;
+    if (audio) {
+        if (B == 1) {
+            tts_tensor * tok = tg::reshape_2d(c, tg::new_tensor_1d(c, TTS_TYPE_I32, (int64_t)n * cf.n_output_heads), n, cf.n_output_heads);
+            p->in_tokens = tok->view_src;
+            tg::set_input(p->in_tokens);
+            for (int i = 0; i < cf.n_output_heads; ++i) {
+                tts_tensor * e = tg::get_rows(c, p->embds[i], tg::view_2d(c, tok, 1, n, tok->nb[1], i * sizeof(int32_t)));
+                inp = i == 0 ? e : tg::add(c, e, inp);
+            }
+        } else {
+            p->in_tokens = tg::new_tensor_1d(c, TTS_TYPE_I32, (int64_t)B * cf.n_output_heads);
+            tg::set_input(p->in_tokens);
+            for (int i = 0; i < cf.n_output_heads; ++i) {
+                tts_tensor * idx = tg::view_2d(c, p->in_tokens, 1, B, cf.n_output_heads * sizeof(int32_t), i * sizeof(int32_t));
+                tts_tensor * e = tg::get_rows(c, p->embds[i], idx);  // [H, 1, B]
+                inp = i == 0 ? e : tg::add(c, e, inp);
+            }
+        }
+    } else {
+        if (B == 1) {
+            p->in_tokens = tg::new_tensor_1d(c, TTS_TYPE_I32, n);
+            tg::set_input(p->in_tokens);
+            inp = tg::get_rows(c, p->prompt_embd, p->in_tokens);
+        } else {
+            p->in_tokens = tg::new_tensor_2d(c, TTS_TYPE_I32, n, B);
+            tg::set_input(p->in_tokens);
+            inp = tg::get_rows(c, p->prompt_embd, p->in_tokens);  // [H, n, B]
+        }
+    }
+    tts_tensor * inpL = tg::add(c, inp, tg::get_rows(c, p->pos_embd, p->in_positions));
+    if (B > 1 && audio) inpL = tg::reshape_3d(c, inpL, H, 1, B);
+
+    // build_attn_mask / build_attn_mask_cross (model.cpp:459-471)
+    p->in_mask = tg::new_tensor_2d(c, TTS_TYPE_F32, full, full);
+    tg::set_input(p->in_mask);
+    p->in_mask_cross = tg::new_tensor_2d(c, TTS_TYPE_F32, cf.n_encode, n);
+    tg::set_input(p->in_mask_cross);
+
+    const float kq_scale = 1.0f / sqrtf((float)hd);
+    tts_tensor * cur = nullptr;
+    for (int l = 0; l < cf.n_layers; ++l) {
+        parler_layer & L = p->layers[l];
+        tts_tensor * residual = inpL;
+        cur = layer_norm(c, inpL, L.sa_norm, L.sa_norm_b);
+        tts_tensor * attn_out;
+        {
+            tts_tensor * Qcur = tg::mul_mat(c, L.q, cur);
+            tts_tensor * Kcur = tg::mul_mat(c, L.k, cur);
+            tts_tensor * Vcur = tg::mul_mat(c, L.v, cur);
+            // parler_build_kv_store (model.cpp:420-439)
+            if (B == 1) {
+                tts_tensor * kv = tg::view_1d(c, p->k_l[l], (int64_t)n * H, tts_row_size(TTS_TYPE_F32, H) * p->position);
+                tg::build_forward_expand(c, tg::cpy(c, Kcur, kv));
+                tts_tensor * vv = tg::view_2d(c, p->v_l[l], n, H, (size_t)cf.max_ctx * 4, (size_t)p->position * 4);
+                tts_tensor * vt = tg::cont(c, tg::transpose(c, Vcur));
+                tg::build_forward_expand(c, tg::cpy(c, vt, vv));
+            } else {
+                tts_tensor * kv = tg::view_2d(c, p->k_l[l], (int64_t)n * H, B, S, tts_row_size(TTS_TYPE_F32, H) * p->position);
+                tg::build_forward_expand(c, tg::cpy(c, Kcur, kv));
+                tts_tensor * vv = tg::view_3d(c, p->v_l[l], n, H, B, (size_t)cf.max_ctx * 4, S, (size_t)p->position * 4);
+                tts_tensor * V3 = tg::reshape_3d(c, Vcur, H, n, B);
+                tts_tensor * vt = tg::cont(c, tg::transpose(c, V3));
+                tg::build_forward_expand(c, tg::cpy(c, vt, vv));
+            }
+            tts_tensor *k, *v, *q;
+            if (B == 1) {
+                k = tg::view_3d(c, p->k_l[l], hd, full, nh, tts_row_size(TTS_TYPE_F32, H), tts_row_size(TTS_TYPE_F32, hd), 0);
+                v = tg::view_3d(c, p->v_l[l], full, hd, nh, 4 * (size_t)cf.max_ctx, 4 * (size_t)cf.max_ctx * hd, 0);
+                Qcur = tg::reshape_3d(c, Qcur, hd, nh, n);
+            } else {
+                k = tg::view_4d(c, p->k_l[l], hd, full, nh, B, tts_row_size(TTS_TYPE_F32, H), tts_row_size(TTS_TYPE_F32, hd), S, 0);
+                v = tg::view_4d(c, p->v_l[l], full, hd, nh, B, 4 * (size_t)cf.max_ctx, 4 * (size_t)cf.max_ctx * hd, S, 0);
+                Qcur = tg::reshape_4d(c, Qcur, hd, nh, n, B);
+            }
+            q = tg::cont(c, tg::permute(c, Qcur, 0, 2, 1, 3));
+            tts_tensor * kq = tg::mul_mat(c, tg::cont(c, k), q);
+            kq = tg::soft_max_ext(c, kq, p->in_mask, kq_scale, 0.0f);
+            tts_tensor * kqv = tg::mul_mat(c, kq, v);
+            tts_tensor * merged = tg::permute(c, kqv, 2, 0, 1, 3);
+            attn_out = B == 1 ? tg::cont_2d(c, merged, H, n) : tg::cont_3d(c, merged, H, n, B);
+            attn_out = tg::mul_mat(c, L.o, attn_out);
+        }
+        cur = tg::add(c, attn_out, residual);
+        if (cf.use_cross_attn) {
+            tts_tensor * residuala = cur;
+            cur = layer_norm(c, cur, L.a_norm, L.a_norm_b);
+            tts_tensor * Qcur = tg::mul_mat(c, L.aq, cur);
+            Qcur = B == 1 ? tg::reshape_3d(c, Qcur, hd, nh, n) : tg::reshape_4d(c, Qcur, hd, nh, n, B);
+            tts_tensor * q = tg::cont(c, tg::permute(c, Qcur, 0, 2, 1, 3));
+            tts_tensor * kq = tg::mul_mat(c, L.cross_k, q);
+            kq = tg::soft_max_ext(c, kq, p->in_mask_cross, kq_scale, 0.0f);
+            tts_tensor * kqv = tg::mul_mat(c, kq, L.cross_v);
+            tts_tensor * merged = tg::permute(c, kqv, 2, 0, 1, 3);
+            cur = B == 1 ? tg::cont_2d(c, merged, H, n) : tg::cont_3d(c, merged, H, n, B);
+            cur = tg::mul_mat(c, L.ao, cur);
+            cur = tg::add(c, cur, residuala);
+        }
+        tts_tensor * residualffn = cur;
+        cur = layer_norm(c, cur, L.f_norm, L.f_norm_b);
+        cur = tg::mul_mat(c, L.fc1, cur);
+        cur = tg::gelu(c, cur);
+        cur = tg::mul_mat(c, L.fc2, cur);
+        cur = tg::add(c, cur, residualffn);
+        inpL = cur;
+    }
+    cur = layer_norm(c, cur, p->norm, p->norm_b);
+    // parler_build_head_outputs (model.cpp:441-457)
+    tts_tensor * out = nullptr;
+    for (int i = 0; i < cf.n_output_heads; ++i) {
+        tts_tensor * h = tg::mul_mat(c, p->heads[i], cur);
+        out = i == 0 ? h : tg::concat(c, out, h, 1);
+    }
+    tg::set_name(out, "final_out");
+    if (B == 1) {
+        const int64_t sql = tg::nelements(out) / ((int64_t)cf.output_vocab * cf.n_output_heads);
+        out = tg::cont_3d(c, out, cf.output_vocab, sql, cf.n_output_heads);
+    }
+    tg::set_output(out);
+    tg::build_forward_expand(c, out);
+    return out;
+}
+
+// set_inputs (model.cpp:616-643): only rows < n of the causal mask are written/read.
+static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n) {
+    const auto & cf = p->cfg;
+    const int B = cf.batch;
+    auto & be = p->be;
+    int st = 0;
+    if (audio) {
+        if (B == 1) {
+            // audio tokens arrive as [heads] for n == 1; layout [heads][n] otherwise
+            st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * cf.n_output_heads);
+        } else {
+            st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * B * cf.n_output_heads);
+        }
+    } else {
+        st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * B);
+    }
+    std::vector<int32_t> pos(n);
+    for (int i = 0; i < n; ++i) pos[i] = p->position + i;
+    st |= be.set(be.ctx, p->in_positions->data, pos.data(), sizeof(int32_t) * n);
+    const int64_t full = p->position + n;
+    std::vector<float> mask((size_t)n * full);
+    for (int i = 0; i < n; ++i)
+        for (int64_t j = 0; j < full; ++j) mask[(size_t)i * full + j] = j > pos[i] ? -INFINITY : 0.0f;
+    st |= be.set(be.ctx, p->in_mask->data, mask.data(), mask.size() * sizeof(float));
+    std::vector<float> mc((size_t)cf.n_encode * n, 0.0f);
+    st |= be.set(be.ctx, p->in_mask_cross->data, mc.data(), mc.size() * sizeof(float));
+    return st;
+}
+
+static int decode(tts_parler * p, const int32_t * tokens, bool audio, int n, float * logits) {
+    const auto & cf = p->cfg;
+    if (p->position + n > cf.max_ctx) return TTS_STATUS_BAD_ARG;
+    tts_tensor * out = build_graph(p, audio, n);
+    if (!run_graph(p, p->gctx)) return TTS_STATUS_ALLOC_FAILED;
+    p->res = out;
+    p->last_nodes = (int32_t)p->gctx.nodes.size();
+    if (set_inputs(p, tokens, audio, n) != 0) return TTS_STATUS_FAILED;
+    int st = p->be.compute(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size());
+    if (st != 0) return st;
+    if (logits) {
+        const size_t bytes = (size_t)cf.batch * n * cf.n_output_heads * cf.output_vocab * sizeof(float);
+        st = p->be.get(p->be.ctx, logits, out->data, bytes);
+        if (st != 0) return st;
+    }
+    p->position += n;
+    return 0;
+}
+
+extern "C" int tts_parler_prefill(tts_parler * p, const int32_t * tokens, int32_t n) {
+    int st = decode(p, tokens, false, n, nullptr);
+    if (st == 0) p->be.synchronize(p->be.ctx);
+    return st;
+}
+
+extern "C" int tts_parler_decode(tts_parler * p, const int32_t * audio_tokens, float * logits) {
+    return decode(p, audio_tokens, true, 1, logits);
+}
+
+// sampler::max (sampler.cpp:185-204) without repetition penalty
+static int32_t argmax_head(const float * l, int vocab) {
+    float mx = -INFINITY;
+    int32_t id = 0;
+    for (int i = 0; i < vocab; ++i) {
+        if (l[i] > mx) {
+            mx = l[i];
+            id = i;
+        }
+    }
+    return id;
+}
+
+extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out) {
+    const auto & cf = p->cfg;
+    const int B = cf.batch, NH = cf.n_output_heads;
+    std::vector<float> logits((size_t)B * NH * cf.output_vocab);
+    std::vector<int32_t> next((size_t)B * NH);
+    for (int s = 0; s < n_steps; ++s) {
+        // next_decoder_token_ids (model.cpp:778-785): BOS until step > head, then last token / EOS
+        for (int b = 0; b < B; ++b) {
+            const auto & ot = p->output_tokens[b];
+            for (int h = 0; h < NH; ++h) {
+                int32_t t;
+                if (p->current_step > h) {
+                    t = p->eos_seen[b][h] ? cf.eos_token : ot[ot.size() - NH + h];
+                } else {
+                    t = cf.bos_token;
+                }
+                next[(size_t)b * NH + h] = t;
+            }
+        }
+        int st = tts_parler_decode(p, next.data(), logits.data());
+        if (st != 0) return st;
+        for (int b = 0; b < B; ++b) {
+            for (int h = 0; h < NH; ++h) {
+                const int32_t t = argmax_head(logits.data() + ((size_t)b * NH + h) * cf.output_vocab, cf.output_vocab);
+                p->output_tokens[b].push_back(t);
+                if (tokens_out) tokens_out[((size_t)b * n_steps + s) * NH + h] = t;
+                p->eos_seen[b][h] = p->eos_seen[b][h] || t == cf.eos_token;
+            }
+        }
+        p->current_step += 1;
+    }
+    return 0;
+}
+
+extern "C" int32_t tts_parler_position(const tts_parler * p) { return p->position; }
+extern "C" int32_t tts_parler_last_graph_nodes(const tts_parler * p) { return p->last_nodes; }
+extern "C" uint64_t tts_parler_weight_bytes(const tts_parler * p) { return p->wbytes; }
+
+extern "C" uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap) {
+    for (auto * t : p->gctx.nodes) {
+        if (strcmp(t->name, name) == 0) {
+            if (!tg::is_contiguous(t)) return 0;
+            size_t nb = tg::nbytes(t);
+            if (nb > cap) return 0;
+            if (p->be.get(p->be.ctx, dst, t->data, nb) != 0) return 0;
+            return nb;
+        }
+    }
+    return 0;
+}

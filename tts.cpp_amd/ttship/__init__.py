@@ -1,0 +1,269 @@
+"""ctypes binding of libtts_hip.so (include/tts_hip.h, include/tts_runners.h).
+
+The product path is the HIP library; there is no Python or CPU fallback: if the shared object is
+missing or no device is visible, the calls below raise.
+"""
+import ctypes
+import os
+import pathlib
+
+_HERE = pathlib.Path(__file__).resolve().parent
+PKG_ROOT = _HERE.parent
+REPO_ROOT = PKG_ROOT.parent
+LIB_PATH = PKG_ROOT / "lib" / "libtts_hip.so"
+
+# ggml type ids (include/tts_hip.h)
+F32, F16, Q4_0, Q8_0, Q4_K, Q8_K, I32 = 0, 1, 2, 8, 12, 15, 26
+
+OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "SUM_ROWS", "REPEAT",
+       "CONCAT", "NORM", "RMS_NORM", "MUL_MAT", "SCALE", "CPY", "CONT", "RESHAPE", "VIEW", "PERMUTE",
+       "TRANSPOSE", "GET_ROWS", "SOFT_MAX", "ROPE", "CLAMP", "CONV_TRANSPOSE_1D", "IM2COL", "UPSCALE",
+       "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
+OP = {n: i for i, n in enumerate(OPS)}
+UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
+
+TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
+BLCK_SIZE = {F32: 1, F16: 1, Q4_K: 256, Q8_0: 32, I32: 1}
+
+
+class TtsTensor(ctypes.Structure):
+    pass
+
+
+TtsTensor._fields_ = [
+    ("type", ctypes.c_int32),
+    ("op", ctypes.c_int32),
+    ("ne", ctypes.c_int64 * 4),
+    ("nb", ctypes.c_uint64 * 4),
+    ("op_params", ctypes.c_int32 * 16),
+    ("src", ctypes.POINTER(TtsTensor) * 4),
+    ("view_src", ctypes.POINTER(TtsTensor)),
+    ("view_offs", ctypes.c_uint64),
+    ("data", ctypes.c_void_p),
+    ("flags", ctypes.c_int32),
+    ("pad_", ctypes.c_int32),
+    ("name", ctypes.c_char * 48),
+]
+
+
+class BackendIface(ctypes.Structure):
+    _fields_ = [
+        ("ctx", ctypes.c_void_p),
+        ("name", ctypes.c_char_p),
+        ("alloc", ctypes.c_void_p),
+        ("free", ctypes.c_void_p),
+        ("set", ctypes.c_void_p),
+        ("get", ctypes.c_void_p),
+        ("memset", ctypes.c_void_p),
+        ("compute", ctypes.c_void_p),
+        ("synchronize", ctypes.c_void_p),
+    ]
+
+
+class ParlerConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", ctypes.c_int32),
+        ("hidden_size", ctypes.c_int32),
+        ("n_attn_heads", ctypes.c_int32),
+        ("ffn_size", ctypes.c_int32),
+        ("n_output_heads", ctypes.c_int32),
+        ("output_vocab", ctypes.c_int32),
+        ("audio_vocab", ctypes.c_int32),
+        ("max_ctx", ctypes.c_int32),
+        ("n_encode", ctypes.c_int32),
+        ("prompt_vocab", ctypes.c_int32),
+        ("max_positions", ctypes.c_int32),
+        ("weight_type", ctypes.c_int32),
+        ("head_type", ctypes.c_int32),
+        ("use_cross_attn", ctypes.c_int32),
+        ("batch", ctypes.c_int32),
+        ("eos_token", ctypes.c_int32),
+        ("bos_token", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+    ]
+
+
+_lib = None
+
+
+def row_size(t, ne0):
+    return TYPE_SIZE[t] * (ne0 // BLCK_SIZE[t])
+
+
+def lib():
+    """Load libtts_hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise RuntimeError(f"{LIB_PATH} missing: run `make -j8` (or __graft_entry__.build())")
+    L = ctypes.CDLL(str(LIB_PATH))
+    vp, i32, i64, u64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
+    sig = {
+        "tts_type_size": (sz, [ctypes.c_int]),
+        "tts_blck_size": (i64, [ctypes.c_int]),
+        "tts_row_size": (sz, [ctypes.c_int, i64]),
+        "tts_type_name": (ctypes.c_char_p, [ctypes.c_int]),
+        "tts_op_name": (ctypes.c_char_p, [ctypes.c_int]),
+        "tts_hip_device_count": (ctypes.c_int, []),
+        "tts_hip_backend_init": (vp, [ctypes.c_int]),
+        "tts_hip_backend_free": (None, [vp]),
+        "tts_hip_backend_name": (ctypes.c_char_p, [vp]),
+        "tts_hip_buffer_alloc": (vp, [vp, sz]),
+        "tts_hip_buffer_free": (None, [vp, vp]),
+        "tts_hip_buffer_alignment": (sz, []),
+        "tts_hip_tensor_set": (ctypes.c_int, [vp, vp, vp, sz]),
+        "tts_hip_tensor_get": (ctypes.c_int, [vp, vp, vp, sz]),
+        "tts_hip_tensor_copy": (ctypes.c_int, [vp, vp, vp, sz]),
+        "tts_hip_memset": (ctypes.c_int, [vp, vp, ctypes.c_int, sz]),
+        "tts_hip_synchronize": (ctypes.c_int, [vp]),
+        "tts_hip_supports_op": (ctypes.c_int, [ctypes.POINTER(TtsTensor)]),
+        "tts_hip_graph_compute": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.POINTER(TtsTensor)), ctypes.c_int]),
+        "tts_hip_set_option": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+        "tts_hip_gemv_stats": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
+                                              ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+        "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
+        "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
+        "tts_parler_default_config": (None, [ctypes.POINTER(ParlerConfig)]),
+        "tts_parler_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(ParlerConfig)]),
+        "tts_parler_free": (None, [vp]),
+        "tts_parler_reset": (None, [vp]),
+        "tts_parler_prefill": (ctypes.c_int, [vp, vp, i32]),
+        "tts_parler_decode": (ctypes.c_int, [vp, vp, vp]),
+        "tts_parler_generate": (ctypes.c_int, [vp, i32, vp]),
+        "tts_parler_position": (i32, [vp]),
+        "tts_parler_last_graph_nodes": (i32, [vp]),
+        "tts_parler_weight_bytes": (u64, [vp]),
+        "tts_parler_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class HipBackend:
+    """One device + one HIP stream (tts_hip_backend_t)."""
+
+    def __init__(self, device=0):
+        L = lib()
+        n = L.tts_hip_device_count()
+        if n <= device:
+            raise RuntimeError(f"no HIP device {device} (device count {n})")
+        self.ptr = L.tts_hip_backend_init(device)
+        if not self.ptr:
+            raise RuntimeError("tts_hip_backend_init failed")
+        self.L = L
+
+    def iface(self):
+        it = BackendIface()
+        if self.L.tts_hip_backend_iface(self.ptr, ctypes.byref(it)) != 0:
+            raise RuntimeError("tts_hip_backend_iface failed")
+        return it
+
+    def alloc(self, nbytes):
+        p = self.L.tts_hip_buffer_alloc(self.ptr, nbytes)
+        if not p:
+            raise MemoryError(f"tts_hip_buffer_alloc({nbytes}) failed")
+        return p
+
+    def free(self, p):
+        self.L.tts_hip_buffer_free(self.ptr, p)
+
+    def set(self, dev, host_arr):
+        st = self.L.tts_hip_tensor_set(self.ptr, dev, host_arr.ctypes.data, host_arr.nbytes)
+        if st != 0:
+            raise RuntimeError(f"tensor_set failed {st}")
+
+    def get(self, host_arr, dev):
+        st = self.L.tts_hip_tensor_get(self.ptr, host_arr.ctypes.data, dev, host_arr.nbytes)
+        if st != 0:
+            raise RuntimeError(f"tensor_get failed {st}")
+
+    def sync(self):
+        if self.L.tts_hip_synchronize(self.ptr) != 0:
+            raise RuntimeError("synchronize failed")
+
+    def set_option(self, opt, value):
+        self.L.tts_hip_set_option(self.ptr, opt, value)
+
+    def gemv_stats(self, wtype=-1, reset=True):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        b = ctypes.c_double()
+        self.L.tts_hip_gemv_stats(self.ptr, wtype, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), 1 if reset else 0)
+        return ms.value, n.value, b.value
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_hip_backend_free(self.ptr)
+            self.ptr = None
+
+
+def parler_config(**kw):
+    cfg = ParlerConfig()
+    lib().tts_parler_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Parler:
+    """Parler-TTS decoder runner over a backend vtable (HIP, or the oracle in tests)."""
+
+    def __init__(self, iface, cfg):
+        import numpy as np  # noqa: F401
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface  # keep alive
+        self.ptr = self.L.tts_parler_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_parler_create failed")
+
+    def prefill(self, tokens):
+        import numpy as np
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        n = tok.shape[-1]
+        st = self.L.tts_parler_prefill(self.ptr, tok.ctypes.data, n)
+        if st != 0:
+            raise RuntimeError(f"prefill failed {st}")
+
+    def decode(self, audio_tokens):
+        import numpy as np
+        c = self.cfg
+        tok = np.ascontiguousarray(audio_tokens, dtype=np.int32)
+        out = np.empty((c.batch, c.n_output_heads, c.output_vocab), dtype=np.float32)
+        st = self.L.tts_parler_decode(self.ptr, tok.ctypes.data, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"decode failed {st}")
+        return out
+
+    def generate(self, n_steps):
+        import numpy as np
+        c = self.cfg
+        out = np.empty((c.batch, n_steps, c.n_output_heads), dtype=np.int32)
+        st = self.L.tts_parler_generate(self.ptr, n_steps, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"generate failed {st}")
+        return out
+
+    def reset(self):
+        self.L.tts_parler_reset(self.ptr)
+
+    @property
+    def position(self):
+        return self.L.tts_parler_position(self.ptr)
+
+    def last_graph_nodes(self):
+        return self.L.tts_parler_last_graph_nodes(self.ptr)
+
+    def weight_bytes(self):
+        return self.L.tts_parler_weight_bytes(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_parler_free(self.ptr)
+            self.ptr = None
