@@ -129,6 +129,13 @@ enum tts_status {
     TTS_STATUS_NO_DEVICE = -5
 };
 
+/* tts_tensor.flags bits */
+#define TTS_FLAG_INPUT 1
+#define TTS_FLAG_HOSTDATA 2 /* data is host memory without a buffer (util.cpp:86-94 trick) */
+#define TTS_FLAG_OUTPUT 4
+#define TTS_FLAG_PERSIST 8
+#define TTS_FLAG_REPACKED 16 /* set by the HIP backend: the tensor is stored in its Q4_K lane layout */
+
 /* Plain mirror of the ggml_tensor fields a backend reads.  `data` is a device pointer for
  * tensors handed to tts_hip_* (a host pointer for the CPU oracle in oracle/).  op_params hold
  * int32 and float (bit-cast) parameters exactly where ggml_set_op_params puts them. */
@@ -172,6 +179,14 @@ int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * 
 int tts_hip_memset(tts_hip_backend_t backend, void * dst_dev, int value, size_t size);
 int tts_hip_synchronize(tts_hip_backend_t backend);
 
+/* ggml_backend_buffer_i::set_tensor / get_tensor for a whole weight tensor.  The HIP buffer keeps
+ * Q4_K matrices in its own lane layout (like ggml-cpu's repack buffer type): set repacks and sets
+ * TTS_FLAG_REPACKED on `t`; get returns ggml's native bytes. */
+int tts_hip_weight_set(tts_hip_backend_t backend, tts_tensor * t, const void * src_host);
+int tts_hip_weight_get(tts_hip_backend_t backend, const tts_tensor * t, void * dst_host);
+/* Host helper: (inverse = 0) ggml Q4_K blocks -> backend lane layout, (1) the reverse. */
+void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse);
+
 int tts_hip_supports_op(const tts_tensor * node);
 int tts_hip_graph_compute(tts_hip_backend_t backend, tts_tensor * const * nodes, int n_nodes);
 
@@ -186,7 +201,8 @@ int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t * launches, double * bytes, int reset);
 
 /* Raw kernel entry points for micro-benchmarks (device pointers, current backend stream).
- * y[M][N] = W[N][K] . x[M][K]; W is `type` (Q4_K / Q8_0 / F16 / F32) row-major, N rows of K. */
+ * y[M][N] = W[N][K] . x[M][K]; W is `type` (Q4_K / Q8_0 / F16 / F32) row-major, N rows of K.
+ * Q4_K weights must already be in the backend lane layout (tts_repack_q4_K). */
 int tts_hip_gemv(tts_hip_backend_t backend, int type, const void * w, const float * x, float * y,
                  int64_t K, int64_t N, int64_t M);
 
@@ -198,6 +214,7 @@ typedef struct tts_backend_iface {
     void * (*alloc)(void * ctx, size_t size);
     void (*free)(void * ctx, void * ptr);
     int (*set)(void * ctx, void * dst, const void * src, size_t size);
+    int (*set_tensor)(void * ctx, tts_tensor * t, const void * src); /* whole weight tensor */
     int (*get)(void * ctx, void * dst, const void * src, size_t size);
     int (*memset)(void * ctx, void * dst, int value, size_t size);
     int (*compute)(void * ctx, tts_tensor * const * nodes, int n_nodes);

@@ -22,6 +22,14 @@
 
 typedef double ggml_float;
 
+/* Transcendental policy: ggml-cpu calls libm expf/sinf/cosf/tanhf (or SIMD approximations in its
+ * vectorised paths), whose last-ulp results are platform-specific.  The oracle pins them to the
+ * correctly rounded f32 value, evaluated in f64; the HIP backend does the same (cr_expf ...). */
+static inline float ref_expf(float x) { return (float)exp((double)x); }
+static inline float ref_sinf(float x) { return (float)sin((double)x); }
+static inline float ref_cosf(float x) { return (float)cos((double)x); }
+static inline float ref_tanhf(float x) { return (float)tanh((double)x); }
+
 /* ------------------------------------------------------------------------------------------ */
 /* fp16 <-> fp32: ggml_compute_fp16_to_fp32 / ggml_compute_fp32_to_fp16 (ggml-impl.h, the     */
 /* FP16 library's bit-exact scalar algorithm; identical to F16C _cvtss_sh RNE results).       */
@@ -490,8 +498,8 @@ static float unary_apply(const tts_tensor * dst, float x) {
     switch (dst->op) {
         case TTS_OP_SQR: return x * x;
         case TTS_OP_SQRT: return sqrtf(x);
-        case TTS_OP_SIN: return sinf(x);
-        case TTS_OP_COS: return cosf(x);
+        case TTS_OP_SIN: return ref_sinf(x);
+        case TTS_OP_COS: return ref_cosf(x);
         case TTS_OP_SCALE: return x * get_op_f(dst, 0);
         case TTS_OP_CLAMP: return MAX(MIN(x, get_op_f(dst, 1)), get_op_f(dst, 0));
         case TTS_OP_LEAKY_RELU: {
@@ -504,12 +512,12 @@ static float unary_apply(const tts_tensor * dst, float x) {
             switch (dst->op_params[0]) {
                 case TTS_UNARY_ABS: return fabsf(x);
                 case TTS_UNARY_NEG: return -x;
-                case TTS_UNARY_TANH: return tanhf(x);
+                case TTS_UNARY_TANH: return ref_tanhf(x);
                 case TTS_UNARY_RELU: return (x > 0.f) ? x : 0.f;
-                case TTS_UNARY_SIGMOID: return 1.f / (1.f + expf(-x));
+                case TTS_UNARY_SIGMOID: return 1.f / (1.f + ref_expf(-x));
                 case TTS_UNARY_GELU: return ref_gelu_table(x);
-                case TTS_UNARY_SILU: return x / (1.0f + expf(-x));
-                case TTS_UNARY_EXP: return expf(x);
+                case TTS_UNARY_SILU: return x / (1.0f + ref_expf(-x));
+                case TTS_UNARY_EXP: return ref_expf(x);
             }
     }
     return x;
@@ -594,7 +602,7 @@ static void op_soft_max(tts_tensor * dst, int ith, int nth) {
         for (int64_t i = 0; i < nc; ++i) max = MAX(max, wp[i]);
         ggml_float sum = 0.0;
         for (int64_t i = 0; i < nc; ++i) {
-            const float val = expf(wp[i] - max);
+            const float val = ref_expf(wp[i] - max);
             sum += (ggml_float)val;
             dp[i] = val;
         }
@@ -747,8 +755,8 @@ static void op_rope(tts_tensor * dst, int ith, int nth) {
             for (int64_t i0 = 0; i0 < a->ne[0]; i0 += 2) {
                 const float f = ff ? ((const float *)ff->data)[i0 / 2] : 1.0f;
                 const float th = freq_scale * (theta / f);
-                cache[i0 + 0] = cosf(th) * attn_factor;
-                cache[i0 + 1] = sinf(th) * attn_factor;
+                cache[i0 + 0] = ref_cosf(th) * attn_factor;
+                cache[i0 + 1] = ref_sinf(th) * attn_factor;
                 theta *= theta_scale;
             }
             for (int64_t i1 = ith; i1 < a->ne[1]; i1 += nth) {
@@ -860,6 +868,12 @@ static void * ob_alloc(void * ctx, size_t size) {
 static void ob_free(void * ctx, void * p) { (void)ctx; free(p); }
 static int ob_set(void * ctx, void * dst, const void * src, size_t n) { (void)ctx; memcpy(dst, src, n); return 0; }
 static int ob_get(void * ctx, void * dst, const void * src, size_t n) { (void)ctx; memcpy(dst, src, n); return 0; }
+static size_t ob_tensor_bytes(const tts_tensor * t) {
+    size_t n = ref_row_size(t->type, t->ne[0]);
+    for (int i = 1; i < 4; ++i) n *= (size_t)t->ne[i];
+    return n;
+}
+static int ob_set_tensor(void * ctx, tts_tensor * t, const void * src) { (void)ctx; memcpy(t->data, src, ob_tensor_bytes(t)); return 0; }
 static int ob_memset(void * ctx, void * dst, int v, size_t n) { (void)ctx; memset(dst, v, n); return 0; }
 static int ob_compute(void * ctx, tts_tensor * const * nodes, int n) { (void)ctx; return oracle_graph_compute(nodes, n, g_oracle_threads); }
 static int ob_sync(void * ctx) { (void)ctx; return 0; }
@@ -871,6 +885,7 @@ int oracle_backend_iface(tts_backend_iface * out, int n_threads) {
     out->alloc = ob_alloc;
     out->free = ob_free;
     out->set = ob_set;
+    out->set_tensor = ob_set_tensor;
     out->get = ob_get;
     out->memset = ob_memset;
     out->compute = ob_compute;

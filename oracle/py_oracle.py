@@ -66,7 +66,7 @@ def gemv(wtype, w_bytes, x, N, n_threads=8):
 
 def dequant_q4_K(w_bytes, K, N):
     import numpy as np
-    w = np.ascontiguousarray(w_bytes, dtype=np.uint8)
+    w = np.ascontiguousarray(w_bytes, dtype=np.uint8).reshape(-1)
     out = np.empty((N, K), dtype=np.float32)
     rs = K // 256 * 144
     for n in range(N):
@@ -76,7 +76,7 @@ def dequant_q4_K(w_bytes, K, N):
 
 def dequant_q8_0(w_bytes, K, N):
     import numpy as np
-    w = np.ascontiguousarray(w_bytes, dtype=np.uint8)
+    w = np.ascontiguousarray(w_bytes, dtype=np.uint8).reshape(-1)
     out = np.empty((N, K), dtype=np.float32)
     rs = K // 32 * 34
     for n in range(N):

@@ -64,6 +64,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     for (auto e : be->ev_free) hipEventDestroy(e);
     hipFree(be->scratch);
     hipFree(be->gelu_table);
+    if (be->repack_tmp) hipFree(be->repack_tmp);
     hipStreamDestroy(be->stream);
     delete be;
 }
@@ -122,6 +123,53 @@ int tts_hip_synchronize(tts_hip_backend_t be) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
     return hipStreamSynchronize(be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+
+void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse) {
+    const uint8_t * s = (const uint8_t *)src;
+    uint8_t * d = (uint8_t *)dst;
+    for (int64_t b = 0; b < nblocks; ++b) {
+        const uint8_t * sb = s + b * 144;
+        uint8_t * db = d + b * 144;
+        memcpy(db, sb, 16);
+        for (int i = 0; i < 128; ++i) {
+            const int l = i >> 4, c = (i >> 2) & 3, k = i & 3;
+            const int nat = 32 * c + 8 * k + l;
+            if (!inverse) db[16 + i] = sb[16 + nat];
+            else db[16 + nat] = sb[16 + i];
+        }
+    }
+}
+
+static size_t tensor_bytes(const tts_tensor * t) {
+    size_t n = tts_row_size(t->type, t->ne[0]);
+    for (int i = 1; i < 4; ++i) n *= (size_t)t->ne[i];
+    return n;
+}
+
+int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
+    if (!be || !t) return TTS_STATUS_BAD_ARG;
+    const size_t n = tensor_bytes(t);
+    if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0) {
+        std::vector<uint8_t> tmp(n);
+        tts_repack_q4_K(src, tmp.data(), (int64_t)(n / 144), 0);
+        int st = tts_hip_tensor_set(be, t->data, tmp.data(), n);
+        if (st == 0) t->flags |= TTS_FLAG_REPACKED;
+        return st;
+    }
+    return tts_hip_tensor_set(be, t->data, src, n);
+}
+
+int tts_hip_weight_get(tts_hip_backend_t be, const tts_tensor * t, void * dst) {
+    if (!be || !t) return TTS_STATUS_BAD_ARG;
+    const size_t n = tensor_bytes(t);
+    if (t->type == TTS_TYPE_Q4_K && (t->flags & TTS_FLAG_REPACKED)) {
+        std::vector<uint8_t> tmp(n);
+        int st = tts_hip_tensor_get(be, tmp.data(), t->data, n);
+        if (st == 0) tts_repack_q4_K(tmp.data(), dst, (int64_t)(n / 144), 1);
+        return st;
+    }
+    return tts_hip_tensor_get(be, dst, t->data, n);
 }
 
 static bool is_f32(const tts_tensor * t) { return t && t->type == TTS_TYPE_F32; }
@@ -216,7 +264,22 @@ static int compute_mul_mat(tts_hip_backend * be, const tts_tensor * n) {
         aq.vtype = TTS_TYPE_F32;
         aq.src = nullptr;
     }
-    launch_gemv(be, a->type, a->data, wrb, (const float *)b->data, xcs, &aq, (float *)n->data, ycs, K, N, M);
+    const void * wdata = a->data;
+    if (a->type == TTS_TYPE_Q4_K && !(a->flags & TTS_FLAG_REPACKED)) {
+        // a Q4_K matrix written with plain tensor_set (native ggml layout): repack to a temp
+        const size_t bytes = (size_t)wrb * (size_t)N;
+        if (be->repack_tmp_size < bytes) {
+            if (be->repack_tmp) {
+                TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+                TTS_HIP_CHECK(hipFree(be->repack_tmp));
+            }
+            TTS_HIP_CHECK(hipMalloc((void **)&be->repack_tmp, bytes));
+            be->repack_tmp_size = bytes;
+        }
+        launch_repack_q4_K(be, a->data, be->repack_tmp, (int64_t)(bytes / 144), 0);
+        wdata = be->repack_tmp;
+    }
+    launch_gemv(be, a->type, wdata, wrb, (const float *)b->data, xcs, &aq, (float *)n->data, ycs, K, N, M);
     return 0;
 }
 
@@ -325,6 +388,7 @@ extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, cons
 static void * hb_alloc(void * c, size_t n) { return tts_hip_buffer_alloc((tts_hip_backend_t)c, n); }
 static void hb_free(void * c, void * p) { tts_hip_buffer_free((tts_hip_backend_t)c, p); }
 static int hb_set(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_set((tts_hip_backend_t)c, d, s, n); }
+static int hb_set_tensor(void * c, tts_tensor * t, const void * s) { return tts_hip_weight_set((tts_hip_backend_t)c, t, s); }
 static int hb_get(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_get((tts_hip_backend_t)c, d, s, n); }
 static int hb_memset(void * c, void * d, int v, size_t n) { return tts_hip_memset((tts_hip_backend_t)c, d, v, n); }
 static int hb_compute(void * c, tts_tensor * const * nodes, int n) { return tts_hip_graph_compute((tts_hip_backend_t)c, nodes, n); }
@@ -337,6 +401,7 @@ extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * o
     out->alloc = hb_alloc;
     out->free = hb_free;
     out->set = hb_set;
+    out->set_tensor = hb_set_tensor;
     out->get = hb_get;
     out->memset = hb_memset;
     out->compute = hb_compute;

@@ -304,6 +304,8 @@ tts_tensor * soft_max_ext(context & c, tts_tensor * a, tts_tensor * mask, float 
 }
 
 tts_tensor * get_rows(context & c, tts_tensor * a, tts_tensor * idx) {
+    // ggml_get_rows: GGML_ASSERT(a->ne[2] == b->ne[1]) -- idx batch dims index a's dims 2/3
+    if (a->ne[2] != idx->ne[1] || idx->type != TTS_TYPE_I32) fail("get_rows: a->ne[2] must equal idx->ne[1]");
     int64_t ne[4] = {a->ne[0], idx->ne[0], idx->ne[1], idx->ne[2]};
     return new_op(c, TTS_OP_GET_ROWS, TTS_TYPE_F32, ne, a, idx);
 }

@@ -30,8 +30,18 @@ struct TD {
     int64_t ne[4];
     int64_t nb[4];
     int32_t type;
-    int32_t pad;
+    int32_t pad;  // tts_tensor.flags (TTS_FLAG_REPACKED matters to kernels)
 };
+
+// Transcendentals pinned to the correctly rounded f32 value (evaluated in f64), the same policy
+// as the oracle (oracle/ggml_ref.c ref_expf ...), so GPU and CPU agree bit-for-bit except when
+// the exact value lies within ~2^-52 of an f32 rounding midpoint.
+#ifdef __HIPCC__
+__device__ __forceinline__ float cr_expf(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float cr_sinf(float x) { return (float)sin((double)x); }
+__device__ __forceinline__ float cr_cosf(float x) { return (float)cos((double)x); }
+__device__ __forceinline__ float cr_tanhf(float x) { return (float)tanh((double)x); }
+#endif
 
 inline TD make_td(const tts_tensor * t) {
     TD d;
@@ -41,7 +51,7 @@ inline TD make_td(const tts_tensor * t) {
         d.nb[i] = (int64_t)t->nb[i];
     }
     d.type = t->type;
-    d.pad = 0;
+    d.pad = t->flags;
     return d;
 }
 
@@ -77,6 +87,8 @@ struct tts_hip_backend {
     std::vector<double> ev_bytes;
     std::vector<int> ev_type;
     std::vector<hipEvent_t> ev_free;
+    char * repack_tmp = nullptr;  // device temp for Q4_K matrices not stored repacked
+    size_t repack_tmp_size = 0;
 };
 
 namespace tts {
@@ -88,6 +100,8 @@ void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64
 void launch_gemv(tts_hip_backend * be, int wtype, const void * w, int64_t w_row_bytes, const float * x, int64_t xcs,
                  const ActQuant * aq, float * y, int64_t ycs, int64_t K, int64_t N, int64_t M);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
+
+void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int64_t nblocks, int inverse);
 
 // ---- launchers (k_ops.hip) ----
 int launch_op(tts_hip_backend * be, const tts_tensor * node);

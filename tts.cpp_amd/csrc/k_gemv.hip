@@ -30,10 +30,14 @@ __device__ __forceinline__ int dev_nearest_int(float f) {
 
 // ------------------------------------------------------------------------------------------
 // quantize_row_q8_K_ref: per 256-block, max |x| (first index on ties), iscale = -127/max,
-// q = min(127, nearest_int(iscale*x)), bsums over 16, d = 1/iscale.  grid (K/256, M), 256 thr.
+// q = min(127, nearest_int(iscale*x)), d = 1/iscale.  grid (K/256, M), 256 threads.
+// Output layout (device scratch, "lane-major", matches the repacked Q4_K weight):
+//   qs  [M][nb][l=0..7][hi=0..1][c=0..3][k=0..3]  element p = 32*(2c+hi) + 8k + l
+//   d   [M][nb]          f32 (y[i].d)
+//   s32 [M][nb][8]       per-32 sums (bsums[2j] + bsums[2j+1]; ggml sums bsums*mins in int32)
 __global__ __launch_bounds__(256) void k_quantize_q8_K(const float * __restrict__ x, int64_t xcs, int64_t K,
                                                        int8_t * __restrict__ qs, float * __restrict__ dout,
-                                                       int32_t * __restrict__ bsums) {
+                                                       int32_t * __restrict__ s32) {
     const int blk = blockIdx.x;
     const int m = blockIdx.y;
     const int t = threadIdx.x;
@@ -68,23 +72,43 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(const float * __restrict_
             imax = s_idx[w];
         }
     }
-    int8_t * q = qs + m * K + (int64_t)blk * QK_K;
-    if (amax == 0.f) {
-        q[t] = 0;
-        if ((t & 15) == 0) bsums[m * (K / 16) + (int64_t)blk * 16 + (t >> 4)] = 0;
-        if (t == 0) dout[m * nb + blk] = 0.f;
-        return;
+    const int j = t >> 5, r = t & 31;
+    const int off = (r & 7) * 32 + (j & 1) * 16 + (j >> 1) * 4 + (r >> 3);
+    int8_t * q = qs + ((int64_t)m * nb + blk) * QK_K;
+    int qi = 0;
+    if (amax != 0.f) {
+        const float mx = s_v[imax];
+        const float iscale = __fdiv_rn(-127.f, mx);
+        qi = dev_nearest_int(__fmul_rn(iscale, v));
+        qi = qi < 127 ? qi : 127;
+        if (t == 0) dout[m * nb + blk] = __fdiv_rn(1.f, iscale);
+    } else if (t == 0) {
+        dout[m * nb + blk] = 0.f;
     }
-    const float mx = s_v[imax];
-    const float iscale = __fdiv_rn(-127.f, mx);
-    int qi = dev_nearest_int(__fmul_rn(iscale, v));
-    qi = qi < 127 ? qi : 127;
-    q[t] = (int8_t)qi;
+    q[off] = (int8_t)qi;
     int s = qi;
 #pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) s += __shfl_xor(s, off);
-    if ((t & 15) == 0) bsums[m * (K / 16) + (int64_t)blk * 16 + (t >> 4)] = s;
-    if (t == 0) dout[m * nb + blk] = __fdiv_rn(1.f, iscale);
+    for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+    if (r == 0) s32[((int64_t)m * nb + blk) * 8 + j] = s;
+}
+
+// Q4_K repack (the backend's own buffer layout for Q4_K matrices, like ggml-cpu's repack
+// buffer type): within each 144-B block the header is unchanged and the 128 nibble bytes are
+// permuted so that lane l of an octet reads, as one 16-B load, the dwords c = 0..3 whose bytes
+// k = 0..3 hold weights 64c + 8k + l (low nibble) and 64c + 32 + 8k + l (high nibble):
+//   repacked[l*16 + c*4 + k] = native[32c + 8k + l].
+// Then sdot4 yields ggml's per-residue partial aux32[l] directly (vec_dot_q4_K_q8_K generic).
+__global__ void k_repack_q4_K(const uint8_t * __restrict__ src, uint8_t * __restrict__ dst, int64_t nblocks, int inverse) {
+    const int64_t b = (int64_t)blockIdx.x * 2 + (threadIdx.x >> 7);
+    const int i = threadIdx.x & 127;
+    if (b >= nblocks) return;
+    const uint8_t * s = src + b * 144;
+    uint8_t * d = dst + b * 144;
+    if (i < 16) d[i] = s[i];
+    const int l = i >> 4, c = (i >> 2) & 3, k = i & 3;
+    const int nat = 32 * c + 8 * k + l;
+    if (!inverse) d[16 + i] = s[16 + nat];
+    else d[16 + nat] = s[16 + i];
 }
 
 // quantize_row_q8_0_ref: per 32-block d = amax/127, id = d ? 1/d : 0, q = roundf(x*id); the
@@ -112,61 +136,62 @@ __global__ void k_quantize_f16(const float * __restrict__ x, int64_t xcs, int64_
 }
 
 // ------------------------------------------------------------------------------------------
-// Q4_K x Q8_K GEMV.  256 threads = 4 waves; each wave covers RPI rows (8 / OPR), each row is
-// split over OPR octets (OPR = min(8, pow2 <= blocks per row)); an octet steps OPR blocks.
+// Q4_K x Q8_K GEMV on repacked weights, reproducing ggml_vec_dot_q4_K_q8_K's generic f32 order
+// exactly: per row, blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7), sumf -= dmin*sumi,
+// then sumf += sums[0..7].  Integer work is spread over octets (one block per octet per
+// iteration); the f32 accumulation is done by the row's leader octet, which pulls each block's
+// aux32[l], d, dmin, sumi from the owning octet with shuffles, in block order.
+// 256 threads = 4 waves; a wave covers RPI = 8/OPR rows, OPR octets per row.
+__device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc, int & mn) {
+    if (j < 4) {
+        sc = q[j] & 63;
+        mn = q[j + 4] & 63;
+    } else {
+        sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        mn = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+    }
+}
+
 template <int MC>
 __global__ __launch_bounds__(256) void k_gemv_q4_K(const uint8_t * __restrict__ W, int64_t w_row_bytes,
                                                    const int8_t * __restrict__ xq, const float * __restrict__ xd,
-                                                   const int32_t * __restrict__ xbs, float * __restrict__ y,
+                                                   const int32_t * __restrict__ xs32, float * __restrict__ y,
                                                    int64_t ycs, int64_t K, int64_t N, int M, int OPR) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int g = lane >> 3;
-    const int t = lane & 7;
+    const int t = lane & 7;  // = residue l
     const int nb = (int)(K / QK_K);
     const int RPI = 8 / OPR;
-    const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RPI + g / OPR;
-    const int og = g % OPR;
-    const int j = t >> 1;
-    const int half = t & 1;
+    const int rg = g / OPR;                 // row group within the wave
+    const int og = g % OPR;                 // octet within the row group
+    const int base = rg * OPR * 8;          // first lane of the row group
+    const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RPI + rg;
     const bool row_ok = row < N;
-    float acc[MC];
+    float sums[MC], sumf[MC];
 #pragma unroll
-    for (int m = 0; m < MC; ++m) acc[m] = 0.f;
-
+    for (int m = 0; m < MC; ++m) {
+        sums[m] = 0.f;
+        sumf[m] = 0.f;
+    }
     const uint8_t * wrow = W + (row_ok ? row : 0) * w_row_bytes;
     const int iters = (nb + OPR - 1) / OPR;
     for (int it = 0; it < iters; ++it) {
         const int blk = og + it * OPR;
         const bool ok = row_ok && blk < nb;
-        uint4 hdr = make_uint4(0, 0, 0, 0);
-        uint4 q = make_uint4(0, 0, 0, 0);
+        u32x4 hdr = {0u, 0u, 0u, 0u};
+        u32x4 q = {0u, 0u, 0u, 0u};
         if (ok) {
             const uint8_t * bp = wrow + (int64_t)blk * 144;
-            const u32x4 h4 = __builtin_nontemporal_load((const u32x4 *)bp);
-            const u32x4 q4 = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + t * 16));
-            hdr = make_uint4(h4.x, h4.y, h4.z, h4.w);
-            q = make_uint4(q4.x, q4.y, q4.z, q4.w);
+            hdr = __builtin_nontemporal_load((const u32x4 *)bp);
+            q = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + t * 16));
         }
-        // header: d | dmin << 16, then scales[12] in hdr.y/.z/.w (little endian bytes)
         const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
         const uint8_t * scb = (const uint8_t *)sw;
-        const int sb0 = 2 * j, sb1 = 2 * j + 1;
-        int sc0, m0, sc1, m1;
-        if (sb0 < 4) {
-            sc0 = scb[sb0] & 63;
-            m0 = scb[sb0 + 4] & 63;
-        } else {
-            sc0 = (scb[sb0 + 4] & 0xF) | ((scb[sb0 - 4] >> 6) << 4);
-            m0 = (scb[sb0 + 4] >> 4) | ((scb[sb0] >> 6) << 4);
-        }
-        if (sb1 < 4) {
-            sc1 = scb[sb1] & 63;
-            m1 = scb[sb1 + 4] & 63;
-        } else {
-            sc1 = (scb[sb1 + 4] & 0xF) | ((scb[sb1 - 4] >> 6) << 4);
-            m1 = (scb[sb1 + 4] >> 4) | ((scb[sb1] >> 6) << 4);
-        }
+        int sc[8], mymin, tmp;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) q4k_scale_min(scb, jj, sc[jj], tmp);
+        q4k_scale_min(scb, t, tmp, mymin);
         const int lo0 = (int)(q.x & 0x0F0F0F0Fu), lo1 = (int)(q.y & 0x0F0F0F0Fu);
         const int lo2 = (int)(q.z & 0x0F0F0F0Fu), lo3 = (int)(q.w & 0x0F0F0F0Fu);
         const int hi0 = (int)((q.x >> 4) & 0x0F0F0F0Fu), hi1 = (int)((q.y >> 4) & 0x0F0F0F0Fu);
@@ -176,91 +201,108 @@ __global__ __launch_bounds__(256) void k_gemv_q4_K(const uint8_t * __restrict__ 
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
             if (m >= M) break;
-            int isum = 0, imin = 0;
-            float dy = 0.f;
+            int aux = 0, smin = 0;
+            float dd = 0.f, dm = 0.f;
             if (ok) {
-                const int8_t * xb = xq + (int64_t)m * K + (int64_t)blk * QK_K + 64 * j + half * 16;
-                const int4 xl = *(const int4 *)xb;
-                const int4 xh = *(const int4 *)(xb + 32);
-                int sl = __builtin_amdgcn_sdot4(lo0, xl.x, 0, false);
-                sl = __builtin_amdgcn_sdot4(lo1, xl.y, sl, false);
-                sl = __builtin_amdgcn_sdot4(lo2, xl.z, sl, false);
-                sl = __builtin_amdgcn_sdot4(lo3, xl.w, sl, false);
-                int sh = __builtin_amdgcn_sdot4(hi0, xh.x, 0, false);
-                sh = __builtin_amdgcn_sdot4(hi1, xh.y, sh, false);
-                sh = __builtin_amdgcn_sdot4(hi2, xh.z, sh, false);
-                sh = __builtin_amdgcn_sdot4(hi3, xh.w, sh, false);
-                isum = sc0 * sl + sc1 * sh;
-                const int32_t * bs = xbs + (int64_t)m * (K / 16) + (int64_t)blk * 16 + 4 * j + half;
-                imin = m0 * bs[0] + m1 * bs[2];
-                dy = xd[(int64_t)m * nb + blk];
+                const int64_t xb = ((int64_t)m * nb + blk);
+                const int4 xl = *(const int4 *)(xq + xb * QK_K + t * 32);
+                const int4 xh = *(const int4 *)(xq + xb * QK_K + t * 32 + 16);
+                aux = sc[0] * __builtin_amdgcn_sdot4(lo0, xl.x, 0, false);
+                aux += sc[2] * __builtin_amdgcn_sdot4(lo1, xl.y, 0, false);
+                aux += sc[4] * __builtin_amdgcn_sdot4(lo2, xl.z, 0, false);
+                aux += sc[6] * __builtin_amdgcn_sdot4(lo3, xl.w, 0, false);
+                aux += sc[1] * __builtin_amdgcn_sdot4(hi0, xh.x, 0, false);
+                aux += sc[3] * __builtin_amdgcn_sdot4(hi1, xh.y, 0, false);
+                aux += sc[5] * __builtin_amdgcn_sdot4(hi2, xh.z, 0, false);
+                aux += sc[7] * __builtin_amdgcn_sdot4(hi3, xh.w, 0, false);
+                smin = mymin * xs32[xb * 8 + t];
+                const float yd = xd[xb];
+                dd = __fmul_rn(dw, yd);
+                dm = __fmul_rn(dmw, yd);
             }
-            isum += __shfl_xor(isum, 1);
-            isum += __shfl_xor(isum, 2);
-            isum += __shfl_xor(isum, 4);
-            imin += __shfl_xor(imin, 1);
-            imin += __shfl_xor(imin, 2);
-            imin += __shfl_xor(imin, 4);
-            const float dd = __fmul_rn(dw, dy);
-            const float dm = __fmul_rn(dmw, dy);
-            acc[m] = __fadd_rn(acc[m], __fsub_rn(__fmul_rn(dd, (float)isum), __fmul_rn(dm, (float)imin)));
+            smin += __shfl_xor(smin, 1);
+            smin += __shfl_xor(smin, 2);
+            smin += __shfl_xor(smin, 4);
+            // ordered f32 accumulation of this iteration's blocks by the leader octet
+            for (int bb = 0; bb < OPR; ++bb) {
+                if (it * OPR + bb >= nb) break;  // uniform across the wave
+                const int src = base + bb * 8 + t;
+                const int a_b = __shfl(aux, src);
+                const float dd_b = __shfl(dd, src);
+                const float dm_b = __shfl(dm, src);
+                const int s_b = __shfl(smin, src);
+                sums[m] = __fadd_rn(sums[m], __fmul_rn(dd_b, (float)a_b));
+                sumf[m] = __fsub_rn(sumf[m], __fmul_rn(dm_b, (float)s_b));
+            }
         }
     }
 #pragma unroll
     for (int m = 0; m < MC; ++m) {
-        float a = acc[m];
-        for (int off = 8; off < OPR * 8; off <<= 1) a = __fadd_rn(a, __shfl_xor(a, off));
-        acc[m] = a;
+        float f = sumf[m];
+        for (int l = 0; l < 8; ++l) f = __fadd_rn(f, __shfl(sums[m], base + l));
+        sumf[m] = f;
     }
     if (row_ok && og == 0 && t == 0) {
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
-            if (m < M) y[m * ycs + row] = acc[m];
+            if (m < M) y[m * ycs + row] = sumf[m];
         }
     }
 }
 
-// Q8_0 x Q8_0 GEMV: one lane per 34-B block (unaligned, 2-byte loads), a wave per row.
+// Q8_0 x Q8_0 GEMV reproducing ggml_vec_dot_q8_0_q8_0's generic order: per row, blocks in
+// ascending order, sumf += (float)sumi * (d_w * d_x).  A wave owns a row: lane = block within a
+// 64-block chunk computes sumi (exact int), then lane 0 folds the chunk in order via shuffles.
 template <int MC>
 __global__ __launch_bounds__(256) void k_gemv_q8_0(const uint8_t * __restrict__ W, int64_t w_row_bytes,
                                                    const int8_t * __restrict__ xq, const float * __restrict__ xd,
                                                    float * __restrict__ y, int64_t ycs, int64_t K, int64_t N, int M) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= N) return;
+    if (row >= N) return;  // wave-uniform
     const int nb = (int)(K / QK8_0);
     const uint8_t * wrow = W + row * w_row_bytes;
     float acc[MC];
 #pragma unroll
     for (int m = 0; m < MC; ++m) acc[m] = 0.f;
-    for (int b = lane; b < nb; b += 64) {
-        const uint16_t * bp = (const uint16_t *)(wrow + (int64_t)b * 34);
-        const float dw = dev_fp16_to_fp32(bp[0]);
-        int wv[8];
+    for (int b0 = 0; b0 < nb; b0 += 64) {
+        const int b = b0 + lane;
+        const bool ok = b < nb;
+        float dw = 0.f;
+        int wv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (ok) {
+            const uint16_t * bp = (const uint16_t *)(wrow + (int64_t)b * 34);
+            dw = dev_fp16_to_fp32(bp[0]);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
+            for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
+        }
+        const int cnt = nb - b0 < 64 ? nb - b0 : 64;
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
             if (m >= M) break;
-            const int4 * xb = (const int4 *)(xq + (int64_t)m * K + (int64_t)b * QK8_0);
-            const int4 x0 = xb[0], x1 = xb[1];
-            int s = __builtin_amdgcn_sdot4(wv[0], x0.x, 0, false);
-            s = __builtin_amdgcn_sdot4(wv[1], x0.y, s, false);
-            s = __builtin_amdgcn_sdot4(wv[2], x0.z, s, false);
-            s = __builtin_amdgcn_sdot4(wv[3], x0.w, s, false);
-            s = __builtin_amdgcn_sdot4(wv[4], x1.x, s, false);
-            s = __builtin_amdgcn_sdot4(wv[5], x1.y, s, false);
-            s = __builtin_amdgcn_sdot4(wv[6], x1.z, s, false);
-            s = __builtin_amdgcn_sdot4(wv[7], x1.w, s, false);
-            const float dxy = __fmul_rn(dw, xd[(int64_t)m * nb + b]);
-            acc[m] = __fadd_rn(acc[m], __fmul_rn((float)s, dxy));
+            int s = 0;
+            float dxy = 0.f;
+            if (ok) {
+                const int4 * xb = (const int4 *)(xq + (int64_t)m * K + (int64_t)b * QK8_0);
+                const int4 x0 = xb[0], x1 = xb[1];
+                s = __builtin_amdgcn_sdot4(wv[0], x0.x, 0, false);
+                s = __builtin_amdgcn_sdot4(wv[1], x0.y, s, false);
+                s = __builtin_amdgcn_sdot4(wv[2], x0.z, s, false);
+                s = __builtin_amdgcn_sdot4(wv[3], x0.w, s, false);
+                s = __builtin_amdgcn_sdot4(wv[4], x1.x, s, false);
+                s = __builtin_amdgcn_sdot4(wv[5], x1.y, s, false);
+                s = __builtin_amdgcn_sdot4(wv[6], x1.z, s, false);
+                s = __builtin_amdgcn_sdot4(wv[7], x1.w, s, false);
+                dxy = __fmul_rn(dw, xd[(int64_t)m * nb + b]);
+            }
+            float a = acc[m];
+            for (int i = 0; i < cnt; ++i) {
+                const int si = __shfl(s, i);
+                const float fi = __shfl(dxy, i);
+                a = __fadd_rn(a, __fmul_rn((float)si, fi));
+            }
+            acc[m] = a;
         }
-    }
-#pragma unroll
-    for (int m = 0; m < MC; ++m) {
-        float a = acc[m];
-        for (int off = 32; off >= 1; off >>= 1) a = __fadd_rn(a, __shfl_xor(a, off));
-        acc[m] = a;
     }
     if (lane == 0) {
 #pragma unroll
@@ -338,7 +380,7 @@ __global__ __launch_bounds__(256) void k_gemv_float(const uint8_t * __restrict__
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M) {
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
     switch (wtype) {
-        case TTS_TYPE_Q4_K: return al(K * M) + al(sizeof(float) * M * (K / QK_K)) + al(sizeof(int32_t) * M * (K / 16));
+        case TTS_TYPE_Q4_K: return al(K * M) + al(sizeof(float) * M * (K / QK_K)) + al(sizeof(int32_t) * M * (K / 32));
         case TTS_TYPE_Q8_0: return al(K * M) + al(sizeof(float) * M * (K / QK8_0));
         case TTS_TYPE_F16: return al(2 * K * M);
         default: return 0;
@@ -374,6 +416,12 @@ void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64
     } else {
         aq.vtype = TTS_TYPE_F32;
     }
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int64_t nblocks, int inverse) {
+    const unsigned grid = (unsigned)((nblocks + 1) / 2);
+    hipLaunchKernelGGL(k_repack_q4_K, dim3(grid), dim3(256), 0, be->stream, (const uint8_t *)src, (uint8_t *)dst, nblocks, inverse);
     TTS_HIP_CHECK(hipGetLastError());
 }
 
@@ -431,7 +479,7 @@ void launch_gemv(tts_hip_backend * be, int wtype, const void * w, int64_t wrb, c
         if (aq->vtype == TTS_TYPE_Q8_K) {
             sub.qs = aq->qs + m0 * K;
             sub.d = aq->d + m0 * (K / QK_K);
-            sub.bsums = aq->bsums + m0 * (K / 16);
+            sub.bsums = aq->bsums + m0 * (K / 32);
         } else if (aq->vtype == TTS_TYPE_Q8_0) {
             sub.qs = aq->qs + m0 * K;
             sub.d = aq->d + m0 * (K / QK8_0);

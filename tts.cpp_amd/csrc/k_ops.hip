@@ -88,8 +88,8 @@ __device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
     switch (P.op) {
         case TTS_OP_SQR: return __fmul_rn(x, x);
         case TTS_OP_SQRT: return __fsqrt_rn(x);
-        case TTS_OP_SIN: return sinf(x);
-        case TTS_OP_COS: return cosf(x);
+        case TTS_OP_SIN: return cr_sinf(x);
+        case TTS_OP_COS: return cr_cosf(x);
         case TTS_OP_SCALE: return __fmul_rn(x, P.p0);
         case TTS_OP_CLAMP: return fmaxf(fminf(x, P.p1), P.p0);
         case TTS_OP_LEAKY_RELU: return __fadd_rn((x > 0.f) ? x : 0.f, __fmul_rn(P.p0, (x < 0.f) ? x : 0.f));
@@ -100,17 +100,17 @@ __device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
     switch (P.uop) {
         case TTS_UNARY_ABS: return fabsf(x);
         case TTS_UNARY_NEG: return -x;
-        case TTS_UNARY_TANH: return tanhf(x);
+        case TTS_UNARY_TANH: return cr_tanhf(x);
         case TTS_UNARY_RELU: return x > 0.f ? x : 0.f;
-        case TTS_UNARY_SIGMOID: return __fdiv_rn(1.f, __fadd_rn(1.f, expf(-x)));
+        case TTS_UNARY_SIGMOID: return __fdiv_rn(1.f, __fadd_rn(1.f, cr_expf(-x)));
         case TTS_UNARY_GELU: {
             if (x <= -10.0f) return 0.0f;
             if (x >= 10.0f) return x;
             const uint16_t h = __half_as_ushort(__float2half_rn(x));
             return __half2float(__ushort_as_half(P.gelu_table[h]));
         }
-        case TTS_UNARY_SILU: return __fdiv_rn(x, __fadd_rn(1.0f, expf(-x)));
-        case TTS_UNARY_EXP: return expf(x);
+        case TTS_UNARY_SILU: return __fdiv_rn(x, __fadd_rn(1.0f, cr_expf(-x)));
+        case TTS_UNARY_EXP: return cr_expf(x);
     }
     return x;
 }
@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void k_soft_max(TD dst, TD a, const char * mas
     mx = block_max(mx, shf);
     double s = 0.0;
     for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
-        const float v = expf(__fsub_rn(dp[i], mx));
+        const float v = cr_expf(__fsub_rn(dp[i], mx));
         dp[i] = v;
         s += (double)v;
     }
@@ -234,6 +234,8 @@ __global__ void k_get_rows(TD dst, TD s0, TD s1) {
             const block_q4_K * b = (const block_q4_K *)src + k / QK_K;
             const int e = (int)(k % QK_K);
             const int j64 = e / 64, w = e % 64, hi = w >= 32, l = w % 32;
+            // repacked lane layout: byte l*16 + c*4 + k holds weights 64c + 8k + l (+32)
+            const int qbyte = (s0.pad & TTS_FLAG_REPACKED) ? ((l & 7) * 16 + j64 * 4 + (l >> 3)) : (32 * j64 + l);
             const int sb = 2 * j64 + hi;
             const uint8_t * q = b->scales;
             int sc, mn;
@@ -246,7 +248,7 @@ __global__ void k_get_rows(TD dst, TD s0, TD s1) {
             }
             const float d = __half2float(__ushort_as_half(b->d));
             const float dm = __half2float(__ushort_as_half(b->dmin));
-            const uint8_t qb = b->qs[32 * j64 + l];
+            const uint8_t qb = b->qs[qbyte];
             const int qv = hi ? (qb >> 4) : (qb & 0xF);
             v = __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
         }
@@ -299,7 +301,7 @@ __global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int 
             for (int64_t k = 0; k < i0 / 2; ++k) theta = __fmul_rn(theta, theta_scale);
             const float f = ff ? ff[i0 / 2] : 1.0f;
             const float th = __fmul_rn(freq_scale, __fdiv_rn(theta, f));
-            const float c = __fmul_rn(cosf(th), attn_factor), s = __fmul_rn(sinf(th), attn_factor);
+            const float c = __fmul_rn(cr_cosf(th), attn_factor), s = __fmul_rn(cr_sinf(th), attn_factor);
             int64_t j0, j1;
             if (neox) {
                 j0 = i0 / 2;

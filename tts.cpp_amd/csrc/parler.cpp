@@ -112,7 +112,8 @@ static bool upload_weights(tts_parler * p, std::vector<wspec> & specs) {
             case 3: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.5f, 0.0f); break;
             default: synth_fill(t->type, host.data(), rows, K, s.seed, std); break;
         }
-        if (p->be.set(p->be.ctx, t->data, host.data(), nb) != 0) return false;
+        // whole-tensor upload: the backend may keep its own layout (HIP: Q4_K lane layout)
+        if (p->be.set_tensor(p->be.ctx, t, host.data()) != 0) return false;
     }
     return true;
 }
@@ -296,11 +297,12 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
                 inp = i == 0 ? e : tg::add(c, e, inp);
             }
         } else {
+            // head-major [heads][B] so that each head's ids are one contiguous 1-D index
             p->in_tokens = tg::new_tensor_1d(c, TTS_TYPE_I32, (int64_t)B * cf.n_output_heads);
             tg::set_input(p->in_tokens);
             for (int i = 0; i < cf.n_output_heads; ++i) {
-                tts_tensor * idx = tg::view_2d(c, p->in_tokens, 1, B, cf.n_output_heads * sizeof(int32_t), i * sizeof(int32_t));
-                tts_tensor * e = tg::get_rows(c, p->embds[i], idx);  // [H, 1, B]
+                tts_tensor * idx = tg::view_1d(c, p->in_tokens, B, (size_t)i * B * sizeof(int32_t));
+                tts_tensor * e = tg::get_rows(c, p->embds[i], idx);  // [H, B]
                 inp = i == 0 ? e : tg::add(c, e, inp);
             }
         }
@@ -310,9 +312,9 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
             tg::set_input(p->in_tokens);
             inp = tg::get_rows(c, p->prompt_embd, p->in_tokens);
         } else {
-            p->in_tokens = tg::new_tensor_2d(c, TTS_TYPE_I32, n, B);
+            p->in_tokens = tg::new_tensor_1d(c, TTS_TYPE_I32, (int64_t)n * B);
             tg::set_input(p->in_tokens);
-            inp = tg::get_rows(c, p->prompt_embd, p->in_tokens);  // [H, n, B]
+            inp = tg::reshape_3d(c, tg::get_rows(c, p->prompt_embd, p->in_tokens), H, n, B);  // [H, n, B]
         }
     }
     tts_tensor * inpL = tg::add(c, inp, tg::get_rows(c, p->pos_embd, p->in_positions));
@@ -419,7 +421,10 @@ static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n)
             // audio tokens arrive as [heads] for n == 1; layout [heads][n] otherwise
             st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * cf.n_output_heads);
         } else {
-            st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * B * cf.n_output_heads);
+            std::vector<int32_t> hm((size_t)B * cf.n_output_heads);  // [B][heads] -> [heads][B]
+            for (int b = 0; b < B; ++b)
+                for (int h = 0; h < cf.n_output_heads; ++h) hm[(size_t)h * B + b] = tokens[(size_t)b * cf.n_output_heads + h];
+            st |= be.set(be.ctx, p->in_tokens->data, hm.data(), sizeof(int32_t) * hm.size());
         }
     } else {
         st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * B);

@@ -53,6 +53,7 @@ class BackendIface(ctypes.Structure):
         ("alloc", ctypes.c_void_p),
         ("free", ctypes.c_void_p),
         ("set", ctypes.c_void_p),
+        ("set_tensor", ctypes.c_void_p),
         ("get", ctypes.c_void_p),
         ("memset", ctypes.c_void_p),
         ("compute", ctypes.c_void_p),
@@ -125,6 +126,9 @@ def lib():
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
         "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
+        "tts_hip_weight_set": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
+        "tts_hip_weight_get": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
+        "tts_repack_q4_K": (None, [vp, vp, i64, ctypes.c_int]),
         "tts_parler_default_config": (None, [ctypes.POINTER(ParlerConfig)]),
         "tts_parler_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(ParlerConfig)]),
         "tts_parler_free": (None, [vp]),
