@@ -37,6 +37,8 @@ typedef struct tts_parler_config {
     int32_t bos_token;       /* 1025 */
     uint64_t seed;           /* synthetic weight seed base (0x5EED) */
     uint64_t arena_bytes;    /* compute arena (0 = default 256 MiB) */
+    int32_t debug_no_reuse;  /* 1 = every node gets its own arena memory (node dumps) */
+    int32_t pad_;
 } tts_parler_config;
 
 typedef struct tts_parler tts_parler;
@@ -59,6 +61,8 @@ int32_t tts_parler_last_graph_nodes(const tts_parler * p);
 uint64_t tts_parler_weight_bytes(const tts_parler * p);
 /* Debug: copy a named node of the last graph to host (returns bytes, 0 if not found). */
 uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap);
+/* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
+uint64_t tts_parler_node(tts_parler * p, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap);
 
 #ifdef __cplusplus
 }

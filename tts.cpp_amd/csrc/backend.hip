@@ -8,9 +8,6 @@
 
 using namespace tts;
 
-namespace tts {
-int launch_fused(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes, int i, int * consumed);
-}
 
 // GGML_GELU_FP16 table: fp16(ggml_gelu_f32(fp16_to_fp32(i))) for every fp16 bit pattern,
 // computed on the host with the same f32 expression ggml uses (no contraction; see Makefile).
@@ -217,110 +214,10 @@ int tts_hip_supports_op(const tts_tensor * n) {
 
 }  // extern "C"
 
-static bool rows_contig_f32(const tts_tensor * t) { return t->type == TTS_TYPE_F32 && t->nb[0] == 4; }
-
-// MUL_MAT with a 2-D weight matrix and a column set whose rows are contiguous: the decode GEMV.
-static bool is_gemv(const tts_tensor * n) {
-    const tts_tensor * a = n->src[0];
-    const tts_tensor * b = n->src[1];
-    if (a->ne[2] != 1 || a->ne[3] != 1) return false;
-    if (!rows_contig_f32(b)) return false;
-    // columns must be evenly strided (b viewed as [K, M] with stride nb[1])
-    if (b->ne[2] * b->ne[3] != 1 && !(b->nb[2] == b->nb[1] * (size_t)b->ne[1] && b->nb[3] == b->nb[2] * (size_t)b->ne[2]))
-        return false;
-    if (n->nb[0] != 4 || (n->ne[2] * n->ne[3] != 1 && !(n->nb[2] == n->nb[1] * (size_t)n->ne[1]))) return false;
-    if (a->nb[0] != tts_type_size(a->type)) return false;
-    if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) {
-        // worthwhile only for weight-shaped operands with K multiple of 4
-        if (a->ne[0] % 4 != 0 || (b->nb[1] % 16) != 0) return false;
-    }
-    if ((b->nb[1] % 4) != 0) return false;
-    return true;
-}
-
-static int compute_mul_mat(tts_hip_backend * be, const tts_tensor * n) {
-    const tts_tensor * a = n->src[0];
-    const tts_tensor * b = n->src[1];
-    if (!is_gemv(n)) {
-        if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) return launch_op(be, n);
-        return TTS_STATUS_UNSUPPORTED;
-    }
-    const int64_t K = a->ne[0], N = a->ne[1];
-    const int64_t M = b->ne[1] * b->ne[2] * b->ne[3];
-    const int64_t xcs = (int64_t)(b->nb[1] / 4);
-    const int64_t ycs = (int64_t)(n->nb[1] / 4);
-    const int64_t wrb = (int64_t)a->nb[1];
-    ActQuant & aq = be->aq;
-    if (a->type != TTS_TYPE_F32) {
-        const int vt = a->type == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : a->type;
-        const bool hit = aq.src == b->data && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
-        if (!hit) {
-            if (act_quant_bytes(a->type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
-            launch_quantize_act(be, a->type, (const float *)b->data, xcs, K, M, aq);
-            aq.src = b->data;
-            aq.graph_epoch = be->graph_epoch;
-        }
-    } else {
-        aq.vtype = TTS_TYPE_F32;
-        aq.src = nullptr;
-    }
-    const void * wdata = a->data;
-    if (a->type == TTS_TYPE_Q4_K && !(a->flags & TTS_FLAG_REPACKED)) {
-        // a Q4_K matrix written with plain tensor_set (native ggml layout): repack to a temp
-        const size_t bytes = (size_t)wrb * (size_t)N;
-        if (be->repack_tmp_size < bytes) {
-            if (be->repack_tmp) {
-                TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
-                TTS_HIP_CHECK(hipFree(be->repack_tmp));
-            }
-            TTS_HIP_CHECK(hipMalloc((void **)&be->repack_tmp, bytes));
-            be->repack_tmp_size = bytes;
-        }
-        launch_repack_q4_K(be, a->data, be->repack_tmp, (int64_t)(bytes / 144), 0);
-        wdata = be->repack_tmp;
-    }
-    launch_gemv(be, a->type, wdata, wrb, (const float *)b->data, xcs, &aq, (float *)n->data, ycs, K, N, M);
-    return 0;
-}
-
-static bool is_view_op(int op) {
-    return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
-}
-
-extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
-    if (!be) return TTS_STATUS_BAD_ARG;
-    hipSetDevice(be->device);
-    be->graph_epoch++;
-    for (int i = 0; i < n_nodes; ++i) {
-        tts_tensor * n = nodes[i];
-        if (is_view_op(n->op)) continue;
-        if (be->fusion) {
-            int consumed = 0;
-            int st = launch_fused(be, nodes, n_nodes, i, &consumed);
-            if (st != 0) return st;
-            if (consumed > 0) {
-                i += consumed - 1;
-                continue;
-            }
-        }
-        int st;
-        if (n->op == TTS_OP_MUL_MAT) st = compute_mul_mat(be, n);
-        else st = launch_op(be, n);
-        if (st != 0) {
-            fprintf(stderr, "tts_hip_graph_compute: node %d (%s, %s) failed: %d\n", i, n->name, tts_op_name(n->op), st);
-            return st;
-        }
-        // any write into a buffer that the cached activation quantization was built from
-        // invalidates it (the cache is keyed by src pointer within this graph)
-        if (be->aq.src && n->data == be->aq.src) be->aq.src = nullptr;
-    }
-    return 0;
-}
-
 extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
     if (!be) return TTS_STATUS_BAD_ARG;
     switch (option) {
-        case TTS_HIP_OPT_FUSION: be->fusion = value != 0; return 0;
+        case TTS_HIP_OPT_FUSION: be->fusion = value; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }
@@ -361,26 +258,6 @@ extern "C" int tts_hip_gemv_stats(tts_hip_backend_t be, int type, double * ms, i
             be->gemv_bytes[ty] = 0;
         }
     }
-    return 0;
-}
-
-extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
-                            int64_t M) {
-    if (!be) return TTS_STATUS_BAD_ARG;
-    if (type == TTS_TYPE_Q4_K && K % 256) return TTS_STATUS_BAD_ARG;
-    if (type == TTS_TYPE_Q8_0 && K % 32) return TTS_STATUS_BAD_ARG;
-    if (type != TTS_TYPE_Q4_K && type != TTS_TYPE_Q8_0 && type != TTS_TYPE_F16 && type != TTS_TYPE_F32) return TTS_STATUS_UNSUPPORTED;
-    if ((type == TTS_TYPE_F32 || type == TTS_TYPE_F16) && K % 4) return TTS_STATUS_BAD_ARG;
-    hipSetDevice(be->device);
-    ActQuant aq;
-    if (type != TTS_TYPE_F32) {
-        if (act_quant_bytes(type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
-        launch_quantize_act(be, type, x, K, K, M, aq);
-    } else {
-        aq.vtype = TTS_TYPE_F32;
-    }
-    be->aq.src = nullptr;  // scratch overwritten
-    launch_gemv(be, type, w, (int64_t)tts_row_size(type, K), x, K, &aq, y, N, K, N, M);
     return 0;
 }
 

@@ -410,7 +410,7 @@ struct FreeList {
 };
 }  // namespace
 
-bool alloc_graph(context & c, char * arena_base, size_t arena_size) {
+bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) {
     FreeList fl;
     fl.cap = arena_size;
     std::unordered_map<tts_tensor *, size_t> offs;
@@ -458,7 +458,7 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size) {
             tts_tensor * b = x->view_src ? x->view_src : x;
             auto it = offs.find(b);
             if (it == offs.end()) continue;
-            if (last_use[b] == i && !(b->flags & (TG_FLAG_OUTPUT | TG_FLAG_INPUT)) && b->op != TTS_OP_NONE) {
+            if (reuse && last_use[b] == i && !(b->flags & (TG_FLAG_OUTPUT | TG_FLAG_INPUT)) && b->op != TTS_OP_NONE) {
                 fl.release(it->second, nbytes(b));
                 offs.erase(it);
             }

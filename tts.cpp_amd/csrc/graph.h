@@ -95,6 +95,6 @@ void build_forward_expand(context & c, tts_tensor * t);
 // ggml-gallocr equivalent: assigns data to every non-view tensor without data from an arena of
 // `arena_size` bytes at `arena_base` (device or host pointer; never dereferenced), reusing
 // memory after a tensor's last use.  Returns false if the arena is too small.
-bool alloc_graph(context & c, char * arena_base, size_t arena_size);
+bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse = true);
 
 }  // namespace tg

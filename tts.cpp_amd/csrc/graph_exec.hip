@@ -1,0 +1,608 @@
+// graph_compute: plans and executes a ggml-style node list on one HIP stream
+// (ggml_backend_i::graph_compute underneath ggml_backend_sched_graph_compute_async,
+// /root/reference/src/models/parler/model.cpp:645).
+//
+// Planning pass (per call): consumer counts per tensor, then pattern fusion, each fused kernel
+// reproducing the unfused ops bit-for-bit (see k_fused.hip / k_gemv.hip):
+//   LN   : NORM -> MUL(w) -> ADD(b)  [-> Q8_K copy for the GEMVs that read it]
+//   GEMV : adjacent MUL_MATs sharing src1 (q/k/v) in one launch; K / V outputs written straight
+//          into the KV-cache views their CPY nodes target (parler_build_kv_store); adjacent
+//          ADD(residual) or GELU consumer folded into the epilogue
+//   HEADS: MUL_MAT_i chained by CONCAT(dim 1) (parler_build_head_outputs) -> one launch writing
+//          each head's rows at its concat offset
+//   ATTN : cont(K)/cont(q) -> MUL_MAT -> SOFT_MAX -> MUL_MAT(V) -> PERMUTE -> CONT
+// A pattern fuses only when every intermediate tensor has a single consumer inside the group
+// and the fused output does not overlap an input it reads (the graph arrives already
+// allocated, so aliasing is checked on the real addresses).
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "hip_internal.h"
+
+using namespace tts;
+
+namespace tts {
+void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
+                        float * out, int hd, int P, int H, int n, int B);
+void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
+                      float eps, bool rms, ActQuant * aq);
+}  // namespace tts
+
+namespace {
+
+size_t tbytes(const tts_tensor * t) {
+    size_t n = tts_type_size(t->type);
+    const int64_t bs = tts_blck_size(t->type);
+    if (bs == 1) {
+        for (int i = 0; i < 4; ++i) n += (size_t)(t->ne[i] - 1) * t->nb[i];
+    } else {
+        n = (size_t)(t->ne[0] / bs) * t->nb[0];
+        for (int i = 1; i < 4; ++i) n += (size_t)(t->ne[i] - 1) * t->nb[i];
+    }
+    return n;
+}
+
+bool overlap(const tts_tensor * a, const tts_tensor * b) {
+    if (!a || !b || !a->data || !b->data) return false;
+    const char * a0 = (const char *)a->data;
+    const char * b0 = (const char *)b->data;
+    return a0 < b0 + tbytes(b) && b0 < a0 + tbytes(a);
+}
+
+bool is_view(int op) {
+    return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
+}
+
+bool contiguous(const tts_tensor * t) {
+    const size_t es = tts_type_size(t->type);
+    return t->nb[0] == es && t->nb[1] == t->nb[0] * (size_t)(t->ne[0] / tts_blck_size(t->type)) &&
+           t->nb[2] == t->nb[1] * (size_t)t->ne[1] && t->nb[3] == t->nb[2] * (size_t)t->ne[2];
+}
+
+bool is_1d_f32(const tts_tensor * t, int64_t n) {
+    return t->type == TTS_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 && t->nb[0] == 4;
+}
+
+float opf(const tts_tensor * t, int i) {
+    float f;
+    memcpy(&f, &t->op_params[i], 4);
+    return f;
+}
+
+// MUL_MAT with a 2-D weight matrix and evenly strided f32 columns: the decode GEMV.
+bool is_gemv(const tts_tensor * n) {
+    const tts_tensor * a = n->src[0];
+    const tts_tensor * b = n->src[1];
+    if (a->ne[2] != 1 || a->ne[3] != 1) return false;
+    if (b->type != TTS_TYPE_F32 || b->nb[0] != 4) return false;
+    if (b->ne[2] * b->ne[3] != 1 && !(b->nb[2] == b->nb[1] * (size_t)b->ne[1] && b->nb[3] == b->nb[2] * (size_t)b->ne[2]))
+        return false;
+    if (n->nb[0] != 4 || (n->ne[2] * n->ne[3] != 1 && !(n->nb[2] == n->nb[1] * (size_t)n->ne[1] && n->nb[3] == n->nb[2] * (size_t)n->ne[2])))
+        return false;
+    if (a->nb[0] != tts_type_size(a->type)) return false;
+    switch (a->type) {
+        case TTS_TYPE_Q4_K: return a->ne[0] % 256 == 0;
+        case TTS_TYPE_Q8_0: return a->ne[0] % 32 == 0;
+        case TTS_TYPE_F32:
+        case TTS_TYPE_F16: return a->ne[0] % 4 == 0 && (b->nb[1] % 16) == 0 && ((uintptr_t)b->data % 16) == 0;
+        default: return false;
+    }
+}
+
+struct GemvTarget {
+    float * y;
+    int64_t ycs, yrs;
+};
+
+struct Item {
+    enum Kind { GEMV, ATTN, LN } kind;
+    // GEMV
+    std::vector<const tts_tensor *> mms;
+    std::vector<GemvTarget> tgt;
+    int epi = EPI_NONE;
+    const tts_tensor * res = nullptr;
+    // ATTN
+    const tts_tensor *q = nullptr, *k = nullptr, *v = nullptr, *mask = nullptr, *out = nullptr;
+    float scale = 1.f;
+    // LN
+    const tts_tensor *x = nullptr, *w = nullptr, *b = nullptr, *dst = nullptr;
+    float eps = 0.f;
+    bool rms = false;
+    bool quant = false;
+};
+
+struct Planner {
+    tts_tensor * const * nodes;
+    int n;
+    std::unordered_map<const tts_tensor *, int> uses;
+    std::unordered_map<const tts_tensor *, int> index;
+    std::unordered_map<const tts_tensor *, std::vector<int>> consumers;
+    std::vector<int> act;  // -1 skip, 0 run node, k>0 run items[k-1]
+    std::vector<Item> items;
+    int mask = 0xFF;
+
+    const tts_tensor * sole_consumer(const tts_tensor * t) {
+        auto it = consumers.find(t);
+        if (it == consumers.end() || it->second.size() != 1 || uses[t] != 1) return nullptr;
+        return nodes[it->second[0]];
+    }
+    // next non-view node index after i (views allocate nothing)
+    int next_real(int i) {
+        for (int j = i + 1; j < n; ++j)
+            if (!is_view(nodes[j]->op)) return j;
+        return -1;
+    }
+
+    void build(tts_tensor * const * nodes_, int n_) {
+        nodes = nodes_;
+        n = n_;
+        act.assign(n, 0);
+        for (int i = 0; i < n; ++i) {
+            index[nodes[i]] = i;
+            for (int s = 0; s < TTS_MAX_SRC; ++s) {
+                const tts_tensor * x = nodes[i]->src[s];
+                if (!x) continue;
+                // a node listing the same source twice counts once
+                bool dup = false;
+                for (int s2 = 0; s2 < s; ++s2) dup |= nodes[i]->src[s2] == x;
+                if (dup) continue;
+                uses[x]++;
+                consumers[x].push_back(i);
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            if (act[i] != 0) continue;
+            const tts_tensor * t = nodes[i];
+            switch (t->op) {
+                case TTS_OP_NORM:
+                case TTS_OP_RMS_NORM: if (mask & TTS_FUSE_LN) try_ln(i); break;
+                case TTS_OP_SOFT_MAX: if (mask & TTS_FUSE_ATTN) try_attn(i); break;
+                case TTS_OP_MUL_MAT:
+                    if (!((mask & TTS_FUSE_HEADS) && try_heads(i)) && (mask & (TTS_FUSE_GROUP | TTS_FUSE_KV | TTS_FUSE_EPI))) try_gemv(i);
+                    break;
+                default: break;
+            }
+        }
+    }
+
+    int add_item(Item && it) {
+        items.push_back(std::move(it));
+        return (int)items.size();
+    }
+
+    void try_ln(int i) {
+        const tts_tensor * N = nodes[i];
+        const tts_tensor * x = N->src[0];
+        if (x->type != TTS_TYPE_F32 || x->nb[0] != 4 || x->ne[0] > 8192) return;
+        const int64_t ne0 = x->ne[0];
+        const tts_tensor * M = sole_consumer(N);
+        if (!M || M->op != TTS_OP_MUL || M->src[0] != N || !is_1d_f32(M->src[1], ne0)) return;
+        if (next_real(i) != index[M]) return;
+        const tts_tensor * A = nullptr;
+        if (N->op == TTS_OP_NORM) {
+            A = sole_consumer(M);
+            if (!A || A->op != TTS_OP_ADD || A->src[0] != M || !is_1d_f32(A->src[1], ne0)) return;
+            if (next_real(index[M]) != index[A]) return;
+        } else {
+            A = M;
+        }
+        if (!contiguous(A) || A->type != TTS_TYPE_F32 || !contiguous(x)) return;
+        if (overlap(A, x) && A->data != x->data) return;  // exact in-place is safe (per-row read-then-write)
+        Item it;
+        it.kind = Item::LN;
+        it.x = x;
+        it.w = M->src[1];
+        it.b = N->op == TTS_OP_NORM ? A->src[1] : nullptr;
+        it.dst = A;
+        it.eps = opf(N, 0);
+        it.rms = N->op == TTS_OP_RMS_NORM;
+        // quantize in-kernel when the output feeds Q4_K GEMVs only as src1
+        bool q = ne0 % 256 == 0;
+        auto itc = consumers.find(A);
+        int n_q4 = 0;
+        if (itc != consumers.end()) {
+            for (int c : itc->second) {
+                const tts_tensor * cn = nodes[c];
+                if (cn->op == TTS_OP_MUL_MAT && cn->src[1] == A && cn->src[0]->type == TTS_TYPE_Q4_K) n_q4++;
+            }
+        }
+        it.quant = q && n_q4 > 0;
+        act[i] = -1;
+        if (A != M) act[index[M]] = -1;
+        act[index[A]] = add_item(std::move(it));
+    }
+
+    // KV-store fusion: the GEMV output goes straight into the CPY destination (decode, 1 token).
+    bool kv_target(const tts_tensor * mm, int64_t M, GemvTarget & t, std::vector<int> & skips) {
+        const tts_tensor * c = sole_consumer(mm);
+        if (!c) return false;
+        const int64_t N = mm->ne[0];
+        if (mm->ne[1] != 1 && M != 1) return false;  // one token per column (decode)
+        if (c->op == TTS_OP_CPY && c->src[0] == mm) {
+            const tts_tensor * D = c;  // view of the K cache: [N] or [N, B] with row stride per sequence
+            if (D->type != TTS_TYPE_F32 || D->nb[0] != 4 || D->ne[0] != N || D->ne[1] != M || D->ne[2] * D->ne[3] != 1) return false;
+            t.y = (float *)D->data;
+            t.yrs = 1;
+            t.ycs = (int64_t)(D->nb[1] / 4);
+            skips.push_back(index[c]);
+            return true;
+        }
+        // mm -> [RESHAPE] -> TRANSPOSE -> CONT -> CPY
+        const tts_tensor * v = c;
+        std::vector<int> vs;
+        while (v && (v->op == TTS_OP_RESHAPE || v->op == TTS_OP_TRANSPOSE) && v->src[0]) {
+            vs.push_back(index[v]);
+            const tts_tensor * nx = sole_consumer(v);
+            if (!nx) return false;
+            if (nx->op == TTS_OP_CONT) {
+                const tts_tensor * C = nx;
+                const tts_tensor * cp = sole_consumer(C);
+                if (!cp || cp->op != TTS_OP_CPY || cp->src[0] != C) return false;
+                const tts_tensor * D = cp;
+                if (D->type != TTS_TYPE_F32 || D->ne[0] != 1 || D->ne[1] != N || D->ne[2] * D->ne[3] != M) return false;
+                t.y = (float *)D->data;
+                t.yrs = (int64_t)(D->nb[1] / 4);
+                t.ycs = (int64_t)(D->nb[2] / 4);
+                skips.push_back(index[C]);
+                skips.push_back(index[cp]);
+                return true;
+            }
+            v = nx;
+        }
+        return false;
+    }
+
+    void try_gemv(int i) {
+        const tts_tensor * mm0 = nodes[i];
+        if (!is_gemv(mm0)) return;
+        const tts_tensor * a0 = mm0->src[0];
+        const tts_tensor * x = mm0->src[1];
+        const int64_t M = x->ne[1] * x->ne[2] * x->ne[3];
+        Item it;
+        it.kind = Item::GEMV;
+        std::vector<int> skips;
+        // group adjacent MUL_MATs sharing src1 and weight type/shape
+        int j = i;
+        while (j < n && (int)it.mms.size() < ((mask & TTS_FUSE_GROUP) ? GEMV_MAX_MATS : 1)) {
+            const tts_tensor * mm = nodes[j];
+            if (mm->op != TTS_OP_MUL_MAT || mm->src[1] != x || !is_gemv(mm)) break;
+            const tts_tensor * a = mm->src[0];
+            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->ne[1] != a0->ne[1] || a->nb[1] != a0->nb[1]) break;
+            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & TTS_FLAG_REPACKED)) break;
+            GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
+            GemvTarget kt;
+            std::vector<int> ks;
+            if ((mask & TTS_FUSE_KV) && mm->ne[1] * mm->ne[2] * mm->ne[3] == M && kv_target(mm, M, kt, ks)) {
+                t = kt;
+                for (int s : ks) skips.push_back(s);
+            }
+            it.mms.push_back(mm);
+            it.tgt.push_back(t);
+            if (j > i) act[j] = -1;
+            ++j;
+        }
+        if (it.mms.size() == 1 && (mask & TTS_FUSE_EPI)) {
+            // epilogue: adjacent GELU or ADD(residual) consuming the single product
+            const tts_tensor * E = sole_consumer(mm0);
+            if (E && next_real(i) == index[E] && E->src[0] == mm0 && E->type == TTS_TYPE_F32 && contiguous(E) && contiguous(mm0)) {
+                if (E->op == TTS_OP_UNARY && E->op_params[0] == TTS_UNARY_GELU) {
+                    it.epi = EPI_GELU;
+                } else if (E->op == TTS_OP_ADD && E->src[1]->type == TTS_TYPE_F32 && contiguous(E->src[1]) &&
+                           E->src[1]->ne[0] == E->ne[0] && E->src[1]->ne[1] == E->ne[1] && E->src[1]->ne[2] == E->ne[2] &&
+                           E->src[1]->ne[3] == E->ne[3] && (!overlap(E, E->src[1]) || E->data == E->src[1]->data)) {
+                    it.epi = EPI_ADD;
+                    it.res = E->src[1];
+                }
+                if (it.epi != EPI_NONE && (a0->type != TTS_TYPE_F32 || !overlap(E, x))) {
+                    it.tgt[0] = GemvTarget{(float *)E->data, (int64_t)(E->nb[1] / 4), 1};
+                    act[index[E]] = -1;
+                } else {
+                    it.epi = EPI_NONE;
+                    it.res = nullptr;
+                }
+            }
+        }
+        for (int s : skips) act[s] = -1;
+        act[i] = add_item(std::move(it));
+    }
+
+    bool try_heads(int i) {
+        const tts_tensor * mm0 = nodes[i];
+        if (!is_gemv(mm0)) return false;
+        const tts_tensor * x = mm0->src[1];
+        const tts_tensor * a0 = mm0->src[0];
+        const tts_tensor * C = sole_consumer(mm0);
+        if (!C || C->op != TTS_OP_CONCAT || C->op_params[0] != 1 || C->src[0] != mm0) return false;
+        Item it;
+        it.kind = Item::GEMV;
+        it.mms.push_back(mm0);
+        std::vector<int> members{i};
+        const tts_tensor * last = nullptr;
+        while (C && C->op == TTS_OP_CONCAT && C->op_params[0] == 1 && (int)it.mms.size() < GEMV_MAX_MATS) {
+            const tts_tensor * mm = C->src[1];
+            if (!mm || mm->op != TTS_OP_MUL_MAT || mm->src[1] != x || !is_gemv(mm) || uses[mm] != 1) return false;
+            const tts_tensor * a = mm->src[0];
+            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->ne[1] != a0->ne[1] || a->nb[1] != a0->nb[1]) return false;
+            if (mm->ne[1] != mm0->ne[1] || mm->ne[2] != mm0->ne[2]) return false;
+            it.mms.push_back(mm);
+            members.push_back(index[mm]);
+            members.push_back(index[C]);
+            last = C;
+            const tts_tensor * nx = sole_consumer(C);
+            if (nx && nx->op == TTS_OP_CONCAT && nx->src[0] == C) C = nx;
+            else C = nullptr;
+        }
+        if (!last || !contiguous(last) || overlap(last, x)) return false;
+        const int64_t n1 = mm0->ne[1], n2 = mm0->ne[2];
+        int64_t ycs;
+        if (n1 == 1) ycs = (int64_t)(last->nb[2] / 4);
+        else if (n2 == 1) ycs = (int64_t)(last->nb[1] / 4);
+        else return false;
+        for (size_t k = 0; k < it.mms.size(); ++k)
+            it.tgt.push_back(GemvTarget{(float *)((char *)last->data + k * n1 * last->nb[1]), ycs, 1});
+        for (int m : members) act[m] = -1;
+        act[index[last]] = add_item(std::move(it));
+        return true;
+    }
+
+    void try_attn(int i) {
+        const tts_tensor * S = nodes[i];
+        const tts_tensor * KQ = S->src[0];
+        const tts_tensor * mask = S->src[1];
+        if (!KQ || KQ->op != TTS_OP_MUL_MAT || uses[KQ] != 1) return;
+        if (opf(S, 1) != 0.0f) return;  // ALiBi not used by TTS graphs
+        const tts_tensor * KQV = sole_consumer(S);
+        if (!KQV || KQV->op != TTS_OP_MUL_MAT || KQV->src[0] != S) return;
+        const tts_tensor * PERM = sole_consumer(KQV);
+        if (!PERM || PERM->op != TTS_OP_PERMUTE || PERM->op_params[0] != 2 || PERM->op_params[1] != 0 || PERM->op_params[2] != 1 ||
+            PERM->op_params[3] != 3)
+            return;
+        const tts_tensor * O = sole_consumer(PERM);
+        if (!O || O->op != TTS_OP_CONT || !contiguous(O) || O->type != TTS_TYPE_F32) return;
+        const tts_tensor * Ka = KQ->src[0];
+        const tts_tensor * Qa = KQ->src[1];
+        const tts_tensor * V = KQV->src[1];
+        const tts_tensor * K = Ka;
+        int skip_k = -1, skip_q = -1;
+        if (Ka->op == TTS_OP_CONT && uses[Ka] == 1) {
+            K = Ka->src[0];
+            skip_k = index[Ka];
+        }
+        const tts_tensor * Q = Qa;
+        if (Qa->op == TTS_OP_CONT && uses[Qa] == 1) {
+            Q = Qa->src[0];
+            skip_q = index[Qa];
+        }
+        if (K->type != TTS_TYPE_F32 || Q->type != TTS_TYPE_F32 || V->type != TTS_TYPE_F32) return;
+        const int64_t hd = Q->ne[0], P = K->ne[1];
+        if (K->ne[0] != hd || hd % 4 || hd > 256 || P > 8192 || S->ne[0] != P || V->ne[0] != P || V->ne[1] != hd) return;
+        if (Q->nb[0] != 4 || K->nb[0] != 4 || V->nb[0] != 4) return;
+        const int64_t H = Q->ne[2], nq = Q->ne[1], B = Q->ne[3];
+        if (H % K->ne[2] || B % K->ne[3] || H % V->ne[2] || B % V->ne[3]) return;
+        if (V->ne[2] != H || V->ne[3] != B) return;  // kqv = mul_mat(kq, V): V carries the batch dims
+        if (mask && (mask->type != TTS_TYPE_F32 || !contiguous(mask) || mask->ne[0] < P)) return;
+        if (mask && mask->ne[0] != P) return;  // ggml reads mask rows with stride ne00 == P
+        if (nq * H * B * hd != O->ne[0] * O->ne[1] * O->ne[2] * O->ne[3]) return;
+        // aliasing: O may coincide exactly with Q's storage (read-before-write per workgroup), nothing else
+        const tts_tensor * Qbase = Q->view_src ? Q->view_src : Q;
+        if (overlap(O, K) || overlap(O, V) || (mask && overlap(O, mask))) return;
+        if (overlap(O, Qbase) && O->data != Qbase->data) return;
+        Item it;
+        it.kind = Item::ATTN;
+        it.q = Q;
+        it.k = K;
+        it.v = V;
+        it.mask = mask;
+        it.out = O;
+        it.scale = opf(S, 0);
+        act[i] = -1;
+        act[index[KQ]] = -1;
+        act[index[KQV]] = -1;
+        if (skip_k >= 0) act[skip_k] = -1;
+        if (skip_q >= 0) act[skip_q] = -1;
+        act[index[O]] = add_item(std::move(it));
+    }
+};
+
+}  // namespace
+
+// ---- activation preparation (cached per graph by src pointer) ----
+static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, int64_t K, int64_t M, ActQuant & out) {
+    ActQuant & aq = be->aq;
+    const int64_t xcs = (int64_t)(b->nb[1] / 4);
+    if (wtype == TTS_TYPE_F32) {
+        out = ActQuant();
+        out.vtype = TTS_TYPE_F32;
+        return 0;
+    }
+    const int vt = wtype == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : wtype;
+    const bool hit = aq.src == b->data && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
+    if (!hit) {
+        if (act_quant_bytes(wtype, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+        launch_quantize_act(be, wtype, (const float *)b->data, xcs, K, M, aq);
+        aq.src = b->data;
+        aq.graph_epoch = be->graph_epoch;
+    }
+    out = aq;
+    return 0;
+}
+
+static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a) {
+    if (a->type != TTS_TYPE_Q4_K || (a->flags & TTS_FLAG_REPACKED)) return a->data;
+    // Q4_K matrix written with plain tensor_set (native ggml layout): repack into a temp
+    const size_t bytes = (size_t)a->nb[1] * (size_t)a->ne[1];
+    if (be->repack_tmp_size < bytes) {
+        if (be->repack_tmp) {
+            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+            TTS_HIP_CHECK(hipFree(be->repack_tmp));
+        }
+        TTS_HIP_CHECK(hipMalloc((void **)&be->repack_tmp, bytes));
+        be->repack_tmp_size = bytes;
+    }
+    launch_repack_q4_K(be, a->data, be->repack_tmp, (int64_t)(bytes / 144), 0);
+    return be->repack_tmp;
+}
+
+static int run_gemv_item(tts_hip_backend * be, const Item & it) {
+    const tts_tensor * mm0 = it.mms[0];
+    const tts_tensor * a0 = mm0->src[0];
+    const tts_tensor * b = mm0->src[1];
+    GemvJob j;
+    j.wtype = a0->type;
+    j.K = a0->ne[0];
+    j.N = a0->ne[1];
+    j.M = b->ne[1] * b->ne[2] * b->ne[3];
+    j.w_row_bytes = (int64_t)a0->nb[1];
+    j.x = (const float *)b->data;
+    j.xcs = (int64_t)(b->nb[1] / 4);
+    j.epi = it.epi;
+    j.gelu = be->gelu_table;
+    if (it.res) {
+        j.res = (const float *)it.res->data;
+        j.rcs = (int64_t)(it.res->nb[1] / 4);
+    }
+    int st = prepare_act(be, j.wtype, b, j.K, j.M, j.aq);
+    if (st) return st;
+    // a Q4_K matrix in native layout goes through the one-matrix repack temp: launch it alone
+    const bool tmp = a0->type == TTS_TYPE_Q4_K && !(a0->flags & TTS_FLAG_REPACKED);
+    size_t k = 0;
+    while (k < it.mms.size()) {
+        GemvJob jj = j;
+        jj.nmat = 0;
+        while (k < it.mms.size() && jj.nmat < GEMV_MAX_MATS) {
+            jj.W[jj.nmat] = (const uint8_t *)weight_ptr(be, it.mms[k]->src[0]);
+            jj.Y[jj.nmat] = it.tgt[k].y;
+            jj.ycs[jj.nmat] = it.tgt[k].ycs;
+            jj.yrs[jj.nmat] = it.tgt[k].yrs;
+            jj.nmat++;
+            k++;
+            if (tmp) break;
+        }
+        launch_gemv_job(be, jj);
+    }
+    return 0;
+}
+
+static int run_node(tts_hip_backend * be, const tts_tensor * n) {
+    if (n->op == TTS_OP_MUL_MAT) {
+        if (is_gemv(n)) {
+            Item it;
+            it.kind = Item::GEMV;
+            it.mms.push_back(n);
+            it.tgt.push_back(GemvTarget{(float *)n->data, (int64_t)(n->nb[1] / 4), 1});
+            return run_gemv_item(be, it);
+        }
+        const int t = n->src[0]->type;
+        if (t == TTS_TYPE_F32 || t == TTS_TYPE_F16) return launch_op(be, n);
+        return TTS_STATUS_UNSUPPORTED;
+    }
+    return launch_op(be, n);
+}
+
+static int run_item(tts_hip_backend * be, const Item & it) {
+    switch (it.kind) {
+        case Item::GEMV: return run_gemv_item(be, it);
+        case Item::ATTN: {
+            const TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
+            launch_attn_decode(be, q, k, v, it.mask ? (const float *)it.mask->data : nullptr, it.scale, (float *)it.out->data,
+                               (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3]);
+            return 0;
+        }
+        case Item::LN: {
+            ActQuant * aqp = nullptr;
+            const int64_t K = it.dst->ne[0];
+            const int64_t M = it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3];
+            if (it.quant && act_quant_bytes(TTS_TYPE_Q4_K, K, M) <= be->scratch_size) {
+                act_quant_layout(TTS_TYPE_Q4_K, be->scratch, K, M, be->aq);
+                be->aq.src = it.dst->data;
+                be->aq.graph_epoch = be->graph_epoch;
+                aqp = &be->aq;
+            }
+            launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms,
+                             aqp);
+            return 0;
+        }
+    }
+    return TTS_STATUS_FAILED;
+}
+
+extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    be->graph_epoch++;
+    be->aq.src = nullptr;
+    Planner pl;
+    pl.mask = be->fusion;
+    if (be->fusion) pl.build(nodes, n_nodes);
+    for (int i = 0; i < n_nodes; ++i) {
+        tts_tensor * n = nodes[i];
+        const int a = be->fusion ? pl.act[i] : 0;
+        if (a < 0) continue;
+        if (a == 0 && is_view(n->op)) continue;
+        const int st = a > 0 ? run_item(be, pl.items[a - 1]) : run_node(be, n);
+        if (st != 0) {
+            fprintf(stderr, "tts_hip_graph_compute: node %d (%s, %s) failed: %d\n", i, n->name, tts_op_name(n->op), st);
+            return st;
+        }
+        // The Q8_K activation cache is keyed by address and the graph reuses freed memory, so it
+        // survives only launches that cannot have written over the cached source: an LN that
+        // just produced it, or GEMVs whose outputs do not overlap it.
+        if (be->aq.src) {
+            const char * s0 = (const char *)be->aq.src;
+            const char * s1 = s0 + (size_t)be->aq.K * (size_t)be->aq.M * 4;
+            bool keep = false;
+            if (a > 0) {
+                const Item & it = pl.items[a - 1];
+                if (it.kind == Item::LN) {
+                    keep = it.quant && it.dst->data == be->aq.src;
+                } else if (it.kind == Item::GEMV) {
+                    keep = true;
+                    for (size_t k = 0; k < it.tgt.size(); ++k) {
+                        const char * y0 = (const char *)it.tgt[k].y;
+                        const tts_tensor * mm = it.mms[k];
+                        const int64_t Mm = mm->ne[1] * mm->ne[2] * mm->ne[3];
+                        const char * y1 = y0 + 4 * (size_t)((Mm - 1) * it.tgt[k].ycs + (mm->ne[0] - 1) * it.tgt[k].yrs + 1);
+                        if (y0 < s1 && s0 < y1) keep = false;
+                    }
+                }
+            } else if (n->op == TTS_OP_MUL_MAT) {
+                const char * y0 = (const char *)n->data;
+                keep = !(y0 < s1 && s0 < y0 + tbytes(n));
+            }
+            if (!keep) be->aq.src = nullptr;
+        }
+    }
+    return 0;
+}
+
+extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
+                            int64_t M) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    if (type == TTS_TYPE_Q4_K && K % 256) return TTS_STATUS_BAD_ARG;
+    if (type == TTS_TYPE_Q8_0 && K % 32) return TTS_STATUS_BAD_ARG;
+    if (type != TTS_TYPE_Q4_K && type != TTS_TYPE_Q8_0 && type != TTS_TYPE_F16 && type != TTS_TYPE_F32) return TTS_STATUS_UNSUPPORTED;
+    if ((type == TTS_TYPE_F32 || type == TTS_TYPE_F16) && K % 4) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    GemvJob j;
+    j.wtype = type;
+    j.K = K;
+    j.N = N;
+    j.M = M;
+    j.w_row_bytes = (int64_t)tts_row_size(type, K);
+    j.W[0] = (const uint8_t *)w;
+    j.Y[0] = y;
+    j.ycs[0] = N;
+    j.yrs[0] = 1;
+    j.x = x;
+    j.xcs = K;
+    if (type != TTS_TYPE_F32) {
+        if (act_quant_bytes(type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+        launch_quantize_act(be, type, x, K, K, M, j.aq);
+    } else {
+        j.aq.vtype = TTS_TYPE_F32;
+    }
+    be->aq.src = nullptr;  // scratch overwritten
+    launch_gemv_job(be, j);
+    return 0;
+}

@@ -41,6 +41,10 @@ __device__ __forceinline__ float cr_expf(float x) { return (float)exp((double)x)
 __device__ __forceinline__ float cr_sinf(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float cr_cosf(float x) { return (float)cos((double)x); }
 __device__ __forceinline__ float cr_tanhf(float x) { return (float)tanh((double)x); }
+// IEEE-exact f32 sqrt / division (gfx950's f32 sqrt lowering is not correctly rounded); the f64
+// result rounded to f32 is the correctly rounded f32 value (53 >= 2*24 + 2).
+__device__ __forceinline__ float cr_sqrtf(float x) { return (float)__dsqrt_rn((double)x); }
+__device__ __forceinline__ float cr_divf(float a, float b) { return (float)__ddiv_rn((double)a, (double)b); }
 #endif
 
 inline TD make_td(const tts_tensor * t) {
@@ -63,7 +67,28 @@ struct ActQuant {
     int64_t graph_epoch = -1;
     int8_t * qs = nullptr;      // [M][K] int8 (Q8_K / Q8_0) or fp16 [M][K] (F16)
     float * d = nullptr;        // [M][K/256] (Q8_K) or [M][K/32] (Q8_0: fp16-rounded d as float)
-    int32_t * bsums = nullptr;  // [M][K/16] (Q8_K)
+    int32_t * bsums = nullptr;  // [M][K/256][8] per-32 sums (Q8_K)
+};
+
+// One GEMV launch: up to GEMV_MAX_MATS weight matrices of identical type/shape sharing one
+// activation (q/k/v; the 9 codebook heads), y(row n, column m) = Y[i][m*ycs + n*yrs], with an
+// optional fused epilogue (GELU table, or + residual(row n, column m) = res[m*rcs + n]).
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_ADD = 2 };
+constexpr int GEMV_MAX_MATS = 16;
+struct GemvJob {
+    int wtype = 0;
+    int nmat = 1;
+    const uint8_t * W[GEMV_MAX_MATS] = {};
+    float * Y[GEMV_MAX_MATS] = {};
+    int64_t w_row_bytes = 0, K = 0, N = 0, M = 0;
+    int64_t ycs[GEMV_MAX_MATS] = {}, yrs[GEMV_MAX_MATS] = {};  // per-matrix output strides
+    const float * res = nullptr;
+    int64_t rcs = 0;
+    int epi = EPI_NONE;
+    const uint16_t * gelu = nullptr;
+    const float * x = nullptr;  // f32 activation (F32 weights)
+    int64_t xcs = 0;
+    ActQuant aq;
 };
 
 }  // namespace tts
@@ -78,7 +103,7 @@ struct tts_hip_backend {
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
-    bool fusion = true;
+    int fusion = 0xFF;  // bitmask of TTS_FUSE_* patterns
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -96,10 +121,10 @@ namespace tts {
 // ---- launchers (k_gemv.hip) ----
 // Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
-// y[m*ycs + n] = dot(W row n, x column m)
-void launch_gemv(tts_hip_backend * be, int wtype, const void * w, int64_t w_row_bytes, const float * x, int64_t xcs,
-                 const ActQuant * aq, float * y, int64_t ycs, int64_t K, int64_t N, int64_t M);
+void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
+// carve an ActQuant layout for weight type `wtype` out of `base` (no launch)
+void act_quant_layout(int wtype, char * base, int64_t K, int64_t M, ActQuant & aq);
 
 void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int64_t nblocks, int inverse);
 

@@ -1,16 +1,284 @@
-// Pattern fusion inside graph_compute.  Returns the number of graph nodes a
-// fused kernel replaced (0 = no pattern at node i).
+// Fused kernels that replace ggml node groups inside graph_compute.
+// Each reproduces the unfused ops' arithmetic exactly (same f32 operations, f64 where ggml-cpu
+// accumulates in ggml_float), so fusion never changes a result bit:
+//
+//  k_attn_decode : cont(K view) -> mul_mat(K, q) -> soft_max_ext(mask, scale) -> mul_mat(kq, V)
+//                  -> permute(2,0,1,3) -> cont        (Parler model.cpp:549-571, 583-594)
+//                  K and V are read in place through their cache views: the reference's per-step
+//                  `cont` copy of K (O(P*d) per layer per step) disappears.
+//  k_layernorm   : norm(eps) -> mul(w) -> add(b)      (parler_build_layer_norm, model.cpp:412-418)
+//                  with an optional Q8_K copy of the output for the GEMVs that consume it.
 #include "hip_internal.h"
 
 namespace tts {
 
-int launch_fused(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes, int i, int * consumed) {
-    (void)be;
-    (void)nodes;
-    (void)n_nodes;
-    (void)i;
-    *consumed = 0;
-    return 0;
+// ------------------------------------------------------------------------------------------
+// Decode attention, one workgroup per (head h, query t, sequence b).
+struct AttnArgs {
+    TD q;      // [hd, n, H, B]   (the permute view feeding ggml's cont(q))
+    TD k;      // [hd, P, Hk, Bk] (K view of the cache, or cross_k)
+    TD v;      // [P, hd, Hv, Bv] (V view of the cache, or cross_v)
+    const float * mask;  // [rows >= n][P] f32, row stride P (ggml soft_max broadcast), or null
+    float scale;
+    float * out;         // [hd, H, n, B] contiguous
+    int hd, P, H, n, B;
+};
+
+constexpr int ATTN_THREADS = 256;
+constexpr int ATTN_MAXP = 8192;
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
+    __shared__ float s_p[ATTN_MAXP];
+    __shared__ double s_red[ATTN_THREADS / 64];
+    __shared__ float s_redf[ATTN_THREADS / 64];
+    const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = a.P, hd = a.hd;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const char * qbase = a.q.data + t * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+
+    // ---- phase A: kq[i] = sum_d (f32)(K[d,i] * q[d]), f64 accumulation (ggml_vec_dot_f32) ----
+    // G lanes per position, each owning hd/G contiguous dims (4 when hd = 4G).
+    const int G = hd / 4 <= 64 ? hd / 4 : 64;  // hd = 64 -> 16 lanes, 128 -> 32 lanes
+    const int per_lane = hd / G;
+    const int slot = tid % G, grp = tid / G, ngrp = ATTN_THREADS / G;
+    float qv[8];
+    for (int e = 0; e < per_lane && e < 8; ++e) qv[e] = *(const float *)(qbase + (int64_t)(slot * per_lane + e) * a.q.nb[0]);
+    const bool vec4 = a.k.nb[0] == 4 && per_lane == 4;
+    for (int i0 = 0; i0 < P; i0 += ngrp * 4) {
+        double part[4];
+        float kvv[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * ngrp + grp;
+            if (i < P) {
+                const char * kr = kbase + (int64_t)i * a.k.nb[1] + (int64_t)(slot * per_lane) * a.k.nb[0];
+                if (vec4) {
+                    const float4 f = *(const float4 *)kr;
+                    kvv[u][0] = f.x; kvv[u][1] = f.y; kvv[u][2] = f.z; kvv[u][3] = f.w;
+                } else {
+                    for (int e = 0; e < 4; ++e) kvv[u][e] = 0.f;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * ngrp + grp;
+            double s = 0.0;
+            if (i < P) {
+                if (vec4) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s += (double)__fmul_rn(kvv[u][e], qv[e]);
+                } else {
+                    const char * kr = kbase + (int64_t)i * a.k.nb[1];
+                    for (int e = 0; e < per_lane; ++e) {
+                        const int d = slot * per_lane + e;
+                        s += (double)__fmul_rn(*(const float *)(kr + (int64_t)d * a.k.nb[0]), qv[e < 8 ? e : 0]);
+                    }
+                }
+            }
+            part[u] = s;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            double s = part[u];
+            for (int off = G / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+            const int i = i0 + u * ngrp + grp;
+            if (slot == 0 && i < P) s_p[i] = (float)s;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum ----
+    const float * mrow = a.mask ? a.mask + (int64_t)t * P : nullptr;
+    float mx = -INFINITY;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        float w = __fmul_rn(s_p[i], a.scale);
+        if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+        s_p[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) s_redf[wave] = mx;
+    __syncthreads();
+    mx = s_redf[0];
+    for (int w = 1; w < ATTN_THREADS / 64; ++w) mx = fmaxf(mx, s_redf[w]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        const float e = cr_expf(__fsub_rn(s_p[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) s_red[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+    for (int w = 0; w < ATTN_THREADS / 64; ++w) sum += s_red[w];
+    const float inv = (float)(1.0 / sum);
+    for (int i = tid; i < P; i += ATTN_THREADS) s_p[i] = __fmul_rn(s_p[i], inv);
+    __syncthreads();
+
+    // ---- phase C: out[d] = sum_i (f32)(p[i] * V[i,d]), f64 accumulation; lanes over i ----
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    float * orow = a.out + (((int64_t)b * a.n + t) * a.H + h) * hd;
+    const int waves = ATTN_THREADS / 64;
+    for (int d0 = wave * 4; d0 < hd; d0 += waves * 4) {
+        double acc[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int i = lane; i < P; i += 64) {
+            const float p = s_p[i];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int d = d0 + u;
+                if (d < hd) {
+                    const float vv = *(const float *)(vbase + (int64_t)d * a.v.nb[1] + (int64_t)i * a.v.nb[0]);
+                    acc[u] += (double)__fmul_rn(p, vv);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double s = wave_sum_d(acc[u]);
+            if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+        }
+    }
+}
+
+void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
+                        float * out, int hd, int P, int H, int n, int B) {
+    AttnArgs a;
+    a.q = q;
+    a.k = k;
+    a.v = v;
+    a.mask = mask;
+    a.scale = scale;
+    a.out = out;
+    a.hd = hd;
+    a.P = P;
+    a.H = H;
+    a.n = n;
+    a.B = B;
+    hipLaunchKernelGGL(k_attn_decode, dim3((unsigned)H, (unsigned)n, (unsigned)B), dim3(ATTN_THREADS), 0, be->stream, a);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm row kernel: y = ((x - mean) * scale) * w + b with ggml's f64 sums; optional RMS
+// variant (no mean, no bias) and optional Q8_K output in the GEMV activation layout.
+template <bool RMS>
+__global__ __launch_bounds__(256) void k_layernorm(TD dst, TD x, const float * __restrict__ w, const float * __restrict__ bias,
+                                                   float eps, int8_t * __restrict__ qs, float * __restrict__ qd,
+                                                   int32_t * __restrict__ qs32) {
+    __shared__ double shd[4];
+    __shared__ float s_y[8192];
+    __shared__ float s_ax[4];
+    __shared__ int s_idx[4];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % x.ne[1], i2 = (r / x.ne[1]) % x.ne[2], i3 = r / (x.ne[1] * x.ne[2]);
+    const float * xr = (const float *)(x.data + i1 * x.nb[1] + i2 * x.nb[2] + i3 * x.nb[3]);
+    float * yr = (float *)(dst.data + i1 * dst.nb[1] + i2 * dst.nb[2] + i3 * dst.nb[3]);
+    const int n = (int)x.ne[0];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    auto bsum = [&](double v) {
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        __syncthreads();
+        if (lane == 0) shd[wave] = v;
+        __syncthreads();
+        return shd[0] + shd[1] + shd[2] + shd[3];
+    };
+    float mean = 0.f;
+    if (!RMS) {
+        double s = 0.0;
+        for (int i = tid; i < n; i += 256) s += (double)xr[i];
+        mean = (float)(bsum(s) / (double)n);
+    }
+    double s2 = 0.0;
+    for (int i = tid; i < n; i += 256) {
+        const float v = RMS ? xr[i] : __fsub_rn(xr[i], mean);
+        s2 += (double)__fmul_rn(v, v);
+    }
+    const float var = (float)(bsum(s2) / (double)n);
+    const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(var, eps)));
+    for (int i = tid; i < n; i += 256) {
+        float v = RMS ? __fmul_rn(xr[i], scale) : __fmul_rn(__fsub_rn(xr[i], mean), scale);
+        v = __fmul_rn(v, w[i]);
+        if (!RMS) v = __fadd_rn(v, bias[i]);
+        yr[i] = v;
+        if (qs) s_y[i] = v;
+    }
+    if (!qs) return;
+    // Q8_K of this row (quantize_row_q8_K_ref), one 256-block per pass
+    const int nb = n / QK_K;
+    __syncthreads();
+    for (int blk = 0; blk < nb; ++blk) {
+        const float v = s_y[blk * QK_K + tid];
+        float ax = fabsf(v);
+        int idx = tid;
+        for (int off = 32; off >= 1; off >>= 1) {
+            const float oax = __shfl_xor(ax, off);
+            const int oidx = __shfl_xor(idx, off);
+            if (oax > ax || (oax == ax && oidx < idx)) {
+                ax = oax;
+                idx = oidx;
+            }
+        }
+        if (lane == 0) {
+            s_ax[wave] = ax;
+            s_idx[wave] = idx;
+        }
+        __syncthreads();
+        float amax = s_ax[0];
+        int imax = s_idx[0];
+        for (int ww = 1; ww < 4; ++ww) {
+            if (s_ax[ww] > amax || (s_ax[ww] == amax && s_idx[ww] < imax)) {
+                amax = s_ax[ww];
+                imax = s_idx[ww];
+            }
+        }
+        const int j = tid >> 5, rr = tid & 31;
+        const int off = (rr & 7) * 32 + (j & 1) * 16 + (j >> 1) * 4 + (rr >> 3);
+        int qi = 0;
+        if (amax != 0.f) {
+            const float iscale = cr_divf(-127.f, s_y[blk * QK_K + imax]);
+            const float val = __fadd_rn(__fmul_rn(iscale, v), 12582912.f);
+            qi = (__float_as_int(val) & 0x007fffff) - 0x00400000;
+            qi = qi < 127 ? qi : 127;
+            if (tid == 0) qd[r * nb + blk] = cr_divf(1.f, iscale);
+        } else if (tid == 0) {
+            qd[r * nb + blk] = 0.f;
+        }
+        qs[(r * nb + blk) * QK_K + off] = (int8_t)qi;
+        int s = qi;
+        for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+        if (rr == 0) qs32[(r * nb + blk) * 8 + j] = s;
+        __syncthreads();
+    }
+}
+
+void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
+                      float eps, bool rms, ActQuant * aq) {
+    const int64_t nr = x->ne[1] * x->ne[2] * x->ne[3];
+    int8_t * qs = nullptr;
+    float * qd = nullptr;
+    int32_t * q32 = nullptr;
+    if (aq) {
+        qs = aq->qs;
+        qd = aq->d;
+        q32 = aq->bsums;
+    }
+    if (rms)
+        hipLaunchKernelGGL(k_layernorm<true>, dim3((unsigned)nr), dim3(256), 0, be->stream, make_td(dst), make_td(x), w, b, eps, qs, qd, q32);
+    else
+        hipLaunchKernelGGL(k_layernorm<false>, dim3((unsigned)nr), dim3(256), 0, be->stream, make_td(dst), make_td(x), w, b, eps, qs, qd, q32);
+    TTS_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace tts

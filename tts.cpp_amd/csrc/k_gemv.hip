@@ -78,10 +78,10 @@ __global__ __launch_bounds__(256) void k_quantize_q8_K(const float * __restrict_
     int qi = 0;
     if (amax != 0.f) {
         const float mx = s_v[imax];
-        const float iscale = __fdiv_rn(-127.f, mx);
+        const float iscale = cr_divf(-127.f, mx);
         qi = dev_nearest_int(__fmul_rn(iscale, v));
         qi = qi < 127 ? qi : 127;
-        if (t == 0) dout[m * nb + blk] = __fdiv_rn(1.f, iscale);
+        if (t == 0) dout[m * nb + blk] = cr_divf(1.f, iscale);
     } else if (t == 0) {
         dout[m * nb + blk] = 0.f;
     }
@@ -122,8 +122,8 @@ __global__ __launch_bounds__(256) void k_quantize_q8_0(const float * __restrict_
     float a = fabsf(v);
 #pragma unroll
     for (int off = 16; off >= 1; off >>= 1) a = fmaxf(a, __shfl_xor(a, off));
-    const float d = __fdiv_rn(a, 127.f);
-    const float id = d != 0.f ? __fdiv_rn(1.f, d) : 0.f;
+    const float d = cr_divf(a, 127.f);
+    const float id = d != 0.f ? cr_divf(1.f, d) : 0.f;
     qs[m * K + i] = (int8_t)roundf(__fmul_rn(v, id));
     if ((threadIdx.x & 31) == 0) dout[m * (K / QK8_0) + i / QK8_0] = __half2float(__float2half_rn(d));
 }
@@ -137,11 +137,19 @@ __global__ void k_quantize_f16(const float * __restrict__ x, int64_t xcs, int64_
 
 // ------------------------------------------------------------------------------------------
 // Q4_K x Q8_K GEMV on repacked weights, reproducing ggml_vec_dot_q4_K_q8_K's generic f32 order
-// exactly: per row, blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7), sumf -= dmin*sumi,
-// then sumf += sums[0..7].  Integer work is spread over octets (one block per octet per
-// iteration); the f32 accumulation is done by the row's leader octet, which pulls each block's
-// aux32[l], d, dmin, sumi from the owning octet with shuffles, in block order.
-// 256 threads = 4 waves; a wave covers RPI = 8/OPR rows, OPR octets per row.
+// exactly: per (row, column), blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7),
+// sumf -= dmin*sumi, then sumf += sums[0..7].
+//
+// One workgroup (256 threads) owns RW consecutive rows of one matrix (gridDim.y = matrices that
+// share the activation, e.g. q/k/v).  Three phases:
+//   0. issue the first weight loads (registers), stage the Q8_K activation of all M columns
+//      in LDS (one HBM/L2 read per workgroup instead of one per octet);
+//   1. integer phase: an octet (8 lanes) per (row, block) pair: lane l's 16-B load holds the
+//      nibbles of residue l (lane layout), 8 x v_dot4_i32_i8 give aux32[l] per column; results,
+//      d*yd and dmin*yd go to LDS;
+//   2. ordered f32 phase: lane = (column m, residue l) walks the row's blocks in order; lane l=0
+//      also carries sumf; one 8-lane fold in order l = 0..7 ends the row.
+// The weight stream is read once with 16-B non-temporal loads; everything else is on-chip.
 __device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc, int & mn) {
     if (j < 4) {
         sc = q[j] & 63;
@@ -152,62 +160,99 @@ __device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc
     }
 }
 
+__device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
+
 template <int MC>
-__global__ __launch_bounds__(256) void k_gemv_q4_K(const uint8_t * __restrict__ W, int64_t w_row_bytes,
-                                                   const int8_t * __restrict__ xq, const float * __restrict__ xd,
-                                                   const int32_t * __restrict__ xs32, float * __restrict__ y,
-                                                   int64_t ycs, int64_t K, int64_t N, int M, int OPR) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int g = lane >> 3;
-    const int t = lane & 7;  // = residue l
-    const int nb = (int)(K / QK_K);
-    const int RPI = 8 / OPR;
-    const int rg = g / OPR;                 // row group within the wave
-    const int og = g % OPR;                 // octet within the row group
-    const int base = rg * OPR * 8;          // first lane of the row group
-    const int64_t row = ((int64_t)blockIdx.x * 4 + wave) * RPI + rg;
-    const bool row_ok = row < N;
-    float sums[MC], sumf[MC];
-#pragma unroll
-    for (int m = 0; m < MC; ++m) {
-        sums[m] = 0.f;
-        sumf[m] = 0.f;
+__device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t row, int m, float v) {
+    if (j.epi == EPI_GELU) {
+        if (v <= -10.0f) v = 0.0f;
+        else if (v < 10.0f) v = __half2float(__ushort_as_half(j.gelu[__half_as_ushort(__float2half_rn(v))]));
+    } else if (j.epi == EPI_ADD) {
+        v = __fadd_rn(v, j.res[m * j.rcs + row]);
     }
-    const uint8_t * wrow = W + (row_ok ? row : 0) * w_row_bytes;
-    const int iters = (nb + OPR - 1) / OPR;
-    for (int it = 0; it < iters; ++it) {
-        const int blk = og + it * OPR;
-        const bool ok = row_ok && blk < nb;
-        u32x4 hdr = {0u, 0u, 0u, 0u};
-        u32x4 q = {0u, 0u, 0u, 0u};
-        if (ok) {
-            const uint8_t * bp = wrow + (int64_t)blk * 144;
-            hdr = __builtin_nontemporal_load((const u32x4 *)bp);
-            q = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + t * 16));
+    j.Y[mat][m * j.ycs[mat] + row * j.yrs[mat]] = v;
+}
+
+constexpr int Q4K_PMAX = 4;  // (row, block) pairs an octet keeps in flight
+
+template <int MC>
+__global__ __launch_bounds__(256) void k_gemv_q4_K(GemvJob j, int RW) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK_K);
+    const int mat = blockIdx.y;
+    const uint8_t * __restrict__ W = j.W[mat];
+    float * Y = j.Y[mat];
+    const int64_t row0 = (int64_t)blockIdx.x * RW;
+    const int rows = (int)((j.N - row0) < RW ? (j.N - row0) : RW);
+    const int M = j.M;
+    int8_t * xq_s = (int8_t *)smem;
+    float * xd_s = (float *)(smem + al16((size_t)MC * j.K));
+    int * xs_s = (int *)((char *)xd_s + al16(sizeof(float) * MC * nb));
+    int * aux_s = (int *)((char *)xs_s + al16(sizeof(int) * MC * nb * 8));
+    float * dd_s = (float *)((char *)aux_s + al16(sizeof(int) * (size_t)RW * nb * MC * 8));
+    float * dm_s = dd_s + (size_t)RW * nb * MC;
+    int * sm_s = (int *)(dm_s + (size_t)RW * nb * MC);
+
+    const int octet = threadIdx.x >> 3, l = threadIdx.x & 7;
+    const int npairs = rows * nb;
+    // phase 0a: first batch of weight loads
+    u32x4 hdr[Q4K_PMAX], q[Q4K_PMAX];
+#pragma unroll
+    for (int i = 0; i < Q4K_PMAX; ++i) {
+        const int p = octet + 32 * i;
+        if (p < npairs) {
+            const uint8_t * bp = W + (row0 + p / nb) * j.w_row_bytes + (int64_t)(p % nb) * 144;
+            hdr[i] = __builtin_nontemporal_load((const u32x4 *)bp);
+            q[i] = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
         }
-        const uint32_t sw[3] = {hdr.y, hdr.z, hdr.w};
-        const uint8_t * scb = (const uint8_t *)sw;
-        int sc[8], mymin, tmp;
+    }
+    // phase 0b: activation -> LDS
+    {
+        const int4 * src = (const int4 *)j.aq.qs;
+        int4 * dst = (int4 *)xq_s;
+        const int n16 = (int)((int64_t)M * j.K / 16);
+        for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
+        for (int i = threadIdx.x; i < M * nb; i += 256) xd_s[i] = j.aq.d[i];
+        for (int i = threadIdx.x; i < M * nb * 8; i += 256) xs_s[i] = j.aq.bsums[i];
+    }
+    __syncthreads();
+    // phase 1: integer work per (row, block) pair
+    for (int base = 0; base < npairs; base += 32 * Q4K_PMAX) {
+        if (base > 0) {
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) q4k_scale_min(scb, jj, sc[jj], tmp);
-        q4k_scale_min(scb, t, tmp, mymin);
-        const int lo0 = (int)(q.x & 0x0F0F0F0Fu), lo1 = (int)(q.y & 0x0F0F0F0Fu);
-        const int lo2 = (int)(q.z & 0x0F0F0F0Fu), lo3 = (int)(q.w & 0x0F0F0F0Fu);
-        const int hi0 = (int)((q.x >> 4) & 0x0F0F0F0Fu), hi1 = (int)((q.y >> 4) & 0x0F0F0F0Fu);
-        const int hi2 = (int)((q.z >> 4) & 0x0F0F0F0Fu), hi3 = (int)((q.w >> 4) & 0x0F0F0F0Fu);
-        const float dw = dev_fp16_to_fp32((uint16_t)(hdr.x & 0xFFFF));
-        const float dmw = dev_fp16_to_fp32((uint16_t)(hdr.x >> 16));
+            for (int i = 0; i < Q4K_PMAX; ++i) {
+                const int p = base + octet + 32 * i;
+                if (p < npairs) {
+                    const uint8_t * bp = W + (row0 + p / nb) * j.w_row_bytes + (int64_t)(p % nb) * 144;
+                    hdr[i] = __builtin_nontemporal_load((const u32x4 *)bp);
+                    q[i] = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
+                }
+            }
+        }
 #pragma unroll
-        for (int m = 0; m < MC; ++m) {
-            if (m >= M) break;
-            int aux = 0, smin = 0;
-            float dd = 0.f, dm = 0.f;
-            if (ok) {
-                const int64_t xb = ((int64_t)m * nb + blk);
-                const int4 xl = *(const int4 *)(xq + xb * QK_K + t * 32);
-                const int4 xh = *(const int4 *)(xq + xb * QK_K + t * 32 + 16);
-                aux = sc[0] * __builtin_amdgcn_sdot4(lo0, xl.x, 0, false);
+        for (int i = 0; i < Q4K_PMAX; ++i) {
+            const int p = base + octet + 32 * i;
+            if (p >= npairs) break;  // octet-uniform
+            const int r = p / nb, b = p % nb;
+            const uint32_t sw[3] = {hdr[i].y, hdr[i].z, hdr[i].w};
+            const uint8_t * scb = (const uint8_t *)sw;
+            int sc[8], mymin, tmp;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) q4k_scale_min(scb, jj, sc[jj], tmp);
+            q4k_scale_min(scb, l, tmp, mymin);
+            const int lo0 = (int)(q[i].x & 0x0F0F0F0Fu), lo1 = (int)(q[i].y & 0x0F0F0F0Fu);
+            const int lo2 = (int)(q[i].z & 0x0F0F0F0Fu), lo3 = (int)(q[i].w & 0x0F0F0F0Fu);
+            const int hi0 = (int)((q[i].x >> 4) & 0x0F0F0F0Fu), hi1 = (int)((q[i].y >> 4) & 0x0F0F0F0Fu);
+            const int hi2 = (int)((q[i].z >> 4) & 0x0F0F0F0Fu), hi3 = (int)((q[i].w >> 4) & 0x0F0F0F0Fu);
+            const float dw = dev_fp16_to_fp32((uint16_t)(hdr[i].x & 0xFFFF));
+            const float dmw = dev_fp16_to_fp32((uint16_t)(hdr[i].x >> 16));
+#pragma unroll
+            for (int m = 0; m < MC; ++m) {
+                if (m >= M) break;
+                const int xb = m * nb + b;
+                const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
+                const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
+                int aux = sc[0] * __builtin_amdgcn_sdot4(lo0, xl.x, 0, false);
                 aux += sc[2] * __builtin_amdgcn_sdot4(lo1, xl.y, 0, false);
                 aux += sc[4] * __builtin_amdgcn_sdot4(lo2, xl.z, 0, false);
                 aux += sc[6] * __builtin_amdgcn_sdot4(lo3, xl.w, 0, false);
@@ -215,144 +260,137 @@ __global__ __launch_bounds__(256) void k_gemv_q4_K(const uint8_t * __restrict__ 
                 aux += sc[3] * __builtin_amdgcn_sdot4(hi1, xh.y, 0, false);
                 aux += sc[5] * __builtin_amdgcn_sdot4(hi2, xh.z, 0, false);
                 aux += sc[7] * __builtin_amdgcn_sdot4(hi3, xh.w, 0, false);
-                smin = mymin * xs32[xb * 8 + t];
-                const float yd = xd[xb];
-                dd = __fmul_rn(dw, yd);
-                dm = __fmul_rn(dmw, yd);
-            }
-            smin += __shfl_xor(smin, 1);
-            smin += __shfl_xor(smin, 2);
-            smin += __shfl_xor(smin, 4);
-            // ordered f32 accumulation of this iteration's blocks by the leader octet
-            for (int bb = 0; bb < OPR; ++bb) {
-                if (it * OPR + bb >= nb) break;  // uniform across the wave
-                const int src = base + bb * 8 + t;
-                const int a_b = __shfl(aux, src);
-                const float dd_b = __shfl(dd, src);
-                const float dm_b = __shfl(dm, src);
-                const int s_b = __shfl(smin, src);
-                sums[m] = __fadd_rn(sums[m], __fmul_rn(dd_b, (float)a_b));
-                sumf[m] = __fsub_rn(sumf[m], __fmul_rn(dm_b, (float)s_b));
+                int smin = mymin * xs_s[xb * 8 + l];
+                smin += __shfl_xor(smin, 1);
+                smin += __shfl_xor(smin, 2);
+                smin += __shfl_xor(smin, 4);
+                const int o = (r * nb + b) * MC + m;
+                aux_s[o * 8 + l] = aux;
+                if (l == 0) {
+                    const float yd = xd_s[xb];
+                    dd_s[o] = __fmul_rn(dw, yd);
+                    dm_s[o] = __fmul_rn(dmw, yd);
+                    sm_s[o] = smin;
+                }
             }
         }
     }
-#pragma unroll
-    for (int m = 0; m < MC; ++m) {
-        float f = sumf[m];
-        for (int l = 0; l < 8; ++l) f = __fadd_rn(f, __shfl(sums[m], base + l));
-        sumf[m] = f;
-    }
-    if (row_ok && og == 0 && t == 0) {
-#pragma unroll
-        for (int m = 0; m < MC; ++m) {
-            if (m < M) y[m * ycs + row] = sumf[m];
+    __syncthreads();
+    // phase 2: ordered f32 accumulation, lane = (m, l)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int m = lane >> 3, l2 = lane & 7;
+    for (int r = wave; r < rows; r += 4) {
+        float sums = 0.f, sumf = 0.f;
+        if (m < M) {
+            for (int b = 0; b < nb; ++b) {
+                const int o = (r * nb + b) * MC + m;
+                sums = __fadd_rn(sums, __fmul_rn(dd_s[o], (float)aux_s[o * 8 + l2]));
+                if (l2 == 0) sumf = __fsub_rn(sumf, __fmul_rn(dm_s[o], (float)sm_s[o]));
+            }
         }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const float v = __shfl(sums, (lane & ~7) + k);
+            if (l2 == 0) sumf = __fadd_rn(sumf, v);
+        }
+        if (l2 == 0 && m < M) gemv_store<MC>(j, mat, row0 + r, m, sumf);
     }
 }
 
-// Q8_0 x Q8_0 GEMV reproducing ggml_vec_dot_q8_0_q8_0's generic order: per row, blocks in
-// ascending order, sumf += (float)sumi * (d_w * d_x).  A wave owns a row: lane = block within a
-// 64-block chunk computes sumi (exact int), then lane 0 folds the chunk in order via shuffles.
+// Q8_0 x Q8_0 GEMV reproducing ggml_vec_dot_q8_0_q8_0's generic order: per (row, column),
+// blocks in ascending order, sumf += (float)sumi * (d_w * d_x).  Phase 1: a thread per
+// (row, block) computes the exact int dots for every column -> LDS; phase 2: a lane per
+// (row, column) folds its blocks in order.
 template <int MC>
-__global__ __launch_bounds__(256) void k_gemv_q8_0(const uint8_t * __restrict__ W, int64_t w_row_bytes,
-                                                   const int8_t * __restrict__ xq, const float * __restrict__ xd,
-                                                   float * __restrict__ y, int64_t ycs, int64_t K, int64_t N, int M) {
-    const int lane = threadIdx.x & 63;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= N) return;  // wave-uniform
-    const int nb = (int)(K / QK8_0);
-    const uint8_t * wrow = W + row * w_row_bytes;
-    float acc[MC];
+__global__ __launch_bounds__(256) void k_gemv_q8_0(GemvJob j, int RW) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK8_0);
+    const int mat = blockIdx.y;
+    const uint8_t * __restrict__ W = j.W[mat];
+    float * Y = j.Y[mat];
+    const int64_t row0 = (int64_t)blockIdx.x * RW;
+    const int rows = (int)((j.N - row0) < RW ? (j.N - row0) : RW);
+    const int M = j.M;
+    int8_t * xq_s = (int8_t *)smem;
+    float * xd_s = (float *)(smem + al16((size_t)MC * j.K));
+    int * s_s = (int *)((char *)xd_s + al16(sizeof(float) * MC * nb));
+    float * f_s = (float *)((char *)s_s + al16(sizeof(int) * (size_t)RW * nb * MC));
+    {
+        const int4 * src = (const int4 *)j.aq.qs;
+        int4 * dst = (int4 *)xq_s;
+        const int n16 = (int)((int64_t)M * j.K / 16);
+        for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
+        for (int i = threadIdx.x; i < M * nb; i += 256) xd_s[i] = j.aq.d[i];
+    }
+    __syncthreads();
+    const int npairs = rows * nb;
+    for (int p = threadIdx.x; p < npairs; p += 256) {
+        const int r = p / nb, b = p % nb;
+        const uint16_t * bp = (const uint16_t *)(W + (row0 + r) * j.w_row_bytes + (int64_t)b * 34);
+        const float dw = dev_fp16_to_fp32(bp[0]);
+        int wv[8];
 #pragma unroll
-    for (int m = 0; m < MC; ++m) acc[m] = 0.f;
-    for (int b0 = 0; b0 < nb; b0 += 64) {
-        const int b = b0 + lane;
-        const bool ok = b < nb;
-        float dw = 0.f;
-        int wv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (ok) {
-            const uint16_t * bp = (const uint16_t *)(wrow + (int64_t)b * 34);
-            dw = dev_fp16_to_fp32(bp[0]);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
-        }
-        const int cnt = nb - b0 < 64 ? nb - b0 : 64;
+        for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
             if (m >= M) break;
-            int s = 0;
-            float dxy = 0.f;
-            if (ok) {
-                const int4 * xb = (const int4 *)(xq + (int64_t)m * K + (int64_t)b * QK8_0);
-                const int4 x0 = xb[0], x1 = xb[1];
-                s = __builtin_amdgcn_sdot4(wv[0], x0.x, 0, false);
-                s = __builtin_amdgcn_sdot4(wv[1], x0.y, s, false);
-                s = __builtin_amdgcn_sdot4(wv[2], x0.z, s, false);
-                s = __builtin_amdgcn_sdot4(wv[3], x0.w, s, false);
-                s = __builtin_amdgcn_sdot4(wv[4], x1.x, s, false);
-                s = __builtin_amdgcn_sdot4(wv[5], x1.y, s, false);
-                s = __builtin_amdgcn_sdot4(wv[6], x1.z, s, false);
-                s = __builtin_amdgcn_sdot4(wv[7], x1.w, s, false);
-                dxy = __fmul_rn(dw, xd[(int64_t)m * nb + b]);
-            }
-            float a = acc[m];
-            for (int i = 0; i < cnt; ++i) {
-                const int si = __shfl(s, i);
-                const float fi = __shfl(dxy, i);
-                a = __fadd_rn(a, __fmul_rn((float)si, fi));
-            }
-            acc[m] = a;
+            const int4 * xb = (const int4 *)(xq_s + (m * nb + b) * QK8_0);
+            const int4 x0 = xb[0], x1 = xb[1];
+            int s = __builtin_amdgcn_sdot4(wv[0], x0.x, 0, false);
+            s = __builtin_amdgcn_sdot4(wv[1], x0.y, s, false);
+            s = __builtin_amdgcn_sdot4(wv[2], x0.z, s, false);
+            s = __builtin_amdgcn_sdot4(wv[3], x0.w, s, false);
+            s = __builtin_amdgcn_sdot4(wv[4], x1.x, s, false);
+            s = __builtin_amdgcn_sdot4(wv[5], x1.y, s, false);
+            s = __builtin_amdgcn_sdot4(wv[6], x1.z, s, false);
+            s = __builtin_amdgcn_sdot4(wv[7], x1.w, s, false);
+            const int o = (r * MC + m) * nb + b;
+            s_s[o] = s;
+            f_s[o] = __fmul_rn(dw, xd_s[m * nb + b]);
         }
     }
-    if (lane == 0) {
-#pragma unroll
-        for (int m = 0; m < MC; ++m)
-            if (m < M) y[m * ycs + row] = acc[m];
+    __syncthreads();
+    for (int t = threadIdx.x; t < rows * MC; t += 256) {
+        const int r = t / MC, m = t % MC;
+        if (m >= M) continue;
+        float a = 0.f;
+        const int o = (r * MC + m) * nb;
+        for (int b = 0; b < nb; ++b) a = __fadd_rn(a, __fmul_rn((float)s_s[o + b], f_s[o + b]));
+        gemv_store<MC>(j, mat, row0 + r, m, a);
     }
 }
 
 // F32 / F16 GEMV: f32 products, f64 accumulation (ggml_vec_dot_f32 / _f16 generic), a wave per
 // row, 16-B loads.  For F16 the activation was rounded to fp16 first (vec_dot_type F16).
 template <int MC, bool F16>
-__global__ __launch_bounds__(256) void k_gemv_float(const uint8_t * __restrict__ W, int64_t w_row_bytes,
-                                                    const void * __restrict__ xv, int64_t xcs,
-                                                    float * __restrict__ y, int64_t ycs, int64_t K, int64_t N, int M) {
+__global__ __launch_bounds__(256) void k_gemv_float(GemvJob j) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= N) return;
+    if (row >= j.N) return;
+    const int mat = blockIdx.y;
+    const int M = j.M;
+    const int64_t K = j.K;
     double acc[MC];
 #pragma unroll
     for (int m = 0; m < MC; ++m) acc[m] = 0.0;
     if (!F16) {
-        const float * w = (const float *)(W + row * w_row_bytes);
-        const float * x = (const float *)xv;
-        const bool vec = (K % 4) == 0;
-        if (vec) {
-            for (int64_t k = lane * 4; k < K; k += 256) {
-                const f32x4 wv = __builtin_nontemporal_load((const f32x4 *)(w + k));
+        const float * w = (const float *)(j.W[mat] + row * j.w_row_bytes);
+        const float * x = j.x;
+        for (int64_t k = lane * 4; k < K; k += 256) {
+            const f32x4 wv = __builtin_nontemporal_load((const f32x4 *)(w + k));
 #pragma unroll
-                for (int m = 0; m < MC; ++m) {
-                    if (m >= M) break;
-                    const float4 xv4 = *(const float4 *)(x + m * xcs + k);
-                    acc[m] += (double)__fmul_rn(wv.x, xv4.x);
-                    acc[m] += (double)__fmul_rn(wv.y, xv4.y);
-                    acc[m] += (double)__fmul_rn(wv.z, xv4.z);
-                    acc[m] += (double)__fmul_rn(wv.w, xv4.w);
-                }
-            }
-        } else {
-            for (int64_t k = lane; k < K; k += 64) {
-                const float wv = w[k];
-#pragma unroll
-                for (int m = 0; m < MC; ++m) {
-                    if (m >= M) break;
-                    acc[m] += (double)__fmul_rn(wv, x[m * xcs + k]);
-                }
+            for (int m = 0; m < MC; ++m) {
+                if (m >= M) break;
+                const float4 xv4 = *(const float4 *)(x + m * j.xcs + k);
+                acc[m] += (double)__fmul_rn(wv.x, xv4.x);
+                acc[m] += (double)__fmul_rn(wv.y, xv4.y);
+                acc[m] += (double)__fmul_rn(wv.z, xv4.z);
+                acc[m] += (double)__fmul_rn(wv.w, xv4.w);
             }
         }
     } else {
-        const __half * w = (const __half *)(W + row * w_row_bytes);
-        const __half * x = (const __half *)xv;  // [M][K] fp16, dense
+        const __half * w = (const __half *)(j.W[mat] + row * j.w_row_bytes);
+        const __half * x = (const __half *)j.aq.qs;  // [M][K] fp16, dense
         for (int64_t k = lane; k < K; k += 64) {
             const float wv = __half2float(w[k]);
 #pragma unroll
@@ -371,7 +409,7 @@ __global__ __launch_bounds__(256) void k_gemv_float(const uint8_t * __restrict__
     if (lane == 0) {
 #pragma unroll
         for (int m = 0; m < MC; ++m)
-            if (m < M) y[m * ycs + row] = (float)acc[m];
+            if (m < M) gemv_store<MC>(j, mat, row, m, (float)acc[m]);
     }
 }
 
@@ -387,34 +425,38 @@ size_t act_quant_bytes(int wtype, int64_t K, int64_t M) {
     }
 }
 
-void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq) {
+void act_quant_layout(int wtype, char * base, int64_t K, int64_t M, ActQuant & aq) {
     auto al = [](size_t n) { return (n + 255) & ~(size_t)255; };
-    char * base = be->scratch;
     aq.K = K;
     aq.M = M;
+    aq.qs = (int8_t *)base;
+    aq.d = nullptr;
+    aq.bsums = nullptr;
     if (wtype == TTS_TYPE_Q4_K) {
         aq.vtype = TTS_TYPE_Q8_K;
-        aq.qs = (int8_t *)base;
         aq.d = (float *)(base + al(K * M));
         aq.bsums = (int32_t *)(base + al(K * M) + al(sizeof(float) * M * (K / QK_K)));
+    } else if (wtype == TTS_TYPE_Q8_0) {
+        aq.vtype = TTS_TYPE_Q8_0;
+        aq.d = (float *)(base + al(K * M));
+    } else if (wtype == TTS_TYPE_F16) {
+        aq.vtype = TTS_TYPE_F16;
+    } else {
+        aq.vtype = TTS_TYPE_F32;
+    }
+}
+
+void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq) {
+    act_quant_layout(wtype, be->scratch, K, M, aq);
+    if (wtype == TTS_TYPE_Q4_K) {
         dim3 grid((unsigned)(K / QK_K), (unsigned)M);
         hipLaunchKernelGGL(k_quantize_q8_K, grid, dim3(256), 0, be->stream, x, xcs, K, aq.qs, aq.d, aq.bsums);
     } else if (wtype == TTS_TYPE_Q8_0) {
-        aq.vtype = TTS_TYPE_Q8_0;
-        aq.qs = (int8_t *)base;
-        aq.d = (float *)(base + al(K * M));
-        aq.bsums = nullptr;
         dim3 grid((unsigned)((K + 255) / 256), (unsigned)M);
         hipLaunchKernelGGL(k_quantize_q8_0, grid, dim3(256), 0, be->stream, x, xcs, K, aq.qs, aq.d);
     } else if (wtype == TTS_TYPE_F16) {
-        aq.vtype = TTS_TYPE_F16;
-        aq.qs = (int8_t *)base;
-        aq.d = nullptr;
-        aq.bsums = nullptr;
         dim3 grid((unsigned)((K + 255) / 256), (unsigned)M);
         hipLaunchKernelGGL(k_quantize_f16, grid, dim3(256), 0, be->stream, x, xcs, K, (__half *)aq.qs);
-    } else {
-        aq.vtype = TTS_TYPE_F32;
     }
     TTS_HIP_CHECK(hipGetLastError());
 }
@@ -425,83 +467,97 @@ void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int6
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+static size_t q4k_lds(int MC, int64_t K, int RW) {
+    const int64_t nb = K / QK_K;
+    auto a = [](size_t n) { return (n + 15) & ~(size_t)15; };
+    return a((size_t)MC * K) + a(4 * MC * nb) + a(4 * MC * nb * 8) + a(4 * (size_t)RW * nb * MC * 8) + 3 * 4 * (size_t)RW * nb * MC;
+}
+static size_t q80_lds(int MC, int64_t K, int RW) {
+    const int64_t nb = K / QK8_0;
+    auto a = [](size_t n) { return (n + 15) & ~(size_t)15; };
+    return a((size_t)MC * K) + a(4 * MC * nb) + a(4 * (size_t)RW * nb * MC) + 4 * (size_t)RW * nb * MC;
+}
+
 template <int MC>
-static void launch_gemv_mc(tts_hip_backend * be, int wtype, const void * w, int64_t wrb, const float * x, int64_t xcs,
-                           const ActQuant * aq, float * y, int64_t ycs, int64_t K, int64_t N, int64_t M) {
-    const uint8_t * W = (const uint8_t *)w;
-    switch (wtype) {
+static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
+    const unsigned nmat = (unsigned)j.nmat;
+    switch (j.wtype) {
         case TTS_TYPE_Q4_K: {
-            const int nb = (int)(K / QK_K);
-            const int OPR = nb >= 8 ? 8 : nb >= 4 ? 4 : nb >= 2 ? 2 : 1;
-            const int rows_per_wg = 4 * (8 / OPR);
-            const unsigned grid = (unsigned)((N + rows_per_wg - 1) / rows_per_wg);
-            hipLaunchKernelGGL(k_gemv_q4_K<MC>, dim3(grid), dim3(256), 0, be->stream, W, wrb, aq->qs, aq->d, aq->bsums, y,
-                               ycs, K, N, (int)M, OPR);
+            int RW = 8;
+            while (RW > 1 && q4k_lds(MC, j.K, RW) > 64 * 1024) RW /= 2;
+            const size_t lds = q4k_lds(MC, j.K, RW);
+            const unsigned grid = (unsigned)((j.N + RW - 1) / RW);
+            hipLaunchKernelGGL(k_gemv_q4_K<MC>, dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
         } break;
         case TTS_TYPE_Q8_0: {
-            const unsigned grid = (unsigned)((N + 3) / 4);
-            hipLaunchKernelGGL(k_gemv_q8_0<MC>, dim3(grid), dim3(256), 0, be->stream, W, wrb, aq->qs, aq->d, y, ycs, K, N,
-                               (int)M);
+            int RW = 8;
+            while (RW > 1 && q80_lds(MC, j.K, RW) > 64 * 1024) RW /= 2;
+            const size_t lds = q80_lds(MC, j.K, RW);
+            const unsigned grid = (unsigned)((j.N + RW - 1) / RW);
+            hipLaunchKernelGGL(k_gemv_q8_0<MC>, dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
         } break;
         case TTS_TYPE_F16: {
-            const unsigned grid = (unsigned)((N + 3) / 4);
-            hipLaunchKernelGGL((k_gemv_float<MC, true>), dim3(grid), dim3(256), 0, be->stream, W, wrb, (const void *)aq->qs,
-                               K, y, ycs, K, N, (int)M);
+            const unsigned grid = (unsigned)((j.N + 3) / 4);
+            hipLaunchKernelGGL((k_gemv_float<MC, true>), dim3(grid, nmat), dim3(256), 0, be->stream, j);
         } break;
         default: {
-            const unsigned grid = (unsigned)((N + 3) / 4);
-            hipLaunchKernelGGL((k_gemv_float<MC, false>), dim3(grid), dim3(256), 0, be->stream, W, wrb, (const void *)x, xcs,
-                               y, ycs, K, N, (int)M);
+            const unsigned grid = (unsigned)((j.N + 3) / 4);
+            hipLaunchKernelGGL((k_gemv_float<MC, false>), dim3(grid, nmat), dim3(256), 0, be->stream, j);
         } break;
     }
 }
 
-void launch_gemv(tts_hip_backend * be, int wtype, const void * w, int64_t wrb, const float * x, int64_t xcs,
-                 const ActQuant * aq, float * y, int64_t ycs, int64_t K, int64_t N, int64_t M) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (be->profile_gemv) {
-        if (be->ev_free.size() < 2) {
-            hipEvent_t a, b;
-            TTS_HIP_CHECK(hipEventCreate(&a));
-            TTS_HIP_CHECK(hipEventCreate(&b));
-            be->ev_free.push_back(a);
-            be->ev_free.push_back(b);
-        }
-        e0 = be->ev_free.back();
-        be->ev_free.pop_back();
-        e1 = be->ev_free.back();
-        be->ev_free.pop_back();
-        TTS_HIP_CHECK(hipEventRecord(e0, be->stream));
+static void profile_begin(tts_hip_backend * be, hipEvent_t & e0, hipEvent_t & e1) {
+    if (be->ev_free.size() < 2) {
+        hipEvent_t a, b;
+        TTS_HIP_CHECK(hipEventCreate(&a));
+        TTS_HIP_CHECK(hipEventCreate(&b));
+        be->ev_free.push_back(a);
+        be->ev_free.push_back(b);
     }
-    for (int64_t m0 = 0; m0 < M; m0 += 8) {
-        const int64_t mc = M - m0 < 8 ? M - m0 : 8;
-        ActQuant sub = *aq;
-        if (aq->vtype == TTS_TYPE_Q8_K) {
-            sub.qs = aq->qs + m0 * K;
-            sub.d = aq->d + m0 * (K / QK_K);
-            sub.bsums = aq->bsums + m0 * (K / 32);
-        } else if (aq->vtype == TTS_TYPE_Q8_0) {
-            sub.qs = aq->qs + m0 * K;
-            sub.d = aq->d + m0 * (K / QK8_0);
-        } else if (aq->vtype == TTS_TYPE_F16) {
-            sub.qs = aq->qs + m0 * K * 2;
+    e0 = be->ev_free.back();
+    be->ev_free.pop_back();
+    e1 = be->ev_free.back();
+    be->ev_free.pop_back();
+    TTS_HIP_CHECK(hipEventRecord(e0, be->stream));
+}
+
+void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (be->profile_gemv) profile_begin(be, e0, e1);
+    const int64_t K = job.K;
+    for (int64_t m0 = 0; m0 < job.M; m0 += 8) {
+        const int64_t mc = job.M - m0 < 8 ? job.M - m0 : 8;
+        GemvJob j = job;
+        j.M = mc;
+        if (job.aq.vtype == TTS_TYPE_Q8_K) {
+            j.aq.qs = job.aq.qs + m0 * K;
+            j.aq.d = job.aq.d + m0 * (K / QK_K);
+            j.aq.bsums = job.aq.bsums + m0 * (K / 32);
+        } else if (job.aq.vtype == TTS_TYPE_Q8_0) {
+            j.aq.qs = job.aq.qs + m0 * K;
+            j.aq.d = job.aq.d + m0 * (K / QK8_0);
+        } else if (job.aq.vtype == TTS_TYPE_F16) {
+            j.aq.qs = job.aq.qs + m0 * K * 2;
         }
-        const float * xs = x ? x + m0 * xcs : nullptr;
-        float * ys = y + m0 * ycs;
+        if (job.x) j.x = job.x + m0 * job.xcs;
+        for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+        if (job.res) j.res = job.res + m0 * job.rcs;
         switch (mc) {
-            case 1: launch_gemv_mc<1>(be, wtype, w, wrb, xs, xcs, &sub, ys, ycs, K, N, mc); break;
-            case 2: launch_gemv_mc<2>(be, wtype, w, wrb, xs, xcs, &sub, ys, ycs, K, N, mc); break;
-            case 3: case 4: launch_gemv_mc<4>(be, wtype, w, wrb, xs, xcs, &sub, ys, ycs, K, N, mc); break;
-            default: launch_gemv_mc<8>(be, wtype, w, wrb, xs, xcs, &sub, ys, ycs, K, N, mc); break;
+            case 1: launch_gemv_mc<1>(be, j); break;
+            case 2: launch_gemv_mc<2>(be, j); break;
+            case 3: case 4: launch_gemv_mc<4>(be, j); break;
+            default: launch_gemv_mc<8>(be, j); break;
         }
     }
     TTS_HIP_CHECK(hipGetLastError());
     if (be->profile_gemv) {
         TTS_HIP_CHECK(hipEventRecord(e1, be->stream));
         be->ev_pending.push_back({e0, e1});
-        // algorithmic bytes: weights once + activations + outputs
-        be->ev_bytes.push_back((double)tts_row_size(wtype, K) * (double)N + 4.0 * (double)K * (double)M + 4.0 * (double)N * (double)M);
-        be->ev_type.push_back(wtype);
+        // algorithmic bytes: every weight byte once + activation + outputs
+        be->ev_bytes.push_back((double)job.nmat * ((double)tts_row_size(job.wtype, K) * (double)job.N + 4.0 * (double)job.N * (double)job.M) +
+                               4.0 * (double)K * (double)job.M);
+        be->ev_type.push_back(job.wtype);
     }
 }
 

@@ -55,7 +55,7 @@ __global__ void k_binary(TD dst, TD a, TD b, int64_t n) {
         if (OP == TTS_OP_ADD) v = __fadd_rn(x, y);
         else if (OP == TTS_OP_SUB) v = __fsub_rn(x, y);
         else if (OP == TTS_OP_MUL) v = __fmul_rn(x, y);
-        else v = __fdiv_rn(x, y);
+        else v = cr_divf(x, y);
         td_store(dst, i0, i1, i2, i3, v);
     }
 }
@@ -71,7 +71,7 @@ __global__ void k_binary_cont(float * __restrict__ dst, const float * __restrict
         if (OP == TTS_OP_ADD) v = __fadd_rn(x, y);
         else if (OP == TTS_OP_SUB) v = __fsub_rn(x, y);
         else if (OP == TTS_OP_MUL) v = __fmul_rn(x, y);
-        else v = __fdiv_rn(x, y);
+        else v = cr_divf(x, y);
         dst[k] = v;
     }
 }
@@ -87,7 +87,7 @@ struct UnaryParams {
 __device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
     switch (P.op) {
         case TTS_OP_SQR: return __fmul_rn(x, x);
-        case TTS_OP_SQRT: return __fsqrt_rn(x);
+        case TTS_OP_SQRT: return cr_sqrtf(x);
         case TTS_OP_SIN: return cr_sinf(x);
         case TTS_OP_COS: return cr_cosf(x);
         case TTS_OP_SCALE: return __fmul_rn(x, P.p0);
@@ -102,14 +102,14 @@ __device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
         case TTS_UNARY_NEG: return -x;
         case TTS_UNARY_TANH: return cr_tanhf(x);
         case TTS_UNARY_RELU: return x > 0.f ? x : 0.f;
-        case TTS_UNARY_SIGMOID: return __fdiv_rn(1.f, __fadd_rn(1.f, cr_expf(-x)));
+        case TTS_UNARY_SIGMOID: return cr_divf(1.f, __fadd_rn(1.f, cr_expf(-x)));
         case TTS_UNARY_GELU: {
             if (x <= -10.0f) return 0.0f;
             if (x >= 10.0f) return x;
             const uint16_t h = __half_as_ushort(__float2half_rn(x));
             return __half2float(__ushort_as_half(P.gelu_table[h]));
         }
-        case TTS_UNARY_SILU: return __fdiv_rn(x, __fadd_rn(1.0f, cr_expf(-x)));
+        case TTS_UNARY_SILU: return cr_divf(x, __fadd_rn(1.0f, cr_expf(-x)));
         case TTS_UNARY_EXP: return cr_expf(x);
     }
     return x;
@@ -172,14 +172,14 @@ __global__ __launch_bounds__(256) void k_norm(TD dst, TD a, float eps) {
         }
         s2 = block_sum<double>(s2, shd);
         const float variance = (float)(s2 / (double)n);
-        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(variance, eps)));
+        const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(variance, eps)));
         for (int64_t i = threadIdx.x; i < n; i += blockDim.x) y[i] = __fmul_rn(__fsub_rn(x[i], mean), scale);
     } else {
         double s = 0.0;
         for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double)__fmul_rn(x[i], x[i]);
         s = block_sum<double>(s, shd);
         const float mean = (float)(s / (double)n);
-        const float scale = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(mean, eps)));
+        const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(mean, eps)));
         for (int64_t i = threadIdx.x; i < n; i += blockDim.x) y[i] = __fmul_rn(x[i], scale);
     }
 }
@@ -300,7 +300,7 @@ __global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int 
             float theta = (float)p;
             for (int64_t k = 0; k < i0 / 2; ++k) theta = __fmul_rn(theta, theta_scale);
             const float f = ff ? ff[i0 / 2] : 1.0f;
-            const float th = __fmul_rn(freq_scale, __fdiv_rn(theta, f));
+            const float th = __fmul_rn(freq_scale, cr_divf(theta, f));
             const float c = __fmul_rn(cr_cosf(th), attn_factor), s = __fmul_rn(cr_sinf(th), attn_factor);
             int64_t j0, j1;
             if (neox) {

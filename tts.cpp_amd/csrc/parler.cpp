@@ -71,6 +71,8 @@ extern "C" void tts_parler_default_config(tts_parler_config * c) {
     c->bos_token = 1025;
     c->seed = 0x5EED;
     c->arena_bytes = 0;
+    c->debug_no_reuse = 0;
+    c->pad_ = 0;
 }
 
 // ---- weights ----
@@ -126,7 +128,7 @@ static tts_tensor * layer_norm(tg::context & c, tts_tensor * x, tts_tensor * w, 
 }
 
 static bool run_graph(tts_parler * p, tg::context & c) {
-    if (!tg::alloc_graph(c, p->arena, p->arena_size)) {
+    if (!tg::alloc_graph(c, p->arena, p->arena_size, !p->cfg.debug_no_reuse)) {
         fprintf(stderr, "parler: compute arena too small (%zu needed)\n", c.arena_used);
         return false;
     }
@@ -337,6 +339,11 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
             tts_tensor * Qcur = tg::mul_mat(c, L.q, cur);
             tts_tensor * Kcur = tg::mul_mat(c, L.k, cur);
             tts_tensor * Vcur = tg::mul_mat(c, L.v, cur);
+            // node order: the three projections adjacent (same values as the reference's order,
+            // where the KV-store expands pull K and V in first; lets graph_compute fuse them)
+            tg::build_forward_expand(c, Qcur);
+            tg::build_forward_expand(c, Kcur);
+            tg::build_forward_expand(c, Vcur);
             // parler_build_kv_store (model.cpp:420-439)
             if (B == 1) {
                 tts_tensor * kv = tg::view_1d(c, p->k_l[l], (int64_t)n * H, tts_row_size(TTS_TYPE_F32, H) * p->position);
@@ -521,6 +528,20 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
 extern "C" int32_t tts_parler_position(const tts_parler * p) { return p->position; }
 extern "C" int32_t tts_parler_last_graph_nodes(const tts_parler * p) { return p->last_nodes; }
 extern "C" uint64_t tts_parler_weight_bytes(const tts_parler * p) { return p->wbytes; }
+
+// Debug: node i of the last step graph -> op, type, ne[4]; copies its bytes if contiguous and cap fits.
+extern "C" uint64_t tts_parler_node(tts_parler * p, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap) {
+    if (i < 0 || i >= (int32_t)p->gctx.nodes.size()) return 0;
+    const tts_tensor * t = p->gctx.nodes[i];
+    *op = t->op;
+    *type = t->type;
+    for (int k = 0; k < 4; ++k) ne[k] = t->ne[k];
+    if (!tg::is_contiguous(t) || !dst) return 0;
+    const size_t nb = tg::nbytes(t);
+    if (nb > cap) return 0;
+    if (p->be.get(p->be.ctx, dst, t->data, nb) != 0) return 0;
+    return nb;
+}
 
 extern "C" uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap) {
     for (auto * t : p->gctx.nodes) {

@@ -82,6 +82,8 @@ class ParlerConfig(ctypes.Structure):
         ("bos_token", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("arena_bytes", ctypes.c_uint64),
+        ("debug_no_reuse", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
     ]
 
 
@@ -140,6 +142,7 @@ def lib():
         "tts_parler_last_graph_nodes": (i32, [vp]),
         "tts_parler_weight_bytes": (u64, [vp]),
         "tts_parler_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
+        "tts_parler_node": (u64, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64), vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -263,6 +266,16 @@ class Parler:
 
     def last_graph_nodes(self):
         return self.L.tts_parler_last_graph_nodes(self.ptr)
+
+    def node(self, i, cap=1 << 26):
+        """(op, type, ne, float32 array or None) of node i of the last step graph (debugging)."""
+        import numpy as np
+        op, ty = ctypes.c_int32(), ctypes.c_int32()
+        ne = (ctypes.c_int64 * 4)()
+        buf = np.empty(cap // 4, dtype=np.float32)
+        n = self.L.tts_parler_node(self.ptr, i, ctypes.byref(op), ctypes.byref(ty), ne, buf.ctypes.data, cap)
+        data = buf[: n // 4].copy() if n else None
+        return OPS[op.value], ty.value, tuple(ne), data
 
     def weight_bytes(self):
         return self.L.tts_parler_weight_bytes(self.ptr)
