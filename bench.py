@@ -105,12 +105,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=400)
     ap.add_argument("--no-fusion", action="store_true")
+    ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
     be = ttship.HipBackend(local)
     if args.no_fusion:
         be.set_option(0, 0)
+    be.set_option(2, args.graphs)
     cfg = ttship.parler_config(batch=args.batch, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 8),
                                arena_bytes=4 << 30)
     runner = ttship.Parler(be.iface(), cfg)
@@ -119,10 +121,12 @@ def main():
     runner.generate(args.warmup)
     barrier_sync(dist, be)
 
+    runner.host_stats(reset=True)
     t0 = time.perf_counter()
     toks = runner.generate(args.steps)
     barrier_sync(dist, be)
     dt = time.perf_counter() - t0
+    host = runner.host_stats(reset=True)
     if dist is not None:
         import torch
         t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
@@ -171,6 +175,7 @@ def main():
                        "kv_len_start": args.ctx, "parallelism": f"dp{world} (prompt shards)",
                        "graph_nodes_per_step": runner.last_graph_nodes()},
             "codec_tokens_per_s": round(tokens_per_s, 1),
+            "host_us_per_step": host,
             "roofline": {"bound": "hbm", "achieved": round(gemv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(gemv_gbs / HBM_PEAK_GBS, 4), "traffic": None,
                          "kernel": "k_gemv_q4_K", "avg_launch_us": round(gemv_avg_us, 3),

@@ -56,6 +56,9 @@ int tts_parler_decode(tts_parler * p, const int32_t * audio_tokens, float * logi
  * current position and writes sampled tokens [batch][n_steps][n_output_heads]. */
 int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out);
 int32_t tts_parler_position(const tts_parler * p);
+/* Host time per phase summed over steps (us): build graph, allocate, set inputs, compute enqueue,
+ * wait for logits.  Returns the step count; reset zeroes the sums. */
+int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset);
 /* Nodes in the last step graph and bytes of the compute arena it used. */
 int32_t tts_parler_last_graph_nodes(const tts_parler * p);
 uint64_t tts_parler_weight_bytes(const tts_parler * p);

@@ -1,0 +1,72 @@
+"""GEMV micro-benchmark (raw tts_hip_gemv entry, HIP-event timed on the backend stream).
+
+Shapes: the Parler-mini decode matrices, Orpheus-3B / Dia sizes, at M = 1 and 8 columns.
+Prints one JSON line per shape with avg us per launch and algorithmic GB/s.
+"""
+import json
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "tts.cpp_amd"))
+import ttship  # noqa: E402
+
+SHAPES = [  # (name, type, K, N)
+    ("parler_qkvo", ttship.Q4_K, 1024, 1024),
+    ("parler_fc1", ttship.Q4_K, 1024, 4096),
+    ("parler_fc2", ttship.Q4_K, 4096, 1024),
+    ("orpheus_up", ttship.Q4_K, 3072, 8192),
+    ("orpheus_down", ttship.Q4_K, 8192, 3072),
+    ("orpheus_head", ttship.Q4_K, 3072, 156940),
+    ("dia_ffn", ttship.Q8_0, 2048, 8192),
+    ("parler_head_f32", ttship.F32, 1024, 1088 * 9),
+]
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    hip = ttship.HipBackend(0)
+    L = ttship.lib()
+    rng = np.random.default_rng(0)
+    for name, wt, K, N in SHAPES:
+        wbytes = ttship.row_size(wt, K) * N
+        w = rng.integers(0, 256, size=wbytes, dtype=np.uint8)
+        if wt == ttship.Q4_K:  # keep d/dmin finite: small fp16 in the block headers
+            blk = w.reshape(-1, 144)
+            blk[:, 0:2] = np.frombuffer(np.float16(1e-3).tobytes(), dtype=np.uint8)
+            blk[:, 2:4] = np.frombuffer(np.float16(1e-3).tobytes(), dtype=np.uint8)
+        elif wt == ttship.Q8_0:
+            blk = w.reshape(-1, 34)
+            blk[:, 0:2] = np.frombuffer(np.float16(1e-3).tobytes(), dtype=np.uint8)
+        else:
+            w = (rng.standard_normal(K * N).astype(np.float32) * 0.02).view(np.uint8)
+        dw = hip.alloc(w.nbytes)
+        hip.set(dw, w)
+        for M in (1, 8):
+            x = rng.standard_normal((M, K)).astype(np.float32)
+            dx = hip.alloc(x.nbytes)
+            dy = hip.alloc(4 * M * N)
+            hip.set(dx, x)
+            for _ in range(3):
+                L.tts_hip_gemv(hip.ptr, wt, dw, dx, dy, K, N, M)
+            hip.sync()
+            hip.set_option(1, 1)
+            hip.gemv_stats(-1, reset=True)
+            for _ in range(reps):
+                L.tts_hip_gemv(hip.ptr, wt, dw, dx, dy, K, N, M)
+            ms, n, nbytes = hip.gemv_stats(wt, reset=True)
+            hip.set_option(1, 0)
+            us = 1000.0 * ms / n
+            print(json.dumps({"shape": name, "type": ttship.lib().tts_type_name(wt).decode(), "K": K, "N": N, "M": M,
+                              "weight_MB": round(wbytes / 1e6, 3), "avg_us": round(us, 2),
+                              "GBps": round(nbytes / n / (us * 1e-6) / 1e9, 1)}), flush=True)
+            hip.free(dx)
+            hip.free(dy)
+        hip.free(dw)
+    hip.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# parity tests, then a short bench (no CPU baseline)
+set -o pipefail
+mkdir -p gpurun_out
+cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --steps 30 --warmup 3 --no-cpu-baseline "$@" > gpurun_out/bench.log 2>&1
+rc=$?
+tail -3 gpurun_out/pytest_gpu.log; tail -1 gpurun_out/bench.log | cut -c1-2500
+exit $rc

@@ -62,6 +62,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->scratch);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
+    if (be->gexec) hipGraphExecDestroy(be->gexec);
     hipStreamDestroy(be->stream);
     delete be;
 }
@@ -219,6 +220,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
     switch (option) {
         case TTS_HIP_OPT_FUSION: be->fusion = value; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
+        case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }
 }

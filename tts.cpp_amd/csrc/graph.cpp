@@ -349,19 +349,20 @@ tts_tensor * rope_ext(context & c, tts_tensor * a, tts_tensor * pos, tts_tensor 
 }
 
 // ---- ggml_build_forward_expand ----
-static void visit(context & c, tts_tensor * t, std::unordered_set<tts_tensor *> & seen) {
-    if (!t || seen.count(t)) return;
-    seen.insert(t);
-    for (int i = 0; i < TTS_MAX_SRC; ++i) visit(c, t->src[i], seen);
+// Visited marks live in the tensors' pad_ field (cleared by the builder that owns them), so an
+// expand is O(new nodes) like ggml's hash set, not O(graph).
+static constexpr int32_t kVisited = 0x5A5A;
+
+static void visit(context & c, tts_tensor * t) {
+    if (!t || t->pad_ == kVisited) return;
+    t->pad_ = kVisited;
+    c.visited.push_back(t);
+    for (int i = 0; i < TTS_MAX_SRC; ++i) visit(c, t->src[i]);
     if (t->op == TTS_OP_NONE) c.leafs.push_back(t);
     else c.nodes.push_back(t);
 }
 
-void build_forward_expand(context & c, tts_tensor * t) {
-    std::unordered_set<tts_tensor *> seen(c.nodes.begin(), c.nodes.end());
-    for (auto * l : c.leafs) seen.insert(l);
-    visit(c, t, seen);
-}
+void build_forward_expand(context & c, tts_tensor * t) { visit(c, t); }
 
 // ---- allocator: first-fit free list with coalescing, freed after last use ----
 namespace {

@@ -20,13 +20,17 @@ struct context {
     std::vector<tts_tensor *> nodes;  // execution order (ggml_cgraph nodes)
     std::vector<tts_tensor *> leafs;
     size_t arena_used = 0;            // bytes of the arena the last alloc used (peak)
+    std::vector<tts_tensor *> visited;  // tensors already in nodes/leafs (flag bit on the tensor)
 
     void reset() {
+        for (auto * t : visited) t->pad_ = 0;  // un-mark shared leaves (weights, caches) first
+        visited.clear();
         tensors.clear();
         nodes.clear();
         leafs.clear();
         arena_used = 0;
     }
+    ~context() { reset(); }
 };
 
 tts_tensor * new_tensor(context & c, int type, int n_dims, const int64_t * ne);

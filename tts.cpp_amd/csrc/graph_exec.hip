@@ -527,9 +527,46 @@ static int run_item(tts_hip_backend * be, const Item & it) {
     return TTS_STATUS_FAILED;
 }
 
+static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes);
+
 extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    if (!be->use_graphs || be->profile_gemv) return graph_compute_launches(be, nodes, n_nodes);
+    // Record the step's launches into a HIP graph and replay it: the kernels then run back to
+    // back on the device instead of at the host's launch rate.  Topology is stable from step to
+    // step (only shapes/offsets move with the KV length), so the executable graph is updated in
+    // place (hipGraphExecUpdate) and re-instantiated only when that fails.
+    TTS_HIP_CHECK(hipStreamBeginCapture(be->stream, hipStreamCaptureModeThreadLocal));
+    const int st = graph_compute_launches(be, nodes, n_nodes);
+    hipGraph_t graph = nullptr;
+    TTS_HIP_CHECK(hipStreamEndCapture(be->stream, &graph));
+    if (st != 0) {
+        if (graph) hipGraphDestroy(graph);
+        return st;
+    }
+    bool ok = false;
+    if (be->gexec) {
+        hipGraphNode_t err_node = nullptr;
+        hipGraphExecUpdateResult res;
+        ok = hipGraphExecUpdate(be->gexec, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess;
+        if (ok) be->graph_updates++;
+        else {
+            (void)hipGetLastError();
+            TTS_HIP_CHECK(hipGraphExecDestroy(be->gexec));
+            be->gexec = nullptr;
+        }
+    }
+    if (!ok) {
+        TTS_HIP_CHECK(hipGraphInstantiate(&be->gexec, graph, nullptr, nullptr, 0));
+        be->graph_instantiations++;
+    }
+    TTS_HIP_CHECK(hipGraphDestroy(graph));
+    TTS_HIP_CHECK(hipGraphLaunch(be->gexec, be->stream));
+    return 0;
+}
+
+static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     be->graph_epoch++;
     be->aq.src = nullptr;
     Planner pl;

@@ -114,6 +114,10 @@ struct tts_hip_backend {
     std::vector<hipEvent_t> ev_free;
     char * repack_tmp = nullptr;  // device temp for Q4_K matrices not stored repacked
     size_t repack_tmp_size = 0;
+    // HIP graph replay of graph_compute (capture -> exec update -> one launch)
+    bool use_graphs = false;
+    hipGraphExec_t gexec = nullptr;
+    int64_t graph_updates = 0, graph_instantiations = 0;
 };
 
 namespace tts {

@@ -24,8 +24,9 @@ struct AttnArgs {
     int hd, P, H, n, B;
 };
 
-constexpr int ATTN_THREADS = 256;
+constexpr int ATTN_THREADS = 512;
 constexpr int ATTN_MAXP = 8192;
+constexpr int ATTN_UK = 8;  // K rows in flight per lane group (phase A)
 
 __device__ __forceinline__ double wave_sum_d(double v) {
     for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
@@ -33,7 +34,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
-    __shared__ float s_p[ATTN_MAXP];
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 4];
     __shared__ double s_red[ATTN_THREADS / 64];
     __shared__ float s_redf[ATTN_THREADS / 64];
     const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
@@ -51,44 +52,31 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     const int slot = tid % G, grp = tid / G, ngrp = ATTN_THREADS / G;
     float qv[8];
     for (int e = 0; e < per_lane && e < 8; ++e) qv[e] = *(const float *)(qbase + (int64_t)(slot * per_lane + e) * a.q.nb[0]);
-    const bool vec4 = a.k.nb[0] == 4 && per_lane == 4;
-    for (int i0 = 0; i0 < P; i0 += ngrp * 4) {
-        double part[4];
-        float kvv[4][4];
+    const bool vec4 = a.k.nb[0] == 4 && per_lane == 4 && (a.k.nb[1] % 16) == 0 && (((uintptr_t)kbase) % 16) == 0;
+    for (int i0 = 0; i0 < P; i0 += ngrp * ATTN_UK) {
+        float4 kvv[ATTN_UK];
+        // issue every row load of the batch before the first use (memory-level parallelism)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < ATTN_UK; ++u) {
             const int i = i0 + u * ngrp + grp;
+            kvv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (i < P) {
                 const char * kr = kbase + (int64_t)i * a.k.nb[1] + (int64_t)(slot * per_lane) * a.k.nb[0];
-                if (vec4) {
-                    const float4 f = *(const float4 *)kr;
-                    kvv[u][0] = f.x; kvv[u][1] = f.y; kvv[u][2] = f.z; kvv[u][3] = f.w;
-                } else {
-                    for (int e = 0; e < 4; ++e) kvv[u][e] = 0.f;
+                if (vec4) kvv[u] = *(const float4 *)kr;
+                else {
+                    kvv[u].x = *(const float *)kr;
+                    kvv[u].y = *(const float *)(kr + a.k.nb[0]);
+                    kvv[u].z = *(const float *)(kr + 2 * a.k.nb[0]);
+                    kvv[u].w = *(const float *)(kr + 3 * a.k.nb[0]);
                 }
             }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int i = i0 + u * ngrp + grp;
-            double s = 0.0;
-            if (i < P) {
-                if (vec4) {
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) s += (double)__fmul_rn(kvv[u][e], qv[e]);
-                } else {
-                    const char * kr = kbase + (int64_t)i * a.k.nb[1];
-                    for (int e = 0; e < per_lane; ++e) {
-                        const int d = slot * per_lane + e;
-                        s += (double)__fmul_rn(*(const float *)(kr + (int64_t)d * a.k.nb[0]), qv[e < 8 ? e : 0]);
-                    }
-                }
-            }
-            part[u] = s;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            double s = part[u];
+        for (int u = 0; u < ATTN_UK; ++u) {
+            double s = (double)__fmul_rn(kvv[u].x, qv[0]);
+            s += (double)__fmul_rn(kvv[u].y, qv[1]);
+            s += (double)__fmul_rn(kvv[u].z, qv[2]);
+            s += (double)__fmul_rn(kvv[u].w, qv[3]);
             for (int off = G / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off);
             const int i = i0 + u * ngrp + grp;
             if (slot == 0 && i < P) s_p[i] = (float)s;
@@ -125,29 +113,74 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     for (int i = tid; i < P; i += ATTN_THREADS) s_p[i] = __fmul_rn(s_p[i], inv);
     __syncthreads();
 
-    // ---- phase C: out[d] = sum_i (f32)(p[i] * V[i,d]), f64 accumulation; lanes over i ----
+    // ---- phase C: out[d] = sum_i (f32)(p[i] * V[i,d]), f64 accumulation ----
+    // V rows (one per d) are contiguous in i: a lane owns 4 consecutive i (16-B loads) and the
+    // wave's DPW dims, so DPW x chunks loads are in flight per lane before the first FMA.
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
     float * orow = a.out + (((int64_t)b * a.n + t) * a.H + h) * hd;
     const int waves = ATTN_THREADS / 64;
-    for (int d0 = wave * 4; d0 < hd; d0 += waves * 4) {
-        double acc[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int i = lane; i < P; i += 64) {
-            const float p = s_p[i];
+    const bool vvec = a.v.nb[0] == 4 && (a.v.nb[1] % 16) == 0 && (((uintptr_t)vbase) % 16) == 0 &&
+                      a.v.nb[1] >= (int64_t)16 * ((P + 3) / 4);
+    if (vvec) {
+        constexpr int DPW = 4;  // dims per pass per wave
+        for (int d0 = wave * DPW; d0 < hd; d0 += waves * DPW) {
+            double acc[DPW] = {0.0, 0.0, 0.0, 0.0};
+            for (int i4 = lane * 4; i4 < P; i4 += 256 * 2) {
+                float4 vv[2][DPW];
+                float4 pp[2];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int d = d0 + u;
-                if (d < hd) {
-                    const float vv = *(const float *)(vbase + (int64_t)d * a.v.nb[1] + (int64_t)i * a.v.nb[0]);
-                    acc[u] += (double)__fmul_rn(p, vv);
+                for (int c = 0; c < 2; ++c) {
+                    const int ii = i4 + c * 256;
+                    pp[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int u = 0; u < DPW; ++u) vv[c][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (ii < P) {
+                        pp[c] = *(const float4 *)(s_p + ii);
+#pragma unroll
+                        for (int u = 0; u < DPW; ++u)
+                            if (d0 + u < hd) vv[c][u] = *(const float4 *)(vbase + (int64_t)(d0 + u) * a.v.nb[1] + (int64_t)ii * 4);
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ii = i4 + c * 256;
+#pragma unroll
+                    for (int u = 0; u < DPW; ++u) {
+                        // positions >= P (vector tail) contribute nothing, as in the scalar sum
+                        if (ii + 0 < P) acc[u] += (double)__fmul_rn(pp[c].x, vv[c][u].x);
+                        if (ii + 1 < P) acc[u] += (double)__fmul_rn(pp[c].y, vv[c][u].y);
+                        if (ii + 2 < P) acc[u] += (double)__fmul_rn(pp[c].z, vv[c][u].z);
+                        if (ii + 3 < P) acc[u] += (double)__fmul_rn(pp[c].w, vv[c][u].w);
+                    }
                 }
             }
-        }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double s = wave_sum_d(acc[u]);
-            if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+            for (int u = 0; u < DPW; ++u) {
+                const double s = wave_sum_d(acc[u]);
+                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+            }
+        }
+    } else {
+        for (int d0 = wave * 4; d0 < hd; d0 += waves * 4) {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int i = lane; i < P; i += 64) {
+                const float p = s_p[i];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int d = d0 + u;
+                    if (d < hd) {
+                        const float vv = *(const float *)(vbase + (int64_t)d * a.v.nb[1] + (int64_t)i * a.v.nb[0]);
+                        acc[u] += (double)__fmul_rn(p, vv);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double s = wave_sum_d(acc[u]);
+                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+            }
         }
     }
 }

@@ -7,6 +7,7 @@
 // Extension (batch > 1): B independent prompts stepped in lockstep share every weight GEMV
 // (M = B columns) while each keeps its own KV cache (attention gets a 4th "sequence" dim).
 // With batch == 1 the node list is exactly the reference's.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -46,6 +47,8 @@ struct tts_parler {
     int32_t position = 0;
     int32_t current_step = 0;
     int32_t last_nodes = 0;
+    double host_us[5] = {0, 0, 0, 0, 0};  // build, alloc, set_inputs, compute (enqueue), get (wait)
+    int64_t host_steps = 0;
     std::vector<std::vector<int32_t>> output_tokens;  // per sequence, flat [steps][heads]
     std::vector<std::vector<char>> eos_seen;
     uint64_t tensor_index = 0;
@@ -452,18 +455,31 @@ static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n)
 static int decode(tts_parler * p, const int32_t * tokens, bool audio, int n, float * logits) {
     const auto & cf = p->cfg;
     if (p->position + n > cf.max_ctx) return TTS_STATUS_BAD_ARG;
+    auto t0 = std::chrono::steady_clock::now();
     tts_tensor * out = build_graph(p, audio, n);
+    auto t1 = std::chrono::steady_clock::now();
     if (!run_graph(p, p->gctx)) return TTS_STATUS_ALLOC_FAILED;
+    auto t2 = std::chrono::steady_clock::now();
     p->res = out;
     p->last_nodes = (int32_t)p->gctx.nodes.size();
     if (set_inputs(p, tokens, audio, n) != 0) return TTS_STATUS_FAILED;
+    auto t3 = std::chrono::steady_clock::now();
     int st = p->be.compute(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size());
     if (st != 0) return st;
+    auto t4 = std::chrono::steady_clock::now();
     if (logits) {
         const size_t bytes = (size_t)cf.batch * n * cf.n_output_heads * cf.output_vocab * sizeof(float);
         st = p->be.get(p->be.ctx, logits, out->data, bytes);
         if (st != 0) return st;
     }
+    auto t5 = std::chrono::steady_clock::now();
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    p->host_us[0] += us(t0, t1);
+    p->host_us[1] += us(t1, t2);
+    p->host_us[2] += us(t2, t3);
+    p->host_us[3] += us(t3, t4);
+    p->host_us[4] += us(t4, t5);
+    p->host_steps += 1;
     p->position += n;
     return 0;
 }
@@ -526,6 +542,16 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
 }
 
 extern "C" int32_t tts_parler_position(const tts_parler * p) { return p->position; }
+
+extern "C" int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset) {
+    for (int i = 0; i < 5; ++i) us5[i] = p->host_us[i];
+    const int64_t n = p->host_steps;
+    if (reset) {
+        for (int i = 0; i < 5; ++i) p->host_us[i] = 0;
+        p->host_steps = 0;
+    }
+    return n;
+}
 extern "C" int32_t tts_parler_last_graph_nodes(const tts_parler * p) { return p->last_nodes; }
 extern "C" uint64_t tts_parler_weight_bytes(const tts_parler * p) { return p->wbytes; }
 

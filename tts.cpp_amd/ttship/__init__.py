@@ -139,6 +139,7 @@ def lib():
         "tts_parler_decode": (ctypes.c_int, [vp, vp, vp]),
         "tts_parler_generate": (ctypes.c_int, [vp, i32, vp]),
         "tts_parler_position": (i32, [vp]),
+        "tts_parler_host_stats": (i64, [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "tts_parler_last_graph_nodes": (i32, [vp]),
         "tts_parler_weight_bytes": (u64, [vp]),
         "tts_parler_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
@@ -266,6 +267,13 @@ class Parler:
 
     def last_graph_nodes(self):
         return self.L.tts_parler_last_graph_nodes(self.ptr)
+
+    def host_stats(self, reset=True):
+        """Mean host microseconds per step: build, alloc, set_inputs, compute enqueue, logits wait."""
+        us = (ctypes.c_double * 5)()
+        n = self.L.tts_parler_host_stats(self.ptr, us, 1 if reset else 0)
+        names = ["build", "alloc", "set_inputs", "compute_enqueue", "logits_wait"]
+        return {k: round(us[i] / max(n, 1), 1) for i, k in enumerate(names)}
 
     def node(self, i, cap=1 << 26):
         """(op, type, ne, float32 array or None) of node i of the last step graph (debugging)."""
