@@ -42,33 +42,67 @@ HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), t
 
 
 def prompt_tokens(batch, n, vocab, offset=0):
+    """Synthetic prompt ids; row b is global prompt (offset + b), so a rank's shard equals the
+    matching rows of the whole batch."""
     out = np.zeros((batch, n), dtype=np.int32)
     for b in range(batch):
-        s = HARVARD[(b + offset) % len(HARVARD)].encode()
+        g = b + offset
+        s = HARVARD[g % len(HARVARD)].encode()
         for i in range(n):
-            out[b, i] = (s[i % len(s)] * 131 + i * 7 + b) % vocab
+            out[b, i] = (s[i % len(s)] * 131 + i * 7 + g) % vocab
     return out
 
 
-def dist_init():
+def dist_init(backend="nccl"):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
         return rank, world, local, dist
     return rank, world, local, None
 
 
+def _comm_device(dist, local):
+    return f"cuda:{local}" if dist.get_backend() == "nccl" else "cpu"
+
+
 def barrier_sync(dist, be):
-    be.sync()
+    if be is not None:
+        be.sync()
     if dist is not None:
         import torch
         dist.barrier()
-        torch.cuda.synchronize()
+        if dist.get_backend() == "nccl":
+            torch.cuda.synchronize()
+
+
+def max_over_ranks(dist, local, dt):
+    """Wall time of the slowest rank (the job finishes when the last shard does)."""
+    if dist is None:
+        return dt
+    import torch
+    t = torch.tensor([dt], device=_comm_device(dist, local), dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_tokens(dist, rank, world, local, toks):
+    """The one cross-rank data exchange: every rank's codec tokens [batch, steps, heads] to rank 0,
+    concatenated along the prompt axis in global prompt order.  Returns None on ranks != 0."""
+    if dist is None:
+        return toks
+    import torch
+    g = torch.from_numpy(np.ascontiguousarray(toks).astype(np.int64)).to(_comm_device(dist, local))
+    parts = [torch.empty_like(g) for _ in range(world)] if rank == 0 else None
+    dist.gather(g, parts, dst=0)
+    if rank != 0:
+        return None
+    return np.concatenate([p.cpu().numpy() for p in parts], axis=0).astype(np.int32)
 
 
 def cpu_baseline(args, n_threads):
@@ -127,15 +161,8 @@ def main():
     barrier_sync(dist, be)
     dt = time.perf_counter() - t0
     host = runner.host_stats(reset=True)
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-        # final gather of every rank's codec tokens to rank 0 (the only cross-rank data exchange)
-        g = torch.from_numpy(toks.astype(np.int64)).to(f"cuda:{local}")
-        gathered = [torch.empty_like(g) for _ in range(world)] if rank == 0 else None
-        dist.gather(g, gathered, dst=0)
+    dt = max_over_ranks(dist, local, dt)
+    gather_tokens(dist, rank, world, local, toks)
 
     total_prompts = args.batch * world
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
