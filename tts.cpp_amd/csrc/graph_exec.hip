@@ -102,6 +102,11 @@ struct Item {
     std::vector<GemvTarget> tgt;
     int epi = EPI_NONE;
     const tts_tensor * res = nullptr;
+    // GEMV with a LayerNorm prologue (Q4_K): src1 = lndst = norm(lnx) * lnw (+ lnb)
+    bool ln = false;
+    const tts_tensor *lnx = nullptr, *lnw = nullptr, *lnb = nullptr, *lndst = nullptr;
+    float lneps = 0.f;
+    bool lnrms = false;
     // ATTN
     const tts_tensor *q = nullptr, *k = nullptr, *v = nullptr, *mask = nullptr, *out = nullptr;
     float scale = 1.f;
@@ -109,7 +114,6 @@ struct Item {
     const tts_tensor *x = nullptr, *w = nullptr, *b = nullptr, *dst = nullptr;
     float eps = 0.f;
     bool rms = false;
-    bool quant = false;
 };
 
 struct Planner {
@@ -164,6 +168,33 @@ struct Planner {
                 default: break;
             }
         }
+        if (mask & TTS_FUSE_LN) fuse_ln_into_gemv();
+    }
+
+    // An LN item directly followed by the Q4_K GEMV item that reads its output becomes that
+    // GEMV's prologue (every workgroup normalizes + quantizes the activation itself; workgroup 0
+    // still writes the LN output tensor).
+    void fuse_ln_into_gemv() {
+        for (int i = 0; i < n; ++i) {
+            const int a = act[i];
+            if (a <= 0 || items[a - 1].kind != Item::LN) continue;
+            const int nx = next_real(i);
+            if (nx < 0 || act[nx] <= 0) continue;
+            Item & L = items[a - 1];
+            Item & G = items[act[nx] - 1];
+            if (G.kind != Item::GEMV || G.ln || G.mms[0]->src[0]->type != TTS_TYPE_Q4_K || G.mms[0]->src[1] != L.dst) continue;
+            const int64_t K = L.dst->ne[0];
+            if (K % 256 || K > 4096) continue;
+            if (((uintptr_t)L.w->data & 15) || (L.b && ((uintptr_t)L.b->data & 15)) || (L.dst->nb[1] & 15)) continue;
+            G.ln = true;
+            G.lnx = L.x;
+            G.lnw = L.w;
+            G.lnb = L.b;
+            G.lndst = L.dst;
+            G.lneps = L.eps;
+            G.lnrms = L.rms;
+            act[i] = -1;
+        }
     }
 
     int add_item(Item && it) {
@@ -197,17 +228,6 @@ struct Planner {
         it.dst = A;
         it.eps = opf(N, 0);
         it.rms = N->op == TTS_OP_RMS_NORM;
-        // quantize in-kernel when the output feeds Q4_K GEMVs only as src1
-        bool q = ne0 % 256 == 0;
-        auto itc = consumers.find(A);
-        int n_q4 = 0;
-        if (itc != consumers.end()) {
-            for (int c : itc->second) {
-                const tts_tensor * cn = nodes[c];
-                if (cn->op == TTS_OP_MUL_MAT && cn->src[1] == A && cn->src[0]->type == TTS_TYPE_Q4_K) n_q4++;
-            }
-        }
-        it.quant = q && n_q4 > 0;
         act[i] = -1;
         if (A != M) act[index[M]] = -1;
         act[index[A]] = add_item(std::move(it));
@@ -462,8 +482,51 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it) {
         j.res = (const float *)it.res->data;
         j.rcs = (int64_t)(it.res->nb[1] / 4);
     }
-    int st = prepare_act(be, j.wtype, b, j.K, j.M, j.aq);
-    if (st) return st;
+    if (j.wtype == TTS_TYPE_Q4_K) {
+        // the kernel quantizes (and normalizes) src1 itself in every workgroup
+        j.pro = it.ln ? PRO_LN : PRO_QUANT;
+        if (it.ln) {
+            j.x = (const float *)it.lnx->data;
+            j.xcs = (int64_t)(it.lnx->nb[1] / 4);
+            j.lnw = (const float *)it.lnw->data;
+            j.lnb = it.lnb ? (const float *)it.lnb->data : nullptr;
+            j.eps = it.lneps;
+            j.rms = it.lnrms ? 1 : 0;
+            j.lnout = (float *)it.lndst->data;
+            j.locs = (int64_t)(it.lndst->nb[1] / 4);
+        }
+        // Outputs written while other workgroups still read src1 must not alias it (arena reuse can
+        // place an epilogue / LN output on memory whose last reader is this item).
+        auto span_y = [&](size_t k, const char *& y0, const char *& y1) {
+            const tts_tensor * mm = it.mms[k];
+            const int64_t Mm = mm->ne[1] * mm->ne[2] * mm->ne[3];
+            y0 = (const char *)it.tgt[k].y;
+            y1 = y0 + 4 * (size_t)((Mm - 1) * it.tgt[k].ycs + (mm->ne[0] - 1) * it.tgt[k].yrs + 1);
+        };
+        const char * x0 = (const char *)j.x;
+        const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
+        const char * l0 = (const char *)j.lnout;
+        const char * l1 = l0 ? l0 + 4 * (size_t)((j.M - 1) * j.locs + j.K) : nullptr;
+        bool x_hit = l0 && l0 < x1 && x0 < l1;
+        for (size_t k = 0; k < it.tgt.size(); ++k) {
+            const char *y0, *y1;
+            span_y(k, y0, y1);
+            x_hit |= y0 < x1 && x0 < y1;
+            if (l0 && y0 < l1 && l0 < y1) j.lnout = nullptr;  // LN output already dead: its memory is an output
+        }
+        // the prologue reads 16-B vectors: x 16-B aligned, columns 16-B strided (contiguous for PRO_QUANT)
+        x_hit |= ((uintptr_t)j.x & 15) != 0 || (j.xcs & 3) != 0 || (j.pro == PRO_QUANT && j.xcs != j.K);
+        if (x_hit) {
+            if ((size_t)(4 * j.K * j.M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+            launch_copy_cols(be, (float *)be->scratch, j.x, j.K, j.xcs, j.M);
+            be->aq.src = nullptr;
+            j.x = (const float *)be->scratch;
+            j.xcs = j.K;
+        }
+    } else {
+        int st = prepare_act(be, j.wtype, b, j.K, j.M, j.aq);
+        if (st) return st;
+    }
     // a Q4_K matrix in native layout goes through the one-matrix repack temp: launch it alone
     const bool tmp = a0->type == TTS_TYPE_Q4_K && !(a0->flags & TTS_FLAG_REPACKED);
     size_t k = 0;
@@ -509,20 +572,10 @@ static int run_item(tts_hip_backend * be, const Item & it) {
                                (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3]);
             return 0;
         }
-        case Item::LN: {
-            ActQuant * aqp = nullptr;
-            const int64_t K = it.dst->ne[0];
-            const int64_t M = it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3];
-            if (it.quant && act_quant_bytes(TTS_TYPE_Q4_K, K, M) <= be->scratch_size) {
-                act_quant_layout(TTS_TYPE_Q4_K, be->scratch, K, M, be->aq);
-                be->aq.src = it.dst->data;
-                be->aq.graph_epoch = be->graph_epoch;
-                aqp = &be->aq;
-            }
+        case Item::LN:
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms,
-                             aqp);
+                             nullptr);
             return 0;
-        }
     }
     return TTS_STATUS_FAILED;
 }
@@ -533,6 +586,12 @@ extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * 
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
     if (!be->use_graphs || be->profile_gemv) return graph_compute_launches(be, nodes, n_nodes);
+    // prompt-sized graphs (many activation columns) run once: launch them directly
+    for (int i = 0; i < n_nodes; ++i) {
+        const tts_tensor * t = nodes[i];
+        if (t->op == TTS_OP_MUL_MAT && t->src[1] && t->src[1]->ne[1] * t->src[1]->ne[2] * t->src[1]->ne[3] > 64)
+            return graph_compute_launches(be, nodes, n_nodes);
+    }
     // Record the step's launches into a HIP graph and replay it: the kernels then run back to
     // back on the device instead of at the host's launch rate.  Topology is stable from step to
     // step (only shapes/offsets move with the KV length), so the executable graph is updated in
@@ -591,9 +650,7 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
             bool keep = false;
             if (a > 0) {
                 const Item & it = pl.items[a - 1];
-                if (it.kind == Item::LN) {
-                    keep = it.quant && it.dst->data == be->aq.src;
-                } else if (it.kind == Item::GEMV) {
+                if (it.kind == Item::GEMV) {
                     keep = true;
                     for (size_t k = 0; k < it.tgt.size(); ++k) {
                         const char * y0 = (const char *)it.tgt[k].y;
@@ -633,7 +690,15 @@ extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, cons
     j.yrs[0] = 1;
     j.x = x;
     j.xcs = K;
-    if (type != TTS_TYPE_F32) {
+    if (type == TTS_TYPE_Q4_K) {
+        j.pro = PRO_QUANT;
+        if ((uintptr_t)x & 15) {  // the prologue reads 16-B vectors
+            if ((size_t)(4 * K * M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+            launch_copy_cols(be, (float *)be->scratch, x, K, K, M);
+            be->aq.src = nullptr;
+            j.x = (const float *)be->scratch;
+        }
+    } else if (type != TTS_TYPE_F32) {
         if (act_quant_bytes(type, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
         launch_quantize_act(be, type, x, K, K, M, j.aq);
     } else {

@@ -23,6 +23,7 @@ namespace tts {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short short2_t __attribute__((ext_vector_type(2)));
 
 // Tensor view handed to kernels by value: data pointer, shape and byte strides (ggml ne/nb).
 struct TD {
@@ -45,6 +46,62 @@ __device__ __forceinline__ float cr_tanhf(float x) { return (float)tanh((double)
 // result rounded to f32 is the correctly rounded f32 value (53 >= 2*24 + 2).
 __device__ __forceinline__ float cr_sqrtf(float x) { return (float)__dsqrt_rn((double)x); }
 __device__ __forceinline__ float cr_divf(float a, float b) { return (float)__ddiv_rn((double)a, (double)b); }
+
+// Compiler memory barrier placed after a batch of independent loads: keeps the compiler from
+// sinking a load into the (guarded) block that uses it, which would serialize the batch into one
+// full memory round trip per load.  Emits no instruction.
+#define TTS_PIN_LOADS() asm volatile("" ::: "memory")
+
+// ---- wave64 cross-lane helpers on DPP + readlane (no LDS crossbar, no lgkmcnt waits) ----
+// DPP controls (gfx9): quad_perm [1,0,3,2] = lane^1, [2,3,0,1] = lane^2, row_half_mirror (i <-> 7-i
+// in each 8), row_mirror (i <-> 15-i in each 16), row_shl:n (lane i reads lane i+n in its row).
+enum { DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_MIRROR = 0x140, DPP_ROW_SHL0 = 0x100 };
+template <int CTRL>
+__device__ __forceinline__ int dpp_i32(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+    return __int_as_float(dpp_i32<CTRL>(__float_as_int(v)));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i32<CTRL>((int)(b & 0xFFFFFFFF)), hi = dpp_i32<CTRL>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xFFFFFFFF), lane), hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// wave-uniform sum; every lane of a 16-lane row holds the same partial (a+b == b+a), the four row
+// partials are added in row order
+__device__ __forceinline__ double wave_sum_f64(double v) {
+    v += dpp_f64<DPP_XOR1>(v);
+    v += dpp_f64<DPP_XOR2>(v);
+    v += dpp_f64<DPP_HALF_MIRROR>(v);
+    v += dpp_f64<DPP_MIRROR>(v);
+    return ((readlane_f64(v, 0) + readlane_f64(v, 16)) + readlane_f64(v, 32)) + readlane_f64(v, 48);
+}
+// wave-uniform max of non-negative floats (compared as their bit patterns)
+__device__ __forceinline__ float wave_max_nonneg(float x) {
+    unsigned v = __float_as_uint(x);
+    v = max(v, (unsigned)dpp_i32<DPP_XOR1>((int)v));
+    v = max(v, (unsigned)dpp_i32<DPP_XOR2>((int)v));
+    v = max(v, (unsigned)dpp_i32<DPP_HALF_MIRROR>((int)v));
+    v = max(v, (unsigned)dpp_i32<DPP_MIRROR>((int)v));
+    const unsigned a = max((unsigned)__builtin_amdgcn_readlane((int)v, 0), (unsigned)__builtin_amdgcn_readlane((int)v, 16));
+    const unsigned b = max((unsigned)__builtin_amdgcn_readlane((int)v, 32), (unsigned)__builtin_amdgcn_readlane((int)v, 48));
+    return __uint_as_float(max(a, b));
+}
+// sum over the 8 lanes of an octet, result in all 8 lanes
+__device__ __forceinline__ int octet_sum_i32(int v) {
+    v += dpp_i32<DPP_XOR1>(v);
+    v += dpp_i32<DPP_XOR2>(v);
+    v += dpp_i32<DPP_HALF_MIRROR>(v);
+    return v;
+}
 #endif
 
 inline TD make_td(const tts_tensor * t) {
@@ -86,10 +143,35 @@ struct GemvJob {
     int64_t rcs = 0;
     int epi = EPI_NONE;
     const uint16_t * gelu = nullptr;
-    const float * x = nullptr;  // f32 activation (F32 weights)
+    const float * x = nullptr;  // f32 activation (F32 weights; Q4_K quantizes it in-kernel)
     int64_t xcs = 0;
     ActQuant aq;
+    // Q4_K prologue: PRO_QUANT = quantize x to Q8_K in LDS; PRO_LN = first x <- norm(x)*w (+b)
+    // (NORM/RMS_NORM -> MUL -> ADD, parler_build_layer_norm), written to lnout by workgroup 0.
+    int pro = 0;
+    const float * lnw = nullptr;
+    const float * lnb = nullptr;
+    float eps = 0.f;
+    int rms = 0;
+    float * lnout = nullptr;
+    int64_t locs = 0;
+    unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
 };
+// In-kernel phase timestamps (s_memrealtime, 100 MHz) per wave, compiled in only by the
+// micro-benchmark build (-DTTS_PHASE_TS): ts[(wg * waves + wave) * 8 + k].
+#ifdef TTS_PHASE_TS
+#define TTS_TS(job, k)                                                                                            \
+    do {                                                                                                          \
+        if ((job).ts && (threadIdx.x & 63) == 0)                                                                  \
+            (job).ts[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + \
+                     (k)] = __builtin_amdgcn_s_memrealtime();                                                     \
+    } while (0)
+#else
+#define TTS_TS(job, k) \
+    do {               \
+    } while (0)
+#endif
+enum { PRO_QUANT = 1, PRO_LN = 2 };
 
 }  // namespace tts
 
@@ -126,6 +208,7 @@ namespace tts {
 // Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
+void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
 // carve an ActQuant layout for weight type `wtype` out of `base` (no launch)
 void act_quant_layout(int wtype, char * base, int64_t K, int64_t M, ActQuant & aq);

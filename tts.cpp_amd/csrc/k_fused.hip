@@ -185,6 +185,160 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Decode attention for hd = 64 * DPR (Parler 64, Dia / Orpheus 128), same numerics as above, laid
+// out for latency: every reduction is a 16-lane DPP row reduction (no LDS crossbar), every load
+// batch is issued before its first use, and the only barriers are the two softmax reductions.
+//   A: a 16-lane row per key position (lane t: dims 4(t + 16c) .. +3, c < DPR), 32 positions per
+//      512-thread step, UK steps of loads in flight;
+//   B: soft_max_ext over the P scores in LDS;
+//   C: a 16-lane row per output dim (lane t: positions 4t + 64k as 16-B loads of the V row when
+//      VVEC, else scalar positions t + 16k), 32 dims per step.
+template <int DPR, bool VVEC>
+__global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    __shared__ float s_wf[ATTN_THREADS / 64];
+    __shared__ double s_wd[ATTN_THREADS / 64];
+    const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane >> 4, t = lane & 15;
+    const int P = a.P;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    constexpr int NW = ATTN_THREADS / 64;
+
+    // ---- A: kq[i] = sum_d (f32)(K[d,i] * q[d]) in f64 ----
+    float qv[DPR][4];
+#pragma unroll
+    for (int c = 0; c < DPR; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qv[c][e] = ((const float *)qbase)[4 * (t + 16 * c) + e];
+    constexpr int UK = 16 / DPR;
+    const int slot = wave * 4 + r;
+    for (int i0 = 0; i0 < P; i0 += 4 * NW * UK) {
+        float4 kv[UK][DPR];
+#pragma unroll
+        for (int u = 0; u < UK; ++u) {
+            const int i = min(i0 + u * 4 * NW + slot, P - 1);
+#pragma unroll
+            for (int c = 0; c < DPR; ++c) kv[u][c] = *(const float4 *)(kbase + (int64_t)i * a.k.nb[1] + 16 * (t + 16 * c));
+        }
+        TTS_PIN_LOADS();
+#pragma unroll
+        for (int u = 0; u < UK; ++u) {
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < DPR; ++c) {
+                s += (double)__fmul_rn(kv[u][c].x, qv[c][0]);
+                s += (double)__fmul_rn(kv[u][c].y, qv[c][1]);
+                s += (double)__fmul_rn(kv[u][c].z, qv[c][2]);
+                s += (double)__fmul_rn(kv[u][c].w, qv[c][3]);
+            }
+            s += dpp_f64<DPP_XOR1>(s);
+            s += dpp_f64<DPP_XOR2>(s);
+            s += dpp_f64<DPP_HALF_MIRROR>(s);
+            s += dpp_f64<DPP_MIRROR>(s);
+            const int i = i0 + u * 4 * NW + slot;
+            if (t == 0 && i < P) s_p[i] = (float)s;
+        }
+    }
+    __syncthreads();
+
+    // ---- B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum; p = e * (1/sum) ----
+    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    float mx = -INFINITY;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        float w = __fmul_rn(s_p[i], a.scale);
+        if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+        s_p[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    if (lane == 0) s_wf[wave] = mx;
+    __syncthreads();
+    mx = s_wf[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, s_wf[w]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        const float e = cr_expf(__fsub_rn(s_p[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_f64(sum);
+    if (lane == 0) s_wd[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += s_wd[w];
+    const float inv = (float)(1.0 / sum);
+    const int P4 = (P + 63) & ~63;
+    for (int i = tid; i < P4; i += ATTN_THREADS) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    __syncthreads();
+
+    // ---- C: out[d] = sum_i (f32)(p[i] * V[d,i]) in f64 ----
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    float * orow = a.out + (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    constexpr int UV = 8;
+    for (int d0 = wave * 4; d0 < a.hd; d0 += 4 * NW) {
+        const int d = d0 + r;
+        const char * vrow = vbase + (int64_t)d * a.v.nb[1];
+        double acc = 0.0;
+        if (VVEC) {
+            const int ilast = ((P - 1) >> 2) << 2;  // last 16-B chunk holding a position < P
+            for (int k0 = 0; k0 < P; k0 += 64 * UV) {
+                float4 vv[UV];
+#pragma unroll
+                for (int u = 0; u < UV; ++u) vv[u] = *(const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast));
+                TTS_PIN_LOADS();
+#pragma unroll
+                for (int u = 0; u < UV; ++u) {
+                    const int i = k0 + 64 * u + 4 * t;
+                    const float4 pp = *(const float4 *)(s_p + min(i, P4 - 4));
+                    // positions >= P (tail and clamped chunks) contribute nothing, as in the scalar sum
+                    acc += i + 0 < P ? (double)__fmul_rn(pp.x, vv[u].x) : 0.0;
+                    acc += i + 1 < P ? (double)__fmul_rn(pp.y, vv[u].y) : 0.0;
+                    acc += i + 2 < P ? (double)__fmul_rn(pp.z, vv[u].z) : 0.0;
+                    acc += i + 3 < P ? (double)__fmul_rn(pp.w, vv[u].w) : 0.0;
+                }
+            }
+        } else {
+            for (int k0 = 0; k0 < P; k0 += 16 * UV) {
+                float vv[UV];
+#pragma unroll
+                for (int u = 0; u < UV; ++u) vv[u] = *(const float *)(vrow + (int64_t)min(k0 + 16 * u + t, P - 1) * a.v.nb[0]);
+                TTS_PIN_LOADS();
+#pragma unroll
+                for (int u = 0; u < UV; ++u) {
+                    const int i = k0 + 16 * u + t;
+                    acc += i < P ? (double)__fmul_rn(s_p[min(i, P - 1)], vv[u]) : 0.0;
+                }
+            }
+        }
+        acc += dpp_f64<DPP_XOR1>(acc);
+        acc += dpp_f64<DPP_XOR2>(acc);
+        acc += dpp_f64<DPP_HALF_MIRROR>(acc);
+        acc += dpp_f64<DPP_MIRROR>(acc);
+        if (t == 0) orow[d] = (float)acc;
+    }
+}
+
+template <int DPR>
+static void launch_attn_rows(tts_hip_backend * be, const AttnArgs & a, bool vvec) {
+    const dim3 grid((unsigned)a.H, (unsigned)a.n, (unsigned)a.B);
+    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+}
+
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
                         float * out, int hd, int P, int H, int n, int B) {
     AttnArgs a;
@@ -199,6 +353,19 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
     a.H = H;
     a.n = n;
     a.B = B;
+    // row kernel: hd = 64/128/256, K rows 16-B vectors (aligned base and row stride)
+    const bool krows = (hd == 64 || hd == 128 || hd == 256) && k.nb[0] == 4 && (k.nb[1] % 16) == 0 &&
+                       (((uintptr_t)k.data) % 16) == 0 && (k.nb[2] % 16) == 0 &&
+                       (k.nb[3] % 16) == 0 && q.nb[0] == 4 && P > 0;
+    if (krows) {
+        const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
+                          (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
+        if (hd == 64) launch_attn_rows<1>(be, a, vvec);
+        else if (hd == 128) launch_attn_rows<2>(be, a, vvec);
+        else launch_attn_rows<4>(be, a, vvec);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(k_attn_decode, dim3((unsigned)H, (unsigned)n, (unsigned)B), dim3(ATTN_THREADS), 0, be->stream, a);
     TTS_HIP_CHECK(hipGetLastError());
 }

@@ -3,17 +3,14 @@
 // Replaces GGML_OP_MUL_MAT at every decode site (Parler model.cpp:544-546,571,583,594,601,603;
 // Dia model.cpp:535-537,...; Orpheus model.cpp:254-256,...).
 //
-// Numerics follow ggml-cpu: the activation column is first quantized to the weight type's
-// vec_dot_type (Q8_K for Q4_K, Q8_0 for Q8_0, F16 for F16) with the exact quantize_row_*_ref
-// arithmetic, the per-block integer dot products are exact (v_dot4_i32_i8), and each block is
-// combined in f32 as d*isum - dmin*imin.  F32/F16 dots take f32 products and accumulate them in
-// f64, as ggml_vec_dot_f32/f16 do.  Only the order of the f32 adds across blocks differs from
-// the CPU, so outputs agree to ~1e-6 relative (tests/test_gemv_parity.py).
+// Numerics are ggml-cpu's generic scalar paths, bit for bit: the activation column is quantized to
+// the weight type's vec_dot_type (Q8_K for Q4_K, Q8_0 for Q8_0, F16 for F16) with the exact
+// quantize_row_*_ref arithmetic, the per-block integer dot products are exact (v_dot4_i32_i8), and
+// the f32 combination follows vec_dot_*'s order exactly.  F32/F16 dots take f32 products and
+// accumulate them in f64, as ggml_vec_dot_f32/f16 do (tests/test_gemv_gpu.py: bit-exact).
 //
-// Memory shape (HBM-bound): one 8-lane octet owns one 144-B Q4_K block per step: lane t loads
-// the 16-B block header and 16 B of nibbles (dwordx4), so a wave streams 8 blocks = 1152 B per
-// load pair; rows are owned by octet groups, the activation (int8, L1/L2-resident) is re-read
-// per column.  No LDS round trip: the weight stream is read once (guide §5 'GEMV / M <= 16').
+// Memory shape (HBM-bound): weights stream once with 16-B non-temporal loads; the activation of a
+// launch is staged in LDS per workgroup (Q4_K: quantized in-kernel, optionally after LayerNorm).
 #include "hip_internal.h"
 
 namespace tts {
@@ -135,21 +132,7 @@ __global__ void k_quantize_f16(const float * __restrict__ x, int64_t xcs, int64_
     if (i < K) out[m * K + i] = __float2half_rn(x[m * xcs + i]);
 }
 
-// ------------------------------------------------------------------------------------------
-// Q4_K x Q8_K GEMV on repacked weights, reproducing ggml_vec_dot_q4_K_q8_K's generic f32 order
-// exactly: per (row, column), blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7),
-// sumf -= dmin*sumi, then sumf += sums[0..7].
-//
-// One workgroup (256 threads) owns RW consecutive rows of one matrix (gridDim.y = matrices that
-// share the activation, e.g. q/k/v).  Three phases:
-//   0. issue the first weight loads (registers), stage the Q8_K activation of all M columns
-//      in LDS (one HBM/L2 read per workgroup instead of one per octet);
-//   1. integer phase: an octet (8 lanes) per (row, block) pair: lane l's 16-B load holds the
-//      nibbles of residue l (lane layout), 8 x v_dot4_i32_i8 give aux32[l] per column; results,
-//      d*yd and dmin*yd go to LDS;
-//   2. ordered f32 phase: lane = (column m, residue l) walks the row's blocks in order; lane l=0
-//      also carries sumf; one 8-lane fold in order l = 0..7 ends the row.
-// The weight stream is read once with 16-B non-temporal loads; everything else is on-chip.
+// get_scale_min_k4: 6-bit scale and min of sub-block j from the 12 packed bytes
 __device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc, int & mn) {
     if (j < 4) {
         sc = q[j] & 63;
@@ -173,128 +156,299 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
     j.Y[mat][m * j.ycs[mat] + row * j.yrs[mat]] = v;
 }
 
-constexpr int Q4K_PMAX = 4;  // (row, block) pairs an octet keeps in flight
+// quantize_row_q8_K_ref for four 256-element blocks per wave: the 16-lane row r = lane >> 4 owns
+// one block, lane t = lane & 15 its elements 16t..16t+15.  max |x| at its first index (strict '>'
+// from 0, as ggml), iscale = -127/x[imax], q = min(127, nearest_int(iscale*x)), d = 1/iscale.
+// Writes the lane-major LDS layout (element p = 64c + 32hi + 8k + l at byte l*32 + hi*16 + c*4 + k;
+// elements 16t+e and 16t+e+8 are adjacent bytes), d and the eight per-32 sums as int16.  All
+// reductions stay inside the row (DPP); the code is branch-free so the compiler can interleave it
+// with neighbouring work.
+__device__ __forceinline__ void q8k_row_block(const float (&v)[16], int lane, int8_t * xq, float * xd, int16_t * xs) {
+    const int t = lane & 15;
+    float lax = 0.f, lval = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const float a = fabsf(v[e]);
+        const bool gt = a > lax;
+        lax = gt ? a : lax;
+        lval = gt ? v[e] : lval;
+    }
+    unsigned mx = __float_as_uint(lax);  // non-negative floats order as their bit patterns
+    mx = max(mx, (unsigned)dpp_i32<DPP_XOR1>((int)mx));
+    mx = max(mx, (unsigned)dpp_i32<DPP_XOR2>((int)mx));
+    mx = max(mx, (unsigned)dpp_i32<DPP_HALF_MIRROR>((int)mx));
+    mx = max(mx, (unsigned)dpp_i32<DPP_MIRROR>((int)mx));
+    const float ax = __uint_as_float(mx);
+    const unsigned long long hit = __ballot(lax == ax);
+    const unsigned rowbits = (unsigned)(hit >> (lane & 48)) & 0xFFFFu;
+    const float val = __shfl(lval, (lane & 48) + (rowbits ? __ffs(rowbits) - 1 : 0));
+    const bool nz = ax != 0.f;
+    const float iscale = nz ? cr_divf(-127.f, val) : 0.f;  // iscale 0 quantizes everything to 0
+    const float d = nz ? cr_divf(1.f, iscale) : 0.f;
+    int q[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) q[e] = min(dev_nearest_int(__fmul_rn(iscale, v[e])), 127);
+    const int base = ((t >> 1) & 1) * 16 + (t >> 2) * 4 + ((2 * t) & 3);
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        *(int16_t *)(xq + e * 32 + base) = (int16_t)((q[e] & 0xFF) | ((q[e + 8] & 0xFF) << 8));
+    int s = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += q[e];
+    s += dpp_i32<DPP_XOR1>(s);  // elements 32j..32j+31 = lanes 2j, 2j+1
+    if ((t & 1) == 0) xs[t >> 1] = (int16_t)s;
+    if (t == 0) *xd = d;
+}
 
-template <int MC>
-__global__ __launch_bounds__(256) void k_gemv_q4_K(GemvJob j, int RW) {
+// Loads are unconditional (addresses clamped into range) so that a wave issues all of them before
+// the first use: a load under a guard is sunk next to its use, and every block then pays a full
+// L2 round trip (measured: 0.4 us per block).  The launcher guarantees 16-B aligned x / lnw / lnb
+// and, for PRO_QUANT, contiguous columns (xcs == K).
+__device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
+    const float4 t = *(const float4 *)p;
+    v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
+}
+
+// Prologue: the Q8_K activation of all M columns into LDS, optionally after LayerNorm / RMSNorm
+// with affine (ggml_compute_forward_norm_f32 / rms_norm_f32: f64 sums, mean and variance rounded
+// to f32, scale = 1/sqrtf(var + eps), then MUL(w) and ADD(b) each rounded).
+template <int PRO, int NCH>
+__device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int r = lane >> 4, t = lane & 15;
+    const int M = (int)j.M;
+    const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
+    if (PRO == PRO_QUANT) {
+        // pass p quantizes blocks 4p..4p+3 (block qb = column m, chunk b at x + qb*256)
+        constexpr int QP = NCH <= 4 ? 2 : 4;  // passes whose loads a wave keeps in flight
+        const int nq = M * nb, npass = (nq + 3) / 4;
+        auto batch = [&](int p0) {
+            float v[QP][16];
+#pragma unroll
+            for (int u = 0; u < QP; ++u) {
+                const int qb = min(4 * min(p0 + u * nw, npass - 1) + r, nq - 1);
+                const float * src = j.x + (int64_t)qb * QK_K + 16 * t;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ld4(src + 4 * k, *(float (*)[4]) & v[u][4 * k]);
+            }
+            TTS_PIN_LOADS();
+#pragma unroll
+            for (int u = 0; u < QP; ++u) {
+                const int p = p0 + u * nw, qb = 4 * p + r;
+                const int slot = (p < npass && qb < nq) ? qb : trash;
+                q8k_row_block(v[u], lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
+            }
+        };
+        // the first batch is peeled out of the loop: a loop header makes the compiler wait for every
+        // outstanding load, including the weight loads issued before the prologue
+        batch(wave);
+        for (int p0 = wave + nw * QP; p0 < npass; p0 += nw * QP) batch(p0);
+    } else {
+        // one column per wave; pass p holds chunks 4p + r (K <= 4096: NP <= 4, host-checked).  For
+        // K <= 1024 the affine parameters are loaded with x, so the prologue pays one L2 round trip.
+        constexpr int NP = (NCH + 3) / 4;
+        constexpr bool PRE = NCH <= 4;
+        const double Kd = (double)j.K;
+        const bool write = j.lnout && blockIdx.x == 0 && blockIdx.y == 0;
+        const float * lnb = j.lnb ? j.lnb : j.lnw;
+        float wp[PRE ? NP : 1][16], bp[PRE ? NP : 1][16];
+        if (PRE) {
+#pragma unroll
+            for (int p = 0; p < (PRE ? NP : 1); ++p) {
+                const int off = min(4 * p + r, nb - 1) * QK_K + 16 * t;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    ld4(j.lnw + off + 4 * k, *(float (*)[4]) & wp[p][4 * k]);
+                    ld4(lnb + off + 4 * k, *(float (*)[4]) & bp[p][4 * k]);
+                }
+            }
+        }
+        auto column = [&](int m) {
+            const float * xr = j.x + m * j.xcs;
+            float v[NP][16];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const int off = min(4 * p + r, nb - 1) * QK_K + 16 * t;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) ld4(xr + off + 4 * k, *(float (*)[4]) & v[p][4 * k]);
+            }
+            TTS_PIN_LOADS();
+            float mean = 0.f;
+            if (!j.rms) {
+                double s = 0.0;
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    double sp = 0.0;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) sp += (double)v[p][e];
+                    s += 4 * p + r < nb ? sp : 0.0;
+                }
+                mean = (float)(wave_sum_f64(s) / Kd);
+            }
+            double s2 = 0.0;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                double sp = 0.0;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const float d = j.rms ? v[p][e] : __fsub_rn(v[p][e], mean);
+                    sp += (double)__fmul_rn(d, d);
+                }
+                s2 += 4 * p + r < nb ? sp : 0.0;
+            }
+            const float var = (float)(wave_sum_f64(s2) / Kd);
+            const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(var, j.eps)));
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                float w16[16], b16[16];
+                const int off = min(4 * p + r, nb - 1) * QK_K + 16 * t;
+                if (PRE) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) w16[e] = wp[PRE ? p : 0][e], b16[e] = bp[PRE ? p : 0][e];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        ld4(j.lnw + off + 4 * k, *(float (*)[4]) & w16[4 * k]);
+                        ld4(lnb + off + 4 * k, *(float (*)[4]) & b16[4 * k]);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    float y = j.rms ? __fmul_rn(v[p][e], scale) : __fmul_rn(__fsub_rn(v[p][e], mean), scale);
+                    y = __fmul_rn(y, w16[e]);
+                    if (j.lnb) y = __fadd_rn(y, b16[e]);
+                    v[p][e] = y;
+                }
+                const bool valid = 4 * p + r < nb;
+                if (write && valid) {
+                    float * o = j.lnout + m * j.locs + off;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) *(float4 *)(o + 4 * k) = make_float4(v[p][4 * k], v[p][4 * k + 1], v[p][4 * k + 2], v[p][4 * k + 3]);
+                }
+                const int slot = valid ? m * nb + 4 * p + r : trash;
+                q8k_row_block(v[p], lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
+            }
+        };
+        if (wave < M) column(wave);  // peeled, as above
+        for (int m = wave + nw; m < M; m += nw) column(m);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Q4_K x Q8_K GEMV on repacked weights, reproducing ggml_vec_dot_q4_K_q8_K's generic f32 order
+// exactly: per (row, column), blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7),
+// sumf -= dmin*sumi, then sumf += sums[0..7].
+//
+// Lane mapping (wave64): lane = (row slot s, column m, residue l) with 8/MC row slots, so a wave
+// covers 8/MC rows x MC columns and every lane does one (row, column, residue) triple: lane l
+// of the octet loads the block header and, as one 16-B load, exactly the nibbles ggml folds
+// into aux32[l] (lane layout, tts_repack_q4_K); the eight sdot4 results times the 6-bit scales
+// are aux32[l]; the lane keeps sums[l] in a register across blocks in ascending order and
+// every lane of the octet carries sumf, so the exact order costs no LDS round trip.
+// Prologue (same workgroup): the activation is quantized to Q8_K straight into LDS, after an
+// optional LayerNorm; the first row's weight loads are issued before it so the HBM latency
+// overlaps the prologue.
+template <int MC, int PRO, int NBMAX>
+__global__ __launch_bounds__(512) void k_gemv_q4_K(GemvJob j) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
     const int mat = blockIdx.y;
     const uint8_t * __restrict__ W = j.W[mat];
-    float * Y = j.Y[mat];
-    const int64_t row0 = (int64_t)blockIdx.x * RW;
-    const int rows = (int)((j.N - row0) < RW ? (j.N - row0) : RW);
-    const int M = j.M;
     int8_t * xq_s = (int8_t *)smem;
-    float * xd_s = (float *)(smem + al16((size_t)MC * j.K));
-    int * xs_s = (int *)((char *)xd_s + al16(sizeof(float) * MC * nb));
-    int * aux_s = (int *)((char *)xs_s + al16(sizeof(int) * MC * nb * 8));
-    float * dd_s = (float *)((char *)aux_s + al16(sizeof(int) * (size_t)RW * nb * MC * 8));
-    float * dm_s = dd_s + (size_t)RW * nb * MC;
-    int * sm_s = (int *)(dm_s + (size_t)RW * nb * MC);
+    const int nslot = MC * nb + 1;  // + the prologue's trash slot
+    float * xd_s = (float *)(smem + al16((size_t)nslot * QK_K));
+    int16_t * xs_s = (int16_t *)((char *)xd_s + al16(sizeof(float) * nslot));
 
-    const int octet = threadIdx.x >> 3, l = threadIdx.x & 7;
-    const int npairs = rows * nb;
-    // phase 0a: first batch of weight loads
-    u32x4 hdr[Q4K_PMAX], q[Q4K_PMAX];
+    constexpr int S = 8 / MC;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int l = lane & 7, m = (lane >> 3) % MC, s = lane / (8 * MC);
+    const int64_t G = (j.N + S - 1) / S;
+    const int64_t gstride = (int64_t)gridDim.x * nw;
+    int64_t g = (int64_t)blockIdx.x * nw + wave;
+
+    u32x4 hdr[NBMAX], q[NBMAX];
+    auto load_row = [&](int64_t gg, int b0) {
+        int64_t row = gg * S + s;
+        row = row < j.N ? row : j.N - 1;
+        const uint8_t * wr = W + row * j.w_row_bytes;
 #pragma unroll
-    for (int i = 0; i < Q4K_PMAX; ++i) {
-        const int p = octet + 32 * i;
-        if (p < npairs) {
-            const uint8_t * bp = W + (row0 + p / nb) * j.w_row_bytes + (int64_t)(p % nb) * 144;
-            hdr[i] = __builtin_nontemporal_load((const u32x4 *)bp);
-            q[i] = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
+        for (int u = 0; u < NBMAX; ++u) {  // unconditional (clamped) so all loads issue before use
+            const int64_t bo = (int64_t)min(b0 + u, nb - 1) * 144;
+            hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
+            q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
         }
-    }
-    // phase 0b: activation -> LDS
-    {
-        const int4 * src = (const int4 *)j.aq.qs;
-        int4 * dst = (int4 *)xq_s;
-        const int n16 = (int)((int64_t)M * j.K / 16);
-        for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
-        for (int i = threadIdx.x; i < M * nb; i += 256) xd_s[i] = j.aq.d[i];
-        for (int i = threadIdx.x; i < M * nb * 8; i += 256) xs_s[i] = j.aq.bsums[i];
-    }
+        TTS_PIN_LOADS();
+    };
+    // short rows: the first row's weights are in flight during the prologue; long rows (NBMAX 16)
+    // would need more registers than the prologue leaves, so they start after it
+    TTS_TS(j, 0);
+    if (NBMAX <= 4 && g < G) load_row(g, 0);
+    TTS_TS(j, 1);
+    q4k_prologue<PRO, NBMAX>(j, nb, xq_s, xd_s, xs_s);
+    TTS_TS(j, 2);
     __syncthreads();
-    // phase 1: integer work per (row, block) pair
-    for (int base = 0; base < npairs; base += 32 * Q4K_PMAX) {
-        if (base > 0) {
-#pragma unroll
-            for (int i = 0; i < Q4K_PMAX; ++i) {
-                const int p = base + octet + 32 * i;
-                if (p < npairs) {
-                    const uint8_t * bp = W + (row0 + p / nb) * j.w_row_bytes + (int64_t)(p % nb) * 144;
-                    hdr[i] = __builtin_nontemporal_load((const u32x4 *)bp);
-                    q[i] = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
-                }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < Q4K_PMAX; ++i) {
-            const int p = base + octet + 32 * i;
-            if (p >= npairs) break;  // octet-uniform
-            const int r = p / nb, b = p % nb;
-            const uint32_t sw[3] = {hdr[i].y, hdr[i].z, hdr[i].w};
-            const uint8_t * scb = (const uint8_t *)sw;
-            int sc[8], mymin, tmp;
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) q4k_scale_min(scb, jj, sc[jj], tmp);
-            q4k_scale_min(scb, l, tmp, mymin);
-            const int lo0 = (int)(q[i].x & 0x0F0F0F0Fu), lo1 = (int)(q[i].y & 0x0F0F0F0Fu);
-            const int lo2 = (int)(q[i].z & 0x0F0F0F0Fu), lo3 = (int)(q[i].w & 0x0F0F0F0Fu);
-            const int hi0 = (int)((q[i].x >> 4) & 0x0F0F0F0Fu), hi1 = (int)((q[i].y >> 4) & 0x0F0F0F0Fu);
-            const int hi2 = (int)((q[i].z >> 4) & 0x0F0F0F0Fu), hi3 = (int)((q[i].w >> 4) & 0x0F0F0F0Fu);
-            const float dw = dev_fp16_to_fp32((uint16_t)(hdr[i].x & 0xFFFF));
-            const float dmw = dev_fp16_to_fp32((uint16_t)(hdr[i].x >> 16));
-#pragma unroll
-            for (int m = 0; m < MC; ++m) {
-                if (m >= M) break;
-                const int xb = m * nb + b;
-                const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
-                const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
-                int aux = sc[0] * __builtin_amdgcn_sdot4(lo0, xl.x, 0, false);
-                aux += sc[2] * __builtin_amdgcn_sdot4(lo1, xl.y, 0, false);
-                aux += sc[4] * __builtin_amdgcn_sdot4(lo2, xl.z, 0, false);
-                aux += sc[6] * __builtin_amdgcn_sdot4(lo3, xl.w, 0, false);
-                aux += sc[1] * __builtin_amdgcn_sdot4(hi0, xh.x, 0, false);
-                aux += sc[3] * __builtin_amdgcn_sdot4(hi1, xh.y, 0, false);
-                aux += sc[5] * __builtin_amdgcn_sdot4(hi2, xh.z, 0, false);
-                aux += sc[7] * __builtin_amdgcn_sdot4(hi3, xh.w, 0, false);
-                int smin = mymin * xs_s[xb * 8 + l];
-                smin += __shfl_xor(smin, 1);
-                smin += __shfl_xor(smin, 2);
-                smin += __shfl_xor(smin, 4);
-                const int o = (r * nb + b) * MC + m;
-                aux_s[o * 8 + l] = aux;
-                if (l == 0) {
-                    const float yd = xd_s[xb];
-                    dd_s[o] = __fmul_rn(dw, yd);
-                    dm_s[o] = __fmul_rn(dmw, yd);
-                    sm_s[o] = smin;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    // phase 2: ordered f32 accumulation, lane = (m, l)
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int m = lane >> 3, l2 = lane & 7;
-    for (int r = wave; r < rows; r += 4) {
+    TTS_TS(j, 3);
+    if (NBMAX > 4 && g < G) load_row(g, 0);
+
+    for (; g < G; g += gstride) {
         float sums = 0.f, sumf = 0.f;
-        if (m < M) {
-            for (int b = 0; b < nb; ++b) {
-                const int o = (r * nb + b) * MC + m;
-                sums = __fadd_rn(sums, __fmul_rn(dd_s[o], (float)aux_s[o * 8 + l2]));
-                if (l2 == 0) sumf = __fsub_rn(sumf, __fmul_rn(dm_s[o], (float)sm_s[o]));
+        for (int b0 = 0; b0 < nb; b0 += NBMAX) {
+            if (b0 > 0) load_row(g, b0);
+#pragma unroll
+            for (int u = 0; u < NBMAX; ++u) {  // branch-free: padding blocks compute and are discarded
+                const bool valid = b0 + u < nb;
+                const int b = min(b0 + u, nb - 1);
+                const uint32_t A = hdr[u].y, B = hdr[u].z, C = hdr[u].w;
+                // 6-bit scales / mins of the eight 32-element sub-blocks, four per word (get_scale_min_k4)
+                const uint32_t sc_lo = A & 0x3F3F3F3Fu, mn_lo = B & 0x3F3F3F3Fu;
+                const uint32_t sc_hi = (C & 0x0F0F0F0Fu) | ((A >> 2) & 0x30303030u);
+                const uint32_t mn_hi = ((C >> 4) & 0x0F0F0F0Fu) | ((B >> 2) & 0x30303030u);
+                const int xb = m * nb + b;
+                const int4 xl = *(const int4 *)(xq_s + (int64_t)xb * QK_K + l * 32);
+                const int4 xh = *(const int4 *)(xq_s + (int64_t)xb * QK_K + l * 32 + 16);
+                const uint32_t w0 = q[u].x, w1 = q[u].y, w2 = q[u].z, w3 = q[u].w;
+                int aux = (int)(sc_lo & 0xFF) * __builtin_amdgcn_sdot4((int)(w0 & 0x0F0F0F0Fu), xl.x, 0, false);
+                aux += (int)((sc_lo >> 8) & 0xFF) * __builtin_amdgcn_sdot4((int)((w0 >> 4) & 0x0F0F0F0Fu), xh.x, 0, false);
+                aux += (int)((sc_lo >> 16) & 0xFF) * __builtin_amdgcn_sdot4((int)(w1 & 0x0F0F0F0Fu), xl.y, 0, false);
+                aux += (int)(sc_lo >> 24) * __builtin_amdgcn_sdot4((int)((w1 >> 4) & 0x0F0F0F0Fu), xh.y, 0, false);
+                aux += (int)(sc_hi & 0xFF) * __builtin_amdgcn_sdot4((int)(w2 & 0x0F0F0F0Fu), xl.z, 0, false);
+                aux += (int)((sc_hi >> 8) & 0xFF) * __builtin_amdgcn_sdot4((int)((w2 >> 4) & 0x0F0F0F0Fu), xh.z, 0, false);
+                aux += (int)((sc_hi >> 16) & 0xFF) * __builtin_amdgcn_sdot4((int)(w3 & 0x0F0F0F0Fu), xl.w, 0, false);
+                aux += (int)(sc_hi >> 24) * __builtin_amdgcn_sdot4((int)((w3 >> 4) & 0x0F0F0F0Fu), xh.w, 0, false);
+                // sumi = sum_j mins[j] * bsum32[j] (int16 pairs, v_dot2)
+                const int4 bs = *(const int4 *)(xs_s + xb * 8);
+                const int mn01 = (int)((mn_lo & 0xFF) | ((mn_lo & 0xFF00) << 8));
+                const int mn23 = (int)(((mn_lo >> 16) & 0xFF) | ((mn_lo >> 8) & 0xFF0000));
+                const int mn45 = (int)((mn_hi & 0xFF) | ((mn_hi & 0xFF00) << 8));
+                const int mn67 = (int)(((mn_hi >> 16) & 0xFF) | ((mn_hi >> 8) & 0xFF0000));
+                int sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn01), __builtin_bit_cast(short2_t, bs.x), 0, false);
+                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn23), __builtin_bit_cast(short2_t, bs.y), sumi, false);
+                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn45), __builtin_bit_cast(short2_t, bs.z), sumi, false);
+                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn67), __builtin_bit_cast(short2_t, bs.w), sumi, false);
+                const float yd = xd_s[xb];
+                const float dw = dev_fp16_to_fp32((uint16_t)(hdr[u].x & 0xFFFF));
+                const float dmw = dev_fp16_to_fp32((uint16_t)(hdr[u].x >> 16));
+                const float ns = __fadd_rn(sums, __fmul_rn(__fmul_rn(dw, yd), (float)aux));
+                const float nf = __fsub_rn(sumf, __fmul_rn(__fmul_rn(dmw, yd), (float)sumi));
+                sums = valid ? ns : sums;
+                sumf = valid ? nf : sumf;
             }
         }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float v = __shfl(sums, (lane & ~7) + k);
-            if (l2 == 0) sumf = __fadd_rn(sumf, v);
-        }
-        if (l2 == 0 && m < M) gemv_store<MC>(j, mat, row0 + r, m, sumf);
+        // sumf += sums[0..7] in order; lane l = 0 of the octet reads lane l = k by row_shl:k
+        float tot = __fadd_rn(sumf, sums);
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 1>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 2>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 3>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 4>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 5>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 6>(sums));
+        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 7>(sums));
+        const int64_t row = g * S + s;
+        TTS_TS(j, 4);
+        if (l == 0 && m < j.M && row < j.N) gemv_store<MC>(j, mat, row, m, tot);
+        if (g + gstride < G) load_row(g + gstride, 0);
     }
+    TTS_TS(j, 5);
 }
 
 // Q8_0 x Q8_0 GEMV reproducing ggml_vec_dot_q8_0_q8_0's generic order: per (row, column),
@@ -461,16 +615,69 @@ void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+__global__ void k_copy_cols(float * __restrict__ dst, const float * __restrict__ src, int64_t K, int64_t scs) {
+    const int64_t m = blockIdx.y;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < K; i += (int64_t)gridDim.x * blockDim.x)
+        dst[m * K + i] = src[m * scs + i];
+}
+
+void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M) {
+    const unsigned gx = (unsigned)((K + 255) / 256 < 64 ? (K + 255) / 256 : 64);
+    hipLaunchKernelGGL(k_copy_cols, dim3(gx, (unsigned)M), dim3(256), 0, be->stream, dst, src, K, scs);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int64_t nblocks, int inverse) {
     const unsigned grid = (unsigned)((nblocks + 1) / 2);
     hipLaunchKernelGGL(k_repack_q4_K, dim3(grid), dim3(256), 0, be->stream, (const uint8_t *)src, (uint8_t *)dst, nblocks, inverse);
     TTS_HIP_CHECK(hipGetLastError());
 }
 
-static size_t q4k_lds(int MC, int64_t K, int RW) {
+static size_t q4k_lds(int MC, int64_t K) {
     const int64_t nb = K / QK_K;
     auto a = [](size_t n) { return (n + 15) & ~(size_t)15; };
-    return a((size_t)MC * K) + a(4 * MC * nb) + a(4 * MC * nb * 8) + a(4 * (size_t)RW * nb * MC * 8) + 3 * 4 * (size_t)RW * nb * MC;
+    const size_t nslot = (size_t)MC * nb + 1;  // kernel: + one trash slot for padding rows
+    return a(nslot * QK_K) + a(4 * nslot) + 16 * nslot;
+}
+
+// columns per Q4_K launch: the whole Q8_K activation of a launch lives in LDS
+static int64_t q4k_max_cols(int64_t K) {
+    const int64_t c = (int64_t)(144 * 1024) / (K + 80);
+    return c >= 8 ? 8 : c >= 4 ? 4 : c >= 2 ? 2 : 1;
+}
+
+template <int MC, int PRO, int NBMAX>
+static void launch_q4k(tts_hip_backend * be, const GemvJob & j, unsigned gx, int nw, size_t lds) {
+    static bool attr_set = false;
+    if (lds > 64 * 1024 && !attr_set) {
+        TTS_HIP_CHECK(hipFuncSetAttribute((const void *)k_gemv_q4_K<MC, PRO, NBMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          160 * 1024));
+        attr_set = true;
+    }
+    hipLaunchKernelGGL((k_gemv_q4_K<MC, PRO, NBMAX>), dim3(gx, (unsigned)j.nmat), dim3(64 * nw), lds, be->stream, j);
+}
+
+// Grid: every workgroup pays the prologue (normalize / quantize the whole activation), so the
+// grid is capped near one workgroup per CU and waves loop over row groups; up to 8 waves per
+// workgroup (one LN column each at M = 8).
+template <int MC>
+static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
+    constexpr int S = 8 / MC;
+    const int64_t G = (j.N + S - 1) / S;  // wave row-groups
+    int nw = 8;
+    while (nw > 1 && ((G + nw - 1) / nw) * j.nmat < 256) nw /= 2;
+    int64_t gx = (G + nw - 1) / nw;
+    const int64_t cap = (512 + j.nmat - 1) / j.nmat;  // ~2 workgroups per CU
+    if (gx > cap) gx = cap;
+    const size_t lds = q4k_lds(MC, j.K);
+    const bool small = j.K <= 4 * QK_K;
+    if (j.pro == PRO_LN) {
+        if (small) launch_q4k<MC, PRO_LN, 4>(be, j, (unsigned)gx, nw, lds);
+        else launch_q4k<MC, PRO_LN, 16>(be, j, (unsigned)gx, nw, lds);
+    } else {
+        if (small) launch_q4k<MC, PRO_QUANT, 4>(be, j, (unsigned)gx, nw, lds);
+        else launch_q4k<MC, PRO_QUANT, 16>(be, j, (unsigned)gx, nw, lds);
+    }
 }
 static size_t q80_lds(int MC, int64_t K, int RW) {
     const int64_t nb = K / QK8_0;
@@ -482,13 +689,7 @@ template <int MC>
 static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
     const unsigned nmat = (unsigned)j.nmat;
     switch (j.wtype) {
-        case TTS_TYPE_Q4_K: {
-            int RW = 8;
-            while (RW > 1 && q4k_lds(MC, j.K, RW) > 64 * 1024) RW /= 2;
-            const size_t lds = q4k_lds(MC, j.K, RW);
-            const unsigned grid = (unsigned)((j.N + RW - 1) / RW);
-            hipLaunchKernelGGL(k_gemv_q4_K<MC>, dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
-        } break;
+        case TTS_TYPE_Q4_K: launch_gemv_q4k_mc<MC>(be, j); break;
         case TTS_TYPE_Q8_0: {
             int RW = 8;
             while (RW > 1 && q80_lds(MC, j.K, RW) > 64 * 1024) RW /= 2;
@@ -526,10 +727,12 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (be->profile_gemv) profile_begin(be, e0, e1);
     const int64_t K = job.K;
-    for (int64_t m0 = 0; m0 < job.M; m0 += 8) {
-        const int64_t mc = job.M - m0 < 8 ? job.M - m0 : 8;
+    const int64_t cmax = job.wtype == TTS_TYPE_Q4_K ? q4k_max_cols(K) : 8;
+    for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {
+        const int64_t mc = job.M - m0 < cmax ? job.M - m0 : cmax;
         GemvJob j = job;
         j.M = mc;
+        if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
         if (job.aq.vtype == TTS_TYPE_Q8_K) {
             j.aq.qs = job.aq.qs + m0 * K;
             j.aq.d = job.aq.d + m0 * (K / QK_K);
