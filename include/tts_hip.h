@@ -189,6 +189,11 @@ void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse)
 
 int tts_hip_supports_op(const tts_tensor * node);
 int tts_hip_graph_compute(tts_hip_backend_t backend, tts_tensor * const * nodes, int n_nodes);
+/* ggml_backend_i::graph_plan_create / graph_plan_compute: record a graph into plan slot 0 or 1
+ * without running it, then launch it later.  A caller records step n+1 on the host while step n
+ * runs on the device (the node array must stay alive until the slot is launched). */
+int tts_hip_graph_prepare(tts_hip_backend_t backend, tts_tensor * const * nodes, int n_nodes, int slot);
+int tts_hip_graph_launch(tts_hip_backend_t backend, int slot);
 
 /* Backend options (env-free knobs used by the bench / tests). */
 enum tts_hip_option {
@@ -221,6 +226,9 @@ typedef struct tts_backend_iface {
     int (*memset)(void * ctx, void * dst, int value, size_t size);
     int (*compute)(void * ctx, tts_tensor * const * nodes, int n_nodes);
     int (*synchronize)(void * ctx);
+    /* optional (NULL = use compute): record into plan slot 0/1 now, launch later */
+    int (*prepare)(void * ctx, tts_tensor * const * nodes, int n_nodes, int slot);
+    int (*launch)(void * ctx, int slot);
 } tts_backend_iface;
 
 /* Fills `out` with the HIP backend's vtable. */

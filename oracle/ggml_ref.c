@@ -890,5 +890,7 @@ int oracle_backend_iface(tts_backend_iface * out, int n_threads) {
     out->memset = ob_memset;
     out->compute = ob_compute;
     out->synchronize = ob_sync;
+    out->prepare = NULL; /* the oracle computes synchronously: callers fall back to compute */
+    out->launch = NULL;
     return 0;
 }

@@ -22,6 +22,7 @@ static void build_gelu_table(uint16_t * t) {
 }
 
 static const size_t kScratchBytes = 64u << 20;
+static const size_t kShadowBytes = 4u << 20;  // private copy of an attention output (decode: 32 KB per 8 prompts)
 
 extern "C" {
 
@@ -38,11 +39,14 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     auto * be = new tts_hip_backend();
     be->device = device;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->stream, hipStreamNonBlocking));
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->cap_stream, hipStreamNonBlocking));
     hipDeviceProp_t prop;
     TTS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     snprintf(be->name, sizeof(be->name), "HIP%d(%s)", device, prop.gcnArchName);
     TTS_HIP_CHECK(hipMalloc((void **)&be->scratch, kScratchBytes));
     be->scratch_size = kScratchBytes;
+    TTS_HIP_CHECK(hipMalloc((void **)&be->shadow, kShadowBytes));
+    be->shadow_size = kShadowBytes;
     std::vector<uint16_t> tab(65536);
     build_gelu_table(tab.data());
     TTS_HIP_CHECK(hipMalloc((void **)&be->gelu_table, 65536 * sizeof(uint16_t)));
@@ -60,10 +64,14 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     }
     for (auto e : be->ev_free) hipEventDestroy(e);
     hipFree(be->scratch);
+    hipFree(be->shadow);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
     if (be->gexec) hipGraphExecDestroy(be->gexec);
+    for (auto & ex : be->pexec)
+        if (ex) hipGraphExecDestroy(ex);
     hipStreamDestroy(be->stream);
+    hipStreamDestroy(be->cap_stream);
     delete be;
 }
 
@@ -272,6 +280,10 @@ static int hb_get(void * c, void * d, const void * s, size_t n) { return tts_hip
 static int hb_memset(void * c, void * d, int v, size_t n) { return tts_hip_memset((tts_hip_backend_t)c, d, v, n); }
 static int hb_compute(void * c, tts_tensor * const * nodes, int n) { return tts_hip_graph_compute((tts_hip_backend_t)c, nodes, n); }
 static int hb_sync(void * c) { return tts_hip_synchronize((tts_hip_backend_t)c); }
+static int hb_prepare(void * c, tts_tensor * const * nodes, int n, int slot) {
+    return tts_hip_graph_prepare((tts_hip_backend_t)c, nodes, n, slot);
+}
+static int hb_launch(void * c, int slot) { return tts_hip_graph_launch((tts_hip_backend_t)c, slot); }
 
 extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * out) {
     if (!be || !out) return TTS_STATUS_BAD_ARG;
@@ -285,5 +297,7 @@ extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * o
     out->memset = hb_memset;
     out->compute = hb_compute;
     out->synchronize = hb_sync;
+    out->prepare = hb_prepare;
+    out->launch = hb_launch;
     return 0;
 }

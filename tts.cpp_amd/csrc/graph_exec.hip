@@ -4,7 +4,7 @@
 //
 // Planning pass (per call): consumer counts per tensor, then pattern fusion, each fused kernel
 // reproducing the unfused ops bit-for-bit (see k_fused.hip / k_gemv.hip):
-//   LN   : NORM -> MUL(w) -> ADD(b)  [-> Q8_K copy for the GEMVs that read it]
+//   LN   : NORM -> MUL(w) -> ADD(b); folded into the prologue of the Q4_K GEMV that reads it
 //   GEMV : adjacent MUL_MATs sharing src1 (q/k/v) in one launch; K / V outputs written straight
 //          into the KV-cache views their CPY nodes target (parler_build_kv_store); adjacent
 //          ADD(residual) or GELU consumer folded into the epilogue
@@ -24,9 +24,9 @@ using namespace tts;
 
 namespace tts {
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
-                        float * out, int hd, int P, int H, int n, int B);
+                        float * out, int hd, int P, int H, int n, int B, float * out2);
 void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
-                      float eps, bool rms, ActQuant * aq);
+                      float eps, bool rms);
 }  // namespace tts
 
 namespace {
@@ -107,6 +107,8 @@ struct Item {
     const tts_tensor *lnx = nullptr, *lnw = nullptr, *lnb = nullptr, *lndst = nullptr;
     float lneps = 0.f;
     bool lnrms = false;
+    bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
+    bool shadow = false;    // ATTN: also write the private copy (be->shadow)
     // ATTN
     const tts_tensor *q = nullptr, *k = nullptr, *v = nullptr, *mask = nullptr, *out = nullptr;
     float scale = 1.f;
@@ -169,6 +171,25 @@ struct Planner {
             }
         }
         if (mask & TTS_FUSE_LN) fuse_ln_into_gemv();
+        link_attn_shadow();
+    }
+
+    // attention output -> [views] -> Q4_K GEMV: the attention kernel also writes a private copy
+    // that the GEMV reads, so the GEMV's outputs may land on the attention output's memory
+    // (arena reuse) without a staging copy.
+    void link_attn_shadow() {
+        for (int i = 0; i < n; ++i) {
+            const int a = act[i];
+            if (a <= 0 || items[a - 1].kind != Item::ATTN) continue;
+            const int nx = next_real(i);
+            if (nx < 0 || act[nx] <= 0) continue;
+            Item & A = items[a - 1];
+            Item & G = items[act[nx] - 1];
+            if (G.kind != Item::GEMV || G.ln || G.mms[0]->src[0]->type != TTS_TYPE_Q4_K) continue;
+            const tts_tensor * x = G.mms[0]->src[1];
+            if (x->data != A.out->data || !contiguous(x) || tbytes(x) != tbytes(A.out)) continue;
+            A.shadow = G.x_shadow = true;
+        }
     }
 
     // An LN item directly followed by the Q4_K GEMV item that reads its output becomes that
@@ -503,6 +524,10 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it) {
             y0 = (const char *)it.tgt[k].y;
             y1 = y0 + 4 * (size_t)((Mm - 1) * it.tgt[k].ycs + (mm->ne[0] - 1) * it.tgt[k].yrs + 1);
         };
+        if (it.x_shadow && (size_t)(4 * j.K * j.M) <= be->shadow_size) {
+            j.x = be->shadow;  // written by the preceding attention item (link_attn_shadow)
+            j.xcs = j.K;
+        }
         const char * x0 = (const char *)j.x;
         const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
         const char * l0 = (const char *)j.lnout;
@@ -568,13 +593,13 @@ static int run_item(tts_hip_backend * be, const Item & it) {
         case Item::GEMV: return run_gemv_item(be, it);
         case Item::ATTN: {
             const TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
+            float * out2 = it.shadow && tbytes(it.out) <= be->shadow_size ? be->shadow : nullptr;
             launch_attn_decode(be, q, k, v, it.mask ? (const float *)it.mask->data : nullptr, it.scale, (float *)it.out->data,
-                               (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3]);
+                               (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3], out2);
             return 0;
         }
         case Item::LN:
-            launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms,
-                             nullptr);
+            launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
             return 0;
     }
     return TTS_STATUS_FAILED;
@@ -582,46 +607,84 @@ static int run_item(tts_hip_backend * be, const Item & it) {
 
 static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes);
 
-extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
-    if (!be) return TTS_STATUS_BAD_ARG;
-    hipSetDevice(be->device);
-    if (!be->use_graphs || be->profile_gemv) return graph_compute_launches(be, nodes, n_nodes);
-    // prompt-sized graphs (many activation columns) run once: launch them directly
+// Replay through a HIP graph only for step-sized graphs: prompt-sized ones (many activation
+// columns) run once and are launched directly.
+static bool capture_worthy(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes) {
+    if (!be->use_graphs || be->profile_gemv) return false;
     for (int i = 0; i < n_nodes; ++i) {
         const tts_tensor * t = nodes[i];
-        if (t->op == TTS_OP_MUL_MAT && t->src[1] && t->src[1]->ne[1] * t->src[1]->ne[2] * t->src[1]->ne[3] > 64)
-            return graph_compute_launches(be, nodes, n_nodes);
+        if (t->op == TTS_OP_MUL_MAT && t->src[1] && t->src[1]->ne[1] * t->src[1]->ne[2] * t->src[1]->ne[3] > 64) return false;
     }
-    // Record the step's launches into a HIP graph and replay it: the kernels then run back to
-    // back on the device instead of at the host's launch rate.  Topology is stable from step to
-    // step (only shapes/offsets move with the KV length), so the executable graph is updated in
-    // place (hipGraphExecUpdate) and re-instantiated only when that fails.
+    return true;
+}
+
+// Record the graph's launches into `ex` without running them.  Topology is stable from step to
+// step (only shapes/offsets move with the KV length), so the executable graph is updated in place
+// (hipGraphExecUpdate) and re-instantiated only when that fails.
+static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes, hipGraphExec_t & ex) {
+    // record on a stream of its own: beginning a capture on the compute stream would first wait
+    // for the step still running there, and the whole point of a prepared plan is to overlap it
+    hipStream_t run = be->stream;
+    be->stream = be->cap_stream;
     TTS_HIP_CHECK(hipStreamBeginCapture(be->stream, hipStreamCaptureModeThreadLocal));
     const int st = graph_compute_launches(be, nodes, n_nodes);
     hipGraph_t graph = nullptr;
     TTS_HIP_CHECK(hipStreamEndCapture(be->stream, &graph));
+    be->stream = run;
     if (st != 0) {
         if (graph) hipGraphDestroy(graph);
         return st;
     }
     bool ok = false;
-    if (be->gexec) {
+    if (ex) {
         hipGraphNode_t err_node = nullptr;
         hipGraphExecUpdateResult res;
-        ok = hipGraphExecUpdate(be->gexec, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess;
+        ok = hipGraphExecUpdate(ex, graph, &err_node, &res) == hipSuccess && res == hipGraphExecUpdateSuccess;
         if (ok) be->graph_updates++;
         else {
             (void)hipGetLastError();
-            TTS_HIP_CHECK(hipGraphExecDestroy(be->gexec));
-            be->gexec = nullptr;
+            TTS_HIP_CHECK(hipGraphExecDestroy(ex));
+            ex = nullptr;
         }
     }
     if (!ok) {
-        TTS_HIP_CHECK(hipGraphInstantiate(&be->gexec, graph, nullptr, nullptr, 0));
+        TTS_HIP_CHECK(hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0));
         be->graph_instantiations++;
     }
     TTS_HIP_CHECK(hipGraphDestroy(graph));
+    return 0;
+}
+
+extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    if (!capture_worthy(be, nodes, n_nodes)) return graph_compute_launches(be, nodes, n_nodes);
+    // the step's launches replay back to back on the device instead of at the host's launch rate
+    const int st = capture_into(be, nodes, n_nodes, be->gexec);
+    if (st != 0) return st;
     TTS_HIP_CHECK(hipGraphLaunch(be->gexec, be->stream));
+    return 0;
+}
+
+// graph_plan_create / graph_plan_compute: record now, launch later.  A plan slot holds either a
+// recorded HIP graph or (graphs off / prompt-sized graphs) the node list, launched eagerly by
+// tts_hip_graph_launch -- so the node array must stay alive until then.
+extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes, int slot) {
+    if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    be->plan_nodes[slot] = nodes;
+    be->plan_n[slot] = n_nodes;
+    be->plan_eager[slot] = !capture_worthy(be, nodes, n_nodes);
+    if (be->plan_eager[slot]) return 0;
+    return capture_into(be, nodes, n_nodes, be->pexec[slot]);
+}
+
+extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
+    if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    if (be->plan_eager[slot]) return graph_compute_launches(be, be->plan_nodes[slot], be->plan_n[slot]);
+    if (!be->pexec[slot]) return TTS_STATUS_BAD_ARG;
+    TTS_HIP_CHECK(hipGraphLaunch(be->pexec[slot], be->stream));
     return 0;
 }
 

@@ -163,7 +163,8 @@ struct GemvJob {
 #define TTS_TS(job, k)                                                                                            \
     do {                                                                                                          \
         if ((job).ts && (threadIdx.x & 63) == 0)                                                                  \
-            (job).ts[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + \
+            (job).ts[((((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * (blockDim.x >> 6) + \
+                      (threadIdx.x >> 6)) * 8 +                                                                   \
                      (k)] = __builtin_amdgcn_s_memrealtime();                                                     \
     } while (0)
 #else
@@ -182,6 +183,10 @@ struct tts_hip_backend {
     // scratch arena for activation quantization
     char * scratch = nullptr;
     size_t scratch_size = 0;
+    // private second copy of an attention output, read by the GEMV that consumes it when the graph
+    // allocator has placed that GEMV's output on the attention output's memory
+    float * shadow = nullptr;
+    size_t shadow_size = 0;
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
@@ -199,7 +204,13 @@ struct tts_hip_backend {
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
     hipGraphExec_t gexec = nullptr;
+    hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;
+    // two prepared plans (tts_hip_graph_prepare / _launch): step n+1 is recorded while step n runs
+    hipGraphExec_t pexec[2] = {nullptr, nullptr};
+    tts_tensor * const * plan_nodes[2] = {nullptr, nullptr};
+    int plan_n[2] = {0, 0};
+    bool plan_eager[2] = {true, true};
 };
 
 namespace tts {

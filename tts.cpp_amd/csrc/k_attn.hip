@@ -1,0 +1,418 @@
+// Fused decode attention: one kernel replaces
+//   cont(K view) -> mul_mat(K, q) -> soft_max_ext(mask, scale) -> mul_mat(kq, V) -> permute(2,0,1,3) -> cont
+// (Parler model.cpp:549-571 self, 583-594 cross; Dia model.cpp:540-615; Orpheus model.cpp:259-285).
+// K and V are read in place through their cache views: the reference's per-step `cont` copy of K
+// (O(P*d) per layer per step) disappears.  Numerics are the unfused ops' exactly: f32 products
+// accumulated in f64 (ggml_vec_dot_f32), ggml's soft_max (scale, mask, max, expf, f64 sum, 1/sum),
+// with expf correctly rounded (transcendental policy, hip_internal.h).
+#include "hip_internal.h"
+
+namespace tts {
+
+// ------------------------------------------------------------------------------------------
+// Decode attention, one workgroup per (head h, query t, sequence b).
+struct AttnArgs {
+    TD q;      // [hd, n, H, B]   (the permute view feeding ggml's cont(q))
+    TD k;      // [hd, P, Hk, Bk] (K view of the cache, or cross_k)
+    TD v;      // [P, hd, Hv, Bv] (V view of the cache, or cross_v)
+    const float * mask;  // [rows >= n][P] f32, row stride P (ggml soft_max broadcast), or null
+    float scale;
+    float * out;         // [hd, H, n, B] contiguous
+    int hd, P, H, n, B;
+    float * out2 = nullptr;  // optional second copy of out (the next GEMV's private input)
+    unsigned long long * ts = nullptr;  // phase timestamps (scripts/attn_phase.hip builds only)
+};
+
+constexpr int ATTN_THREADS = 512;
+constexpr int ATTN_MAXP = 8192;
+constexpr int ATTN_UK = 8;  // K rows in flight per lane group (phase A)
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 4];
+    __shared__ double s_red[ATTN_THREADS / 64];
+    __shared__ float s_redf[ATTN_THREADS / 64];
+    const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = a.P, hd = a.hd;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const char * qbase = a.q.data + t * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+
+    // ---- phase A: kq[i] = sum_d (f32)(K[d,i] * q[d]), f64 accumulation (ggml_vec_dot_f32) ----
+    // G lanes per position, each owning hd/G contiguous dims (4 when hd = 4G).
+    const int G = hd / 4 <= 64 ? hd / 4 : 64;  // hd = 64 -> 16 lanes, 128 -> 32 lanes
+    const int per_lane = hd / G;
+    const int slot = tid % G, grp = tid / G, ngrp = ATTN_THREADS / G;
+    float qv[8];
+    for (int e = 0; e < per_lane && e < 8; ++e) qv[e] = *(const float *)(qbase + (int64_t)(slot * per_lane + e) * a.q.nb[0]);
+    const bool vec4 = a.k.nb[0] == 4 && per_lane == 4 && (a.k.nb[1] % 16) == 0 && (((uintptr_t)kbase) % 16) == 0;
+    for (int i0 = 0; i0 < P; i0 += ngrp * ATTN_UK) {
+        float4 kvv[ATTN_UK];
+        // issue every row load of the batch before the first use (memory-level parallelism)
+#pragma unroll
+        for (int u = 0; u < ATTN_UK; ++u) {
+            const int i = i0 + u * ngrp + grp;
+            kvv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i < P) {
+                const char * kr = kbase + (int64_t)i * a.k.nb[1] + (int64_t)(slot * per_lane) * a.k.nb[0];
+                if (vec4) kvv[u] = *(const float4 *)kr;
+                else {
+                    kvv[u].x = *(const float *)kr;
+                    kvv[u].y = *(const float *)(kr + a.k.nb[0]);
+                    kvv[u].z = *(const float *)(kr + 2 * a.k.nb[0]);
+                    kvv[u].w = *(const float *)(kr + 3 * a.k.nb[0]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < ATTN_UK; ++u) {
+            double s = (double)__fmul_rn(kvv[u].x, qv[0]);
+            s += (double)__fmul_rn(kvv[u].y, qv[1]);
+            s += (double)__fmul_rn(kvv[u].z, qv[2]);
+            s += (double)__fmul_rn(kvv[u].w, qv[3]);
+            for (int off = G / 2; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+            const int i = i0 + u * ngrp + grp;
+            if (slot == 0 && i < P) s_p[i] = (float)s;
+        }
+    }
+    __syncthreads();
+
+    // ---- phase B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum ----
+    const float * mrow = a.mask ? a.mask + (int64_t)t * P : nullptr;
+    float mx = -INFINITY;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        float w = __fmul_rn(s_p[i], a.scale);
+        if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+        s_p[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    for (int off = 32; off >= 1; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+    if (lane == 0) s_redf[wave] = mx;
+    __syncthreads();
+    mx = s_redf[0];
+    for (int w = 1; w < ATTN_THREADS / 64; ++w) mx = fmaxf(mx, s_redf[w]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        const float e = cr_expf(__fsub_rn(s_p[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_d(sum);
+    if (lane == 0) s_red[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+    for (int w = 0; w < ATTN_THREADS / 64; ++w) sum += s_red[w];
+    const float inv = (float)(1.0 / sum);
+    for (int i = tid; i < P; i += ATTN_THREADS) s_p[i] = __fmul_rn(s_p[i], inv);
+    __syncthreads();
+
+    // ---- phase C: out[d] = sum_i (f32)(p[i] * V[i,d]), f64 accumulation ----
+    // V rows (one per d) are contiguous in i: a lane owns 4 consecutive i (16-B loads) and the
+    // wave's DPW dims, so DPW x chunks loads are in flight per lane before the first FMA.
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    float * orow = a.out + (((int64_t)b * a.n + t) * a.H + h) * hd;
+    const int waves = ATTN_THREADS / 64;
+    const bool vvec = a.v.nb[0] == 4 && (a.v.nb[1] % 16) == 0 && (((uintptr_t)vbase) % 16) == 0 &&
+                      a.v.nb[1] >= (int64_t)16 * ((P + 3) / 4);
+    if (vvec) {
+        constexpr int DPW = 4;  // dims per pass per wave
+        for (int d0 = wave * DPW; d0 < hd; d0 += waves * DPW) {
+            double acc[DPW] = {0.0, 0.0, 0.0, 0.0};
+            for (int i4 = lane * 4; i4 < P; i4 += 256 * 2) {
+                float4 vv[2][DPW];
+                float4 pp[2];
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ii = i4 + c * 256;
+                    pp[c] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                    for (int u = 0; u < DPW; ++u) vv[c][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (ii < P) {
+                        pp[c] = *(const float4 *)(s_p + ii);
+#pragma unroll
+                        for (int u = 0; u < DPW; ++u)
+                            if (d0 + u < hd) vv[c][u] = *(const float4 *)(vbase + (int64_t)(d0 + u) * a.v.nb[1] + (int64_t)ii * 4);
+                    }
+                }
+#pragma unroll
+                for (int c = 0; c < 2; ++c) {
+                    const int ii = i4 + c * 256;
+#pragma unroll
+                    for (int u = 0; u < DPW; ++u) {
+                        // positions >= P (vector tail) contribute nothing, as in the scalar sum
+                        if (ii + 0 < P) acc[u] += (double)__fmul_rn(pp[c].x, vv[c][u].x);
+                        if (ii + 1 < P) acc[u] += (double)__fmul_rn(pp[c].y, vv[c][u].y);
+                        if (ii + 2 < P) acc[u] += (double)__fmul_rn(pp[c].z, vv[c][u].z);
+                        if (ii + 3 < P) acc[u] += (double)__fmul_rn(pp[c].w, vv[c][u].w);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < DPW; ++u) {
+                const double s = wave_sum_d(acc[u]);
+                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+            }
+        }
+    } else {
+        for (int d0 = wave * 4; d0 < hd; d0 += waves * 4) {
+            double acc[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int i = lane; i < P; i += 64) {
+                const float p = s_p[i];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int d = d0 + u;
+                    if (d < hd) {
+                        const float vv = *(const float *)(vbase + (int64_t)d * a.v.nb[1] + (int64_t)i * a.v.nb[0]);
+                        acc[u] += (double)__fmul_rn(p, vv);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double s = wave_sum_d(acc[u]);
+                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Decode attention for hd = 64 * DPR (Parler 64, Dia / Orpheus 128), same numerics as above, laid
+// out for memory latency (a round trip is ~0.8 us cold; the kernel is a handful of them):
+//   - K, V (when PF: P <= 512 for hd 64) and q are all requested at kernel entry, so the whole
+//     kernel waits on ONE memory round trip; V sits in registers until the softmax is done;
+//   - A: a quad (4 lanes) per key position, lane q owning 16*DPR dims; 128 positions per 512-thread
+//     step; the f64 dot is finished with two DPP quad steps;
+//   - B: soft_max_ext over the P scores in LDS (two barrier-separated reductions);
+//   - C: a 16-lane row per output dim (lane t: positions 4t + 64u as 16-B loads of the V row when
+//     VVEC, else scalar positions t + 16u), 32 dims per pass, DPP row reduction in f64.
+// No reduction goes through the LDS crossbar and every load batch is issued before its first use.
+constexpr int ATTN_UV = 8;  // V chunks (per lane, per dim pass) in flight
+
+template <int DPR, bool VVEC, bool PF>
+__global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    __shared__ float s_wf[ATTN_THREADS / 64];
+    __shared__ double s_wd[ATTN_THREADS / 64];
+    constexpr int NW = ATTN_THREADS / 64;
+    constexpr int F = 4 * DPR;                      // float4 per lane per key position (hd / 4 dims)
+    constexpr int KS = PF ? 512 / ATTN_THREADS * 4 : 2;  // key steps of 128 positions in flight
+    constexpr int NPASS = 2 * DPR;                  // dim passes in C (32 dims each)
+    const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane >> 4, t = lane & 15, qd = lane & 3;
+    const int P = a.P;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const int64_t knb1 = a.k.nb[1], vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
+    TTS_TS(a, 0);
+
+    // ---- loads: q (this lane's dims), K for the first KS steps, V for every pass (PF) ----
+    float qv[F][4];
+#pragma unroll
+    for (int c = 0; c < F; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qv[c][e] = ((const float *)qbase)[16 * DPR * qd + 4 * c + e];
+    const int pos0 = wave * 16 + (lane >> 2);  // this quad's position within a 128-step
+    float4 kv[KS][F];
+    auto load_k = [&](int i0) {
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            const int i = min(i0 + 128 * u + pos0, P - 1);
+#pragma unroll
+            for (int c = 0; c < F; ++c) kv[u][c] = *(const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + c));
+        }
+    };
+    load_k(0);
+    constexpr int VL = PF ? NPASS * ATTN_UV : 1;
+    float4 vv4[VVEC ? VL : 1];
+    float vv1[VVEC ? 1 : VL];
+    const int ilast = ((P - 1) >> 2) << 2;  // last 16-B chunk holding a position < P
+    if (PF) {
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+            const char * vrow = vbase + (int64_t)(ps * 32 + wave * 4 + r) * vnb1;
+#pragma unroll
+            for (int u = 0; u < ATTN_UV; ++u) {
+                if (VVEC) vv4[VVEC ? ps * ATTN_UV + u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(64 * u + 4 * t, ilast));
+                else vv1[VVEC ? 0 : ps * ATTN_UV + u] = *(const float *)(vrow + (int64_t)min(16 * u + t, P - 1) * vnb0);
+            }
+        }
+    }
+    TTS_PIN_LOADS();
+
+    // ---- A: kq[i] = sum_d (f32)(K[d,i] * q[d]) in f64 ----
+    for (int i0 = 0; i0 < P; i0 += 128 * KS) {
+        if (i0 > 0) {
+            load_k(i0);
+            TTS_PIN_LOADS();
+        }
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < F; ++c) {
+                s += (double)__fmul_rn(kv[u][c].x, qv[c][0]);
+                s += (double)__fmul_rn(kv[u][c].y, qv[c][1]);
+                s += (double)__fmul_rn(kv[u][c].z, qv[c][2]);
+                s += (double)__fmul_rn(kv[u][c].w, qv[c][3]);
+            }
+            s += dpp_f64<DPP_XOR1>(s);
+            s += dpp_f64<DPP_XOR2>(s);
+            const int i = i0 + 128 * u + pos0;
+            if (qd == 0 && i < P) s_p[i] = (float)s;
+        }
+    }
+    __syncthreads();
+    TTS_TS(a, 1);
+
+    // ---- B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum; p = e * (1/sum) ----
+    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    float mx = -INFINITY;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        float w = __fmul_rn(s_p[i], a.scale);
+        if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+        s_p[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    if (lane == 0) s_wf[wave] = mx;
+    __syncthreads();
+    mx = s_wf[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, s_wf[w]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += ATTN_THREADS) {
+        const float e = cr_expf(__fsub_rn(s_p[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_f64(sum);
+    if (lane == 0) s_wd[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += s_wd[w];
+    const float inv = (float)(1.0 / sum);
+    const int P64 = (P + 63) & ~63;
+    for (int i = tid; i < P64; i += ATTN_THREADS) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    __syncthreads();
+    TTS_TS(a, 3);
+
+    // ---- C: out[d] = sum_i (f32)(p[i] * V[d,i]) in f64 ----
+    float * orow = a.out + (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    float * orow2 = a.out2 ? a.out2 + (((int64_t)b * a.n + tq) * a.H + h) * a.hd : nullptr;
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+        const int d = ps * 32 + wave * 4 + r;
+        const char * vrow = vbase + (int64_t)d * vnb1;
+        double acc = 0.0;
+        const int kstep = VVEC ? 64 * ATTN_UV : 16 * ATTN_UV;
+        for (int k0 = 0; k0 < P; k0 += kstep) {
+            float4 w4[VVEC ? ATTN_UV : 1];
+            float w1[VVEC ? 1 : ATTN_UV];
+            if (PF) {
+#pragma unroll
+                for (int u = 0; u < ATTN_UV; ++u) {
+                    if (VVEC) w4[VVEC ? u : 0] = vv4[VVEC ? ps * ATTN_UV + u : 0];
+                    else w1[VVEC ? 0 : u] = vv1[VVEC ? 0 : ps * ATTN_UV + u];
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < ATTN_UV; ++u) {
+                    if (VVEC) w4[VVEC ? u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast));
+                    else w1[VVEC ? 0 : u] = *(const float *)(vrow + (int64_t)min(k0 + 16 * u + t, P - 1) * vnb0);
+                }
+                TTS_PIN_LOADS();
+            }
+#pragma unroll
+            for (int u = 0; u < ATTN_UV; ++u) {
+                if (VVEC) {
+                    const int i = k0 + 64 * u + 4 * t;
+                    const float4 pp = *(const float4 *)(s_p + min(i, P64 - 4));
+                    const float4 vq = w4[VVEC ? u : 0];
+                    // positions >= P (tail and clamped chunks) contribute nothing, as in the scalar sum
+                    acc += i + 0 < P ? (double)__fmul_rn(pp.x, vq.x) : 0.0;
+                    acc += i + 1 < P ? (double)__fmul_rn(pp.y, vq.y) : 0.0;
+                    acc += i + 2 < P ? (double)__fmul_rn(pp.z, vq.z) : 0.0;
+                    acc += i + 3 < P ? (double)__fmul_rn(pp.w, vq.w) : 0.0;
+                } else {
+                    const int i = k0 + 16 * u + t;
+                    acc += i < P ? (double)__fmul_rn(s_p[min(i, P - 1)], w1[VVEC ? 0 : u]) : 0.0;
+                }
+            }
+        }
+        acc += dpp_f64<DPP_XOR1>(acc);
+        acc += dpp_f64<DPP_XOR2>(acc);
+        acc += dpp_f64<DPP_HALF_MIRROR>(acc);
+        acc += dpp_f64<DPP_MIRROR>(acc);
+        if (t == 0 && d < a.hd) {
+            orow[d] = (float)acc;
+            if (orow2) orow2[d] = (float)acc;
+        }
+    }
+    TTS_TS(a, 4);
+}
+
+template <int DPR, bool PF>
+static void launch_attn_rows(tts_hip_backend * be, const AttnArgs & a, bool vvec) {
+    const dim3 grid((unsigned)a.H, (unsigned)a.n, (unsigned)a.B);
+    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true, PF>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false, PF>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+}
+
+void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
+                        float * out, int hd, int P, int H, int n, int B, float * out2) {
+    AttnArgs a;
+    a.out2 = out2;
+    a.q = q;
+    a.k = k;
+    a.v = v;
+    a.mask = mask;
+    a.scale = scale;
+    a.out = out;
+    a.hd = hd;
+    a.P = P;
+    a.H = H;
+    a.n = n;
+    a.B = B;
+    // row kernel: hd = 64/128, K rows 16-B vectors (aligned base and row stride)
+    const bool krows = (hd == 64 || hd == 128) && k.nb[0] == 4 && (k.nb[1] % 16) == 0 &&
+                       (((uintptr_t)k.data) % 16) == 0 && (k.nb[2] % 16) == 0 &&
+                       (k.nb[3] % 16) == 0 && q.nb[0] == 4 && P > 0;
+    if (krows) {
+        const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
+                          (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
+        // PF: the whole V slice fits the registers of one pass (16 x 16-B or 16 scalar loads per lane)
+        const bool pf = hd == 64 && P <= (vvec ? 64 * ATTN_UV : 16 * ATTN_UV);
+        if (hd == 64 && pf) launch_attn_rows<1, true>(be, a, vvec);
+        else if (hd == 64) launch_attn_rows<1, false>(be, a, vvec);
+        else launch_attn_rows<2, false>(be, a, vvec);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    hipLaunchKernelGGL(k_attn_decode, dim3((unsigned)H, (unsigned)n, (unsigned)B), dim3(ATTN_THREADS), 0, be->stream, a);
+    TTS_HIP_CHECK(hipGetLastError());
+    if (out2)
+        TTS_HIP_CHECK(hipMemcpyAsync(out2, out, sizeof(float) * (size_t)hd * H * n * B, hipMemcpyDeviceToDevice, be->stream));
+}
+
+}  // namespace tts

@@ -47,7 +47,12 @@ struct tts_parler {
     int32_t position = 0;
     int32_t current_step = 0;
     int32_t last_nodes = 0;
-    double host_us[5] = {0, 0, 0, 0, 0};  // build, alloc, set_inputs, compute (enqueue), get (wait)
+    double host_us[5] = {0, 0, 0, 0, 0};  // build, alloc, set_inputs, compute (record + launch), get (wait)
+    bool prepared = false;  // a step is built and recorded, waiting for launch_step
+    int prep_slot = 0, prep_n = 0;
+    bool prep_audio = true;
+    void * launched_out = nullptr;  // logits of the last launched step (device)
+    int launched_n = 0;
     int64_t host_steps = 0;
     std::vector<std::vector<int32_t>> output_tokens;  // per sequence, flat [steps][heads]
     std::vector<std::vector<char>> eos_seen;
@@ -272,6 +277,7 @@ extern "C" void tts_parler_free(tts_parler * p) {
 extern "C" void tts_parler_reset(tts_parler * p) {
     p->position = 0;
     p->current_step = 0;
+    p->prepared = false;
     p->output_tokens.assign(p->cfg.batch, {});
     p->eos_seen.assign(p->cfg.batch, std::vector<char>(p->cfg.n_output_heads, 0));
 }
@@ -452,36 +458,73 @@ static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n)
     return st;
 }
 
-static int decode(tts_parler * p, const int32_t * tokens, bool audio, int n, float * logits) {
+// A step is prepared (graph built, allocated and recorded into backend plan slot `slot`), then
+// launched with its inputs, then finished (logits read).  generate() prepares step s+1 while the
+// device runs step s, so the host's graph work overlaps the device (ggml's graph_plan_create /
+// graph_plan_compute split).
+static int prepare_step(tts_parler * p, bool audio, int n) {
     const auto & cf = p->cfg;
     if (p->position + n > cf.max_ctx) return TTS_STATUS_BAD_ARG;
     auto t0 = std::chrono::steady_clock::now();
-    tts_tensor * out = build_graph(p, audio, n);
+    p->res = build_graph(p, audio, n);
     auto t1 = std::chrono::steady_clock::now();
     if (!run_graph(p, p->gctx)) return TTS_STATUS_ALLOC_FAILED;
     auto t2 = std::chrono::steady_clock::now();
-    p->res = out;
     p->last_nodes = (int32_t)p->gctx.nodes.size();
-    if (set_inputs(p, tokens, audio, n) != 0) return TTS_STATUS_FAILED;
-    auto t3 = std::chrono::steady_clock::now();
-    int st = p->be.compute(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size());
-    if (st != 0) return st;
-    auto t4 = std::chrono::steady_clock::now();
-    if (logits) {
-        const size_t bytes = (size_t)cf.batch * n * cf.n_output_heads * cf.output_vocab * sizeof(float);
-        st = p->be.get(p->be.ctx, logits, out->data, bytes);
+    p->prep_slot = (int)(p->host_steps & 1);
+    p->prep_audio = audio;
+    p->prep_n = n;
+    if (p->be.prepare) {
+        const int st = p->be.prepare(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size(), p->prep_slot);
         if (st != 0) return st;
     }
-    auto t5 = std::chrono::steady_clock::now();
+    auto t3 = std::chrono::steady_clock::now();
+    p->prepared = true;
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
     p->host_us[0] += us(t0, t1);
     p->host_us[1] += us(t1, t2);
-    p->host_us[2] += us(t2, t3);
-    p->host_us[3] += us(t3, t4);
-    p->host_us[4] += us(t4, t5);
-    p->host_steps += 1;
-    p->position += n;
+    p->host_us[3] += us(t2, t3);
     return 0;
+}
+
+static int launch_step(tts_parler * p, const int32_t * tokens) {
+    if (!p->prepared) return TTS_STATUS_FAILED;
+    auto t0 = std::chrono::steady_clock::now();
+    if (set_inputs(p, tokens, p->prep_audio, p->prep_n) != 0) return TTS_STATUS_FAILED;
+    auto t1 = std::chrono::steady_clock::now();
+    const int st = p->be.launch ? p->be.launch(p->be.ctx, p->prep_slot)
+                                : p->be.compute(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size());
+    if (st != 0) return st;
+    auto t2 = std::chrono::steady_clock::now();
+    p->prepared = false;
+    p->launched_out = p->res->data;
+    p->launched_n = p->prep_n;
+    p->position += p->prep_n;
+    p->host_steps += 1;
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    p->host_us[2] += us(t0, t1);
+    p->host_us[3] += us(t1, t2);
+    return 0;
+}
+
+static int finish_step(tts_parler * p, float * logits) {
+    const auto & cf = p->cfg;
+    auto t0 = std::chrono::steady_clock::now();
+    int st = 0;
+    if (logits) {
+        const size_t bytes = (size_t)cf.batch * p->launched_n * cf.n_output_heads * cf.output_vocab * sizeof(float);
+        st = p->be.get(p->be.ctx, logits, p->launched_out, bytes);
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    p->host_us[4] += std::chrono::duration<double, std::micro>(t1 - t0).count();
+    return st;
+}
+
+static int decode(tts_parler * p, const int32_t * tokens, bool audio, int n, float * logits) {
+    int st = prepare_step(p, audio, n);
+    if (st == 0) st = launch_step(p, tokens);
+    if (st == 0) st = finish_step(p, logits);
+    return st;
 }
 
 extern "C" int tts_parler_prefill(tts_parler * p, const int32_t * tokens, int32_t n) {
@@ -526,7 +569,10 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
                 next[(size_t)b * NH + h] = t;
             }
         }
-        int st = tts_parler_decode(p, next.data(), logits.data());
+        int st = p->prepared ? 0 : prepare_step(p, true, 1);
+        if (st == 0) st = launch_step(p, next.data());
+        if (st == 0 && s + 1 < n_steps) st = prepare_step(p, true, 1);  // overlaps the device's step s
+        if (st == 0) st = finish_step(p, logits.data());
         if (st != 0) return st;
         for (int b = 0; b < B; ++b) {
             for (int h = 0; h < NH; ++h) {

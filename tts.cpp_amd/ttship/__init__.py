@@ -58,6 +58,8 @@ class BackendIface(ctypes.Structure):
         ("memset", ctypes.c_void_p),
         ("compute", ctypes.c_void_p),
         ("synchronize", ctypes.c_void_p),
+        ("prepare", ctypes.c_void_p),
+        ("launch", ctypes.c_void_p),
     ]
 
 
