@@ -349,28 +349,35 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 // optional LayerNorm; the first row's weight loads are issued before it so the HBM latency
 // overlaps the prologue.
 template <int MC, int PRO, int NBMAX>
-__global__ __launch_bounds__(512) void k_gemv_q4_K(GemvJob j) {
+__global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
-    const int mat = blockIdx.y;
-    const uint8_t * __restrict__ W = j.W[mat];
     int8_t * xq_s = (int8_t *)smem;
     const int nslot = MC * nb + 1;  // + the prologue's trash slot
     float * xd_s = (float *)(smem + al16((size_t)nslot * QK_K));
     int16_t * xs_s = (int16_t *)((char *)xd_s + al16(sizeof(float) * nslot));
 
+    // rows of all j.nmat matrices form one flat range (the launcher guarantees N % S == 0 when
+    // nmat > 1, so a wave's S rows never straddle two matrices)
     constexpr int S = 8 / MC;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int l = lane & 7, m = (lane >> 3) % MC, s = lane / (8 * MC);
-    const int64_t G = (j.N + S - 1) / S;
+    const int64_t G = ((int64_t)j.nmat * j.N + S - 1) / S;
     const int64_t gstride = (int64_t)gridDim.x * nw;
     int64_t g = (int64_t)blockIdx.x * nw + wave;
+    auto mat_of = [&](int64_t flat) {  // wave-uniform; nmat <= 16, so no 64-bit division
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        return mt;
+    };
 
     u32x4 hdr[NBMAX], q[NBMAX];
     auto load_row = [&](int64_t gg, int b0) {
-        int64_t row = gg * S + s;
+        const int64_t flat0 = gg * S;
+        const int mat = mat_of(flat0);
+        int64_t row = flat0 - (int64_t)mat * j.N + s;
         row = row < j.N ? row : j.N - 1;
-        const uint8_t * wr = W + row * j.w_row_bytes;
+        const uint8_t * wr = j.W[mat] + row * j.w_row_bytes;
 #pragma unroll
         for (int u = 0; u < NBMAX; ++u) {  // unconditional (clamped) so all loads issue before use
             const int64_t bo = (int64_t)min(b0 + u, nb - 1) * 144;
@@ -404,17 +411,18 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K(GemvJob j) {
                 const uint32_t sc_hi = (C & 0x0F0F0F0Fu) | ((A >> 2) & 0x30303030u);
                 const uint32_t mn_hi = ((C >> 4) & 0x0F0F0F0Fu) | ((B >> 2) & 0x30303030u);
                 const int xb = m * nb + b;
-                const int4 xl = *(const int4 *)(xq_s + (int64_t)xb * QK_K + l * 32);
-                const int4 xh = *(const int4 *)(xq_s + (int64_t)xb * QK_K + l * 32 + 16);
+                const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
+                const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
                 const uint32_t w0 = q[u].x, w1 = q[u].y, w2 = q[u].z, w3 = q[u].w;
-                int aux = (int)(sc_lo & 0xFF) * __builtin_amdgcn_sdot4((int)(w0 & 0x0F0F0F0Fu), xl.x, 0, false);
-                aux += (int)((sc_lo >> 8) & 0xFF) * __builtin_amdgcn_sdot4((int)((w0 >> 4) & 0x0F0F0F0Fu), xh.x, 0, false);
-                aux += (int)((sc_lo >> 16) & 0xFF) * __builtin_amdgcn_sdot4((int)(w1 & 0x0F0F0F0Fu), xl.y, 0, false);
-                aux += (int)(sc_lo >> 24) * __builtin_amdgcn_sdot4((int)((w1 >> 4) & 0x0F0F0F0Fu), xh.y, 0, false);
-                aux += (int)(sc_hi & 0xFF) * __builtin_amdgcn_sdot4((int)(w2 & 0x0F0F0F0Fu), xl.z, 0, false);
-                aux += (int)((sc_hi >> 8) & 0xFF) * __builtin_amdgcn_sdot4((int)((w2 >> 4) & 0x0F0F0F0Fu), xh.z, 0, false);
-                aux += (int)((sc_hi >> 16) & 0xFF) * __builtin_amdgcn_sdot4((int)(w3 & 0x0F0F0F0Fu), xl.w, 0, false);
-                aux += (int)(sc_hi >> 24) * __builtin_amdgcn_sdot4((int)((w3 >> 4) & 0x0F0F0F0Fu), xh.w, 0, false);
+                // aux32[l] = sum_j scale_j * dot4_j; |dot4| <= 7620 and scale <= 63 fit the 24-bit multiplier
+                int aux = __mul24((int)(sc_lo & 0xFF), __builtin_amdgcn_sdot4((int)(w0 & 0x0F0F0F0Fu), xl.x, 0, false));
+                aux += __mul24((int)((sc_lo >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w0 >> 4) & 0x0F0F0F0Fu), xh.x, 0, false));
+                aux += __mul24((int)((sc_lo >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w1 & 0x0F0F0F0Fu), xl.y, 0, false));
+                aux += __mul24((int)(sc_lo >> 24), __builtin_amdgcn_sdot4((int)((w1 >> 4) & 0x0F0F0F0Fu), xh.y, 0, false));
+                aux += __mul24((int)(sc_hi & 0xFF), __builtin_amdgcn_sdot4((int)(w2 & 0x0F0F0F0Fu), xl.z, 0, false));
+                aux += __mul24((int)((sc_hi >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w2 >> 4) & 0x0F0F0F0Fu), xh.z, 0, false));
+                aux += __mul24((int)((sc_hi >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w3 & 0x0F0F0F0Fu), xl.w, 0, false));
+                aux += __mul24((int)(sc_hi >> 24), __builtin_amdgcn_sdot4((int)((w3 >> 4) & 0x0F0F0F0Fu), xh.w, 0, false));
                 // sumi = sum_j mins[j] * bsum32[j] (int16 pairs, v_dot2)
                 const int4 bs = *(const int4 *)(xs_s + xb * 8);
                 const int mn01 = (int)((mn_lo & 0xFF) | ((mn_lo & 0xFF00) << 8));
@@ -443,9 +451,11 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K(GemvJob j) {
         tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 5>(sums));
         tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 6>(sums));
         tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 7>(sums));
-        const int64_t row = g * S + s;
+        const int64_t flat0 = g * S;
+        const int mat = mat_of(flat0);
+        const int64_t row = flat0 - (int64_t)mat * j.N + s;
         TTS_TS(j, 4);
-        if (l == 0 && m < j.M && row < j.N) gemv_store<MC>(j, mat, row, m, tot);
+        if (l == 0 && m < j.M && row < j.N && mat < j.nmat) gemv_store<MC>(j, mat, row, m, tot);
         if (g + gstride < G) load_row(g + gstride, 0);
     }
     TTS_TS(j, 5);
@@ -654,29 +664,40 @@ static void launch_q4k(tts_hip_backend * be, const GemvJob & j, unsigned gx, int
                                           160 * 1024));
         attr_set = true;
     }
-    hipLaunchKernelGGL((k_gemv_q4_K<MC, PRO, NBMAX>), dim3(gx, (unsigned)j.nmat), dim3(64 * nw), lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4_K<MC, PRO, NBMAX>), dim3(gx), dim3(64 * nw), lds, be->stream, j);
 }
 
-// Grid: every workgroup pays the prologue (normalize / quantize the whole activation), so the
-// grid is capped near one workgroup per CU and waves loop over row groups; up to 8 waves per
-// workgroup (one LN column each at M = 8).
 template <int MC>
 static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
     constexpr int S = 8 / MC;
-    const int64_t G = (j.N + S - 1) / S;  // wave row-groups
-    int nw = 8;
-    while (nw > 1 && ((G + nw - 1) / nw) * j.nmat < 256) nw /= 2;
-    int64_t gx = (G + nw - 1) / nw;
-    const int64_t cap = (512 + j.nmat - 1) / j.nmat;  // ~2 workgroups per CU
-    if (gx > cap) gx = cap;
-    const size_t lds = q4k_lds(MC, j.K);
+    if (j.nmat > 1 && j.N % S) {  // a wave's S rows must not straddle two matrices: one launch each
+        for (int i = 0; i < j.nmat; ++i) {
+            GemvJob one = j;
+            one.nmat = 1;
+            one.W[0] = j.W[i], one.Y[0] = j.Y[i], one.ycs[0] = j.ycs[i], one.yrs[0] = j.yrs[i];
+            launch_gemv_q4k_mc<MC>(be, one);
+        }
+        return;
+    }
+    // One workgroup per CU with enough waves that every wave owns ~1 row group of the flat
+    // (matrix, row) range: the prologue (norm + quantize of the whole activation) is paid once per
+    // CU and the rows run in parallel waves rather than one after another in a wave.  An LN
+    // prologue wants a wave per column.  Big matrices loop (2 workgroups per CU).
     const bool small = j.K <= 4 * QK_K;
+    const int nw_max = small ? 16 : 8;
+    const int64_t G = ((int64_t)j.nmat * j.N + S - 1) / S;
+    int64_t nw = (G + 255) / 256;
+    if (j.pro == PRO_LN && nw < j.M) nw = j.M;
+    nw = nw < 1 ? 1 : nw > nw_max ? nw_max : nw;
+    int64_t gx = (G + nw - 1) / nw;
+    if (gx > 512) gx = 512;
+    const size_t lds = q4k_lds(MC, j.K);
     if (j.pro == PRO_LN) {
-        if (small) launch_q4k<MC, PRO_LN, 4>(be, j, (unsigned)gx, nw, lds);
-        else launch_q4k<MC, PRO_LN, 16>(be, j, (unsigned)gx, nw, lds);
+        if (small) launch_q4k<MC, PRO_LN, 4>(be, j, (unsigned)gx, (int)nw, lds);
+        else launch_q4k<MC, PRO_LN, 16>(be, j, (unsigned)gx, (int)nw, lds);
     } else {
-        if (small) launch_q4k<MC, PRO_QUANT, 4>(be, j, (unsigned)gx, nw, lds);
-        else launch_q4k<MC, PRO_QUANT, 16>(be, j, (unsigned)gx, nw, lds);
+        if (small) launch_q4k<MC, PRO_QUANT, 4>(be, j, (unsigned)gx, (int)nw, lds);
+        else launch_q4k<MC, PRO_QUANT, 16>(be, j, (unsigned)gx, (int)nw, lds);
     }
 }
 static size_t q80_lds(int MC, int64_t K, int RW) {
