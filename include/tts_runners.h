@@ -67,6 +67,33 @@ uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint
 /* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
 uint64_t tts_parler_node(tts_parler * p, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap);
 
+/* DAC decoder (codec tokens -> PCM): dac_runner::run / build_dac_graph,
+ * /root/reference/src/decoder/dac_model.cpp:139-212.  Defaults = DAC 44.1 kHz as used by
+ * Parler-TTS mini v1 (9 codebooks x 1024 x 8, latent 1024, decoder 1536, rates 8,8,4,2: 512
+ * samples per latent frame). */
+typedef struct tts_dac_config {
+    int32_t n_codebooks;   /* 9 */
+    int32_t codebook_size; /* 1024 */
+    int32_t codebook_dim;  /* 8 */
+    int32_t latent_dim;    /* 1024 */
+    int32_t decoder_dim;   /* 1536; halves per layer */
+    int32_t n_layers;      /* 4 */
+    int32_t rates[8];      /* 8, 8, 4, 2 (upsampling stride per layer) */
+    int32_t max_frames;    /* latent frames per decode call (arena sizing) */
+    int32_t pad_;
+    uint64_t seed;         /* synthetic weight seed base */
+    uint64_t arena_bytes;  /* compute arena (0 = sized from max_frames) */
+} tts_dac_config;
+
+typedef struct tts_dac tts_dac;
+void tts_dac_default_config(tts_dac_config * cfg);
+tts_dac * tts_dac_create(const tts_backend_iface * be, const tts_dac_config * cfg);
+void tts_dac_free(tts_dac * d);
+/* codes: [T][n_codebooks] int32 (time-major, dac_build_audio_inputs' view); pcm: [T * hop] f32. */
+int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, float * pcm);
+int64_t tts_dac_hop(const tts_dac * d);
+int32_t tts_dac_last_graph_nodes(const tts_dac * d);
+
 #ifdef __cplusplus
 }
 #endif

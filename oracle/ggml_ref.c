@@ -659,6 +659,61 @@ static void op_mul_mat(tts_tensor * dst, int ith, int nth) {
     free(xq);
 }
 
+/* ggml_compute_forward_im2col, 1-D (is_2D = 0): dst (ic*K + k, ol, n) = src1[ol*s0 + k*d0 - p0, ic, n]
+ * or 0 outside the input, stored as dst->type (F16 rounds to nearest even, ggml_conv_1d's choice).
+ * op_params {s0, s1, p0, p1, d0, d1, is_2D}. */
+static void op_im2col(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    const int s0 = dst->op_params[0], p0 = dst->op_params[2], d0 = dst->op_params[4];
+    const int64_t K = a->ne[0], IC = b->ne[1], L = b->ne[0], OL = dst->ne[1], N = dst->ne[2];
+    const int64_t nr = OL * N;
+    const int64_t dr = (nr + nth - 1) / nth;
+    const int64_t r0 = dr * ith, r1 = MIN(r0 + dr, nr);
+    for (int64_t r = r0; r < r1; ++r) {
+        const int64_t ol = r % OL, n = r / OL;
+        for (int64_t ic = 0; ic < IC; ++ic) {
+            for (int64_t k = 0; k < K; ++k) {
+                const int64_t il = ol * s0 + k * d0 - p0;
+                const float v = (il >= 0 && il < L) ? load_elem(b, il, ic, n, 0) : 0.0f;
+                store_elem(dst, ic * K + k, ol, n, 0, v);
+            }
+        }
+    }
+}
+
+/* Fork op conv_transpose_1d(a = kernel [K, OC/g, IC], b = input [L, IC]) with PyTorch
+ * ConvTranspose1d semantics (the fork's source is absent, its converters
+ * keep torch's (IC, OC/g, K) weight order): y[oc, o] = sum over ic in oc's group, k with
+ * o = i*s0 - p0 + k*d0 of x[i, ic] * w[k, oc mod OC/g, ic].  f64 accumulation, one rounding.
+ * op_params {s0, p0, d0, output_padding, groups}. */
+static void op_conv_transpose_1d(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    const int s0 = dst->op_params[0], p0 = dst->op_params[1], d0 = dst->op_params[2], g = dst->op_params[4];
+    const int64_t K = a->ne[0], OCg = a->ne[1], IC = b->ne[1], L = b->ne[0];
+    const int64_t OL = dst->ne[0], OC = dst->ne[1], ICg = IC / g;
+    const int64_t dr = (OC + nth - 1) / nth;
+    const int64_t c0 = dr * ith, c1 = MIN(c0 + dr, OC);
+    for (int64_t oc = c0; oc < c1; ++oc) {
+        const int64_t grp = oc / OCg, ocl = oc % OCg;
+        for (int64_t o = 0; o < OL; ++o) {
+            ggml_float acc = 0.0;
+            for (int64_t k = 0; k < K; ++k) {
+                const int64_t num = o + p0 - k * d0;
+                if (num < 0 || num % s0) continue;
+                const int64_t i = num / s0;
+                if (i >= L) continue;
+                for (int64_t icl = 0; icl < ICg; ++icl) {
+                    const int64_t ic = grp * ICg + icl;
+                    acc += (ggml_float)load_elem(b, i, ic, 0, 0) * (ggml_float)load_elem(a, k, ocl, ic, 0);
+                }
+            }
+            *PF(dst, o, oc, 0, 0) = (float)acc;
+        }
+    }
+}
+
 /* ggml_compute_forward_get_rows (f32 / f16 / q4_K / q8_0 source; I32 index). */
 static void op_get_rows(tts_tensor * dst, int ith, int nth) {
     const tts_tensor * s0 = dst->src[0];
@@ -804,6 +859,8 @@ static int compute_node_mt(tts_tensor * node, int ith, int nth) {
         case TTS_OP_SUM_ROWS: op_sum_rows(node, ith, nth); return 0;
         case TTS_OP_REPEAT: op_repeat(node, ith, nth); return 0;
         case TTS_OP_ROPE: op_rope(node, ith, nth); return 0;
+        case TTS_OP_IM2COL: op_im2col(node, ith, nth); return 0;
+        case TTS_OP_CONV_TRANSPOSE_1D: op_conv_transpose_1d(node, ith, nth); return 0;
         default: return TTS_STATUS_UNSUPPORTED;
     }
 }

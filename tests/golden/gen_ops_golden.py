@@ -63,6 +63,31 @@ def main():
     d["rope_pos"] = pos.numpy()
     d["rope_ff"] = ff.numpy()
     d["rope_y"] = torch.cat([x1 * c - x2 * s, x1 * s + x2 * c], -1).float().numpy()
+    # conv_transpose_1d (fork op, PyTorch ConvTranspose1d semantics): DAC-style upsampler
+    # (K = 2s, p = ceil(s/2), op = s % 2), a depthwise Kokoro-style one, and a dilated one.
+    # torch weight layout (IC, OC/g, K) = ggml ne [K, OC/g, IC].
+    for name, (IC, OC, L, K, s, p, dil, op, grp) in {
+        "ct_dac": (8, 4, 5, 16, 8, 4, 1, 0, 1),
+        "ct_dw": (6, 6, 7, 3, 2, 1, 1, 1, 6),
+        "ct_dil": (5, 3, 4, 3, 3, 2, 2, 1, 1),
+    }.items():
+        x = rn(1, IC, L)
+        w = rn(IC, OC // grp, K, scale=0.3)
+        y = torch.nn.functional.conv_transpose1d(x.double(), w.double(), stride=s, padding=p, output_padding=op,
+                                                 groups=grp, dilation=dil)
+        d[name + "_x"] = x[0].numpy()
+        d[name + "_w"] = w.numpy()
+        d[name + "_y"] = y[0].float().numpy()
+        d[name + "_prm"] = np.array([s, p, dil, op, grp], dtype=np.int32)
+    # conv_1d = im2col(F16) . mul_mat: both operands rounded to fp16, products exact, f64 sums
+    IC, OC, L, K, s, p, dil = 16, 12, 40, 7, 1, 9, 3
+    x = rn(1, IC, L)
+    w = rn(OC, IC, K, scale=0.2)
+    y = torch.nn.functional.conv1d(x.half().double(), w.half().double(), stride=s, padding=p, dilation=dil)
+    d["c1_x"] = x[0].numpy()
+    d["c1_w"] = w.numpy()
+    d["c1_y"] = y[0].float().numpy()
+    d["c1_prm"] = np.array([s, p, dil], dtype=np.int32)
     np.savez_compressed(OUT, **d)
     print("wrote", OUT, sorted(d))
 

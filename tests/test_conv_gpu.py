@@ -1,0 +1,92 @@
+"""Codec convolutions on the HIP backend vs the CPU oracle.
+
+These ops are floating point with a different accumulation on each side (oracle: f64 sums, as
+ggml's generic dot; GPU: f32 MFMA / FMA accumulation), so the bar is a relative tolerance, 1e-5 of
+the output's scale -- far inside the PCM bar (1e-4 absolute) the codec tests check end to end.
+im2col is a pure gather + fp16 rounding and must be bit-exact; the MFMA lane mapping is checked
+bit-exactly with small-integer data (exact in f32 whatever the order).
+"""
+import numpy as np
+import pytest
+
+import convs
+import nodes as nd
+import ttship
+
+F32, F16 = ttship.F32, ttship.F16
+
+
+def run_both(hip, build):
+    g1, g2 = nd.Graph(), nd.Graph()
+    o1, o2 = build(g1), build(g2)
+    g1.run_hip(hip)
+    g2.run_oracle()
+    return [(g1.node_array(a), g2.node_array(b)) for a, b in zip(o1, o2)]
+
+
+def rnd(seed, *shape, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+def assert_rel(gpu, ref, rel=1e-5):
+    scale = max(float(np.max(np.abs(ref))), 1e-30)
+    err = float(np.max(np.abs(gpu.astype(np.float64) - ref.astype(np.float64))))
+    assert err <= rel * scale, f"max err {err:.3e} vs scale {scale:.3e}"
+
+
+CT_CASES = [  # IC, OC, L, K, s, p, d, op, groups
+    (8, 4, 5, 16, 8, 4, 1, 0, 1),       # DAC upsampler shape (K = 2s)
+    (96, 48, 40, 16, 8, 4, 1, 0, 1),    # DAC-like channel counts
+    (64, 32, 33, 4, 2, 1, 1, 0, 1),     # DAC last stage (s = 2)
+    (6, 6, 7, 3, 2, 1, 1, 1, 6),        # Kokoro depthwise (2,1,1,1,C)
+    (16, 8, 12, 20, 10, 5, 1, 0, 1),    # Kokoro generator (stride 10)
+    (5, 3, 4, 3, 3, 2, 2, 1, 1),        # dilated
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CT_CASES)
+def test_conv_transpose_1d(hip, case):
+    IC, OC, L, K, s, p, d, op, grp = case
+    x = rnd(1, IC, L)
+    w = rnd(2, IC, OC // grp, K, scale=0.2)
+    (gpu, ref), = run_both(hip, lambda g: [convs.conv_transpose_1d(g, x, w, s, p, d, op, grp)])
+    assert_rel(gpu, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", [(16, 12, 40, 7, 1, 9, 3), (8, 64, 33, 1, 1, 0, 1), (64, 96, 300, 7, 1, 3, 1), (96, 1, 100, 7, 1, 3, 1)])
+def test_conv_1d(hip, case):
+    IC, OC, L, K, s, p, d = case
+    x = rnd(3, IC, L)
+    w = rnd(4, OC, IC, K, scale=0.1)
+    (gpu, ref), = run_both(hip, lambda g: [convs.conv_1d(g, x, w, s, p, d)])
+    assert_rel(gpu, ref)
+
+
+@pytest.mark.gpu
+def test_im2col_bit_exact(hip):
+    IC, L, K, s, p, d = 24, 57, 7, 1, 9, 3
+    x = rnd(5, IC, L, scale=3.0)
+    w = rnd(6, 1, IC, K)
+
+    OL = (L + 2 * p - d * (K - 1) - 1) // s + 1
+    g1, g2 = nd.Graph(), nd.Graph()
+    o1, o2 = [g.node("IM2COL", F16, [IC * K, OL, 1], [g.leaf(w), g.leaf(x)], params=[s, 1, p, 0, d, 1, 0]) for g in (g1, g2)]
+    g1.run_hip(hip)
+    g2.run_oracle()
+    gpu, ref = g1.node_array(o1, dtype=np.float16), g2.node_array(o2, dtype=np.float16)
+    assert np.array_equal(gpu.view(np.uint16), ref.view(np.uint16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wtype", [F32, F16])
+def test_gemm_mfma_integer_exact(hip, wtype):
+    """Small integers: every product and partial sum is exact in f32, so any correct lane
+    mapping gives the oracle's bits; an asymmetric B catches a transposed store."""
+    rng = np.random.default_rng(7)
+    IC, OC, L, K = 40, 37, 70, 3
+    x = rng.integers(-3, 4, size=(IC, L)).astype(np.float32)
+    w = (rng.integers(-4, 5, size=(OC, IC, K)) + np.arange(OC)[:, None, None] * 0.25).astype(np.float32)
+    (gpu, ref), = run_both(hip, lambda g: [convs.conv_1d(g, x, w, 1, 1, 1, wtype=wtype)])
+    assert np.array_equal(gpu, ref)

@@ -203,6 +203,10 @@ int tts_hip_supports_op(const tts_tensor * n) {
             return is_f32(n->src[0]);
         case TTS_OP_ROPE:
             return is_f32(n->src[0]);
+        case TTS_OP_IM2COL:
+            return is_f32(n->src[1]) && n->op_params[6] == 0 && (n->type == TTS_TYPE_F16 || n->type == TTS_TYPE_F32);
+        case TTS_OP_CONV_TRANSPOSE_1D:
+            return is_f32(n->src[0]) && is_f32(n->src[1]) && n->op_params[4] >= 1;
         case TTS_OP_GET_ROWS:
             return n->src[1]->type == TTS_TYPE_I32 &&
                    (n->src[0]->type == TTS_TYPE_F32 || n->src[0]->type == TTS_TYPE_F16 || n->src[0]->type == TTS_TYPE_Q4_K ||
@@ -229,6 +233,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_FUSION: be->fusion = value; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
+        case TTS_HIP_OPT_CONV_F32ACC: be->conv_f32acc = value != 0; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }
 }

@@ -296,6 +296,44 @@ tts_tensor * mul_mat(context & c, tts_tensor * a, tts_tensor * b) {
     return new_op(c, TTS_OP_MUL_MAT, TTS_TYPE_F32, ne, a, b);
 }
 
+// ggml_im2col, 1-D form (is_2D = false): a = kernel [K, IC, OC], b = input [L, IC, N] ->
+// [IC*K, OL, N] with element (ic*K + k, ol, n) = b[ol*s0 + k*d0 - p0, ic, n] (0 outside),
+// op_params {s0, s1, p0, p1, d0, d1, is_2D} as ggml.
+tts_tensor * im2col(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0, int dst_type) {
+    const int64_t K = a->ne[0], IC = b->ne[1];
+    if (a->ne[1] != IC) fail("im2col: channel mismatch");
+    const int64_t OL = (b->ne[0] + 2 * p0 - d0 * (K - 1) - 1) / s0 + 1;
+    if (OL <= 0) fail("im2col: empty output");
+    int64_t ne[4] = {IC * K, OL, b->ne[2], 1};
+    tts_tensor * t = new_op(c, TTS_OP_IM2COL, dst_type, ne, a, b);
+    const int32_t prm[7] = {s0, 1, p0, 0, d0, 1, 0};
+    for (int i = 0; i < 7; ++i) t->op_params[i] = prm[i];
+    return t;
+}
+
+// ggml_conv_1d = im2col (F16) -> mul_mat -> reshape: [OL, OC, N]
+tts_tensor * conv_1d(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0) {
+    tts_tensor * col = im2col(c, a, b, s0, p0, d0, TTS_TYPE_F16);
+    tts_tensor * r = mul_mat(c, reshape_2d(c, col, col->ne[0], col->ne[2] * col->ne[1]), reshape_2d(c, a, a->ne[0] * a->ne[1], a->ne[2]));
+    return reshape_3d(c, r, col->ne[1], a->ne[2], col->ne[2]);
+}
+
+// Fork op ggml_conv_transpose_1d(a, b, s0, p0, d0, output_padding, groups) with PyTorch
+// ConvTranspose1d semantics: a = kernel [K, OC/g, IC], b = input [L, IC] ->
+// [(L-1)*s0 - 2*p0 + d0*(K-1) + op + 1, OC]; op_params {s0, p0, d0, op, g}.
+tts_tensor * conv_transpose_1d(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0, int op, int g) {
+    const int64_t K = a->ne[0], IC = b->ne[1];
+    if (a->ne[2] != IC || IC % g != 0) fail("conv_transpose_1d: channel mismatch");
+    const int64_t OC = a->ne[1] * g;
+    const int64_t OL = (b->ne[0] - 1) * s0 - 2 * p0 + d0 * (K - 1) + op + 1;
+    if (OL <= 0) fail("conv_transpose_1d: empty output");
+    int64_t ne[4] = {OL, OC, 1, 1};
+    tts_tensor * t = new_op(c, TTS_OP_CONV_TRANSPOSE_1D, TTS_TYPE_F32, ne, a, b);
+    const int32_t prm[5] = {s0, p0, d0, op, g};
+    for (int i = 0; i < 5; ++i) t->op_params[i] = prm[i];
+    return t;
+}
+
 tts_tensor * soft_max_ext(context & c, tts_tensor * a, tts_tensor * mask, float scale_, float max_bias) {
     tts_tensor * t = new_op(c, TTS_OP_SOFT_MAX, TTS_TYPE_F32, a->ne, a, mask);
     set_f(t, 0, scale_);

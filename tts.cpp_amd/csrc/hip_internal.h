@@ -203,6 +203,7 @@ struct tts_hip_backend {
     size_t repack_tmp_size = 0;
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
+    bool conv_f32acc = false;  // conv GEMM on f16 MFMA with f32 accumulation (faster, misses the PCM bar)
     hipGraphExec_t gexec = nullptr;
     hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;
@@ -220,6 +221,9 @@ namespace tts {
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
+void launch_im2col(tts_hip_backend * be, const tts_tensor * node);
+void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node);
+bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
 // carve an ActQuant layout for weight type `wtype` out of `base` (no launch)
 void act_quant_layout(int wtype, char * base, int64_t K, int64_t M, ActQuant & aq);

@@ -1,0 +1,270 @@
+// Codec convolutions (DAC / SNAC / Kokoro vocoders):
+//
+//  k_im2col          : GGML_OP_IM2COL, 1-D form used by ggml_conv_1d (general_neural_audio_codec.cpp
+//                      :133-149, dac_model.cpp:158,164): dst (ic*K + k, ol) = x[ol*s + k*d - p, ic],
+//                      F16 (round to nearest even) or F32.
+//  k_gemm_f16_mfma   : the MUL_MAT that follows it (src0 = im2col F16 [K', OL], src1 = kernel [K', OC]
+//                      F32/F16, converted to F16 = ggml's vec_dot_type for an F16 src0) on the matrix
+//                      cores: v_mfma_f32_16x16x32_f16, f32 accumulation.  fp16 x fp16 products are
+//                      exact in f32; only the accumulation order/precision differs from ggml-cpu's
+//                      f64 generic dot, so results agree to ~1e-6 relative (tests: conv vs oracle).
+//  k_conv_transpose_1d: the fork's GGML_OP_CONV_TRANSPOSE_1D (general_neural_audio_codec.cpp:153,
+//                      kokoro model.cpp:104,211) with PyTorch ConvTranspose1d semantics, one output
+//                      per lane, only the taps that land on it (k = r + j*s for dilation 1), f64
+//                      accumulation in the oracle's order.
+#include "hip_internal.h"
+
+namespace tts {
+
+// ------------------------------------------------------------------------------------------
+template <bool F16OUT>
+__global__ void k_im2col(TD dst, TD x, int K, int s0, int p0, int d0, int64_t n) {
+    const int64_t KW = dst.ne[0];  // IC*K
+    const int64_t OL = dst.ne[1];
+    const int64_t L = x.ne[0];
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kk = e % KW;
+        const int64_t ol = (e / KW) % OL;
+        const int64_t nn = e / (KW * OL);
+        const int64_t ic = kk / K, k = kk % K;
+        const int64_t il = ol * s0 + k * d0 - p0;
+        float v = 0.f;
+        if (il >= 0 && il < L) v = *(const float *)(x.data + il * x.nb[0] + ic * x.nb[1] + nn * x.nb[2]);
+        char * o = dst.data + kk * dst.nb[0] + ol * dst.nb[1] + nn * dst.nb[2];
+        if (F16OUT) *(__half *)o = __float2half_rn(v);
+        else *(float *)o = v;
+    }
+}
+
+void launch_im2col(tts_hip_backend * be, const tts_tensor * node) {
+    const tts_tensor * a = node->src[0];
+    const tts_tensor * b = node->src[1];
+    const int64_t n = node->ne[0] * node->ne[1] * node->ne[2];
+    const unsigned grid = (unsigned)std::min<int64_t>((n + 255) / 256, 65535 * 8);
+    const int K = (int)a->ne[0], s0 = node->op_params[0], p0 = node->op_params[2], d0 = node->op_params[4];
+    if (node->type == TTS_TYPE_F16)
+        hipLaunchKernelGGL(k_im2col<true>, dim3(grid), dim3(256), 0, be->stream, make_td(node), make_td(b), K, s0, p0, d0, n);
+    else
+        hipLaunchKernelGGL(k_im2col<false>, dim3(grid), dim3(256), 0, be->stream, make_td(node), make_td(b), K, s0, p0, d0, n);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// dst[j][i] = sum_k A[i][k] * B[j][k] (ggml mul_mat: i = src0 row, j = src1 column).
+// A F16 rows (stride lda elements), B F32 or F16 columns (stride ldb elements), K % 8 == 0, rows
+// 16-B aligned.  Wave tile 32 (i) x 32 (j) = 2 x 2 MFMA 16x16x32 tiles; workgroup 2 x 2 waves =
+// 64 x 64.  Lane l holds A[row l&15][k = 8(l>>4) .. +7] and B[k = 8(l>>4) .. +7][col l&15]; the
+// accumulator's column is l&15 (j) and its row (l>>4)*4 + reg (i), so each lane stores 4
+// consecutive i of one j.  Fragments for step k+32 are loaded before the MFMAs of step k.
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <bool BF16>
+__device__ __forceinline__ half8_t load_b_frag(const void * B, int64_t ldb, int64_t col, int64_t k) {
+    half8_t r;
+    if (BF16) {
+        const uint4 u = *(const uint4 *)((const __half *)B + col * ldb + k);
+        r = __builtin_bit_cast(half8_t, u);
+    } else {
+        const float4 lo = *(const float4 *)((const float *)B + col * ldb + k);
+        const float4 hi = *(const float4 *)((const float *)B + col * ldb + k + 4);
+        r[0] = (_Float16)__float2half_rn(lo.x), r[1] = (_Float16)__float2half_rn(lo.y);
+        r[2] = (_Float16)__float2half_rn(lo.z), r[3] = (_Float16)__float2half_rn(lo.w);
+        r[4] = (_Float16)__float2half_rn(hi.x), r[5] = (_Float16)__float2half_rn(hi.y);
+        r[6] = (_Float16)__float2half_rn(hi.z), r[7] = (_Float16)__float2half_rn(hi.w);
+    }
+    return r;
+}
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void k_gemm_f16_mfma(const __half * __restrict__ A, int64_t lda, const void * __restrict__ B, int64_t ldb,
+                                                       float * __restrict__ D, int64_t ldd, int64_t M, int64_t N, int64_t K) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t i0 = (int64_t)blockIdx.x * 64 + (wave & 1) * 32;
+    const int64_t j0 = (int64_t)blockIdx.y * 64 + (wave >> 1) * 32;
+    const int r16 = lane & 15, kq = lane >> 4;
+    int64_t ia[2], jb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        ia[t] = min(i0 + 16 * t + r16, M - 1);
+        jb[t] = min(j0 + 16 * t + r16, N - 1);
+    }
+    f32x4_t acc[2][2] = {};
+    half8_t a[2], b[2], an[2], bn[2];
+    auto load = [&](int64_t k0, half8_t (&fa)[2], half8_t (&fb)[2]) {
+        const int64_t k = k0 + 8 * kq;
+        const bool kin = k < K;  // K % 8 == 0: a lane's 8 elements are all in or all out
+        const int64_t kc = kin ? k : 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            half8_t va = __builtin_bit_cast(half8_t, *(const uint4 *)(A + ia[t] * lda + kc));
+            half8_t vb = load_b_frag<BF16>(B, ldb, jb[t], kc);
+            const half8_t z = {};
+            fa[t] = kin ? va : z;
+            fb[t] = kin ? vb : z;
+        }
+    };
+    load(0, a, b);
+    for (int64_t k0 = 0; k0 < K; k0 += 32) {
+        if (k0 + 32 < K) load(k0 + 32, an, bn);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ti], b[tj], acc[ti][tj], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[t] = an[t], b[t] = bn[t];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int64_t j = j0 + 16 * tj + r16;
+            const int64_t i = i0 + 16 * ti + 4 * kq;
+            if (j >= N) continue;
+            float * dp = D + j * ldd + i;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (i + e < M) dp[e] = acc[ti][tj][e];
+        }
+    }
+}
+
+// The same product accumulated in f64 on the f64 matrix cores (v_mfma_f64_16x16x4_f64): fp16 x fp16
+// products are exact in f64 and ggml-cpu's generic F16 dot sums them in f64 (ggml_vec_dot_f16), so
+// the f32 result equals the oracle's except for f64 near-ties -- which keeps a deep codec (the fp16
+// re-rounding of every conv input amplifies 1e-7 differences into 5e-4 PCM errors) inside the
+// PCM bar.  Lane l covers k = k0 + 8(l>>4) + t at MFMA step t = 0..7 of a 32-wide K step: every k
+// of the step is used once, so the lane loads its 8 contiguous k as one 16-B fragment.
+// MFMA f64 16x16x4 maps: A[i = l&15][k], B[k][j = l&15]; D col = l&15 (j), row = (l>>4) + 4*reg (i).
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+
+template <bool BF16>
+__global__ __launch_bounds__(256) void k_gemm_f16_f64acc(const __half * __restrict__ A, int64_t lda, const void * __restrict__ B, int64_t ldb,
+                                                         float * __restrict__ D, int64_t ldd, int64_t M, int64_t N, int64_t K) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t i0 = (int64_t)blockIdx.x * 64 + (wave & 1) * 32;
+    const int64_t j0 = (int64_t)blockIdx.y * 64 + (wave >> 1) * 32;
+    const int r16 = lane & 15, kq = lane >> 4;
+    int64_t ia[2], jb[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        ia[t] = min(i0 + 16 * t + r16, M - 1);
+        jb[t] = min(j0 + 16 * t + r16, N - 1);
+    }
+    f64x4_t acc[2][2] = {};
+    half8_t a[2], b[2], an[2], bn[2];
+    auto load = [&](int64_t k0, half8_t (&fa)[2], half8_t (&fb)[2]) {
+        const int64_t k = k0 + 8 * kq;
+        const bool kin = k < K;
+        const int64_t kc = kin ? k : 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            half8_t va = __builtin_bit_cast(half8_t, *(const uint4 *)(A + ia[t] * lda + kc));
+            half8_t vb = load_b_frag<BF16>(B, ldb, jb[t], kc);
+            const half8_t z = {};
+            fa[t] = kin ? va : z;
+            fb[t] = kin ? vb : z;
+        }
+    };
+    load(0, a, b);
+    for (int64_t k0 = 0; k0 < K; k0 += 32) {
+        if (k0 + 32 < K) load(k0 + 32, an, bn);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+            double ad[2], bd[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) ad[u] = (double)(float)a[u][t], bd[u] = (double)(float)b[u][t];
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int tj = 0; tj < 2; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(ad[ti], bd[tj], acc[ti][tj], 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) a[t] = an[t], b[t] = bn[t];
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int64_t j = j0 + 16 * tj + r16;
+            if (j >= N) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t i = i0 + 16 * ti + kq + 4 * e;
+                if (i < M) D[j * ldd + i] = (float)acc[ti][tj][e];
+            }
+        }
+    }
+}
+
+// MUL_MAT with an F16 src0 and many src1 columns (the conv_1d GEMM).  Returns false when the
+// shapes do not fit the MFMA kernels (the caller then uses the generic path).  Default: the f64
+// accumulating kernel (PCM parity); TTS_HIP_OPT_CONV_F32ACC selects the f16 MFMA / f32 accumulator.
+bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node) {
+    const tts_tensor * a = node->src[0];
+    const tts_tensor * b = node->src[1];
+    if (a->type != TTS_TYPE_F16 || (b->type != TTS_TYPE_F32 && b->type != TTS_TYPE_F16)) return false;
+    if (a->ne[2] * a->ne[3] != 1 || b->ne[2] * b->ne[3] != 1 || node->type != TTS_TYPE_F32) return false;
+    const int64_t K = a->ne[0], M = a->ne[1], N = b->ne[1];
+    const size_t bes = tts_type_size(b->type);
+    if (K % 8 || a->nb[0] != 2 || b->nb[0] != bes || node->nb[0] != 4) return false;
+    if (a->nb[1] % 16 || b->nb[1] % 16 || ((uintptr_t)a->data % 16) || ((uintptr_t)b->data % 16)) return false;
+    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64));
+    if (!be->conv_f32acc) {
+        if (b->type == TTS_TYPE_F16)
+            hipLaunchKernelGGL(k_gemm_f16_f64acc<true>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
+                               (int64_t)(b->nb[1] / 2), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+        else
+            hipLaunchKernelGGL(k_gemm_f16_f64acc<false>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
+                               (int64_t)(b->nb[1] / 4), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+        TTS_HIP_CHECK(hipGetLastError());
+        return true;
+    }
+    if (b->type == TTS_TYPE_F16)
+        hipLaunchKernelGGL(k_gemm_f16_mfma<true>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
+                           (int64_t)(b->nb[1] / 2), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+    else
+        hipLaunchKernelGGL(k_gemm_f16_mfma<false>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
+                           (int64_t)(b->nb[1] / 4), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+    TTS_HIP_CHECK(hipGetLastError());
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// y[oc][o] = sum over (k, i) with o = i*s - p + k*d, ic in oc's group: x[i][ic] * w[k][oc%OCg][ic]
+// One output position per lane; for d = 1 only taps k = r + j*s (r = (o+p) mod s) land on o.
+__global__ __launch_bounds__(256) void k_conv_transpose_1d(TD y, TD x, TD w, int s, int p, int d, int g) {
+    const int64_t OL = y.ne[0];
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int oc = blockIdx.y;
+    if (o >= OL) return;
+    const int K = (int)w.ne[0], OCg = (int)w.ne[1];
+    const int64_t L = x.ne[0];
+    const int IC = (int)x.ne[1], ICg = IC / g;
+    const int grp = oc / OCg, ocl = oc % OCg;
+    double acc = 0.0;  // f32 x f32 products are exact in f64; same (k, ic) order as the oracle
+    const int64_t num0 = o + p;
+    for (int k = (d == 1 ? (int)(num0 % s) : 0); k < K; k += (d == 1 ? s : 1)) {
+        const int64_t num = num0 - (int64_t)k * d;
+        if (num < 0) break;  // d == 1: num only decreases as k grows
+        if (num % s) continue;
+        const int64_t i = num / s;
+        if (i >= L) continue;
+        const char * xp = x.data + i * x.nb[0] + (int64_t)grp * ICg * x.nb[1];
+        const char * wp = w.data + (int64_t)k * w.nb[0] + (int64_t)ocl * w.nb[1] + (int64_t)grp * ICg * w.nb[2];
+        for (int icl = 0; icl < ICg; ++icl)
+            acc = __fma_rn((double)*(const float *)(xp + icl * x.nb[1]), (double)*(const float *)(wp + icl * w.nb[2]), acc);
+    }
+    *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc;
+}
+
+void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
+    const tts_tensor * w = node->src[0];
+    const tts_tensor * x = node->src[1];
+    const dim3 grid((unsigned)((node->ne[0] + 255) / 256), (unsigned)node->ne[1]);
+    hipLaunchKernelGGL(k_conv_transpose_1d, grid, dim3(256), 0, be->stream, make_td(node), make_td(x), make_td(w), node->op_params[0],
+                       node->op_params[1], node->op_params[2], node->op_params[4]);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tts

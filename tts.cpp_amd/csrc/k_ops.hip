@@ -464,10 +464,14 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
                                ff ? (const float *)ff->data : nullptr, n_dims, (mode & 2) ? 1 : 0, theta_scale, freq_scale, attn_factor);
         } break;
         case TTS_OP_MUL_MAT: {
-            // generic float path (quantized weights go through launch_gemv in backend.hip)
+            // F16 src0 with many columns (conv_1d's GEMM) on the matrix cores; otherwise the generic
+            // float path (quantized weights go through the GEMV kernels)
+            if (launch_gemm_f16(be, node)) return 0;
             const int64_t nout = nel(node);
             hipLaunchKernelGGL(k_mul_mat_f32, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
         } break;
+        case TTS_OP_IM2COL: launch_im2col(be, node); return 0;
+        case TTS_OP_CONV_TRANSPOSE_1D: launch_conv_transpose_1d(be, node); return 0;
         default:
             return TTS_STATUS_UNSUPPORTED;
     }

@@ -89,6 +89,22 @@ class ParlerConfig(ctypes.Structure):
     ]
 
 
+class DacConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_codebooks", ctypes.c_int32),
+        ("codebook_size", ctypes.c_int32),
+        ("codebook_dim", ctypes.c_int32),
+        ("latent_dim", ctypes.c_int32),
+        ("decoder_dim", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("rates", ctypes.c_int32 * 8),
+        ("max_frames", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+    ]
+
+
 _lib = None
 
 
@@ -146,6 +162,12 @@ def lib():
         "tts_parler_weight_bytes": (u64, [vp]),
         "tts_parler_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
         "tts_parler_node": (u64, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64), vp, u64]),
+        "tts_dac_default_config": (None, [ctypes.POINTER(DacConfig)]),
+        "tts_dac_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(DacConfig)]),
+        "tts_dac_free": (None, [vp]),
+        "tts_dac_decode": (ctypes.c_int, [vp, vp, i32, vp]),
+        "tts_dac_hop": (i64, [vp]),
+        "tts_dac_last_graph_nodes": (i32, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -293,4 +315,51 @@ class Parler:
     def close(self):
         if self.ptr:
             self.L.tts_parler_free(self.ptr)
+            self.ptr = None
+
+
+def dac_config(**kw):
+    cfg = DacConfig()
+    lib().tts_dac_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        if k == "rates":
+            for i, r in enumerate(v):
+                cfg.rates[i] = r
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+class Dac:
+    """DAC decoder runner (codec tokens -> PCM) over a backend vtable (HIP, or the oracle in tests)."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_dac_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_dac_create failed")
+
+    @property
+    def hop(self):
+        return self.L.tts_dac_hop(self.ptr)
+
+    def decode(self, codes):
+        """codes: (T, n_codebooks) int -> (T * hop,) float32 PCM."""
+        import numpy as np
+        c = np.ascontiguousarray(codes, dtype=np.int32)
+        T = c.shape[0]
+        pcm = np.empty(T * self.hop, dtype=np.float32)
+        st = self.L.tts_dac_decode(self.ptr, c.ctypes.data, T, pcm.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"tts_dac_decode failed {st}")
+        return pcm
+
+    def last_graph_nodes(self):
+        return self.L.tts_dac_last_graph_nodes(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_dac_free(self.ptr)
             self.ptr = None
