@@ -81,6 +81,8 @@ bool is_gemv(const tts_tensor * n) {
     if (n->nb[0] != 4 || (n->ne[2] * n->ne[3] != 1 && !(n->nb[2] == n->nb[1] * (size_t)n->ne[1] && n->nb[3] == n->nb[2] * (size_t)n->ne[2])))
         return false;
     if (a->nb[0] != tts_type_size(a->type)) return false;
+    // float weights against many columns (conv_1d's im2col GEMM) belong to the matrix cores
+    if ((a->type == TTS_TYPE_F16 || a->type == TTS_TYPE_F32) && b->ne[1] * b->ne[2] * b->ne[3] > 64) return false;
     switch (a->type) {
         case TTS_TYPE_Q4_K: return a->ne[0] % 256 == 0;
         case TTS_TYPE_Q8_0: return a->ne[0] % 32 == 0;

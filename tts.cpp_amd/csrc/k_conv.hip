@@ -258,9 +258,64 @@ __global__ __launch_bounds__(256) void k_conv_transpose_1d(TD y, TD x, TD w, int
     *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc;
 }
 
+// Polyphase form on the f64 matrix cores (dilation 1, groups 1): outputs o = q*s + rr - p of one
+// residue rr receive taps k = rr + s*j only, so per residue
+//   y[oc][q*s + rr - p] = sum_{j, ic} w[k = rr + s*j][oc][ic] * x[q - j][ic]
+// is a GEMM (rows oc, columns q, K = J*IC).  One wave per 16 (oc) x 16 (q) tile of one residue,
+// v_mfma_f64_16x16x4_f64 (A[oc = l&15][kk], B[kk][q = l&15], kk = 4 consecutive ic per step):
+// f32 x f32 products are exact in f64, so only the order of the f64 sum differs from the oracle.
+__global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w, int s, int p) {
+    const int lane = threadIdx.x, r16 = lane & 15, kq = lane >> 4;
+    const int rr = blockIdx.z;
+    const int64_t q0 = (int64_t)blockIdx.x * 16;
+    const int oc0 = blockIdx.y * 16;
+    const int K = (int)w.ne[0], OC = (int)w.ne[1], IC = (int)w.ne[2];
+    const int64_t L = x.ne[0], OL = y.ne[0];
+    const int J = (K - rr + s - 1) / s;
+    const int oca = min(oc0 + r16, OC - 1);
+    const int64_t qb = q0 + r16;
+    f64x4_t acc = {};
+    for (int j = 0; j < J; ++j) {
+        const int k = rr + s * j;
+        const int64_t i = qb - j;
+        const bool iin = i >= 0 && i < L;
+        const char * wp = w.data + (int64_t)k * w.nb[0] + (int64_t)oca * w.nb[1];
+        const char * xp = x.data + (iin ? i : 0) * x.nb[0];
+        for (int ic0 = 0; ic0 < IC; ic0 += 16) {
+            double av[4], bv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int ic = ic0 + 4 * u + kq;
+                const int icc = min(ic, IC - 1);
+                const float wa = *(const float *)(wp + (int64_t)icc * w.nb[2]);
+                const float xb = *(const float *)(xp + (int64_t)icc * x.nb[1]);
+                av[u] = ic < IC ? (double)wa : 0.0;
+                bv[u] = (ic < IC && iin) ? (double)xb : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc, 0, 0, 0);
+        }
+    }
+    const int64_t o = qb * s + rr - p;
+    if (o < 0 || o >= OL) return;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const int oc = oc0 + kq + 4 * e;
+        if (oc < OC) *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc[e];
+    }
+}
+
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
     const tts_tensor * w = node->src[0];
     const tts_tensor * x = node->src[1];
+    const int s = node->op_params[0], p = node->op_params[1], d = node->op_params[2], g = node->op_params[4];
+    if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16) {
+        const int64_t nq = (node->ne[0] + p) / s + 1;  // q with q*s + rr - p < OL for some rr
+        const dim3 grid((unsigned)((nq + 15) / 16), (unsigned)((w->ne[1] + 15) / 16), (unsigned)s);
+        hipLaunchKernelGGL(k_conv_transpose_1d_mfma, grid, dim3(64), 0, be->stream, make_td(node), make_td(x), make_td(w), s, p);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const dim3 grid((unsigned)((node->ne[0] + 255) / 256), (unsigned)node->ne[1]);
     hipLaunchKernelGGL(k_conv_transpose_1d, grid, dim3(256), 0, be->stream, make_td(node), make_td(x), make_td(w), node->op_params[0],
                        node->op_params[1], node->op_params[2], node->op_params[4]);
