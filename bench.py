@@ -1,17 +1,19 @@
 #!/usr/bin/env python3
-"""Throughput bench: Parler-TTS-mini v1, Q4_K decoder, autoregressive decode on MI355X.
+"""Throughput bench: Parler-TTS-mini v1 Q4_K on MI355X -- autoregressive decode + DAC decode
+(BASELINE.json configs[2], "AR decode + DAC conv_transpose_1d").
 
-One "step" = one AR decode step (build_parler_graph + compute + greedy sample) for every prompt of
+A "step" is one AR decode step (build_parler_graph + compute + greedy sample) for every prompt of
 this rank's shard of the prompt batch (default 8 prompts per GPU = the 64-prompt batch over 8 GPUs,
 weak scaling).  Each step produces 512 samples @ 44.1 kHz = 11.61 ms of audio and 9 codec tokens
-per prompt.  value = audio-seconds produced by all ranks / wall seconds (RTF^-1).
+per prompt.  After the K timed steps every prompt's K codec frames are decoded to PCM by the DAC-44k
+decoder inside the same timed region.  value = audio-seconds produced by all ranks / wall seconds
+(RTF^-1) of AR + DAC; the AR-only and DAC-only rates are reported beside it.
 
 Multi-GPU: one process per GPU (torchrun); prompts shard with no data-path collective; RCCL
 (backend "nccl") carries only the barrier / max-over-ranks timing reduction and the final token
 gather (the codec-token stream every rank produced, gathered to rank 0).
 """
 import argparse
-import ctypes
 import json
 import os
 import pathlib
@@ -28,6 +30,7 @@ SAMPLES_PER_STEP = 512          # DAC hop: one Parler step = 512 samples
 SAMPLE_RATE = 44100.0
 HEADS = 9
 HBM_PEAK_GBS = 8000.0           # MI355X spec (MI355X_MICROARCH.md chip table)
+PMC_FILE = ROOT / "profiles" / "r01" / "pmc_gemv_q4k.json"  # offline rocprofv3 --pmc result
 
 HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), token ids derived from bytes
     "The birch canoe slid on the smooth planks.",
@@ -51,6 +54,13 @@ def prompt_tokens(batch, n, vocab, offset=0):
         for i in range(n):
             out[b, i] = (s[i % len(s)] * 131 + i * 7 + g) % vocab
     return out
+
+
+def dac_codes(toks, codebook_size):
+    """Parler codec tokens [steps, heads] -> DAC input [frames, codebooks].  The synthetic decoder's
+    tokens include the delay pattern's BOS / EOS ids (>= 1024); they are folded into the codebook
+    range (a trained model's output after the delay is undone is already in range)."""
+    return np.ascontiguousarray(toks % codebook_size, dtype=np.int32)
 
 
 def dist_init(backend="nccl"):
@@ -106,7 +116,8 @@ def gather_tokens(dist, rank, world, local, toks):
 
 
 def cpu_baseline(args, n_threads):
-    """Oracle (C restatement of ggml-cpu) running the same Parler step graph on host cores."""
+    """Oracle (C restatement of ggml-cpu) running the same Parler step graph and the same DAC graph
+    on host cores; end-to-end rate = 1 / (1/AR + 1/DAC) per audio-second."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import py_oracle
     cfg = ttship.parler_config(batch=1, max_ctx=args.ctx + 64)
@@ -118,20 +129,52 @@ def cpu_baseline(args, n_threads):
         while steps < args.cpu_steps and (steps < 2 or time.perf_counter() - t0 < args.cpu_seconds):
             p.generate(1)
             steps += 1
-        dt = time.perf_counter() - t0
+        dt_ar = time.perf_counter() - t0
+        toks = p.generate(2)[0]
     finally:
         p.close()
-    audio = steps * SAMPLES_PER_STEP / SAMPLE_RATE
-    return {"value": audio / dt, "unit": "audio-sec/wall-sec", "cores": n_threads, "kind": "port",
-            "sample": f"{steps} Parler-mini Q4_K decode steps, batch 1, KV length ~10 "
+    dcfg = ttship.dac_config(max_frames=2)
+    dac = ttship.Dac(py_oracle.iface(n_threads), dcfg)
+    try:
+        t0 = time.perf_counter()
+        dac.decode(dac_codes(toks, dcfg.codebook_size))
+        dt_dac = time.perf_counter() - t0
+    finally:
+        dac.close()
+    ar = steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt_ar
+    dac_rate = 2 * SAMPLES_PER_STEP / SAMPLE_RATE / dt_dac
+    return {"value": 1.0 / (1.0 / ar + 1.0 / dac_rate), "unit": "audio-sec/wall-sec", "cores": n_threads, "kind": "port",
+            "sample": f"{steps} Parler-mini Q4_K decode steps (batch 1, KV length ~10) + DAC-44k decode of 2 frames "
                       f"(oracle/ggml_ref.c, C restatement of ggml-cpu scalar paths; reference ggml-cpu unbuildable offline)",
-            "codec_tokens_per_s": steps * HEADS / dt}
+            "ar_audio_sec_per_s": round(ar, 5), "dac_audio_sec_per_s": round(dac_rate, 5),
+            "codec_tokens_per_s": steps * HEADS / dt_ar}
+
+
+def gemv_roofline(be, runner, steps):
+    """Dominant kernel (Q4_K dequant-GEMV): algorithmic bytes per launch / its average duration,
+    HIP events on the backend stream around each launch during profiled decode steps."""
+    be.set_option(1, 1)
+    be.gemv_stats(-1, reset=True)
+    runner.generate(steps)
+    ms, launches, nbytes = be.gemv_stats(ttship.Q4_K, reset=True)
+    be.set_option(1, 0)
+    avg_us = 1000.0 * ms / max(launches, 1)
+    bpl = nbytes / max(launches, 1)
+    gbs = bpl / (avg_us * 1e-6) / 1e9 if launches else 0.0
+    traffic, src = None, None
+    if PMC_FILE.exists():
+        pmc = json.loads(PMC_FILE.read_text())
+        traffic, src = pmc.get("hbm_bytes_per_launch"), str(PMC_FILE.relative_to(ROOT))
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
+            "kernel": "k_gemv_q4_K", "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(bpl, 1),
+            "launches_sampled": launches}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="prompts per GPU (64-prompt batch / 8 GPUs)")
     ap.add_argument("--ctx", type=int, default=448, help="KV length when timing starts (prompt prefill)")
@@ -139,6 +182,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=400)
     ap.add_argument("--no-fusion", action="store_true")
+    ap.add_argument("--no-dac", action="store_true", help="AR decode only")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     args = ap.parse_args()
 
@@ -147,9 +191,14 @@ def main():
     if args.no_fusion:
         be.set_option(0, 0)
     be.set_option(2, args.graphs)
-    cfg = ttship.parler_config(batch=args.batch, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 8),
+    cfg = ttship.parler_config(batch=args.batch, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
                                arena_bytes=4 << 30)
     runner = ttship.Parler(be.iface(), cfg)
+    dac = None
+    if not args.no_dac:
+        dcfg = ttship.dac_config(max_frames=args.steps)
+        dac = ttship.Dac(be.iface(), dcfg)
+        dac.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
     # text-prompt pass to reach the measured KV length
     runner.prefill(prompt_tokens(args.batch, args.ctx, cfg.prompt_vocab, offset=rank * args.batch))
     runner.generate(args.warmup)
@@ -158,35 +207,32 @@ def main():
     runner.host_stats(reset=True)
     t0 = time.perf_counter()
     toks = runner.generate(args.steps)
+    be.sync()
+    t1 = time.perf_counter()
+    if dac is not None:
+        for b in range(args.batch):
+            dac.decode(dac_codes(toks[b], dcfg.codebook_size))
     barrier_sync(dist, be)
-    dt = time.perf_counter() - t0
+    t2 = time.perf_counter()
     host = runner.host_stats(reset=True)
-    dt = max_over_ranks(dist, local, dt)
+    dt = max_over_ranks(dist, local, t2 - t0)
+    dt_ar = max_over_ranks(dist, local, t1 - t0)
+    dt_dac = max_over_ranks(dist, local, t2 - t1)
     gather_tokens(dist, rank, world, local, toks)
 
     total_prompts = args.batch * world
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
-    value = audio_s / dt
-    tokens_per_s = total_prompts * args.steps * HEADS / dt
+    roof = gemv_roofline(be, runner, max(5, min(40, args.steps // 5)))
 
-    # ---- roofline of the dominant kernel (Q4_K dequant-GEMV), HIP events on the backend stream ----
-    be.set_option(1, 1)
-    be.gemv_stats(-1, reset=True)
-    runner.generate(max(5, args.steps // 5))
-    ms, launches, nbytes = be.gemv_stats(ttship.Q4_K, reset=True)
-    be.set_option(1, 0)
-    gemv_avg_us = 1000.0 * ms / max(launches, 1)
-    gemv_gbs = (nbytes / max(launches, 1)) / (gemv_avg_us * 1e-6) / 1e9 if launches else 0.0
-
-    result = None
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             ncpu = min(16, len(os.sched_getaffinity(0)))
             cpu = cpu_baseline(args, ncpu)
+        what = "AR decode + DAC decode" if dac is not None else "AR decode"
         result = {
-            "metric": "audio-sec/wall-sec (RTF^-1), Parler-TTS-mini v1 Q4_K AR decode",
-            "value": round(value, 3),
+            "metric": f"audio-sec/wall-sec (RTF^-1), Parler-TTS-mini v1 Q4_K {what}",
+            "value": round(audio_s / dt, 3),
             "unit": "audio-sec/wall-sec",
             "n_gpus": world,
             "steps": args.steps,
@@ -195,21 +241,24 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "q4_K weights x q8_K activations (int dot), f32 accumulate",
-            "data": "synthetic (deterministic Q4_K/F32 weights of Parler-mini v1 shapes; token ids from Harvard sentences)",
-            "config": {"workload": "Parler-TTS-mini-v1 Q4_K decoder, greedy AR decode (BASELINE configs[2])",
+            "dtype": "q4_K weights x q8_K activations (int dot, f32 combine); DAC f16 im2col x f32 weights, f64 accumulate",
+            "data": "synthetic (deterministic weights in Parler-mini v1 Q4_K and DAC-44k shapes; token ids from Harvard sentences)",
+            "config": {"workload": f"Parler-TTS-mini-v1 Q4_K, greedy AR decode + DAC-44k (BASELINE configs[2])",
                        "model": "parler-tts-mini-v1", "prompts_per_gpu": args.batch, "global_batch": total_prompts,
-                       "kv_len_start": args.ctx, "parallelism": f"dp{world} (prompt shards)",
-                       "graph_nodes_per_step": runner.last_graph_nodes()},
-            "codec_tokens_per_s": round(tokens_per_s, 1),
+                       "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
+                       "parallelism": f"dp{world} (prompt shards)", "graph_nodes_per_step": runner.last_graph_nodes(),
+                       "dac_graph_nodes": dac.last_graph_nodes() if dac is not None else None},
+            "ar_audio_sec_per_s": round(audio_s / dt_ar, 3),
+            "ar_ms_per_step": round(1000.0 * dt_ar / args.steps, 4),
+            "dac_audio_sec_per_s": round(audio_s / dt_dac, 3) if dac is not None else None,
+            "codec_tokens_per_s": round(total_prompts * args.steps * HEADS / dt_ar, 1),
             "host_us_per_step": host,
-            "roofline": {"bound": "hbm", "achieved": round(gemv_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(gemv_gbs / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "k_gemv_q4_K", "avg_launch_us": round(gemv_avg_us, 3),
-                         "bytes_per_launch": round(nbytes / max(launches, 1), 1), "launches_sampled": launches},
+            "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
+    if dac is not None:
+        dac.close()
     runner.close()
     be.close()
     if dist is not None:

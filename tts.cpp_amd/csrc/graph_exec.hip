@@ -693,6 +693,7 @@ extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
 static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     be->graph_epoch++;
     be->aq.src = nullptr;
+    if (be->profile_gemv) launch_profile_spin(be, 4000.0);  // see launch_profile_spin (k_gemv.hip)
     Planner pl;
     pl.mask = be->fusion;
     if (be->fusion) pl.build(nodes, n_nodes);

@@ -221,6 +221,7 @@ namespace tts {
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
+void launch_profile_spin(tts_hip_backend * be, double us);
 void launch_im2col(tts_hip_backend * be, const tts_tensor * node);
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node);
 bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node);
