@@ -837,6 +837,177 @@ static void op_rope(tts_tensor * dst, int ith, int nth) {
     free(cache);
 }
 
+/* ---- fork audio ops (Kokoro sine source / iSTFTNet head) ----------------
+ * The fork's ggml_cumsum / ggml_upscale_linear / ggml_stft / ggml_istft sources are absent
+ * (SURVEY.md §8c); they restate PyTorch (Kokoro's torch model: cumsum, F.interpolate linear,
+ * torch.stft(center, reflect) -> abs/angle, torch.istft), which is what tests/golden pins them to.
+ * Call sites: build_sin_gen src/models/kokoro/model.cpp:173-193, build_generator :195-244,
+ * stft/istft wrappers src/util.cpp:111-130. */
+
+/* ggml_cumsum (dim 0): torch.cumsum on CPU accumulates float in double, one rounding per output. */
+static void op_cumsum(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const int64_t nr = nrows(dst);
+    for (int64_t r = ith; r < nr; r += nth) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        ggml_float s = 0.0;
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0) {
+            s += (ggml_float)load_elem(a, i0, i1, i2, i3);
+            store_elem(dst, i0, i1, i2, i3, (float)s);
+        }
+    }
+}
+
+/* UPSCALE, op_params[0] = mode.
+ * 0 (ggml_upscale_ext, upstream nearest): dst[i] = src[(int64)(i / sf)], sf = (float)ne_dst/ne_src per dim.
+ * 1 (fork ggml_upscale_linear, dim 0 only): torch F.interpolate(mode="linear", align_corners=False)
+ *   as ATen's CPU kernel computes it: src index = fma(1/s, i + 0.5, -0.5) clamped at 0, lambda in
+ *   float, out = fma(x0, l0, x1 * l1) (the contractions ATen's vectorised build performs). */
+static void op_upscale(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const int mode = dst->op_params[0];
+    const int64_t nr = nrows(dst);
+    const float sc = (float)((double)a->ne[0] / (double)dst->ne[0]);
+    float sf[4];
+    for (int d = 0; d < 4; ++d) sf[d] = (float)dst->ne[d] / (float)a->ne[d];
+    for (int64_t r = ith; r < nr; r += nth) {
+        const int64_t i3 = r / (dst->ne[2] * dst->ne[1]);
+        const int64_t i2 = (r - i3 * dst->ne[2] * dst->ne[1]) / dst->ne[1];
+        const int64_t i1 = r - i3 * dst->ne[2] * dst->ne[1] - i2 * dst->ne[1];
+        for (int64_t i0 = 0; i0 < dst->ne[0]; ++i0) {
+            float v;
+            if (mode == 0) {
+                v = load_elem(a, (int64_t)((float)i0 / sf[0]), (int64_t)((float)i1 / sf[1]), (int64_t)((float)i2 / sf[2]),
+                              (int64_t)((float)i3 / sf[3]));
+            } else {
+                float x = fmaf(sc, (float)i0 + 0.5f, -0.5f);
+                if (x < 0.f) x = 0.f;
+                const int64_t j0 = (int64_t)x;
+                const int64_t j1 = j0 + (j0 < a->ne[0] - 1 ? 1 : 0);
+                const float l1 = MIN(MAX(x - (float)j0, 0.f), 1.f);
+                const float l0 = 1.f - l1;
+                v = fmaf(load_elem(a, j0, i1, i2, i3), l0, load_elem(a, j1, i1, i2, i3) * l1);
+            }
+            store_elem(dst, i0, i1, i2, i3, v);
+        }
+    }
+}
+
+/* Twiddle cos/sin(2*pi*m/n): exact octant reduction, then fixed Taylor polynomials in f64 with
+ * every operation written out (no libm), so the HIP kernels reproduce each bit
+ * (tts.cpp_amd/csrc/k_audio.hip tw_sincos). */
+static void tw_sincos(int64_t m, int64_t n, double * c, double * s) {
+    m %= n;
+    if (m < 0) m += n;
+    const int64_t q = (4 * m) / n, r = 4 * m - q * n; /* angle = pi/2 * (q + r/n) */
+    const int comp = 2 * r > n;
+    const int64_t rr = comp ? n - r : r;               /* reduced angle pi/2 * rr/n in [0, pi/4] */
+    const double x = (double)rr * (1.5707963267948966 / (double)n);
+    const double x2 = x * x;
+    const double sp = x * (1.0 + x2 * (-1.0 / 6 + x2 * (1.0 / 120 + x2 * (-1.0 / 5040 + x2 * (1.0 / 362880 + x2 * (-1.0 / 39916800 +
+                      x2 * (1.0 / 6227020800.0 + x2 * (-1.0 / 1307674368000.0 + x2 * (1.0 / 355687428096000.0)))))))));
+    const double cp = 1.0 + x2 * (-0.5 + x2 * (1.0 / 24 + x2 * (-1.0 / 720 + x2 * (1.0 / 40320 + x2 * (-1.0 / 3628800 +
+                      x2 * (1.0 / 479001600.0 + x2 * (-1.0 / 87178291200.0 + x2 * (1.0 / 20922789888000.0))))))));
+    const double c0 = comp ? sp : cp, s0 = comp ? cp : sp;
+    switch (q) {
+        case 0: *c = c0; *s = s0; break;
+        case 1: *c = -s0; *s = c0; break;
+        case 2: *c = -c0; *s = -s0; break;
+        default: *c = s0; *s = -c0; break;
+    }
+}
+
+/* ggml_stft(a = signal [L, B], window [N]) -> [N, F, B, 2], F = L/hop + 1: torch.stft(center=True,
+ * pad_mode="reflect", onesided=False) per frame, direct DFT in f64 (x*w exact, n ascending), one
+ * rounding to f32; DC and Nyquist imag = +0 (rfft convention).  abs_and_angle: [..,0] = |z|
+ * (f64 sqrt of the f32 parts = hypotf), [..,1] = atan2f(im, re); else [..,0] = re, [..,1] = im.
+ * op_params {n_fft, hop, abs_and_angle}. */
+static void op_stft(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * win = dst->src[1];
+    const int64_t N = dst->op_params[0], H = dst->op_params[1];
+    const int abs_angle = dst->op_params[2];
+    const int64_t L = a->ne[0], F = dst->ne[1], B = dst->ne[2];
+    double * tc = (double *)malloc(2 * N * sizeof(double));
+    for (int64_t m = 0; m < N; ++m) tw_sincos(m, N, &tc[2 * m], &tc[2 * m + 1]);
+    for (int64_t r = ith; r < F * B; r += nth) {
+        const int64_t t = r % F, b = r / F;
+        for (int64_t k = 0; k < N; ++k) {
+            double re = 0.0, im = 0.0;
+            for (int64_t n = 0; n < N; ++n) {
+                int64_t j = t * H + n - N / 2;
+                if (j < 0) j = -j;
+                if (j >= L) j = 2 * (L - 1) - j;
+                const double xw = (double)load_elem(a, j, b, 0, 0) * (double)load_elem(win, n, 0, 0, 0);
+                const int64_t m = (k * n) % N;
+                re += xw * tc[2 * m];
+                im -= xw * tc[2 * m + 1];
+            }
+            float fr = (float)re, fi = (float)im;
+            if (k == 0 || 2 * k == N) fi = 0.0f;
+            float o0 = fr, o1 = fi;
+            if (abs_angle) {
+                o0 = (float)sqrt((double)fr * (double)fr + (double)fi * (double)fi);
+                o1 = (float)atan2((double)fi, (double)fr);
+            }
+            store_elem(dst, k, t, b, 0, o0);
+            store_elem(dst, k, t, b, 1, o1);
+        }
+    }
+    free(tc);
+}
+
+/* ggml_istft(a = one-sided spectrum [N/2+1, F, B, 2], window [N]) -> [(F-1)*hop, B]: torch.istft
+ * (center=True, onesided) without the window-envelope division, which TTS.cpp applies as a separate
+ * DIV by window_sq_sum (src/util.cpp:122-130).  abs_and_angle: z = a0 * e^{i*a1}, else z = a0 + i*a1.
+ * Per output sample p (padded index j + N/2): for each covering frame t ascending,
+ * v = (sum_k w_k * (Re_k cos(2pi kn/N) - Im_k sin(2pi kn/N))) / N, w_k = 1 for DC / Nyquist (their
+ * imag ignored, c2r), else 2; y += v * window[n]; all in f64, one rounding. */
+static double istft_frame_val(const tts_tensor * a, int64_t t, int64_t b, int64_t n, int64_t N, int abs_angle, const double * tc) {
+    const int64_t K = a->ne[0];
+    double acc = 0.0;
+    for (int64_t k = 0; k < K; ++k) {
+        const double a0 = (double)load_elem(a, k, t, b, 0), a1 = (double)load_elem(a, k, t, b, 1);
+        double re = a0, im = a1;
+        if (abs_angle) {
+            re = a0 * cos(a1);
+            im = a0 * sin(a1);
+        }
+        const int64_t m = (k * n) % N;
+        double term;
+        if (k == 0 || 2 * k == N) term = re * tc[2 * m];
+        else term = 2.0 * (re * tc[2 * m] - im * tc[2 * m + 1]);
+        acc += term;
+    }
+    return acc / (double)N;
+}
+
+static void op_istft(tts_tensor * dst, int ith, int nth) {
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * win = dst->src[1];
+    const int64_t N = dst->op_params[0], H = dst->op_params[1];
+    const int abs_angle = dst->op_params[2];
+    const int64_t F = a->ne[1], B = dst->ne[1], Lout = dst->ne[0];
+    double * tc = (double *)malloc(2 * N * sizeof(double));
+    for (int64_t m = 0; m < N; ++m) tw_sincos(m, N, &tc[2 * m], &tc[2 * m + 1]);
+    for (int64_t r = ith; r < Lout * B; r += nth) {
+        const int64_t j = r % Lout, b = r / Lout;
+        const int64_t p = j + N / 2;
+        int64_t t0 = p - N + 1 > 0 ? (p - N + 1 + H - 1) / H : 0;
+        int64_t t1 = p / H;
+        if (t1 > F - 1) t1 = F - 1;
+        double y = 0.0;
+        for (int64_t t = t0; t <= t1; ++t) {
+            const int64_t n = p - t * H;
+            y += istft_frame_val(a, t, b, n, N, abs_angle, tc) * (double)load_elem(win, n, 0, 0, 0);
+        }
+        store_elem(dst, j, b, 0, 0, (float)y);
+    }
+    free(tc);
+}
+
 static int is_view_op(int op) {
     return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
 }
@@ -861,6 +1032,10 @@ static int compute_node_mt(tts_tensor * node, int ith, int nth) {
         case TTS_OP_ROPE: op_rope(node, ith, nth); return 0;
         case TTS_OP_IM2COL: op_im2col(node, ith, nth); return 0;
         case TTS_OP_CONV_TRANSPOSE_1D: op_conv_transpose_1d(node, ith, nth); return 0;
+        case TTS_OP_CUMSUM: op_cumsum(node, ith, nth); return 0;
+        case TTS_OP_UPSCALE: op_upscale(node, ith, nth); return 0;
+        case TTS_OP_STFT: op_stft(node, ith, nth); return 0;
+        case TTS_OP_ISTFT: op_istft(node, ith, nth); return 0;
         default: return TTS_STATUS_UNSUPPORTED;
     }
 }

@@ -88,6 +88,46 @@ def main():
     d["c1_w"] = w.numpy()
     d["c1_y"] = y[0].float().numpy()
     d["c1_prm"] = np.array([s, p, dil], dtype=np.int32)
+
+    # ---- Kokoro sine source / iSTFTNet head (fork ops, float32 torch as Kokoro runs it) ----
+    # sine source front: mod 1 -> cumsum (dim of time) -> x600pi -> linear x300
+    f0 = torch.rand(1, 23, generator=g) * 400.0
+    h = (torch.arange(1, 10).float() / 24000.0)[:, None]
+    rad = torch.fmod(f0 * h, 1.0)                         # [9, 23]
+    d["sg_f0"] = f0[0].numpy()
+    d["sg_rad"] = rad.numpy()
+    d["sg_cumsum"] = torch.cumsum(rad, dim=1).numpy()     # CPU: double accumulator
+    ph = torch.cumsum(rad, dim=1) * np.float32(600.0 * np.pi)
+    d["sg_phase"] = ph.numpy()
+    d["sg_up"] = torch.nn.functional.interpolate(ph[None], scale_factor=300, mode="linear")[0].numpy()
+    d["sg_f0_up"] = torch.nn.functional.interpolate(f0[None], scale_factor=300, mode="nearest")[0].numpy()
+    # linear upscale of a non-integer-friendly length and a 2x factor
+    x = rn(3, 7)
+    d["ul_x"] = x.numpy()
+    d["ul_y2"] = torch.nn.functional.interpolate(x[None], scale_factor=2, mode="linear")[0].numpy()
+    d["ul_y5"] = torch.nn.functional.interpolate(x[None], scale_factor=5, mode="linear")[0].numpy()
+    # STFT: Kokoro n_fft 20 / hop 5, periodic hann computed as src/util.cpp:132-137 does (float of
+    # the double sin^2), center=True reflect, abs & angle; plus a re/im case (n_fft 16, hop 4)
+    for name, (N, H, L) in {"stft20": (20, 5, 300 * 4), "stft16": (16, 4, 160)}.items():
+        win = torch.tensor([np.float32(np.sin(np.pi * i / N) ** 2) for i in range(N)], dtype=torch.float32)
+        x = rn(1, L, scale=0.3)
+        S = torch.stft(x, N, H, N, window=win, center=True, pad_mode="reflect", return_complex=True, onesided=False)
+        d[name + "_x"] = x[0].numpy()
+        d[name + "_win"] = win.numpy()
+        d[name + "_abs"] = S.abs()[0].numpy()        # [N, F]
+        d[name + "_angle"] = S.angle()[0].numpy()
+        d[name + "_re"] = S.real[0].numpy()
+        d[name + "_im"] = S.imag[0].numpy()
+    # iSTFT of exp(spec) * e^{i sin(phase)} (build_generator), n_fft 20 / hop 5, F frames
+    N, H, F = 20, 5, 97
+    win = torch.tensor([np.float32(np.sin(np.pi * i / N) ** 2) for i in range(N)], dtype=torch.float32)
+    mag = torch.exp(rn(N // 2 + 1, F, scale=0.5))
+    pha = torch.sin(rn(N // 2 + 1, F, scale=2.0))
+    y = torch.istft((mag * torch.exp(pha * 1j))[None], N, H, N, window=win, center=True)
+    d["istft_mag"] = mag.numpy()
+    d["istft_phase"] = pha.numpy()
+    d["istft_win"] = win.numpy()
+    d["istft_y"] = y[0].numpy()                      # [(F-1)*H]
     np.savez_compressed(OUT, **d)
     print("wrote", OUT, sorted(d))
 

@@ -115,6 +115,30 @@ inline TD make_td(const tts_tensor * t) {
     d.pad = t->flags;
     return d;
 }
+#ifdef __HIPCC__
+// element access through a ggml view (F32 / F16 / I32), as the oracle's load_elem / store_elem
+static __device__ __forceinline__ void unravel(int64_t k, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
+    i0 = k % ne[0];
+    k /= ne[0];
+    i1 = k % ne[1];
+    k /= ne[1];
+    i2 = k % ne[2];
+    i3 = k / ne[2];
+}
+
+static __device__ __forceinline__ float td_load(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
+    const char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
+    if (t.type == TTS_TYPE_F16) return __half2float(*(const __half *)p);
+    if (t.type == TTS_TYPE_I32) return (float)*(const int32_t *)p;
+    return *(const float *)p;
+}
+static __device__ __forceinline__ void td_store(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3, float v) {
+    char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
+    if (t.type == TTS_TYPE_F16) *(__half *)p = __float2half_rn(v);
+    else if (t.type == TTS_TYPE_I32) *(int32_t *)p = (int32_t)v;
+    else *(float *)p = v;
+}
+#endif
 
 // Device scratch for quantized activations (Q8_K / Q8_0 / F16 copies of a mul_mat src1).
 struct ActQuant {
@@ -223,6 +247,8 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
 void launch_profile_spin(tts_hip_backend * be, double us);
 void launch_im2col(tts_hip_backend * be, const tts_tensor * node);
+bool audio_op_supported(const tts_tensor * n);
+int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node);
 bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);

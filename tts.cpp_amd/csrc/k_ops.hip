@@ -7,27 +7,6 @@
 
 namespace tts {
 
-__device__ __forceinline__ float td_load(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
-    const char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
-    if (t.type == TTS_TYPE_F16) return __half2float(*(const __half *)p);
-    if (t.type == TTS_TYPE_I32) return (float)*(const int32_t *)p;
-    return *(const float *)p;
-}
-__device__ __forceinline__ void td_store(const TD & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3, float v) {
-    char * p = t.data + i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
-    if (t.type == TTS_TYPE_F16) *(__half *)p = __float2half_rn(v);
-    else if (t.type == TTS_TYPE_I32) *(int32_t *)p = (int32_t)v;
-    else *(float *)p = v;
-}
-__device__ __forceinline__ void unravel(int64_t k, const int64_t * ne, int64_t & i0, int64_t & i1, int64_t & i2, int64_t & i3) {
-    i0 = k % ne[0];
-    k /= ne[0];
-    i1 = k % ne[1];
-    k /= ne[1];
-    i2 = k % ne[2];
-    i3 = k / ne[2];
-}
-
 // ---- copies: element k of src (flattened, i0 fastest) -> element k of dst (ggml dup/cpy) ----
 __global__ void k_cpy(TD dst, TD src, int64_t n) {
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
@@ -472,6 +451,7 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
         } break;
         case TTS_OP_IM2COL: launch_im2col(be, node); return 0;
         case TTS_OP_CONV_TRANSPOSE_1D: launch_conv_transpose_1d(be, node); return 0;
+        case TTS_OP_CUMSUM: case TTS_OP_UPSCALE: case TTS_OP_STFT: case TTS_OP_ISTFT: return launch_audio_op(be, node);
         default:
             return TTS_STATUS_UNSUPPORTED;
     }
