@@ -68,12 +68,12 @@ __global__ void k_upscale(TD dst, TD a, int mode, float sc, float sf0, float sf1
 // ---- twiddles ---------------------------------------------------------------------------------
 // cos/sin(2*pi*m/n) by exact octant reduction and fixed f64 Taylor polynomials, operation for
 // operation the oracle's tw_sincos (the build compiles with -ffp-contract=off, so no fusion).
-__device__ void tw_sincos(int64_t m, int64_t n, double & c, double & s) {
+__device__ __forceinline__ double2 tw_sincos(int m, int n) {
     m %= n;
     if (m < 0) m += n;
-    const int64_t q = (4 * m) / n, r = 4 * m - q * n;
+    const int q = (4 * m) / n, r = 4 * m - q * n;
     const bool comp = 2 * r > n;
-    const int64_t rr = comp ? n - r : r;
+    const int rr = comp ? n - r : r;
     const double x = __dmul_rn((double)rr, __ddiv_rn(1.5707963267948966, (double)n));
     const double x2 = x * x;
     const double sp = x * (1.0 + x2 * (-1.0 / 6 + x2 * (1.0 / 120 + x2 * (-1.0 / 5040 + x2 * (1.0 / 362880 + x2 * (-1.0 / 39916800 +
@@ -81,12 +81,10 @@ __device__ void tw_sincos(int64_t m, int64_t n, double & c, double & s) {
     const double cp = 1.0 + x2 * (-0.5 + x2 * (1.0 / 24 + x2 * (-1.0 / 720 + x2 * (1.0 / 40320 + x2 * (-1.0 / 3628800 +
                       x2 * (1.0 / 479001600.0 + x2 * (-1.0 / 87178291200.0 + x2 * (1.0 / 20922789888000.0))))))));
     const double c0 = comp ? sp : cp, s0 = comp ? cp : sp;
-    switch (q) {
-        case 0: c = c0; s = s0; break;
-        case 1: c = -s0; s = c0; break;
-        case 2: c = -c0; s = -s0; break;
-        default: c = s0; s = -c0; break;
-    }
+    double2 o;
+    o.x = q == 0 ? c0 : q == 1 ? -s0 : q == 2 ? -c0 : s0;
+    o.y = q == 0 ? s0 : q == 1 ? c0 : q == 2 ? -s0 : -c0;
+    return o;
 }
 
 // ---- STFT -------------------------------------------------------------------------------------
@@ -95,7 +93,11 @@ __device__ void tw_sincos(int64_t m, int64_t n, double & c, double & s) {
 // live in LDS.  Per output: N-term f64 DFT in n order, one rounding, rfft's +0 imag at DC/Nyquist.
 __global__ __launch_bounds__(256) void k_stft(TD dst, TD a, TD win, int N, int H, int abs_angle) {
     extern __shared__ double tw[];  // [N][2]
-    for (int m = threadIdx.x; m < N; m += blockDim.x) tw_sincos(m, N, tw[2 * m], tw[2 * m + 1]);
+    for (int m = threadIdx.x; m < N; m += blockDim.x) {
+        const double2 cs = tw_sincos(m, N);
+        tw[2 * m] = cs.x;
+        tw[2 * m + 1] = cs.y;
+    }
     __syncthreads();
     const int64_t F = dst.ne[1], B = dst.ne[2], L = a.ne[0];
     const int64_t total = (int64_t)N * F * B;
@@ -148,7 +150,11 @@ __global__ __launch_bounds__(ISTFT_TILE) void k_istft(TD dst, TD a, TD win, int 
     const int nt = (int)(t_hi - t_lo + 1);
     double * tw = lds;                 // [N][2]
     double * z = lds + 2 * N;          // [nt][K][2]
-    for (int m = threadIdx.x; m < N; m += blockDim.x) tw_sincos(m, N, tw[2 * m], tw[2 * m + 1]);
+    for (int m = threadIdx.x; m < N; m += blockDim.x) {
+        const double2 cs = tw_sincos(m, N);
+        tw[2 * m] = cs.x;
+        tw[2 * m + 1] = cs.y;
+    }
     for (int i = threadIdx.x; i < nt * K; i += blockDim.x) {
         const int tt = i / K, k = i - tt * K;
         const double a0 = (double)td_load(a, k, t_lo + tt, b, 0), a1 = (double)td_load(a, k, t_lo + tt, b, 1);
