@@ -202,11 +202,17 @@ enum tts_hip_option {
     TTS_HIP_OPT_GRAPHS = 2,       /* 1 = replay each graph_compute as a HIP graph (capture + exec update) */
     TTS_HIP_OPT_CONV_F32ACC = 3   /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
 };
-enum tts_fuse_bits { TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32 };
+enum tts_fuse_bits {
+    TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
+    TTS_FUSE_LSTM = 64 /* Kokoro build_lstm_run's unrolled recurrence -> one kernel per step, no O(T^2) concat */
+};
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for
  * weight type `type` (-1 = all types). */
 int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t * launches, double * bytes, int reset);
+/* Diagnostic counters since creation: out[0] HIP-graph exec updates, [1] instantiations,
+ * [2] fused LSTM chains, [3] fused LSTM steps.  Returns the number written (<= n). */
+int tts_hip_counters(tts_hip_backend_t backend, int64_t * out, int n);
 
 /* Raw kernel entry points for micro-benchmarks (device pointers, current backend stream).
  * y[M][N] = W[N][K] . x[M][K]; W is `type` (Q4_K / Q8_0 / F16 / F32) row-major, N rows of K.

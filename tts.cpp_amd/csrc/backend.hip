@@ -23,6 +23,7 @@ static void build_gelu_table(uint16_t * t) {
 
 static const size_t kScratchBytes = 64u << 20;
 static const size_t kShadowBytes = 4u << 20;  // private copy of an attention output (decode: 32 KB per 8 prompts)
+static const size_t kLstmFloats = 4u << 20;   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
 
 extern "C" {
 
@@ -47,6 +48,8 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     be->scratch_size = kScratchBytes;
     TTS_HIP_CHECK(hipMalloc((void **)&be->shadow, kShadowBytes));
     be->shadow_size = kShadowBytes;
+    TTS_HIP_CHECK(hipMalloc((void **)&be->lstm_buf, kLstmFloats * sizeof(float)));
+    be->lstm_floats = kLstmFloats;
     std::vector<uint16_t> tab(65536);
     build_gelu_table(tab.data());
     TTS_HIP_CHECK(hipMalloc((void **)&be->gelu_table, 65536 * sizeof(uint16_t)));
@@ -65,6 +68,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     for (auto e : be->ev_free) hipEventDestroy(e);
     hipFree(be->scratch);
     hipFree(be->shadow);
+    hipFree(be->lstm_buf);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
     if (be->gexec) hipGraphExecDestroy(be->gexec);
@@ -238,6 +242,14 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_CONV_F32ACC: be->conv_f32acc = value != 0; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }
+}
+
+extern "C" int tts_hip_counters(tts_hip_backend_t be, int64_t * out, int n) {
+    if (!be || !out) return TTS_STATUS_BAD_ARG;
+    const int64_t v[4] = {be->graph_updates, be->graph_instantiations, be->lstm_chains, be->lstm_steps};
+    int k = 0;
+    for (; k < n && k < 4; ++k) out[k] = v[k];
+    return k;
 }
 
 extern "C" int tts_hip_gemv_stats(tts_hip_backend_t be, int type, double * ms, int64_t * launches, double * bytes, int reset) {

@@ -98,7 +98,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -118,6 +118,12 @@ struct Item {
     const tts_tensor *x = nullptr, *w = nullptr, *b = nullptr, *dst = nullptr;
     float eps = 0.f;
     bool rms = false;
+    // LSTM: bit 1 = run recurrence step `ls`, bit 2 = write the chain's output `lfinal` from `lhist`
+    int lkind = 0;
+    LstmStepArgs ls{};
+    const tts_tensor * lfinal = nullptr;
+    const float * lhist = nullptr;
+    int64_t lHd = 0, lT = 0;
 };
 
 struct Planner {
@@ -129,6 +135,8 @@ struct Planner {
     std::vector<int> act;  // -1 skip, 0 run node, k>0 run items[k-1]
     std::vector<Item> items;
     int mask = 0xFF;
+    float * lstm_buf = nullptr;  // backend scratch for fused LSTM chains (hidden history + cell)
+    size_t lstm_cap = 0, lstm_used = 0;
 
     const tts_tensor * sole_consumer(const tts_tensor * t) {
         auto it = consumers.find(t);
@@ -159,6 +167,7 @@ struct Planner {
                 consumers[x].push_back(i);
             }
         }
+        if (mask & TTS_FUSE_LSTM) try_lstm();
         for (int i = 0; i < n; ++i) {
             if (act[i] != 0) continue;
             const tts_tensor * t = nodes[i];
@@ -389,6 +398,193 @@ struct Planner {
         return true;
     }
 
+    // ---- LSTM recurrences (Kokoro build_lstm / build_lstm_run, src/models/kokoro/model.cpp:35-86) ----
+    // Per time step the reference emits, for gates I, F, G, O (weights[1], [3], [5], [7]):
+    //   act(ADD(VIEW(pre, column t), ADD(MUL_MAT(W_hh, h_prev), b_hh)))
+    // then c = ADD(MUL(F, c_prev), MUL(I, G)), h = MUL(TANH(c), O), and
+    // outputs = CONCAT(outputs, h, 1) (reversed: CONCAT(h, outputs, 1)).  A chain of such steps
+    // linked through h / c becomes one k_lstm_step launch per step, writing h into a private
+    // history; the intermediate concats (O(T^2) bytes of copies) disappear and one launch writes
+    // the final concat's [Hd, T] output.  Fused only when nothing outside the chain reads any
+    // intermediate (gates, c, h, partial concats), so skipping them is invisible.
+    struct LGate {
+        const tts_tensor *act, *addp, *view, *addb, *mm;
+    };
+    struct LStep {
+        const tts_tensor *h = nullptr, *th = nullptr, *c = nullptr, *mf = nullptr, *mig = nullptr, *hprev = nullptr, *cprev = nullptr;
+        LGate g[4];
+        int64_t col = 0;
+        int prev = -1, next = -1;
+    };
+
+    static bool f32_vec(const tts_tensor * t, int64_t ne0) {
+        return t && t->type == TTS_TYPE_F32 && t->ne[0] == ne0 && t->ne[1] * t->ne[2] * t->ne[3] == 1 && t->nb[0] == 4;
+    }
+
+    bool lstm_gate(const tts_tensor * a, int uop, int64_t Hd, LGate & g) {
+        if (!a || a->op != TTS_OP_UNARY || a->op_params[0] != uop || !f32_vec(a, Hd)) return false;
+        const tts_tensor * ap = a->src[0];
+        if (!ap || ap->op != TTS_OP_ADD || !f32_vec(ap, Hd)) return false;
+        const tts_tensor *v = ap->src[0], *ab = ap->src[1];
+        if (!v || v->op != TTS_OP_VIEW || !ab || ab->op != TTS_OP_ADD || !f32_vec(ab, Hd) || !f32_vec(v, Hd)) return false;
+        const tts_tensor * mm = ab->src[0];
+        if (!mm || mm->op != TTS_OP_MUL_MAT || !f32_vec(mm, Hd) || !f32_vec(ab->src[1], Hd)) return false;
+        const tts_tensor * w = mm->src[0];
+        if (!w || (w->type != TTS_TYPE_F32 && w->type != TTS_TYPE_F16) || w->ne[1] != Hd || w->ne[2] * w->ne[3] != 1 ||
+            w->nb[0] != tts_type_size(w->type) || (w->nb[1] & 15) || ((uintptr_t)w->data & 15))
+            return false;
+        const tts_tensor * pre = v->src[0];
+        if (!pre || pre->type != TTS_TYPE_F32 || pre->nb[0] != 4 || pre->ne[0] != Hd || pre->ne[2] * pre->ne[3] != 1) return false;
+        g = LGate{a, ap, v, ab, mm};
+        return true;
+    }
+
+    bool lstm_step(const tts_tensor * h, LStep & s) {
+        if (h->op != TTS_OP_MUL) return false;
+        const int64_t Hd = h->ne[0];
+        if (!f32_vec(h, Hd) || Hd % 4) return false;
+        const tts_tensor *th = h->src[0], *O = h->src[1];
+        if (!th || th->op != TTS_OP_UNARY || th->op_params[0] != TTS_UNARY_TANH || !f32_vec(th, Hd)) return false;
+        const tts_tensor * c = th->src[0];
+        if (!c || c->op != TTS_OP_ADD || !f32_vec(c, Hd)) return false;
+        const tts_tensor *mf = c->src[0], *mig = c->src[1];
+        if (!mf || mf->op != TTS_OP_MUL || !mig || mig->op != TTS_OP_MUL || !f32_vec(mf, Hd) || !f32_vec(mig, Hd)) return false;
+        if (!lstm_gate(mig->src[0], TTS_UNARY_SIGMOID, Hd, s.g[0]) || !lstm_gate(mf->src[0], TTS_UNARY_SIGMOID, Hd, s.g[1]) ||
+            !lstm_gate(mig->src[1], TTS_UNARY_TANH, Hd, s.g[2]) || !lstm_gate(O, TTS_UNARY_SIGMOID, Hd, s.g[3]))
+            return false;
+        s.hprev = s.g[0].mm->src[1];
+        const tts_tensor * w0 = s.g[0].mm->src[0];
+        const int64_t K = w0->ne[0];
+        if (K % 4 || !f32_vec(s.hprev, K) || ((uintptr_t)s.hprev->data & 15)) return false;
+        s.cprev = mf->src[1];
+        if (!f32_vec(s.cprev, Hd)) return false;
+        for (int g = 0; g < 4; ++g) {
+            const tts_tensor * w = s.g[g].mm->src[0];
+            if (s.g[g].mm->src[1] != s.hprev || w->type != w0->type || w->ne[0] != K) return false;
+            const tts_tensor * pre = s.g[g].view->src[0];
+            const ptrdiff_t off = (const char *)s.g[g].view->data - (const char *)pre->data;
+            if (off < 0 || off % (ptrdiff_t)pre->nb[1]) return false;
+            const int64_t col = off / (ptrdiff_t)pre->nb[1];
+            if (col >= pre->ne[1] || (g > 0 && col != s.col)) return false;
+            s.col = col;
+        }
+        s.h = h;
+        s.th = th;
+        s.c = c;
+        s.mf = mf;
+        s.mig = mig;
+        return true;
+    }
+
+    void try_lstm() {
+        std::vector<LStep> st;
+        std::unordered_map<const tts_tensor *, int> by_h;
+        for (int i = 0; i < n; ++i) {
+            LStep s;
+            if (nodes[i]->op == TTS_OP_MUL && lstm_step(nodes[i], s)) {
+                by_h[s.h] = (int)st.size();
+                st.push_back(s);
+            }
+        }
+        for (size_t k = 0; k < st.size(); ++k) {
+            auto it = by_h.find(st[k].hprev);
+            if (it == by_h.end()) continue;
+            LStep & p = st[it->second];
+            if (p.c != st[k].cprev || p.next != -1 || p.h->ne[0] != st[k].hprev->ne[0]) return;  // ambiguous: fuse nothing
+            st[k].prev = it->second;
+            p.next = (int)k;
+        }
+        for (size_t k0 = 0; k0 < st.size(); ++k0) {
+            if (st[k0].prev != -1) continue;
+            std::vector<int> seq;
+            for (int k = (int)k0; k != -1; k = st[k].next) seq.push_back(k);
+            lstm_chain(st, seq);
+        }
+    }
+
+    void lstm_chain(const std::vector<LStep> & st, const std::vector<int> & seq) {
+        const int64_t T = (int64_t)seq.size();
+        const LStep & s0 = st[seq[0]];
+        const int64_t Hd = s0.h->ne[0];
+        int dir = 1;
+        if (T > 1) dir = (int)(st[seq[1]].col - s0.col);
+        if (dir != 1 && dir != -1) return;
+        if (s0.col != (dir == 1 ? 0 : T - 1)) return;
+        for (int64_t s = 1; s < T; ++s)
+            if (st[seq[s]].col != s0.col + dir * s) return;
+        // the concat chain that accumulates the outputs
+        std::unordered_map<const tts_tensor *, int> mem;  // chain members
+        auto add = [&](const tts_tensor * t) { mem[t] = 1; };
+        const tts_tensor * out = s0.h;
+        for (int64_t s = 0; s < T; ++s) {
+            const LStep & S = st[seq[s]];
+            add(S.h), add(S.th), add(S.c), add(S.mf), add(S.mig);
+            for (int g = 0; g < 4; ++g) add(S.g[g].act), add(S.g[g].addp), add(S.g[g].view), add(S.g[g].addb), add(S.g[g].mm);
+            if (s == 0) continue;
+            const tts_tensor * C = nullptr;
+            auto cs = consumers.find(S.h);
+            if (cs == consumers.end()) return;
+            for (int j : cs->second) {
+                const tts_tensor * x = nodes[j];
+                if (x->op != TTS_OP_CONCAT || x->op_params[0] != 1) continue;
+                if ((dir == 1 && x->src[0] == out && x->src[1] == S.h) || (dir == -1 && x->src[0] == S.h && x->src[1] == out)) C = x;
+            }
+            if (!C) return;
+            add(C);
+            out = C;
+        }
+        const tts_tensor * fin = out;
+        if (fin->type != TTS_TYPE_F32 || fin->ne[0] != Hd || fin->ne[1] != T || fin->ne[2] * fin->ne[3] != 1 || fin->nb[0] != 4) return;
+        // nothing outside the chain may read an intermediate (the final output excepted)
+        for (const auto & kv : mem) {
+            if (kv.first == fin) continue;
+            auto cs = consumers.find(kv.first);
+            if (cs == consumers.end()) continue;
+            for (int j : cs->second)
+                if (!mem.count(nodes[j])) return;
+        }
+        for (const auto & kv : mem)
+            if (act[index[kv.first]] != 0) return;
+        const size_t need = (size_t)Hd * (size_t)(T + 1);
+        if (!lstm_buf || lstm_used + need > lstm_cap) return;
+        float * cbuf = lstm_buf + lstm_used;
+        float * hist = cbuf + Hd;
+        lstm_used += (need + 63) & ~(size_t)63;
+        for (const auto & kv : mem) act[index[kv.first]] = -1;
+        for (int64_t s = 0; s < T; ++s) {
+            const LStep & S = st[seq[s]];
+            Item it;
+            it.kind = Item::LSTM;
+            it.lkind = 1;
+            LstmStepArgs & a = it.ls;
+            for (int g = 0; g < 4; ++g) {
+                a.pre[g] = (const float *)S.g[g].view->data;
+                a.w[g] = S.g[g].mm->src[0]->data;
+                a.w_rs[g] = (int64_t)S.g[g].mm->src[0]->nb[1];
+                a.bias[g] = (const float *)S.g[g].addb->src[1]->data;
+            }
+            a.hprev = s == 0 ? (const float *)S.hprev->data : hist + st[seq[s - 1]].col * Hd;
+            a.cprev = s == 0 ? (const float *)S.cprev->data : cbuf;
+            a.h = hist + S.col * Hd;
+            a.c = cbuf;
+            a.Hd = (int)Hd;
+            a.K = (int)S.g[0].mm->src[0]->ne[0];
+            a.wtype = S.g[0].mm->src[0]->type;
+            if (s == T - 1 && T == 1) {
+                it.lkind = 3;
+                it.lfinal = fin, it.lhist = hist, it.lHd = Hd, it.lT = T;
+            }
+            act[index[S.h]] = add_item(std::move(it));
+        }
+        if (T > 1) {
+            Item it;
+            it.kind = Item::LSTM;
+            it.lkind = 2;
+            it.lfinal = fin, it.lhist = hist, it.lHd = Hd, it.lT = T;
+            act[index[fin]] = add_item(std::move(it));
+        }
+    }
+
     void try_attn(int i) {
         const tts_tensor * S = nodes[i];
         const tts_tensor * KQ = S->src[0];
@@ -603,6 +799,16 @@ static int run_item(tts_hip_backend * be, const Item & it) {
         case Item::LN:
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
             return 0;
+        case Item::LSTM:
+            if (it.lkind & 1) {
+                launch_lstm_step(be, it.ls);
+                be->lstm_steps++;
+            }
+            if (it.lkind & 2) {
+                launch_lstm_finish(be, it.lfinal, it.lhist, it.lHd, it.lT);
+                be->lstm_chains++;
+            }
+            return 0;
     }
     return TTS_STATUS_FAILED;
 }
@@ -696,6 +902,8 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     if (be->profile_gemv) launch_profile_spin(be, 4000.0);  // see launch_profile_spin (k_gemv.hip)
     Planner pl;
     pl.mask = be->fusion;
+    pl.lstm_buf = be->lstm_buf;
+    pl.lstm_cap = be->lstm_floats;
     if (be->fusion) pl.build(nodes, n_nodes);
     for (int i = 0; i < n_nodes; ++i) {
         tts_tensor * n = nodes[i];

@@ -211,6 +211,8 @@ struct tts_hip_backend {
     // allocator has placed that GEMV's output on the attention output's memory
     float * shadow = nullptr;
     size_t shadow_size = 0;
+    float * lstm_buf = nullptr;  // fused LSTM chains: per chain [Hd] cell state + [Hd, T] hidden history
+    size_t lstm_floats = 0;
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
@@ -231,6 +233,7 @@ struct tts_hip_backend {
     hipGraphExec_t gexec = nullptr;
     hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;
+    int64_t lstm_chains = 0, lstm_steps = 0;  // fused LSTM recurrences launched (tts_hip_counters)
     // two prepared plans (tts_hip_graph_prepare / _launch): step n+1 is recorded while step n runs
     hipGraphExec_t pexec[2] = {nullptr, nullptr};
     tts_tensor * const * plan_nodes[2] = {nullptr, nullptr};
@@ -247,6 +250,22 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
 void launch_profile_spin(tts_hip_backend * be, double us);
 void launch_im2col(tts_hip_backend * be, const tts_tensor * node);
+// One fused LSTM recurrence step (Kokoro build_lstm_run, src/models/kokoro/model.cpp:56-86): the
+// four h-GEMVs, bias and input-projection adds, gate activations and the cell update, gate order
+// I, F, G, O (weights[1], [3], [5], [7] of the reference's cell).
+struct LstmStepArgs {
+    const float * pre[4];   // column t of each gate's input projection (W_ih x + b_ih), Hd floats
+    const void * w[4];      // W_hh [Hd rows of K], F32 or F16
+    int64_t w_rs[4];        // row stride, bytes
+    const float * bias[4];  // b_hh [Hd]
+    const float * hprev;    // [K]
+    const float * cprev;    // [Hd]
+    float * h;              // [Hd] out
+    float * c;              // [Hd] out (may alias cprev: per-unit read-then-write)
+    int Hd, K, wtype;
+};
+void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
+void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);
 int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node);

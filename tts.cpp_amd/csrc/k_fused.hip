@@ -55,4 +55,83 @@ void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_te
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- fused LSTM step (Kokoro build_lstm_run, src/models/kokoro/model.cpp:56-86) ------------------
+// The reference unrolls each time step into ~26 ggml nodes: four h-GEMVs (W_hh . h), bias adds,
+// adds of the precomputed input projection column, sigmoid/tanh, the cell update and a concat
+// that re-copies the whole output so far.  Here one launch runs a step: wave w of workgroup b owns
+// hidden unit u = 4b + w and computes its four gate rows together (each lane keeps 4 partial f64
+// sums over its k-slice, as ggml_vec_dot_f32 / _f16 accumulate in double), reduces them, and lane
+// 0 applies the node chain in the reference's order with every intermediate rounded to f32:
+//   g = act(pre[u] + (float(W_g[u] . h) + b_g[u]))      act = sigmoid for I, F, O; tanh for G
+//   c = F*c_prev + I*G,  h = tanh(c) * O
+// F16 weights take the activation rounded to fp16 first (ggml's vec_dot_type for F16).
+__global__ __launch_bounds__(256) void k_lstm_step(LstmStepArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (u >= a.Hd) return;
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = lane * 4; k < a.K; k += 256) {
+        float4 h = *(const float4 *)(a.hprev + k);
+        if (a.wtype == TTS_TYPE_F16) {
+            h.x = __half2float(__float2half_rn(h.x));
+            h.y = __half2float(__float2half_rn(h.y));
+            h.z = __half2float(__float2half_rn(h.z));
+            h.w = __half2float(__float2half_rn(h.w));
+        }
+        float4 w[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const char * row = (const char *)a.w[g] + (int64_t)u * a.w_rs[g];
+            if (a.wtype == TTS_TYPE_F16) {
+                const __half2 * hp = (const __half2 *)(row + 2 * (int64_t)k);
+                const float2 lo = __half22float2(hp[0]), hi = __half22float2(hp[1]);
+                w[g] = make_float4(lo.x, lo.y, hi.x, hi.y);
+            } else {
+                w[g] = *(const float4 *)(row + 4 * (int64_t)k);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            acc[g] += (double)__fmul_rn(w[g].x, h.x);
+            acc[g] += (double)__fmul_rn(w[g].y, h.y);
+            acc[g] += (double)__fmul_rn(w[g].z, h.z);
+            acc[g] += (double)__fmul_rn(w[g].w, h.w);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) acc[g] = wave_sum_f64(acc[g]);
+    if (lane != 0) return;
+    float gv[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const float t1 = __fadd_rn((float)acc[g], a.bias[g][u]);
+        const float x = __fadd_rn(a.pre[g][u], t1);
+        gv[g] = g == 2 ? cr_tanhf(x) : cr_divf(1.f, __fadd_rn(1.f, cr_expf(-x)));
+    }
+    const float c = __fadd_rn(__fmul_rn(gv[1], a.cprev[u]), __fmul_rn(gv[0], gv[2]));
+    a.c[u] = c;
+    a.h[u] = __fmul_rn(cr_tanhf(c), gv[3]);
+}
+
+void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a) {
+    hipLaunchKernelGGL(k_lstm_step, dim3((unsigned)((a.Hd + 3) / 4)), dim3(256), 0, be->stream, a);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+// The chain's output (the last concat node, [Hd, T]) from the private hidden-state history.
+__global__ void k_lstm_finish(TD out, const float * __restrict__ hist, int64_t Hd, int64_t n) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = e % Hd, t = e / Hd;
+        *(float *)(out.data + k * out.nb[0] + t * out.nb[1]) = hist[e];
+    }
+}
+
+void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * out, const float * hist, int64_t Hd, int64_t T) {
+    const int64_t n = Hd * T;
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_lstm_finish, dim3((unsigned)g), dim3(256), 0, be->stream, make_td(out), hist, Hd, n);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts

@@ -145,6 +145,7 @@ def lib():
         "tts_hip_gemv_stats": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
+        "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
         "tts_hip_weight_set": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_hip_weight_get": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
@@ -228,6 +229,13 @@ class HipBackend:
         b = ctypes.c_double()
         self.L.tts_hip_gemv_stats(self.ptr, wtype, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(b), 1 if reset else 0)
         return ms.value, n.value, b.value
+
+    def counters(self):
+        """{graph_updates, graph_instantiations, lstm_chains, lstm_steps} since creation."""
+        out = (ctypes.c_int64 * 4)()
+        n = self.L.tts_hip_counters(self.ptr, out, 4)
+        keys = ("graph_updates", "graph_instantiations", "lstm_chains", "lstm_steps")
+        return {keys[i]: int(out[i]) for i in range(n)}
 
     def close(self):
         if self.ptr:
