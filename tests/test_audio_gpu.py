@@ -119,3 +119,51 @@ def test_kokoro_sine_source_chain(hip):
     assert np.array_equal(u, ur)
     assert np.array_equal(s, sr)
     assert_ulp(st, str_)
+
+
+def _snake_graph(g, x, alpha):
+    """snake_1d (src/util.cpp:98-101) with reciprocal() as DIV of a broadcast 1.0 (util.cpp:86-94)."""
+    T, C = x.shape[1], x.shape[0]
+    xl, al = g.leaf(x), g.leaf(alpha.reshape(C, 1))
+    one = g.leaf(np.ones((1, 1), np.float32))
+    onev = g.view(one, [1, C, 1, 1], [4, 0, 0, 0])
+    recip = g.node("DIV", F32, [1, C], [onev, al])
+    m1 = g.node("MUL", F32, [T, C], [xl, al])
+    s = g.node("SIN", F32, [T, C], [m1])
+    q = g.node("SQR", F32, [T, C], [s])
+    m2 = g.node("MUL", F32, [T, C], [q, recip])
+    return g.node("ADD", F32, [T, C], [xl, m2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,T", [(96, 4096), (7, 33), (1536, 16)])
+@pytest.mark.parametrize("fused", [True, False])
+def test_snake_bit_exact(hip, C, T, fused):
+    rng = np.random.default_rng(C + T)
+    x = (rng.standard_normal((C, T)) * 2).astype(np.float32)
+    alpha = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    if not fused:
+        hip.set_option(0, 0xFF & ~128)
+    try:
+        (gpu, ref), = run_both(hip, lambda g: [_snake_graph(g, x, alpha)])
+    finally:
+        hip.set_option(0, 0xFF)
+    assert np.array_equal(gpu, ref)
+    want = x.astype(np.float64) + np.sin(alpha[:, None].astype(np.float64) * x) ** 2 / alpha[:, None]
+    assert np.max(np.abs(ref.reshape(C, T) - want)) < 1e-5 * np.max(np.abs(want))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(96, 4096), (5, 3), (64, 100)])
+def test_row_broadcast_binary_bit_exact(hip, shape):
+    """ADD / MUL / DIV of a [T, C] activation by a per-channel [1, C] vector (conv bias, alpha)."""
+    C, T = shape
+    rng = np.random.default_rng(T)
+    x = rng.standard_normal((C, T)).astype(np.float32)
+    b = (rng.standard_normal((C, 1)) + 3).astype(np.float32)
+
+    def build(g):
+        xl, bl = g.leaf(x), g.leaf(b)
+        return [g.node(op, F32, [T, C], [xl, bl]) for op in ("ADD", "SUB", "MUL", "DIV")]
+    for gpu, ref in run_both(hip, build):
+        assert np.array_equal(gpu, ref)

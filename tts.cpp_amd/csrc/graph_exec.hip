@@ -98,7 +98,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -175,6 +175,7 @@ struct Planner {
                 case TTS_OP_NORM:
                 case TTS_OP_RMS_NORM: if (mask & TTS_FUSE_LN) try_ln(i); break;
                 case TTS_OP_SOFT_MAX: if (mask & TTS_FUSE_ATTN) try_attn(i); break;
+                case TTS_OP_ADD: if (mask & TTS_FUSE_SNAKE) try_snake(i); break;
                 case TTS_OP_MUL_MAT:
                     if (!((mask & TTS_FUSE_HEADS) && try_heads(i)) && (mask & (TTS_FUSE_GROUP | TTS_FUSE_KV | TTS_FUSE_EPI))) try_gemv(i);
                     break;
@@ -585,6 +586,38 @@ struct Planner {
         }
     }
 
+    // snake_1d (src/util.cpp:98-101): ADD(x, MUL(SQR(SIN(MUL(x, alpha))), recip)) -> one pass.
+    // recip (reciprocal(alpha), a DIV node) is computed where it stands; alpha / recip are [1, C].
+    static bool chan_vec(const tts_tensor * t, int64_t C) {
+        return t && t->type == TTS_TYPE_F32 && contiguous(t) && t->ne[0] == 1 && (t->ne[1] == C || t->ne[1] == 1) && t->ne[2] * t->ne[3] == 1;
+    }
+    void try_snake(int i) {
+        const tts_tensor * A = nodes[i];
+        const tts_tensor *x = A->src[0], *M2 = A->src[1];
+        if (!x || !M2 || M2->op != TTS_OP_MUL || sole_consumer(M2) != A) return;
+        const tts_tensor *Q = M2->src[0], *R = M2->src[1];
+        if (!Q || Q->op != TTS_OP_SQR || sole_consumer(Q) != M2) return;
+        const tts_tensor * S = Q->src[0];
+        if (!S || S->op != TTS_OP_SIN || sole_consumer(S) != Q) return;
+        const tts_tensor * M1 = S->src[0];
+        if (!M1 || M1->op != TTS_OP_MUL || sole_consumer(M1) != S || M1->src[0] != x) return;
+        const tts_tensor * alpha = M1->src[1];
+        const tts_tensor * same[5] = {x, M1, S, Q, M2};
+        for (const tts_tensor * t : same)
+            if (t->type != TTS_TYPE_F32 || !contiguous(t) || t->ne[0] != A->ne[0] || t->ne[1] != A->ne[1] || t->ne[2] != A->ne[2] ||
+                t->ne[3] != A->ne[3])
+                return;
+        if (A->type != TTS_TYPE_F32 || !contiguous(A) || x->ne[0] < 2) return;
+        if (!chan_vec(alpha, x->ne[1]) || !chan_vec(R, x->ne[1]) || alpha->ne[1] != R->ne[1]) return;
+        if (overlap(A, x) && A->data != x->data) return;
+        if (overlap(A, alpha) || overlap(A, R)) return;
+        Item it;
+        it.kind = Item::SNAKE;
+        it.x = x, it.w = alpha, it.b = R, it.dst = A;
+        act[index[M1]] = act[index[S]] = act[index[Q]] = act[index[M2]] = -1;
+        act[i] = add_item(std::move(it));
+    }
+
     void try_attn(int i) {
         const tts_tensor * S = nodes[i];
         const tts_tensor * KQ = S->src[0];
@@ -798,6 +831,9 @@ static int run_item(tts_hip_backend * be, const Item & it) {
         }
         case Item::LN:
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
+            return 0;
+        case Item::SNAKE:
+            launch_snake(be, it.dst, it.x, it.w, it.b);
             return 0;
         case Item::LSTM:
             if (it.lkind & 1) {

@@ -265,6 +265,7 @@ struct LstmStepArgs {
     int Hd, K, wtype;
 };
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
+void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip);
 void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);
 int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);

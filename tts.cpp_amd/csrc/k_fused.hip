@@ -134,4 +134,46 @@ void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * out, const floa
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- snake_1d (src/util.cpp:98-101) ------------------------------------------------------------
+// ADD(x, MUL(SQR(SIN(MUL(x, alpha))), recip)) in one pass instead of five, keeping each node's f32
+// rounding: m = x*a, s = sin(m) (correctly rounded), q = s*s, r = q*recip, y = x + r.  alpha and
+// recip are per-channel ([1, C]: one value per row of the [T, C] activation).
+template <int V>
+__global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, const float * __restrict__ alpha,
+                        const float * __restrict__ recip, int64_t n, int64_t ne0, int64_t nc) {
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V; k < n; k += (int64_t)gridDim.x * blockDim.x * V) {
+        const int64_t c = (k / ne0) % nc;
+        const float a = alpha[c], r = recip[c];
+        float xv[V], y[V];
+        if (V == 4) {
+            const float4 t = *(const float4 *)(x + k);
+            xv[0] = t.x, xv[1] = t.y, xv[2] = t.z, xv[3] = t.w;
+        } else {
+            xv[0] = x[k];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const float sn = cr_sinf(__fmul_rn(xv[e], a));
+            y[e] = __fadd_rn(xv[e], __fmul_rn(__fmul_rn(sn, sn), r));
+        }
+        if (V == 4) *(float4 *)(dst + k) = make_float4(y[0], y[1], y[2], y[3]);
+        else dst[k] = y[0];
+    }
+}
+
+void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip) {
+    const int64_t n = dst->ne[0] * dst->ne[1] * dst->ne[2] * dst->ne[3];
+    const int64_t ne0 = x->ne[0], nc = alpha->ne[1];
+    const bool v4 = ne0 % 4 == 0 && ((uintptr_t)dst->data % 16) == 0 && ((uintptr_t)x->data % 16) == 0;
+    int64_t g = ((v4 ? n / 4 : n) + 255) / 256;
+    if (g > 65536) g = 65536;
+    if (v4)
+        hipLaunchKernelGGL(k_snake<4>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
+                           (const float *)alpha->data, (const float *)recip->data, n, ne0, nc);
+    else
+        hipLaunchKernelGGL(k_snake<1>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
+                           (const float *)alpha->data, (const float *)recip->data, n, ne0, nc);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts

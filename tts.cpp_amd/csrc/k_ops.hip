@@ -55,6 +55,32 @@ __global__ void k_binary_cont(float * __restrict__ dst, const float * __restrict
     }
 }
 
+// Row broadcast (src1 [1, C]: a per-row scalar, e.g. a conv bias or snake's alpha), both sides
+// contiguous, 4 elements per lane when rows are a multiple of 4.
+template <int OP, int V>
+__global__ void k_binary_rowbc(float * __restrict__ dst, const float * __restrict__ a, const float * __restrict__ b, int64_t n,
+                               int64_t ne0, int64_t nb1) {
+    for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V; k < n; k += (int64_t)gridDim.x * blockDim.x * V) {
+        const float y = b[(k / ne0) % nb1];
+        float x[V], v[V];
+        if (V == 4) {
+            const float4 t = *(const float4 *)(a + k);
+            x[0] = t.x, x[1] = t.y, x[2] = t.z, x[3] = t.w;
+        } else {
+            x[0] = a[k];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            if (OP == TTS_OP_ADD) v[e] = __fadd_rn(x[e], y);
+            else if (OP == TTS_OP_SUB) v[e] = __fsub_rn(x[e], y);
+            else if (OP == TTS_OP_MUL) v[e] = __fmul_rn(x[e], y);
+            else v[e] = cr_divf(x[e], y);
+        }
+        if (V == 4) *(float4 *)(dst + k) = make_float4(v[0], v[1], v[2], v[3]);
+        else dst[k] = v[0];
+    }
+}
+
 // ---- unary maps ----
 struct UnaryParams {
     int op;
@@ -371,7 +397,26 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
                               (n % nel(s1)) == 0 &&
                               (s1->ne[1] == s0->ne[1] || s1->ne[1] == 1) && s1->ne[2] == 1 && s1->ne[3] == 1;
             const dim3 g(grid_for(n)), b(256);
-            if (fast) {
+            const bool rowbc = !fast && is_cont(node) && is_cont(s0) && is_cont(s1) && node->type == TTS_TYPE_F32 && s0->type == TTS_TYPE_F32 &&
+                               s1->type == TTS_TYPE_F32 && s1->ne[0] == 1 && s0->ne[0] > 1 && (s1->ne[1] == s0->ne[1] || s1->ne[1] == 1) &&
+                               s1->ne[2] == 1 && s1->ne[3] == 1 && nel(node) == nel(s0);
+            if (rowbc) {
+                const int64_t ne0 = s0->ne[0], nb1 = s1->ne[1];
+                const bool v4 = ne0 % 4 == 0 && ((uintptr_t)node->data % 16) == 0 && ((uintptr_t)s0->data % 16) == 0;
+                const dim3 g4(grid_for(v4 ? n / 4 : n));
+                float * D = (float *)node->data;
+                const float *A = (const float *)s0->data, *B = (const float *)s1->data;
+#define TTS_ROWBC(OPV)                                                                                   \
+    if (v4) hipLaunchKernelGGL((k_binary_rowbc<OPV, 4>), g4, b, 0, st, D, A, B, n, ne0, nb1);             \
+    else hipLaunchKernelGGL((k_binary_rowbc<OPV, 1>), g4, b, 0, st, D, A, B, n, ne0, nb1);
+                switch (node->op) {
+                    case TTS_OP_ADD: TTS_ROWBC(TTS_OP_ADD) break;
+                    case TTS_OP_SUB: TTS_ROWBC(TTS_OP_SUB) break;
+                    case TTS_OP_MUL: TTS_ROWBC(TTS_OP_MUL) break;
+                    default: TTS_ROWBC(TTS_OP_DIV) break;
+                }
+#undef TTS_ROWBC
+            } else if (fast) {
                 const int64_t nb_el = nel(s1);
                 switch (node->op) {
                     case TTS_OP_ADD: hipLaunchKernelGGL(k_binary_cont<TTS_OP_ADD>, g, b, 0, st, (float *)node->data, (const float *)s0->data, (const float *)s1->data, n, nb_el); break;
