@@ -175,7 +175,10 @@ size_t tts_hip_buffer_alignment(void);
 
 int tts_hip_tensor_set(tts_hip_backend_t backend, void * dst_dev, const void * src_host, size_t size);
 int tts_hip_tensor_get(tts_hip_backend_t backend, void * dst_host, const void * src_dev, size_t size);
-int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size);
+int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size); /* stream-ordered */
+/* ggml_backend_i::set_tensor_async: `src_host` is staged at once (reusable on return), the copy runs
+ * in stream order after the work already queued. */
+int tts_hip_tensor_set_async(tts_hip_backend_t backend, void * dst_dev, const void * src_host, size_t size);
 int tts_hip_memset(tts_hip_backend_t backend, void * dst_dev, int value, size_t size);
 int tts_hip_synchronize(tts_hip_backend_t backend);
 
@@ -211,6 +214,13 @@ int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for
  * weight type `type` (-1 = all types). */
 int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t * launches, double * bytes, int reset);
+/* Greedy sampling on the device for an AR step (stream-ordered, no host round trip): for each
+ * (prompt b, head h) row of logits [B][NH][V] the first strict maximum (sampler::max,
+ * src/sampler.cpp:185-204) -> hist[b*NH + h]; eos_seen[b*NH + h] |= (token == eos); and the next
+ * step's input token (next_decoder_token_ids, src/models/parler/model.cpp:778-785):
+ * next[h*B + b] = step + 1 > h ? (eos_seen ? eos : token) : bos. */
+int tts_hip_greedy_step(tts_hip_backend_t backend, const float * logits, int32_t B, int32_t NH, int32_t V, int32_t step,
+                        int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
 /* Diagnostic counters since creation: out[0] HIP-graph exec updates, [1] instantiations,
  * [2] fused LSTM chains, [3] fused LSTM steps.  Returns the number written (<= n). */
 int tts_hip_counters(tts_hip_backend_t backend, int64_t * out, int n);
@@ -237,6 +247,11 @@ typedef struct tts_backend_iface {
     /* optional (NULL = use compute): record into plan slot 0/1 now, launch later */
     int (*prepare)(void * ctx, tts_tensor * const * nodes, int n_nodes, int slot);
     int (*launch)(void * ctx, int slot);
+    /* optional (NULL = host sampling path): stream-ordered set / device copy / greedy step */
+    int (*set_async)(void * ctx, void * dst, const void * src, size_t size);
+    int (*copy)(void * ctx, void * dst, const void * src, size_t size);
+    int (*greedy_step)(void * ctx, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
+                       int32_t * hist, int32_t * next);
 } tts_backend_iface;
 
 /* Fills `out` with the HIP backend's vtable. */

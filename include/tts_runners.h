@@ -55,6 +55,9 @@ int tts_parler_decode(tts_parler * p, const int32_t * audio_tokens, float * logi
 /* Greedy generation loop (generate_from_batch with sampler::max): runs n_steps AR steps after the
  * current position and writes sampled tokens [batch][n_steps][n_output_heads]. */
 int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out);
+/* 1 (default): greedy sampling stays on the device when the backend offers greedy_step (the host
+ * never waits per step); 0: logits are read back and sampled on the host every step. */
+void tts_parler_set_device_sampling(tts_parler * p, int32_t on);
 int32_t tts_parler_position(const tts_parler * p);
 /* Host time per phase summed over steps (us): build graph, allocate, set inputs, compute enqueue,
  * wait for logits.  Returns the step count; reset zeroes the sums. */

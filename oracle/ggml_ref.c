@@ -1124,5 +1124,8 @@ int oracle_backend_iface(tts_backend_iface * out, int n_threads) {
     out->synchronize = ob_sync;
     out->prepare = NULL; /* the oracle computes synchronously: callers fall back to compute */
     out->launch = NULL;
+    out->set_async = NULL;
+    out->copy = NULL;
+    out->greedy_step = NULL;
     return 0;
 }

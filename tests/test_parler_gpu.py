@@ -55,3 +55,51 @@ def test_full_parler_mini_q4k_tokens(hip):
     finally:
         g.close()
         c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_sampling", [True, False])
+def test_generate_in_chunks_and_sampling_paths(hip, device_sampling):
+    """generate(5) + generate(7) on the HIP runner (device-resident greedy loop or host sampling)
+    == generate(12) on the oracle: the EOS / last-token state carries across calls."""
+    g, c = make_pair(hip, batch=3, **TINY)
+    try:
+        g.set_device_sampling(device_sampling)
+        prompt = (np.arange(21, dtype=np.int32).reshape(3, 7) * 53) % 512
+        g.prefill(prompt)
+        c.prefill(prompt)
+        tg = np.concatenate([g.generate(5), g.generate(7)], axis=1)
+        tc = c.generate(12)
+        assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
+    finally:
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
+def test_device_sampling_eos_rule(hip):
+    """Pick an EOS id the model actually emits (from an oracle run), so heads hit EOS mid-run and
+    must keep feeding EOS afterwards (next_decoder_token_ids); device path == oracle."""
+    prompt = (np.arange(14, dtype=np.int32).reshape(2, 7) * 41) % 512
+    probe = ttship.Parler(py_oracle.iface(8), ttship.parler_config(batch=2, **TINY))
+    try:
+        probe.prefill(prompt)
+        t = probe.generate(10)
+    finally:
+        probe.close()
+    vals, counts = np.unique(t[:, 3:6, :], return_counts=True)
+    eos = int(vals[np.argmax(counts)])
+    kw = dict(TINY, batch=2)
+    cfg_g, cfg_c = ttship.parler_config(**kw), ttship.parler_config(**kw)
+    cfg_g.eos_token = cfg_c.eos_token = eos
+    g = ttship.Parler(hip.iface(), cfg_g)
+    c = ttship.Parler(py_oracle.iface(8), cfg_c)
+    try:
+        g.prefill(prompt)
+        c.prefill(prompt)
+        tg, tc = g.generate(12), c.generate(12)
+        assert (tc == eos).any()
+        assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
+    finally:
+        g.close()
+        c.close()

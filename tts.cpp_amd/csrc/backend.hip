@@ -23,7 +23,8 @@ static void build_gelu_table(uint16_t * t) {
 
 static const size_t kScratchBytes = 64u << 20;
 static const size_t kShadowBytes = 4u << 20;  // private copy of an attention output (decode: 32 KB per 8 prompts)
-static const size_t kLstmFloats = 4u << 20;   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
+static const size_t kLstmFloats = 4u << 20;
+static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tensor_async   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
 
 extern "C" {
 
@@ -50,6 +51,9 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     be->shadow_size = kShadowBytes;
     TTS_HIP_CHECK(hipMalloc((void **)&be->lstm_buf, kLstmFloats * sizeof(float)));
     be->lstm_floats = kLstmFloats;
+    TTS_HIP_CHECK(hipHostMalloc((void **)&be->pin, kPinBytes, hipHostMallocDefault));
+    be->pin_size = kPinBytes;
+    for (auto & e : be->plan_ev) TTS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     std::vector<uint16_t> tab(65536);
     build_gelu_table(tab.data());
     TTS_HIP_CHECK(hipMalloc((void **)&be->gelu_table, 65536 * sizeof(uint16_t)));
@@ -66,6 +70,10 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
         hipEventDestroy(p.second);
     }
     for (auto e : be->ev_free) hipEventDestroy(e);
+    for (auto & r : be->pin_pending) hipEventDestroy(r.ev);
+    for (auto e : be->pin_events) hipEventDestroy(e);
+    for (auto e : be->plan_ev) hipEventDestroy(e);
+    hipHostFree(be->pin);
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->lstm_buf);
@@ -104,6 +112,56 @@ int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_
     // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
     if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
     if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    return 0;
+}
+
+// ggml_backend_i::set_tensor_async: the bytes are staged in pinned memory now (the caller may reuse
+// `src` at once) and copied in stream order, so the host does not wait for work already queued.
+int tts_hip_tensor_set_async(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
+    if (!be) return TTS_STATUS_BAD_ARG;
+    if (size == 0) return 0;
+    hipSetDevice(be->device);
+    if (size > be->pin_size / 2) return tts_hip_tensor_set(be, dst, src, size);
+    // recycle finished regions
+    while (!be->pin_pending.empty() && hipEventQuery(be->pin_pending.front().ev) == hipSuccess) {
+        be->pin_events.push_back(be->pin_pending.front().ev);
+        be->pin_pending.pop_front();
+    }
+    size_t off = (be->pin_head + 255) & ~(size_t)255;
+    if (off + size > be->pin_size) off = 0;
+    // wait for the newest pending copy whose staging overlaps; older ones finished before it
+    int last = -1;
+    for (int i = 0; i < (int)be->pin_pending.size(); ++i) {
+        const auto & r = be->pin_pending[i];
+        if (r.off < off + size && off < r.off + r.size) last = i;
+    }
+    if (last >= 0) {
+        if (hipEventSynchronize(be->pin_pending[last].ev) != hipSuccess) return TTS_STATUS_FAILED;
+        for (int i = 0; i <= last; ++i) {
+            be->pin_events.push_back(be->pin_pending.front().ev);
+            be->pin_pending.pop_front();
+        }
+    }
+    memcpy(be->pin + off, src, size);
+    if (hipMemcpyAsync(dst, be->pin + off, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    hipEvent_t ev;
+    if (be->pin_events.empty()) {
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return TTS_STATUS_FAILED;
+    } else {
+        ev = be->pin_events.back();
+        be->pin_events.pop_back();
+    }
+    if (hipEventRecord(ev, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    be->pin_pending.push_back({off, size, ev});
+    be->pin_head = off + size;
+    return 0;
+}
+
+int tts_hip_greedy_step(tts_hip_backend_t be, const float * logits, int32_t B, int32_t NH, int32_t V, int32_t step, int32_t bos,
+                        int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next) {
+    if (!be || !logits || B <= 0 || NH <= 0 || V <= 0) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    launch_greedy_step(be, logits, B, NH, V, step, bos, eos, eos_seen, hist, next);
     return 0;
 }
 
@@ -303,6 +361,11 @@ static int hb_prepare(void * c, tts_tensor * const * nodes, int n, int slot) {
     return tts_hip_graph_prepare((tts_hip_backend_t)c, nodes, n, slot);
 }
 static int hb_launch(void * c, int slot) { return tts_hip_graph_launch((tts_hip_backend_t)c, slot); }
+static int hb_set_async(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_set_async((tts_hip_backend_t)c, d, s, n); }
+static int hb_copy(void * c, void * d, const void * s, size_t n) { return tts_hip_tensor_copy((tts_hip_backend_t)c, d, s, n); }
+static int hb_greedy(void * c, const float * l, int B, int NH, int V, int step, int bos, int eos, int32_t * seen, int32_t * hist, int32_t * next) {
+    return tts_hip_greedy_step((tts_hip_backend_t)c, l, B, NH, V, step, bos, eos, seen, hist, next);
+}
 
 extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * out) {
     if (!be || !out) return TTS_STATUS_BAD_ARG;
@@ -318,5 +381,8 @@ extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * o
     out->synchronize = hb_sync;
     out->prepare = hb_prepare;
     out->launch = hb_launch;
+    out->set_async = hb_set_async;
+    out->copy = hb_copy;
+    out->greedy_step = hb_greedy;
     return 0;
 }

@@ -916,6 +916,10 @@ extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * 
 extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes, int slot) {
     if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    if (be->plan_ev_pending[slot]) {  // the slot's previous launch must have run before it is re-recorded
+        TTS_HIP_CHECK(hipEventSynchronize(be->plan_ev[slot]));
+        be->plan_ev_pending[slot] = false;
+    }
     be->plan_nodes[slot] = nodes;
     be->plan_n[slot] = n_nodes;
     be->plan_eager[slot] = !capture_worthy(be, nodes, n_nodes);
@@ -926,9 +930,15 @@ extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * 
 extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
     if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
-    if (be->plan_eager[slot]) return graph_compute_launches(be, be->plan_nodes[slot], be->plan_n[slot]);
-    if (!be->pexec[slot]) return TTS_STATUS_BAD_ARG;
-    TTS_HIP_CHECK(hipGraphLaunch(be->pexec[slot], be->stream));
+    if (be->plan_eager[slot]) {
+        const int st = graph_compute_launches(be, be->plan_nodes[slot], be->plan_n[slot]);
+        if (st != 0) return st;
+    } else {
+        if (!be->pexec[slot]) return TTS_STATUS_BAD_ARG;
+        TTS_HIP_CHECK(hipGraphLaunch(be->pexec[slot], be->stream));
+    }
+    TTS_HIP_CHECK(hipEventRecord(be->plan_ev[slot], be->stream));
+    be->plan_ev_pending[slot] = true;
     return 0;
 }
 

@@ -6,6 +6,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <deque>
 #include <vector>
 
 #include "common.h"
@@ -211,6 +212,20 @@ struct tts_hip_backend {
     // allocator has placed that GEMV's output on the attention output's memory
     float * shadow = nullptr;
     size_t shadow_size = 0;
+    // tts_hip_tensor_set_async staging: a pinned ring; a region is reused once the event recorded
+    // after its copy has completed (ggml_backend_i::set_tensor_async semantics: the caller may
+    // reuse its buffer at once, the copy is ordered on the compute stream)
+    uint8_t * pin = nullptr;
+    size_t pin_size = 0, pin_head = 0;
+    struct PinRec {
+        size_t off, size;
+        hipEvent_t ev;
+    };
+    std::deque<PinRec> pin_pending;
+    std::vector<hipEvent_t> pin_events;
+    // completion of each plan slot's last launch: a slot is re-recorded only after it ran
+    hipEvent_t plan_ev[2] = {nullptr, nullptr};
+    bool plan_ev_pending[2] = {false, false};
     float * lstm_buf = nullptr;  // fused LSTM chains: per chain [Hd] cell state + [Hd, T] hidden history
     size_t lstm_floats = 0;
     tts::ActQuant aq;
@@ -265,6 +280,8 @@ struct LstmStepArgs {
     int Hd, K, wtype;
 };
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
+void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
+                        int32_t * hist, int32_t * next);
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip);
 void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);

@@ -176,4 +176,48 @@ void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- greedy sampling step (sampler::max, src/sampler.cpp:185-204) --------------------------------
+// One wave per (prompt b, head h) row of the step's logits [B][NH][V]: each lane scans its strided
+// slice keeping the first strict maximum (indices ascend within a lane), then the lanes combine by
+// (larger value, then smaller index) -- the sequential scan's answer, NaN skipped, 0 when no value
+// exceeds -inf.  Lane 0 applies Parler's next-token rule (next_decoder_token_ids, model.cpp:778-785).
+__global__ __launch_bounds__(256) void k_greedy_step(const float * __restrict__ logits, int B, int NH, int V, int step, int bos, int eos,
+                                                     int32_t * eos_seen, int32_t * hist, int32_t * next) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= B * NH) return;
+    const float * l = logits + (int64_t)row * V;
+    float best = -INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int i = lane; i < V; i += 64) {
+        const float v = l[i];
+        if (v > best) {
+            best = v;
+            bi = i;
+        }
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float ov = __shfl_xor(best, off);
+        const int oi = __shfl_xor(bi, off);
+        if (ov > best || (ov == best && oi < bi)) {
+            best = ov;
+            bi = oi;
+        }
+    }
+    if (lane != 0) return;
+    const int tok = bi == 0x7FFFFFFF ? 0 : bi;
+    const int b = row / NH, h = row % NH;
+    hist[row] = tok;
+    const int seen = eos_seen[row] | (tok == eos);
+    eos_seen[row] = seen;
+    next[h * B + b] = step + 1 > h ? (seen ? eos : tok) : bos;
+}
+
+void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
+                        int32_t * hist, int32_t * next) {
+    hipLaunchKernelGGL(k_greedy_step, dim3((unsigned)((B * NH + 3) / 4)), dim3(256), 0, be->stream, logits, B, NH, V, step, bos, eos, eos_seen,
+                       hist, next);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace tts

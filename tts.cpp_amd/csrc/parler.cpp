@@ -49,6 +49,7 @@ struct tts_parler {
     int32_t last_nodes = 0;
     double host_us[5] = {0, 0, 0, 0, 0};  // build, alloc, set_inputs, compute (record + launch), get (wait)
     bool prepared = false;  // a step is built and recorded, waiting for launch_step
+    bool device_sampling = true;  // greedy sampling on the device when the backend offers it
     int prep_slot = 0, prep_n = 0;
     bool prep_audio = true;
     void * launched_out = nullptr;  // logits of the last launched step (device)
@@ -427,12 +428,20 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
 }
 
 // set_inputs (model.cpp:616-643): only rows < n of the causal mask are written/read.
-static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n) {
+static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n, bool async = false) {
     const auto & cf = p->cfg;
     const int B = cf.batch;
-    auto & be = p->be;
+    auto & be0 = p->be;
+    struct {
+        tts_backend_iface & b;
+        bool a;
+        void * ctx;
+        int set(void *, void * d, const void * s, size_t n) { return a ? b.set_async(b.ctx, d, s, n) : b.set(b.ctx, d, s, n); }
+    } be{be0, async && be0.set_async, be0.ctx};
     int st = 0;
-    if (audio) {
+    if (audio && !tokens) {
+        // tokens already on the device (device sampling path)
+    } else if (audio) {
         if (B == 1) {
             // audio tokens arrive as [heads] for n == 1; layout [heads][n] otherwise
             st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * cf.n_output_heads);
@@ -487,10 +496,10 @@ static int prepare_step(tts_parler * p, bool audio, int n) {
     return 0;
 }
 
-static int launch_step(tts_parler * p, const int32_t * tokens) {
+static int launch_step(tts_parler * p, const int32_t * tokens, bool async = false) {
     if (!p->prepared) return TTS_STATUS_FAILED;
     auto t0 = std::chrono::steady_clock::now();
-    if (set_inputs(p, tokens, p->prep_audio, p->prep_n) != 0) return TTS_STATUS_FAILED;
+    if (set_inputs(p, tokens, p->prep_audio, p->prep_n, async) != 0) return TTS_STATUS_FAILED;
     auto t1 = std::chrono::steady_clock::now();
     const int st = p->be.launch ? p->be.launch(p->be.ctx, p->prep_slot)
                                 : p->be.compute(p->be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size());
@@ -550,8 +559,68 @@ static int32_t argmax_head(const float * l, int vocab) {
     return id;
 }
 
+// Device-resident greedy loop (backends with set_async / copy / greedy_step): the step's logits
+// never leave the device.  After step s is launched the host records step s+1, then queues the
+// greedy step (tokens of step s -> history, EOS state, step s+1's input tokens) and step s+1's
+// positions / masks behind it, and launches step s+1 -- the host never waits for the device, so
+// its graph work hides completely behind the device's step.  Tokens are identical to the host
+// path (same first-maximum rule, same next-token rule); tests/test_parler_gpu.py checks them
+// against the oracle.
+static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out) {
+    const auto & cf = p->cfg;
+    const int B = cf.batch, NH = cf.n_output_heads, V = cf.output_vocab;
+    auto & be = p->be;
+    const size_t rowi = (size_t)B * NH * sizeof(int32_t);
+    int32_t * d_seen = (int32_t *)be.alloc(be.ctx, rowi);
+    int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
+    int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
+    if (!d_seen || !d_next || !d_hist) return TTS_STATUS_ALLOC_FAILED;
+    std::vector<int32_t> seen((size_t)B * NH), next((size_t)B * NH);
+    for (int b = 0; b < B; ++b)
+        for (int h = 0; h < NH; ++h) {
+            seen[(size_t)b * NH + h] = p->eos_seen[b][h] ? 1 : 0;
+            const auto & ot = p->output_tokens[b];
+            next[(size_t)b * NH + h] = p->current_step > h ? (p->eos_seen[b][h] ? cf.eos_token : ot[ot.size() - NH + h]) : cf.bos_token;
+        }
+    int st = be.set(be.ctx, d_seen, seen.data(), rowi);
+    if (st == 0 && !p->prepared) st = prepare_step(p, true, 1);
+    if (st == 0) st = launch_step(p, next.data(), true);
+    for (int s = 0; st == 0 && s < n_steps; ++s) {
+        const float * logits = (const float *)p->launched_out;
+        if (s + 1 < n_steps) st = prepare_step(p, true, 1);  // records step s+1 while the device runs step s
+        if (st == 0)
+            st = be.greedy_step(be.ctx, logits, B, NH, V, p->current_step + s, cf.bos_token, cf.eos_token, d_seen,
+                                d_hist + (size_t)s * B * NH, d_next);
+        if (st == 0 && s + 1 < n_steps) {
+            st = be.copy(be.ctx, p->in_tokens->data, d_next, rowi);
+            if (st == 0) st = launch_step(p, nullptr, true);
+        }
+    }
+    std::vector<int32_t> hist((size_t)n_steps * B * NH);
+    if (st == 0) st = be.get(be.ctx, hist.data(), d_hist, hist.size() * sizeof(int32_t));
+    if (st == 0) st = be.get(be.ctx, seen.data(), d_seen, rowi);
+    be.free(be.ctx, d_seen);
+    be.free(be.ctx, d_next);
+    be.free(be.ctx, d_hist);
+    if (st != 0) return st;
+    for (int s = 0; s < n_steps; ++s)
+        for (int b = 0; b < B; ++b)
+            for (int h = 0; h < NH; ++h) {
+                const int32_t t = hist[((size_t)s * B + b) * NH + h];
+                p->output_tokens[b].push_back(t);
+                if (tokens_out) tokens_out[((size_t)b * n_steps + s) * NH + h] = t;
+            }
+    for (int b = 0; b < B; ++b)
+        for (int h = 0; h < NH; ++h) p->eos_seen[b][h] = seen[(size_t)b * NH + h] != 0;
+    p->current_step += n_steps;
+    return 0;
+}
+
 extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out) {
     const auto & cf = p->cfg;
+    if (n_steps <= 0) return 0;
+    if (p->be.greedy_step && p->be.set_async && p->be.copy && p->be.prepare && p->device_sampling)
+        return generate_device(p, n_steps, tokens_out);
     const int B = cf.batch, NH = cf.n_output_heads;
     std::vector<float> logits((size_t)B * NH * cf.output_vocab);
     std::vector<int32_t> next((size_t)B * NH);
@@ -588,6 +657,7 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
 }
 
 extern "C" int32_t tts_parler_position(const tts_parler * p) { return p->position; }
+extern "C" void tts_parler_set_device_sampling(tts_parler * p, int32_t on) { p->device_sampling = on != 0; }
 
 extern "C" int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset) {
     for (int i = 0; i < 5; ++i) us5[i] = p->host_us[i];

@@ -60,6 +60,9 @@ class BackendIface(ctypes.Structure):
         ("synchronize", ctypes.c_void_p),
         ("prepare", ctypes.c_void_p),
         ("launch", ctypes.c_void_p),
+        ("set_async", ctypes.c_void_p),
+        ("copy", ctypes.c_void_p),
+        ("greedy_step", ctypes.c_void_p),
     ]
 
 
@@ -153,6 +156,7 @@ def lib():
         "tts_parler_default_config": (None, [ctypes.POINTER(ParlerConfig)]),
         "tts_parler_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(ParlerConfig)]),
         "tts_parler_free": (None, [vp]),
+        "tts_parler_set_device_sampling": (None, [vp, ctypes.c_int32]),
         "tts_parler_reset": (None, [vp]),
         "tts_parler_prefill": (ctypes.c_int, [vp, vp, i32]),
         "tts_parler_decode": (ctypes.c_int, [vp, vp, vp]),
@@ -292,6 +296,10 @@ class Parler:
 
     def reset(self):
         self.L.tts_parler_reset(self.ptr)
+
+    def set_device_sampling(self, on):
+        """Greedy sampling on the device (default when the backend supports it) or on the host."""
+        self.L.tts_parler_set_device_sampling(self.ptr, 1 if on else 0)
 
     @property
     def position(self):
