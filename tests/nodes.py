@@ -90,7 +90,10 @@ class Graph:
         for i in range(4):
             ne[ax[i]] = a.ne[i]
             nb[ax[i]] = a.nb[i]
-        return self.view(a, ne, nb, 0, op="PERMUTE")
+        t = self.view(a, ne, nb, 0, op="PERMUTE")
+        for i in range(4):
+            t.op_params[i] = ax[i]  # ggml_permute's op params (the attention fusion matches on them)
+        return t
 
     def transpose(self, a):
         return self.permute(a, (1, 0, 2, 3))

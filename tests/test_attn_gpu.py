@@ -1,0 +1,60 @@
+"""Fused decode attention vs the oracle running the reference's unfused node chain
+(Parler model.cpp:549-571): cont(K view) -> mul_mat(K, q) -> soft_max_ext(mask, 1/sqrt(hd)) ->
+mul_mat(kq, V view) -> permute(2, 0, 1, 3) -> cont, with K / V read from cache layouts.
+
+Kernel choice depends on the context length (k_attn.hip): P <= 64 -> k_attn_small (sequential
+sums, bit-exact), P <= 512 / 1024 -> k_attn_decode_rows with V prefetched (8 / 16 chunks per lane),
+longer -> streamed V; hd 128 (Dia / Orpheus head size).  The row kernel reassociates
+the f64 sums (quad / row DPP reductions), so it is held to <= 1 ulp with almost all elements exact.
+"""
+import numpy as np
+import pytest
+
+import audio_ops as ao
+import nodes as nd
+import ttship
+
+F32 = ttship.F32
+
+
+def build(g, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx):
+    """q (B, H, hd); kc (B, P_cap, Hk*hd) position-major K cache; vc (B, Hk*hd, max_ctx) transposed V."""
+    ql = g.leaf(q.reshape(B, 1, H, hd))                       # ne [hd, H, 1, B]
+    qp = g.permute(ql, (0, 2, 1, 3))                          # [hd, 1, H, B]
+    qc = g.node("CONT", F32, [hd, 1, H, B], [qp])
+    kl = g.leaf(kc)                                           # ne [Hk*hd, P_cap, B]
+    k = g.view(kl, [hd, P, Hk, B], [4, Hk * hd * 4, hd * 4, kl.nb[2]])
+    kcont = g.node("CONT", F32, [hd, P, Hk, B], [k])
+    kq = g.node("MUL_MAT", F32, [P, 1, H, B], [kcont, qc])
+    ml = g.leaf(mask.reshape(1, P))
+    sm = g.node("SOFT_MAX", F32, [P, 1, H, B], [kq, ml], fparams={0: float(1.0 / np.sqrt(hd)), 1: 0.0})
+    vl = g.leaf(vc)                                           # ne [max_ctx, Hk*hd, B]
+    v = g.view(vl, [P, hd, Hk, B], [4, max_ctx * 4, max_ctx * hd * 4, vl.nb[2]])
+    kqv = g.node("MUL_MAT", F32, [1, hd, H, B], [sm, v])
+    merged = g.permute(kqv, (2, 0, 1, 3))                     # [hd, H, 1, B]
+    return g.node("CONT", F32, [hd, H, 1, B], [merged])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,hd,H,Hk,B", [(3, 64, 16, 16, 2), (64, 64, 16, 16, 1), (65, 64, 4, 4, 1), (500, 64, 16, 16, 2),
+                                         (700, 64, 16, 16, 1), (1024, 64, 4, 4, 1), (1500, 64, 4, 4, 1),
+                                         (37, 128, 16, 16, 2), (430, 128, 8, 8, 1), (1, 64, 4, 4, 1)])
+def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B):
+    rng = np.random.default_rng(P * 7 + hd)
+    max_ctx = P + 40
+    q = rng.standard_normal((B, H, hd)).astype(np.float32)
+    kc = rng.standard_normal((B, max_ctx, Hk * hd)).astype(np.float32)
+    vc = rng.standard_normal((B, Hk * hd, max_ctx)).astype(np.float32)
+    mask = np.zeros(P, np.float32)
+    if P > 4:
+        mask[P // 3] = -np.inf  # a masked key inside the window
+    g1, g2 = nd.Graph(), nd.Graph()
+    o1 = build(g1, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx)
+    o2 = build(g2, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx)
+    g1.run_hip(hip)
+    g2.run_oracle(n_threads=8)
+    gpu, ref = g1.node_array(o1), g2.node_array(o2)
+    if P <= 64:
+        assert np.array_equal(gpu, ref)
+    else:
+        assert ao.ulp_diff(gpu, ref) <= 1 and np.mean(gpu != ref) <= 1e-3

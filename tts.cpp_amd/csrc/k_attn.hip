@@ -195,9 +195,8 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
 //   - C: a 16-lane row per output dim (lane t: positions 4t + 64u as 16-B loads of the V row when
 //     VVEC, else scalar positions t + 16u), 32 dims per pass, DPP row reduction in f64.
 // No reduction goes through the LDS crossbar and every load batch is issued before its first use.
-constexpr int ATTN_UV = 8;  // V chunks (per lane, per dim pass) in flight
-
-template <int DPR, bool VVEC, bool PF>
+// ATTN_UV: V chunks (per lane, per dim pass) in flight.
+template <int DPR, bool VVEC, bool PF, int ATTN_UV>
 __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
     __shared__ float s_wf[ATTN_THREADS / 64];
@@ -372,11 +371,94 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     TTS_TS(a, 4);
 }
 
-template <int DPR, bool PF>
+template <int DPR, bool PF, int UV = 8>
 static void launch_attn_rows(tts_hip_backend * be, const AttnArgs & a, bool vvec) {
     const dim3 grid((unsigned)a.H, (unsigned)a.n, (unsigned)a.B);
-    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true, PF>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
-    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false, PF>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true, PF, UV>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false, PF, UV>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// Short contexts (P <= 64: Parler's cross-attention over the T5 prompt encoding, n_enc = 3; the
+// first decode steps): one wave per (head, query, sequence), lane = key position, every sum in the
+// oracle's sequential order -- the q.K dot over d, the soft_max denominator over positions (lane 0
+// walks the lanes' exponentials), and each output dim over positions.  All of K, q and V are
+// requested at entry; there is no LDS and no barrier.
+template <int HD>
+__global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
+    constexpr int F = HD / 4;
+    const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
+    const int lane = threadIdx.x;
+    const int P = a.P;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const int p = min(lane, P - 1);
+    float4 kr[F];
+#pragma unroll
+    for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+    float qv[HD];
+#pragma unroll
+    for (int d = 0; d < HD; ++d) qv[d] = *(const float *)(qbase + (int64_t)d * a.q.nb[0]);
+    constexpr int VB = 8;  // V positions per batch, per output dim
+    float vv[HD / 64][VB];
+    auto load_v = [&](int i0) {
+#pragma unroll
+        for (int j = 0; j < HD / 64; ++j)
+#pragma unroll
+            for (int u = 0; u < VB; ++u)
+                vv[j][u] = *(const float *)(vbase + (int64_t)(lane + 64 * j) * a.v.nb[1] + (int64_t)min(i0 + u, P - 1) * a.v.nb[0]);
+    };
+    load_v(0);
+    TTS_PIN_LOADS();
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < F; ++c) {
+        acc += (double)__fmul_rn(kr[c].x, qv[4 * c + 0]);
+        acc += (double)__fmul_rn(kr[c].y, qv[4 * c + 1]);
+        acc += (double)__fmul_rn(kr[c].z, qv[4 * c + 2]);
+        acc += (double)__fmul_rn(kr[c].w, qv[4 * c + 3]);
+    }
+    float w = __fmul_rn((float)acc, a.scale);
+    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, a.mask[(int64_t)tq * P + p]));
+    if (lane >= P) w = -INFINITY;
+    float mx = w;
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    const float e = lane < P ? cr_expf(__fsub_rn(w, mx)) : 0.f;
+    double sum = 0.0;
+    for (int i = 0; i < P; ++i) sum += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), i));
+    const float pr = __fmul_rn(e, (float)(1.0 / sum));
+    double o[HD / 64];
+#pragma unroll
+    for (int j = 0; j < HD / 64; ++j) o[j] = 0.0;
+    for (int i0 = 0; i0 < P; i0 += VB) {
+        if (i0 > 0) {
+            load_v(i0);
+            TTS_PIN_LOADS();
+        }
+#pragma unroll
+        for (int u = 0; u < VB; ++u) {
+            if (i0 + u >= P) break;
+            const float pi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), i0 + u));
+#pragma unroll
+            for (int j = 0; j < HD / 64; ++j) o[j] += (double)__fmul_rn(pi, vv[j][u]);
+        }
+    }
+    const int64_t orow = (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+#pragma unroll
+    for (int j = 0; j < HD / 64; ++j) {
+        a.out[orow + lane + 64 * j] = (float)o[j];
+        if (a.out2) a.out2[orow + lane + 64 * j] = (float)o[j];
+    }
 }
 
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
@@ -398,11 +480,19 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
     const bool krows = (hd == 64 || hd == 128) && k.nb[0] == 4 && (k.nb[1] % 16) == 0 &&
                        (((uintptr_t)k.data) % 16) == 0 && (k.nb[2] % 16) == 0 &&
                        (k.nb[3] % 16) == 0 && q.nb[0] == 4 && P > 0;
+    if (krows && P <= 64) {
+        const dim3 grid((unsigned)H, (unsigned)n, (unsigned)B);
+        if (hd == 64) hipLaunchKernelGGL(k_attn_small<64>, grid, dim3(64), 0, be->stream, a);
+        else hipLaunchKernelGGL(k_attn_small<128>, grid, dim3(64), 0, be->stream, a);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (krows) {
         const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
                           (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
         // PF: the whole V slice fits the registers of one pass (16 x 16-B or 16 scalar loads per lane)
-        const bool pf = hd == 64 && P <= (vvec ? 64 * ATTN_UV : 16 * ATTN_UV);
+        const bool pf = hd == 64 && P <= (vvec ? 64 * 8 : 16 * 8);
+        // (a 16-chunk prefetch covering P <= 1024 measured slower than streaming V: 20.3 vs 16.7 us)
         if (hd == 64 && pf) launch_attn_rows<1, true>(be, a, vvec);
         else if (hd == 64) launch_attn_rows<1, false>(be, a, vvec);
         else launch_attn_rows<2, false>(be, a, vvec);
