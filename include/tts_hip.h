@@ -200,7 +200,7 @@ int tts_hip_graph_launch(tts_hip_backend_t backend, int slot);
 
 /* Backend options (env-free knobs used by the bench / tests). */
 enum tts_hip_option {
-    TTS_HIP_OPT_FUSION = 0,      /* TTS_FUSE_* bitmask of enabled patterns (default 0xFF, 0 = off) */
+    TTS_HIP_OPT_FUSION = 0,      /* TTS_FUSE_* bitmask of enabled patterns (default: all bits, 0 = off) */
     TTS_HIP_OPT_PROFILE_GEMV = 1, /* 1 = time quantized GEMV launches with HIP events */
     TTS_HIP_OPT_GRAPHS = 2,       /* 1 = replay each graph_compute as a HIP graph (capture + exec update) */
     TTS_HIP_OPT_CONV_F32ACC = 3   /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
@@ -208,7 +208,8 @@ enum tts_hip_option {
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
     TTS_FUSE_LSTM = 64, /* Kokoro build_lstm_run's unrolled recurrence -> one kernel per step, no O(T^2) concat */
-    TTS_FUSE_SNAKE = 128 /* snake_1d's five elementwise nodes -> one pass */
+    TTS_FUSE_SNAKE = 128, /* snake_1d's five elementwise nodes -> one pass */
+    TTS_FUSE_EMBED = 256  /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

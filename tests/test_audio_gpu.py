@@ -143,11 +143,11 @@ def test_snake_bit_exact(hip, C, T, fused):
     x = (rng.standard_normal((C, T)) * 2).astype(np.float32)
     alpha = rng.uniform(0.5, 1.5, C).astype(np.float32)
     if not fused:
-        hip.set_option(0, 0xFF & ~128)
+        hip.set_option(0, ttship.FUSE_ALL & ~128)
     try:
         (gpu, ref), = run_both(hip, lambda g: [_snake_graph(g, x, alpha)])
     finally:
-        hip.set_option(0, 0xFF)
+        hip.set_option(0, ttship.FUSE_ALL)
     assert np.array_equal(gpu, ref)
     want = x.astype(np.float64) + np.sin(alpha[:, None].astype(np.float64) * x) ** 2 / alpha[:, None]
     assert np.max(np.abs(ref.reshape(C, T) - want)) < 1e-5 * np.max(np.abs(want))

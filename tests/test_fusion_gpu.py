@@ -9,7 +9,7 @@ import ttship
 
 TINY = dict(n_layers=2, hidden_size=256, n_attn_heads=4, ffn_size=1024, output_vocab=1088, max_ctx=96,
             prompt_vocab=512, max_positions=128)
-MASKS = {"off": 0, "ln": 1, "group": 2, "kv": 2 | 4, "epi": 8, "heads": 16, "attn": 32, "all": 0xFF}
+MASKS = {"off": 0, "ln": 1, "group": 2, "kv": 2 | 4, "epi": 8, "heads": 16, "attn": 32, "embed": 256, "all": ttship.FUSE_ALL}
 
 
 @pytest.fixture(scope="module")
@@ -39,7 +39,7 @@ def test_fusion_bit_exact(hip, oracle_runs, batch, name):
         logits = g.decode(np.full((batch, 9), 7, dtype=np.int32))
         g.close()
     finally:
-        hip.set_option(0, 0xFF)
+        hip.set_option(0, ttship.FUSE_ALL)
     assert np.array_equal(toks, toks_ref), f"{name}: tokens differ\n{toks}\n{toks_ref}"
     diff = np.abs(logits.astype(np.float64) - logits_ref)
     assert np.array_equal(logits.view(np.uint32), logits_ref.view(np.uint32)), f"{name}: max |dlogit| {diff.max()}"

@@ -65,13 +65,13 @@ def test_lstm_unfused_generic_path(hip):
     rng = np.random.default_rng(5)
     x = (rng.standard_normal((T, n_in)) * 0.5).astype(np.float32)
     dirs = lstm.lstm_weights(6, n_in, hd)
-    hip.set_option(0, 0xFF & ~64)
+    hip.set_option(0, ttship.FUSE_ALL & ~64)
     try:
         before = hip.counters()
         gpu, ref = run_both(hip, lambda g: lstm.lstm(g, x, dirs))
         assert hip.counters()["lstm_steps"] == before["lstm_steps"]
     finally:
-        hip.set_option(0, 0xFF)
+        hip.set_option(0, ttship.FUSE_ALL)
     check(gpu, ref)
 
 

@@ -98,7 +98,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -118,6 +118,8 @@ struct Item {
     const tts_tensor *x = nullptr, *w = nullptr, *b = nullptr, *dst = nullptr;
     float eps = 0.f;
     bool rms = false;
+    // EMBED: GET_ROWS terms summed in order into dst
+    std::vector<const tts_tensor *> terms;
     // LSTM: bit 1 = run recurrence step `ls`, bit 2 = write the chain's output `lfinal` from `lhist`
     int lkind = 0;
     LstmStepArgs ls{};
@@ -168,6 +170,9 @@ struct Planner {
             }
         }
         if (mask & TTS_FUSE_LSTM) try_lstm();
+        if (mask & TTS_FUSE_EMBED)  // roots first: a chain is claimed whole by its last ADD
+            for (int i = n - 1; i >= 0; --i)
+                if (act[i] == 0 && nodes[i]->op == TTS_OP_ADD) try_embed(i);
         for (int i = 0; i < n; ++i) {
             if (act[i] != 0) continue;
             const tts_tensor * t = nodes[i];
@@ -618,6 +623,60 @@ struct Planner {
         act[i] = add_item(std::move(it));
     }
 
+    // ADD chain over GET_ROWS terms (parler_build_inp_embd, model.cpp:387-410) -> one launch.
+    // Linear chains only (each ADD has at most one ADD operand), evaluated innermost pair first.
+    bool embed_terms(const tts_tensor * a, const tts_tensor * root, std::vector<const tts_tensor *> & terms, std::vector<int> & members) {
+        if (a->op != TTS_OP_ADD || a->type != TTS_TYPE_F32) return false;
+        for (int d = 0; d < 4; ++d)
+            if (a->ne[d] != root->ne[d]) return false;
+        const tts_tensor *l = a->src[0], *r = a->src[1];
+        if (!l || !r) return false;
+        const bool la = l->op == TTS_OP_ADD, ra = r->op == TTS_OP_ADD;
+        if (la && ra) return false;
+        auto leaf_ok = [&](const tts_tensor * g) {
+            if (g->op != TTS_OP_GET_ROWS || sole_consumer(g) != a || g->type != TTS_TYPE_F32) return false;
+            const tts_tensor *tab = g->src[0], *idx = g->src[1];
+            if (tab->type != TTS_TYPE_F32 && tab->type != TTS_TYPE_F16 && tab->type != TTS_TYPE_Q8_0 && tab->type != TTS_TYPE_Q4_K) return false;
+            if (idx->type != TTS_TYPE_I32 || idx->ne[1] * idx->ne[2] * idx->ne[3] != 1 || (idx->nb[0] % 4)) return false;
+            if (tab->ne[0] != root->ne[0] || g->ne[0] != root->ne[0] || tab->ne[2] * tab->ne[3] != 1) return false;
+            const int64_t rows = g->ne[1] * g->ne[2] * g->ne[3], M = root->ne[1] * root->ne[2] * root->ne[3];
+            return idx->ne[0] == rows && (rows == 1 || rows == M);
+        };
+        if (la || ra) {
+            const tts_tensor * inner = la ? l : r;
+            const tts_tensor * leaf = la ? r : l;
+            if (sole_consumer(inner) != a || !leaf_ok(leaf)) return false;
+            if (!embed_terms(inner, root, terms, members)) return false;
+            terms.push_back(leaf);
+            members.push_back(index[leaf]);
+            members.push_back(index[inner]);
+            return true;
+        }
+        if (!leaf_ok(l) || !leaf_ok(r)) return false;
+        terms.push_back(l);
+        terms.push_back(r);
+        members.push_back(index[l]);
+        members.push_back(index[r]);
+        return true;
+    }
+    void try_embed(int i) {
+        const tts_tensor * R = nodes[i];
+        if (!contiguous(R)) return;
+        std::vector<const tts_tensor *> terms;
+        std::vector<int> members;
+        if (!embed_terms(R, R, terms, members) || terms.size() < 2 || terms.size() > (size_t)EMBED_MAX_TERMS) return;
+        for (const tts_tensor * g : terms)
+            if (overlap(R, g->src[0]) || overlap(R, g->src[1])) return;
+        for (int m : members)
+            if (act[m] != 0) return;
+        Item it;
+        it.kind = Item::EMBED;
+        it.dst = R;
+        it.terms = terms;
+        for (int m : members) act[m] = -1;
+        act[i] = add_item(std::move(it));
+    }
+
     void try_attn(int i) {
         const tts_tensor * S = nodes[i];
         const tts_tensor * KQ = S->src[0];
@@ -831,6 +890,9 @@ static int run_item(tts_hip_backend * be, const Item & it) {
         }
         case Item::LN:
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
+            return 0;
+        case Item::EMBED:
+            launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::SNAKE:
             launch_snake(be, it.dst, it.x, it.w, it.b);

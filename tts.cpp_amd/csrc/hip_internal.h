@@ -231,7 +231,7 @@ struct tts_hip_backend {
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
-    int fusion = 0xFF;  // bitmask of TTS_FUSE_* patterns
+    int fusion = 0x1FF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -282,6 +282,8 @@ struct LstmStepArgs {
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                         int32_t * hist, int32_t * next);
+constexpr int EMBED_MAX_TERMS = 16;
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n);
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip);
 void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);

@@ -221,6 +221,37 @@ __global__ __launch_bounds__(256) void k_soft_max(TD dst, TD a, const char * mas
 }
 
 // ---- GET_ROWS (f32 / f16 / q4_K / q8_0 source, i32 index) ----
+// element k of a table row (dequantize_row_q4_K / q8_0 arithmetic for quantized tables)
+__device__ __forceinline__ float table_elem(const TD & s0, const char * src, int64_t k) {
+    if (s0.type == TTS_TYPE_F32) return ((const float *)src)[k];
+    if (s0.type == TTS_TYPE_F16) return __half2float(((const __half *)src)[k]);
+    if (s0.type == TTS_TYPE_Q8_0) {
+        const block_q8_0 * b = (const block_q8_0 *)src + k / QK8_0;
+        return __fmul_rn((float)b->qs[k % QK8_0], __half2float(__ushort_as_half(b->d)));
+    }
+    // Q4_K: dequantize_row_q4_K
+    const block_q4_K * b = (const block_q4_K *)src + k / QK_K;
+    const int e = (int)(k % QK_K);
+    const int j64 = e / 64, w = e % 64, hi = w >= 32, l = w % 32;
+    // repacked lane layout: byte l*16 + c*4 + k holds weights 64c + 8k + l (+32)
+    const int qbyte = (s0.pad & TTS_FLAG_REPACKED) ? ((l & 7) * 16 + j64 * 4 + (l >> 3)) : (32 * j64 + l);
+    const int sb = 2 * j64 + hi;
+    const uint8_t * q = b->scales;
+    int sc, mn;
+    if (sb < 4) {
+        sc = q[sb] & 63;
+        mn = q[sb + 4] & 63;
+    } else {
+        sc = (q[sb + 4] & 0xF) | ((q[sb - 4] >> 6) << 4);
+        mn = (q[sb + 4] >> 4) | ((q[sb] >> 6) << 4);
+    }
+    const float d = __half2float(__ushort_as_half(b->d));
+    const float dm = __half2float(__ushort_as_half(b->dmin));
+    const uint8_t qb = b->qs[qbyte];
+    const int qv = hi ? (qb >> 4) : (qb & 0xF);
+    return __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
+}
+
 __global__ void k_get_rows(TD dst, TD s0, TD s1) {
     const int64_t i = blockIdx.x;  // index into flattened s1
     const int64_t i10 = i % s1.ne[0], i11 = (i / s1.ne[0]) % s1.ne[1], i12 = i / (s1.ne[0] * s1.ne[1]);
@@ -228,37 +259,54 @@ __global__ void k_get_rows(TD dst, TD s0, TD s1) {
     const char * src = s0.data + i01 * s0.nb[1] + i11 * s0.nb[2] + i12 * s0.nb[3];
     float * out = (float *)(dst.data + i10 * dst.nb[1] + i11 * dst.nb[2] + i12 * dst.nb[3]);
     const int64_t nc = s0.ne[0];
-    for (int64_t k = threadIdx.x; k < nc; k += blockDim.x) {
-        float v;
-        if (s0.type == TTS_TYPE_F32) v = ((const float *)src)[k];
-        else if (s0.type == TTS_TYPE_F16) v = __half2float(((const __half *)src)[k]);
-        else if (s0.type == TTS_TYPE_Q8_0) {
-            const block_q8_0 * b = (const block_q8_0 *)src + k / QK8_0;
-            v = __fmul_rn((float)b->qs[k % QK8_0], __half2float(__ushort_as_half(b->d)));
-        } else {  // Q4_K: dequantize_row_q4_K
-            const block_q4_K * b = (const block_q4_K *)src + k / QK_K;
-            const int e = (int)(k % QK_K);
-            const int j64 = e / 64, w = e % 64, hi = w >= 32, l = w % 32;
-            // repacked lane layout: byte l*16 + c*4 + k holds weights 64c + 8k + l (+32)
-            const int qbyte = (s0.pad & TTS_FLAG_REPACKED) ? ((l & 7) * 16 + j64 * 4 + (l >> 3)) : (32 * j64 + l);
-            const int sb = 2 * j64 + hi;
-            const uint8_t * q = b->scales;
-            int sc, mn;
-            if (sb < 4) {
-                sc = q[sb] & 63;
-                mn = q[sb + 4] & 63;
-            } else {
-                sc = (q[sb + 4] & 0xF) | ((q[sb - 4] >> 6) << 4);
-                mn = (q[sb + 4] >> 4) | ((q[sb] >> 6) << 4);
-            }
-            const float d = __half2float(__ushort_as_half(b->d));
-            const float dm = __half2float(__ushort_as_half(b->dmin));
-            const uint8_t qb = b->qs[qbyte];
-            const int qv = hi ? (qb >> 4) : (qb & 0xF);
-            v = __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
-        }
-        out[k] = v;
+    for (int64_t k = threadIdx.x; k < nc; k += blockDim.x) out[k] = table_elem(s0, src, k);
+}
+
+// A chain of ADDs over GET_ROWS terms (parler_build_inp_embd, model.cpp:387-410: the 9 codebook
+// embeddings summed, then the positional row) in one launch.  Terms are added in the chain's
+// evaluation order, each add rounded to f32 as the unfused ADD nodes do; a term with one index
+// row broadcasts over the output columns (ggml's ADD broadcast of src1).
+struct EmbedTerm {
+    TD table;
+    const int32_t * idx;
+    int64_t idx_stride;  // elements
+    int64_t rows;        // 1 = broadcast
+};
+struct EmbedArgs {
+    EmbedTerm t[EMBED_MAX_TERMS];
+    int n;
+    float * out;
+    int64_t H, M;
+};
+
+__global__ void k_embed_sum(EmbedArgs a) {
+    const int64_t m = blockIdx.y;
+    const int64_t h = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= a.H) return;
+    float acc = 0.f;
+    for (int t = 0; t < a.n; ++t) {
+        const EmbedTerm & T = a.t[t];
+        const int64_t r = T.idx[(T.rows == 1 ? 0 : m) * T.idx_stride];
+        const float v = table_elem(T.table, T.table.data + r * T.table.nb[1], h);
+        acc = t == 0 ? v : __fadd_rn(acc, v);
     }
+    a.out[m * a.H + h] = acc;
+}
+
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n) {
+    EmbedArgs a{};
+    a.n = n;
+    a.out = (float *)out->data;
+    a.H = out->ne[0];
+    a.M = out->ne[1] * out->ne[2] * out->ne[3];
+    for (int i = 0; i < n; ++i) {
+        a.t[i].table = make_td(gr[i]->src[0]);
+        a.t[i].idx = (const int32_t *)gr[i]->src[1]->data;
+        a.t[i].idx_stride = (int64_t)(gr[i]->src[1]->nb[0] / 4);
+        a.t[i].rows = gr[i]->ne[1] * gr[i]->ne[2] * gr[i]->ne[3];
+    }
+    hipLaunchKernelGGL(k_embed_sum, dim3((unsigned)((a.H + 255) / 256), (unsigned)a.M), dim3(256), 0, be->stream, a);
+    TTS_HIP_CHECK(hipGetLastError());
 }
 
 // ---- CONCAT / REPEAT / SUM_ROWS ----

@@ -20,6 +20,9 @@ OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "
        "TRANSPOSE", "GET_ROWS", "SOFT_MAX", "ROPE", "CLAMP", "CONV_TRANSPOSE_1D", "IM2COL", "UPSCALE",
        "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
 OP = {n: i for i, n in enumerate(OPS)}
+# TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
+FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256}
+FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
