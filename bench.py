@@ -174,7 +174,7 @@ def gemv_roofline(be, runner, steps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--steps", type=int, default=861, help="AR steps per prompt (861 = 10.0 s of audio, SURVEY §8d)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="prompts per GPU (64-prompt batch / 8 GPUs)")
     ap.add_argument("--ctx", type=int, default=448, help="KV length when timing starts (prompt prefill)")
