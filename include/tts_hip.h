@@ -203,7 +203,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_FUSION = 0,      /* TTS_FUSE_* bitmask of enabled patterns (default: all bits, 0 = off) */
     TTS_HIP_OPT_PROFILE_GEMV = 1, /* 1 = time quantized GEMV launches with HIP events */
     TTS_HIP_OPT_GRAPHS = 2,       /* 1 = replay each graph_compute as a HIP graph (capture + exec update) */
-    TTS_HIP_OPT_CONV_F32ACC = 3   /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
+    TTS_HIP_OPT_CONV_F32ACC = 3,  /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
+    TTS_HIP_OPT_CONVT_LDS = 4     /* 1 (default) = conv_transpose_1d on the LDS-staged f64 MFMA kernel, 0 = per-wave kernel */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

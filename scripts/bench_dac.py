@@ -21,8 +21,9 @@ def main():
     cfg = ttship.dac_config(max_frames=max(frames))
     dac = ttship.Dac(be.iface(), cfg)
     rng = np.random.default_rng(0)
-    for f32acc in (0, 1):
+    for f32acc, convt in ((0, 1), (0, 0), (1, 1)):
         be.set_option(3, f32acc)
+        be.set_option(4, convt)
         for T in frames:
             codes = rng.integers(0, cfg.codebook_size, size=(T, cfg.n_codebooks))
             dac.decode(codes)
@@ -32,10 +33,11 @@ def main():
                 pcm = dac.decode(codes)
             dt = (time.perf_counter() - t0) / reps
             audio = T * dac.hop / 44100.0
-            print(json.dumps({"frames": T, "conv_f32acc": f32acc, "ms_per_decode": round(1000 * dt, 3),
+            print(json.dumps({"frames": T, "conv_f32acc": f32acc, "convt_lds": convt, "ms_per_decode": round(1000 * dt, 3),
                               "audio_sec_per_s": round(audio / dt, 2), "nodes": dac.last_graph_nodes(),
                               "pcm_std": round(float(np.std(pcm)), 4)}), flush=True)
     be.set_option(3, 0)
+    be.set_option(4, 1)
     dac.close()
     be.close()
 

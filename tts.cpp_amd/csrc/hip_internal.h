@@ -231,6 +231,7 @@ struct tts_hip_backend {
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
+    bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
     int fusion = 0x1FF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};

@@ -305,10 +305,129 @@ __global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w,
     }
 }
 
+// Polyphase conv_transpose_1d on the f64 matrix cores with LDS-staged operands.  A workgroup owns
+// 32 output channels x 64 polyphase positions q (all S residues: outputs o = q*S + rr - p), and
+// walks the input channels in chunks of 16: the x slice (positions q0 - J + 1 .. q0 + 63) and the
+// weight slice (every tap k, 32 channels; contiguous K*32 floats per input channel in ggml's
+// [K][OC][IC] layout) are staged in LDS with coalesced loads, then each wave (16 positions) runs
+// v_mfma_f64_16x16x4_f64 over (ic quad, tap j, residue, channel half): one x operand feeds 2*S
+// products.  f32 x f32 products are exact in f64; only the f64 summation order differs from the
+// oracle (tests: rel 1e-5 per layer, PCM 1e-4 end to end).
+template <int S>
+__global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p) {
+    constexpr int JM = 2, K = 2 * S;  // DAC / SNAC upsamplers: kernel = 2 * stride
+    constexpr int QT = 64, OCT = 32, ICC = 16, XW = QT + JM - 1;
+    constexpr int NX = ICC * XW, NW4 = ICC * K * OCT / 4;
+    constexpr int XR = (NX + 255) / 256, WR = (NW4 + 255) / 256;
+    __shared__ float xs[ICC][XW];
+    __shared__ float ws[ICC * K * OCT];  // [ic][k][oc]
+    const int lane = threadIdx.x & 63, qw = threadIdx.x >> 6;
+    const int c16 = lane & 15, kq = lane >> 4;
+    const int OC = (int)w.ne[1], IC = (int)w.ne[2];
+    const int64_t L = x.ne[0], OL = y.ne[0];
+    const int64_t q0 = (int64_t)blockIdx.x * QT;
+    const int oc0 = blockIdx.y * OCT;
+    f64x4_t acc[S][2];
+#pragma unroll
+    for (int r = 0; r < S; ++r) acc[r][0] = acc[r][1] = (f64x4_t){0.0, 0.0, 0.0, 0.0};
+    // next chunk's operands are fetched into registers while the current one computes
+    float xr[XR];
+    float4 wr[WR];
+    auto fetch = [&](int ic0) {
+#pragma unroll
+        for (int u = 0; u < XR; ++u) {
+            const int t = threadIdx.x + 256 * u;
+            const int ic = t / XW, qq = t - ic * XW;
+            const int64_t pos = q0 - (JM - 1) + qq;
+            const bool ok = t < NX && pos >= 0 && pos < L && ic0 + ic < IC;
+            xr[u] = ok ? *(const float *)(x.data + pos * x.nb[0] + (int64_t)(ic0 + ic) * x.nb[1]) : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < WR; ++u) {
+            const int t = threadIdx.x + 256 * u;       // float4 index within [ic][oc][k] (global order)
+            const int ic = t / (K * OCT / 4), rem = (t - ic * (K * OCT / 4)) * 4;
+            const int oc = rem / K;
+            const bool ok = t < NW4 && oc0 + oc < OC && ic0 + ic < IC;
+            wr[u] = ok ? *(const float4 *)(w.data + (int64_t)(oc0 + oc) * w.nb[1] + (int64_t)(ic0 + ic) * w.nb[2] + (rem - oc * K) * 4)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int u = 0; u < XR; ++u) {
+            const int t = threadIdx.x + 256 * u;
+            if (t < NX) xs[t / XW][t % XW] = xr[u];
+        }
+#pragma unroll
+        for (int u = 0; u < WR; ++u) {
+            const int t = threadIdx.x + 256 * u;
+            if (t >= NW4) continue;
+            const int ic = t / (K * OCT / 4), rem = (t - ic * (K * OCT / 4)) * 4;
+            const int oc = rem / K, k = rem - oc * K;  // 4 consecutive taps k..k+3 of channel oc
+            float * o = ws + (ic * K + k) * OCT + oc;
+            o[0] = wr[u].x, o[OCT] = wr[u].y, o[2 * OCT] = wr[u].z, o[3 * OCT] = wr[u].w;
+        }
+    };
+    fetch(0);
+    for (int ic0 = 0; ic0 < IC; ic0 += ICC) {
+        stage();
+        __syncthreads();
+        if (ic0 + ICC < IC) fetch(ic0 + ICC);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int icl = 4 * kk + kq;
+            // every operand of this ic quad read from LDS first, then the MFMAs back to back
+            float bx[JM], aw[JM][S][2];
+#pragma unroll
+            for (int j = 0; j < JM; ++j) {
+                bx[j] = xs[icl][qw * 16 + c16 + (JM - 1) - j];
+#pragma unroll
+                for (int r = 0; r < S; ++r)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) aw[j][r][h] = ws[(icl * K + r + S * j) * OCT + h * 16 + c16];
+            }
+#pragma unroll
+            for (int j = 0; j < JM; ++j) {
+                const double bv = (double)bx[j];
+#pragma unroll
+                for (int r = 0; r < S; ++r)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) acc[r][h] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)aw[j][r][h], bv, acc[r][h], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t q = q0 + qw * 16 + c16;
+#pragma unroll
+    for (int r = 0; r < S; ++r) {
+        const int64_t o = q * S + r - p;
+        if (o < 0 || o >= OL) continue;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int oc = oc0 + h * 16 + kq + 4 * e;
+                if (oc < OC) *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc[r][h][e];
+            }
+    }
+}
+
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
     const tts_tensor * w = node->src[0];
     const tts_tensor * x = node->src[1];
     const int s = node->op_params[0], p = node->op_params[1], d = node->op_params[2], g = node->op_params[4];
+    // the LDS kernel reads whole 4-tap float4 rows of the weight: contiguous taps (nb0 = 4), 16-B rows
+    const bool wvec = w->nb[0] == 4 && w->nb[1] % 16 == 0 && w->nb[2] % 16 == 0 && ((uintptr_t)w->data % 16) == 0;
+    if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16 && (s == 2 || s == 4 || s == 8) && w->ne[0] == 2 * s && wvec && be->convt_lds) {
+        const int64_t nq = (node->ne[0] + p) / s + 1;
+        const dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((w->ne[1] + 31) / 32));
+        const TD Y = make_td(node), X = make_td(x), W = make_td(w);
+        if (s == 2) hipLaunchKernelGGL((k_convt_f64_lds<2>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        else if (s == 4) hipLaunchKernelGGL((k_convt_f64_lds<4>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        else hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16) {
         const int64_t nq = (node->ne[0] + p) / s + 1;  // q with q*s + rr - p < OL for some rr
         const dim3 grid((unsigned)((nq + 15) / 16), (unsigned)((w->ne[1] + 15) / 16), (unsigned)s);
