@@ -359,6 +359,41 @@ tts_tensor * concat(context & c, tts_tensor * a, tts_tensor * b, int dim) {
     return t;
 }
 
+// ---- fork audio ops (Kokoro sine source / iSTFTNet head), PyTorch semantics (oracle/ggml_ref.c) ----
+tts_tensor * cumsum(context & c, tts_tensor * a) { return new_op(c, TTS_OP_CUMSUM, TTS_TYPE_F32, a->ne, a); }
+
+// ggml_upscale_ext (nearest, upstream) to the given shape
+tts_tensor * upscale_ext(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int64_t ne2, int64_t ne3) {
+    int64_t ne[4] = {ne0, ne1, ne2, ne3};
+    tts_tensor * t = new_op(c, TTS_OP_UPSCALE, TTS_TYPE_F32, ne, a);
+    t->op_params[0] = 0;
+    return t;
+}
+
+// fork ggml_upscale_linear(a, factor): linear interpolation (align_corners = false) along ne0
+tts_tensor * upscale_linear(context & c, tts_tensor * a, int factor) {
+    int64_t ne[4] = {a->ne[0] * factor, a->ne[1], a->ne[2], a->ne[3]};
+    tts_tensor * t = new_op(c, TTS_OP_UPSCALE, TTS_TYPE_F32, ne, a);
+    t->op_params[0] = 1;
+    return t;
+}
+
+// fork ggml_stft(a = [L, B], window [n_fft]) -> [n_fft, L/hop + 1, B, 2] (centre, reflect)
+tts_tensor * stft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, int hop, bool abs_and_angle) {
+    int64_t ne[4] = {n_fft, (a->ne[0] + 2 * (n_fft / 2) - n_fft) / hop + 1, a->ne[1], 2};
+    tts_tensor * t = new_op(c, TTS_OP_STFT, TTS_TYPE_F32, ne, a, window);
+    t->op_params[0] = n_fft, t->op_params[1] = hop, t->op_params[2] = abs_and_angle ? 1 : 0;
+    return t;
+}
+
+// fork ggml_istft(a = [n_fft/2+1, F, B, 2], window) -> [(F-1)*hop, B] (no envelope division)
+tts_tensor * istft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, int hop, bool abs_and_angle) {
+    int64_t ne[4] = {(a->ne[1] - 1) * hop, a->ne[2], 1, 1};
+    tts_tensor * t = new_op(c, TTS_OP_ISTFT, TTS_TYPE_F32, ne, a, window);
+    t->op_params[0] = n_fft, t->op_params[1] = hop, t->op_params[2] = abs_and_angle ? 1 : 0;
+    return t;
+}
+
 tts_tensor * sum_rows(context & c, tts_tensor * a) {
     int64_t ne[4] = {1, a->ne[1], a->ne[2], a->ne[3]};
     return new_op(c, TTS_OP_SUM_ROWS, TTS_TYPE_F32, ne, a);

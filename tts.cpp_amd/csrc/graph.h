@@ -91,6 +91,11 @@ tts_tensor * conv_transpose_1d(context & c, tts_tensor * a, tts_tensor * b, int 
 tts_tensor * get_rows(context & c, tts_tensor * a, tts_tensor * idx);
 tts_tensor * concat(context & c, tts_tensor * a, tts_tensor * b, int dim);
 tts_tensor * sum_rows(context & c, tts_tensor * a);
+tts_tensor * cumsum(context & c, tts_tensor * a);
+tts_tensor * upscale_ext(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int64_t ne2, int64_t ne3);
+tts_tensor * upscale_linear(context & c, tts_tensor * a, int factor);
+tts_tensor * stft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, int hop, bool abs_and_angle);
+tts_tensor * istft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, int hop, bool abs_and_angle);
 tts_tensor * repeat(context & c, tts_tensor * a, tts_tensor * shape);
 tts_tensor * rope_ext(context & c, tts_tensor * a, tts_tensor * pos, tts_tensor * freq_factors, int n_dims, int mode,
                       int n_ctx_orig, float freq_base, float freq_scale, float ext_factor, float attn_factor,
