@@ -97,6 +97,56 @@ int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, float * pcm);
 int64_t tts_dac_hop(const tts_dac * d);
 int32_t tts_dac_last_graph_nodes(const tts_dac * d);
 
+/* Kokoro-82M iSTFTNet generator (decoder features + F0 + style -> 24 kHz PCM): build_generator,
+ * build_sin_gen, build_noise_block and build_kokoro_generator_res_block,
+ * /root/reference/src/models/kokoro/model.cpp:136-244, fed as kokoro_runner::set_inputs feeds it
+ * (model.cpp:1256-1262): the uv/noise custom map (util.cpp:140-170) and the squared-window
+ * envelope (util.cpp:203-217) are computed on the host, as the reference does on its CPU.
+ * Defaults = Kokoro-82M (upsample_initial_channel 512, rates 10,6, kernels 20,12, resblock
+ * kernels 3,7,11 x dilations 1,3,5, gen_istft_n_fft 20, hop 5: 300 samples per input frame). */
+typedef struct tts_kokoro_gen_config {
+    int32_t in_channels;          /* 512 (halves per upsampler) */
+    int32_t style_dim;            /* 128 (style_half_size) */
+    int32_t n_ups;                /* 2 */
+    int32_t up_rates[4];          /* 10, 6 */
+    int32_t up_kernels[4];        /* 20, 12 */
+    int32_t n_kernels;            /* 3 residual blocks per level */
+    int32_t res_kernels[4];       /* 3, 7, 11 */
+    int32_t res_dilations[3];     /* 1, 3, 5 */
+    int32_t noise_res_kernels[4]; /* 7, 11 */
+    int32_t n_fft;                /* 20 (true_n_fft) */
+    int32_t hop;                  /* 5 (stft_hop) */
+    int32_t harmonic_num;         /* 8 */
+    float sample_rate;            /* 24000 */
+    float sin_amp;                /* 0.1 */
+    float noise_std;              /* 0.003 */
+    float voice_threshold;        /* 10 */
+    int32_t max_frames;           /* generator input frames per call (arena sizing) */
+    int32_t debug_no_reuse;       /* 1 = every node keeps its own arena memory (node dumps) */
+    uint64_t seed;                /* synthetic weight seed base */
+    uint64_t arena_bytes;         /* compute arena (0 = sized from max_frames) */
+} tts_kokoro_gen_config;
+
+typedef struct tts_kokoro_gen tts_kokoro_gen;
+void tts_kokoro_gen_default_config(tts_kokoro_gen_config * cfg);
+/* NULL when prod(up_rates) * hop != 300 (build_sin_gen's fixed x300 interpolation). */
+tts_kokoro_gen * tts_kokoro_gen_create(const tts_backend_iface * be, const tts_kokoro_gen_config * cfg);
+void tts_kokoro_gen_free(tts_kokoro_gen * k);
+/* x: [T][in_channels] decoder features (channel fastest); f0: [T] Hz; style: [style_dim];
+ * rand: [harmonic_num+1][300*T] uniform [0,1) noise draws (random_uniform_gen) or NULL for the
+ * runner's own seeded draws; pcm: [300*T] f32. */
+int tts_kokoro_gen_run(tts_kokoro_gen * k, const float * x, const float * f0, const float * style, const float * rand, int32_t T,
+                       float * pcm);
+int64_t tts_kokoro_gen_samples_per_frame(const tts_kokoro_gen * k);
+int32_t tts_kokoro_gen_last_graph_nodes(const tts_kokoro_gen * k);
+/* Weight introspection for tests: count, then name / ne[4] / f32 values of weight i (bytes). */
+int32_t tts_kokoro_gen_n_weights(const tts_kokoro_gen * k);
+uint64_t tts_kokoro_gen_weight(tts_kokoro_gen * k, int32_t i, char * name, uint64_t name_cap, int64_t * ne, float * dst, uint64_t cap);
+/* Debug: bytes of the named node of the last graph ("sine_source", "har_spec", "up.<i>",
+ * "noise_conv.<i>", "noise_res.<i>", "level.<i>", "conv_post", "after_res_gen"), copied to dst
+ * when cap suffices; 0 if absent. */
+uint64_t tts_kokoro_gen_get_node(tts_kokoro_gen * k, const char * name, void * dst, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -111,6 +111,31 @@ class DacConfig(ctypes.Structure):
     ]
 
 
+class KokoroGenConfig(ctypes.Structure):
+    _fields_ = [
+        ("in_channels", ctypes.c_int32),
+        ("style_dim", ctypes.c_int32),
+        ("n_ups", ctypes.c_int32),
+        ("up_rates", ctypes.c_int32 * 4),
+        ("up_kernels", ctypes.c_int32 * 4),
+        ("n_kernels", ctypes.c_int32),
+        ("res_kernels", ctypes.c_int32 * 4),
+        ("res_dilations", ctypes.c_int32 * 3),
+        ("noise_res_kernels", ctypes.c_int32 * 4),
+        ("n_fft", ctypes.c_int32),
+        ("hop", ctypes.c_int32),
+        ("harmonic_num", ctypes.c_int32),
+        ("sample_rate", ctypes.c_float),
+        ("sin_amp", ctypes.c_float),
+        ("noise_std", ctypes.c_float),
+        ("voice_threshold", ctypes.c_float),
+        ("max_frames", ctypes.c_int32),
+        ("debug_no_reuse", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+    ]
+
+
 _lib = None
 
 
@@ -176,6 +201,15 @@ def lib():
         "tts_dac_decode": (ctypes.c_int, [vp, vp, i32, vp]),
         "tts_dac_hop": (i64, [vp]),
         "tts_dac_last_graph_nodes": (i32, [vp]),
+        "tts_kokoro_gen_default_config": (None, [ctypes.POINTER(KokoroGenConfig)]),
+        "tts_kokoro_gen_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(KokoroGenConfig)]),
+        "tts_kokoro_gen_free": (None, [vp]),
+        "tts_kokoro_gen_run": (ctypes.c_int, [vp, vp, vp, vp, vp, i32, vp]),
+        "tts_kokoro_gen_samples_per_frame": (i64, [vp]),
+        "tts_kokoro_gen_last_graph_nodes": (i32, [vp]),
+        "tts_kokoro_gen_n_weights": (i32, [vp]),
+        "tts_kokoro_gen_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
+        "tts_kokoro_gen_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -381,4 +415,88 @@ class Dac:
     def close(self):
         if self.ptr:
             self.L.tts_dac_free(self.ptr)
+            self.ptr = None
+
+
+def kokoro_gen_config(**kw):
+    cfg = KokoroGenConfig()
+    lib().tts_kokoro_gen_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        if isinstance(v, (list, tuple)):
+            arr = getattr(cfg, k)
+            for i, r in enumerate(v):
+                arr[i] = r
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+class KokoroGenerator:
+    """Kokoro iSTFTNet generator runner (features + F0 + style -> PCM) over a backend vtable."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_kokoro_gen_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_kokoro_gen_create failed")
+
+    @property
+    def samples_per_frame(self):
+        return self.L.tts_kokoro_gen_samples_per_frame(self.ptr)
+
+    def run(self, x, f0, style, rand=None, out=None):
+        """x: (T, in_channels), f0: (T,), style: (style_dim,), rand: (harmonic_num+1, 300*T) or
+        None -> (300*T,) float32 PCM."""
+        import numpy as np
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        f0 = np.ascontiguousarray(f0, dtype=np.float32)
+        style = np.ascontiguousarray(style, dtype=np.float32)
+        T = x.shape[0]
+        assert x.shape[1] == self.cfg.in_channels and f0.shape == (T,) and style.shape == (self.cfg.style_dim,)
+        rp = None
+        if rand is not None:
+            rand = np.ascontiguousarray(rand, dtype=np.float32)
+            assert rand.shape == (self.cfg.harmonic_num + 1, T * self.samples_per_frame)
+            rp = rand.ctypes.data
+        pcm = out if out is not None else np.empty(T * self.samples_per_frame, dtype=np.float32)
+        st = self.L.tts_kokoro_gen_run(self.ptr, x.ctypes.data, f0.ctypes.data, style.ctypes.data, rp, T,
+                                       pcm.ctypes.data if pcm is not None else None)
+        if st != 0:
+            raise RuntimeError(f"tts_kokoro_gen_run failed {st}")
+        return pcm
+
+    def weights(self):
+        """{name: float32 array shaped like torch (reversed ggml ne, leading 1s dropped)}."""
+        import numpy as np
+        out = {}
+        for i in range(self.L.tts_kokoro_gen_n_weights(self.ptr)):
+            name = ctypes.create_string_buffer(128)
+            ne = (ctypes.c_int64 * 4)()
+            n = self.L.tts_kokoro_gen_weight(self.ptr, i, name, 128, ne, None, 0)
+            a = np.empty(n // 4, dtype=np.float32)
+            self.L.tts_kokoro_gen_weight(self.ptr, i, name, 128, ne, a.ctypes.data, n)
+            shape = [int(v) for v in reversed(list(ne))]
+            while len(shape) > 1 and shape[0] == 1:
+                shape.pop(0)
+            out[name.value.decode()] = a.reshape(shape)
+        return out
+
+    def node(self, name):
+        """float32 values of a named node of the last run (flat), or None."""
+        import numpy as np
+        n = self.L.tts_kokoro_gen_get_node(self.ptr, name.encode(), None, 0)
+        if not n:
+            return None
+        a = np.empty(n // 4, dtype=np.float32)
+        self.L.tts_kokoro_gen_get_node(self.ptr, name.encode(), a.ctypes.data, n)
+        return a
+
+    def last_graph_nodes(self):
+        return self.L.tts_kokoro_gen_last_graph_nodes(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_kokoro_gen_free(self.ptr)
             self.ptr = None
