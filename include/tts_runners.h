@@ -146,6 +146,8 @@ uint64_t tts_kokoro_gen_weight(tts_kokoro_gen * k, int32_t i, char * name, uint6
  * "noise_conv.<i>", "noise_res.<i>", "level.<i>", "conv_post", "after_res_gen"), copied to dst
  * when cap suffices; 0 if absent. */
 uint64_t tts_kokoro_gen_get_node(tts_kokoro_gen * k, const char * name, void * dst, uint64_t cap);
+/* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
+uint64_t tts_kokoro_gen_node(tts_kokoro_gen * k, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap);
 
 #ifdef __cplusplus
 }

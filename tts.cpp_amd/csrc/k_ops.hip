@@ -373,7 +373,10 @@ __global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int 
     }
 }
 
-// ---- generic f32 x f32 MUL_MAT (attention products): one wave per output, f64 accumulation ----
+// ---- generic MUL_MAT (attention products, small conv GEMMs): one wave per output, f64
+// accumulation.  With an F16 src0, ggml converts src1 to F16 (vec_dot_type) before the dot
+// (ggml_vec_dot_f16), so each src1 element is rounded to f16 here too; f16 x f16 products are
+// exact in f32. ----
 __global__ __launch_bounds__(256) void k_mul_mat_f32(TD dst, TD s0, TD s1, int64_t nout) {
     const int lane = threadIdx.x & 63;
     const int64_t o = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -391,7 +394,8 @@ __global__ __launch_bounds__(256) void k_mul_mat_f32(TD dst, TD s0, TD s1, int64
     const int64_t K = s0.ne[0];
     for (int64_t k = lane; k < K; k += 64) {
         const float x = s0.type == TTS_TYPE_F16 ? __half2float(*(const __half *)(a + k * s0.nb[0])) : *(const float *)(a + k * s0.nb[0]);
-        const float y = *(const float *)(b + k * s1.nb[0]);
+        float y = s1.type == TTS_TYPE_F16 ? __half2float(*(const __half *)(b + k * s1.nb[0])) : *(const float *)(b + k * s1.nb[0]);
+        if (s0.type == TTS_TYPE_F16) y = __half2float(__float2half_rn(y));
         acc += (double)__fmul_rn(x, y);
     }
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);

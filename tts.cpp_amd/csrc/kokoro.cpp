@@ -431,3 +431,16 @@ extern "C" uint64_t tts_kokoro_gen_get_node(tts_kokoro_gen * k, const char * nam
     }
     return 0;
 }
+
+// Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size).
+extern "C" uint64_t tts_kokoro_gen_node(tts_kokoro_gen * k, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap) {
+    if (!k || i < 0 || i >= (int32_t)k->gctx.nodes.size()) return 0;
+    const tts_tensor * t = k->gctx.nodes[i];
+    *op = t->op;
+    *type = t->type;
+    for (int d = 0; d < 4; ++d) ne[d] = t->ne[d];
+    if (!tg::is_contiguous(t) || !dst) return 0;
+    const uint64_t n = tg::nbytes(t);
+    if (n > cap || k->be.get(k->be.ctx, dst, t->data, n) != 0) return 0;
+    return n;
+}

@@ -209,6 +209,7 @@ def lib():
         "tts_kokoro_gen_last_graph_nodes": (i32, [vp]),
         "tts_kokoro_gen_n_weights": (i32, [vp]),
         "tts_kokoro_gen_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
+        "tts_kokoro_gen_node": (u64, [vp, i32, vp, vp, vp, vp, u64]),
         "tts_kokoro_gen_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
     }
     for name, (res, args) in sig.items():
@@ -482,6 +483,15 @@ class KokoroGenerator:
                 shape.pop(0)
             out[name.value.decode()] = a.reshape(shape)
         return out
+
+    def node_at(self, i, cap=1 << 26):
+        """(op, type, ne, float32 array or None) of node i of the last graph (debugging)."""
+        import numpy as np
+        op, ty = ctypes.c_int32(), ctypes.c_int32()
+        ne = (ctypes.c_int64 * 4)()
+        buf = np.empty(cap // 4, dtype=np.float32)
+        n = self.L.tts_kokoro_gen_node(self.ptr, i, ctypes.byref(op), ctypes.byref(ty), ne, buf.ctypes.data, cap)
+        return OPS[op.value], ty.value, tuple(ne), (buf[: n // 4].copy() if n else None)
 
     def node(self, name):
         """float32 values of a named node of the last run (flat), or None."""
