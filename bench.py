@@ -171,6 +171,18 @@ def gemv_roofline(be, runner, steps):
             "launches_sampled": launches}
 
 
+def kokoro_inputs(cfg, T, rank):
+    """Synthetic generator inputs: decoder features, a voiced F0 contour with unvoiced gaps, a
+    style vector and the uniform noise draws (seeded per rank)."""
+    rng = np.random.default_rng(1000 + rank)
+    x = (rng.standard_normal((T, cfg.in_channels)) * 0.5).astype(np.float32)
+    f0 = (120.0 + 40.0 * np.sin(np.arange(T) / 9.0)).astype(np.float32)
+    f0[(np.arange(T) // 25) % 4 == 3] = 0.0
+    style = rng.standard_normal(cfg.style_dim).astype(np.float32)
+    rand = rng.random((cfg.harmonic_num + 1, 300 * T), dtype=np.float32)
+    return x, f0, style, rand
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,6 +196,8 @@ def main():
     ap.add_argument("--no-fusion", action="store_true")
     ap.add_argument("--no-dac", action="store_true", help="AR decode only")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
+    ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
+    ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
@@ -199,6 +213,13 @@ def main():
         dcfg = ttship.dac_config(max_frames=args.steps)
         dac = ttship.Dac(be.iface(), dcfg)
         dac.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+    kok = None
+    if args.kokoro_calls > 0:
+        kcfg = ttship.kokoro_gen_config(max_frames=args.kokoro_frames)
+        kok = ttship.KokoroGenerator(be.iface(), kcfg)
+        kin = kokoro_inputs(kcfg, args.kokoro_frames, rank)
+        kpcm = np.empty(300 * args.kokoro_frames, dtype=np.float32)
+        kok.run(*kin, out=kpcm)  # warm (code objects, arena)
     # text-prompt pass to reach the measured KV length
     runner.prefill(prompt_tokens(args.batch, args.ctx, cfg.prompt_vocab, offset=rank * args.batch))
     runner.generate(args.warmup)
@@ -215,6 +236,22 @@ def main():
     barrier_sync(dist, be)
     t2 = time.perf_counter()
     host = runner.host_stats(reset=True)
+    kres = None
+    if kok is not None:
+        # BASELINE configs[1]: the Kokoro-82M iSTFTNet vocoder path, timed on its own
+        barrier_sync(dist, be)
+        t3 = time.perf_counter()
+        for _ in range(args.kokoro_calls):
+            kok.run(*kin, out=kpcm)
+        barrier_sync(dist, be)
+        dt_k = max_over_ranks(dist, local, time.perf_counter() - t3)
+        k_audio = world * args.kokoro_calls * args.kokoro_frames * 300 / kcfg.sample_rate
+        kres = {"workload": "Kokoro-82M iSTFTNet generator (BASELINE configs[1] vocoder path), synthetic weights",
+                "audio_sec_per_s": round(k_audio / dt_k, 3), "ms_per_call": round(1000.0 * dt_k / args.kokoro_calls, 3),
+                "frames_per_call": args.kokoro_frames, "audio_sec_per_call": args.kokoro_frames * 300 / kcfg.sample_rate,
+                "calls_per_gpu": args.kokoro_calls, "graph_nodes": kok.last_graph_nodes(),
+                "dtype": "f32 activations, f16 conv operands (ggml im2col), f64 conv accumulate",
+                "pcm_std": round(float(np.std(kpcm)), 4)}
     dt = max_over_ranks(dist, local, t2 - t0)
     dt_ar = max_over_ranks(dist, local, t1 - t0)
     dt_dac = max_over_ranks(dist, local, t2 - t1)
@@ -253,12 +290,15 @@ def main():
             "dac_audio_sec_per_s": round(audio_s / dt_dac, 3) if dac is not None else None,
             "codec_tokens_per_s": round(total_prompts * args.steps * HEADS / dt_ar, 1),
             "host_us_per_step": host,
+            "kokoro": kres,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
     if dac is not None:
         dac.close()
+    if kok is not None:
+        kok.close()
     runner.close()
     be.close()
     if dist is not None:

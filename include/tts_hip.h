@@ -210,7 +210,8 @@ enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
     TTS_FUSE_LSTM = 64, /* Kokoro build_lstm_run's unrolled recurrence -> one kernel per step, no O(T^2) concat */
     TTS_FUSE_SNAKE = 128, /* snake_1d's five elementwise nodes -> one pass */
-    TTS_FUSE_EMBED = 256  /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
+    TTS_FUSE_EMBED = 256, /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
+    TTS_FUSE_CONV = 512   /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

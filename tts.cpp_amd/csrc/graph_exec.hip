@@ -98,7 +98,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -126,6 +126,8 @@ struct Item {
     const tts_tensor * lfinal = nullptr;
     const float * lhist = nullptr;
     int64_t lHd = 0, lT = 0;
+    // CONV: implicit-GEMM conv_1d with its bias / residual ADDs
+    Conv1dArgs conv{};
 };
 
 struct Planner {
@@ -181,6 +183,7 @@ struct Planner {
                 case TTS_OP_RMS_NORM: if (mask & TTS_FUSE_LN) try_ln(i); break;
                 case TTS_OP_SOFT_MAX: if (mask & TTS_FUSE_ATTN) try_attn(i); break;
                 case TTS_OP_ADD: if (mask & TTS_FUSE_SNAKE) try_snake(i); break;
+                case TTS_OP_IM2COL: if (mask & TTS_FUSE_CONV) try_conv(i); break;
                 case TTS_OP_MUL_MAT:
                     if (!((mask & TTS_FUSE_HEADS) && try_heads(i)) && (mask & (TTS_FUSE_GROUP | TTS_FUSE_KV | TTS_FUSE_EPI))) try_gemv(i);
                     break;
@@ -623,6 +626,97 @@ struct Planner {
         act[i] = add_item(std::move(it));
     }
 
+    // ggml_conv_1d's IM2COL(F16) -> RESHAPE -> MUL_MAT -> RESHAPE, then optionally ADD of a
+    // per-channel bias and ADD of a same-shape residual (build_residual_unit,
+    // general_neural_audio_codec.cpp:133-149; build_kokoro_generator_res_block,
+    // kokoro/model.cpp:136-165) -> one implicit-GEMM kernel that never writes the im2col matrix.
+    static const tts_tensor * through_view(const tts_tensor * t) { return t && t->op == TTS_OP_RESHAPE ? t->src[0] : t; }
+    void try_conv(int i) {
+        const tts_tensor * col = nodes[i];
+        const tts_tensor *kern = col->src[0], *x = col->src[1];
+        if (col->type != TTS_TYPE_F16 || col->op_params[6] != 0 || col->ne[2] * col->ne[3] != 1) return;  // 1-D, one batch
+        if (!x || x->type != TTS_TYPE_F32 || x->ne[2] * x->ne[3] != 1) return;
+        if (!kern || (kern->type != TTS_TYPE_F32 && kern->type != TTS_TYPE_F16) || kern->ne[3] != 1) return;
+        const tts_tensor * cv = sole_consumer(col);
+        if (!cv || cv->op != TTS_OP_RESHAPE || !contiguous(col)) return;
+        const tts_tensor * mm = sole_consumer(cv);
+        if (!mm || mm->op != TTS_OP_MUL_MAT || mm->src[0] != cv || mm->type != TTS_TYPE_F32) return;
+        const tts_tensor * wv = mm->src[1];
+        if (!wv || through_view(wv) != kern) return;
+        const int K = (int)kern->ne[0];
+        const int64_t IC = kern->ne[1], OC = kern->ne[2], L = x->ne[0], OL = col->ne[1];
+        if (x->ne[1] != IC || mm->ne[0] != OL || mm->ne[1] != OC || !contiguous(mm)) return;
+        const int s = col->op_params[0], p = col->op_params[2], d = col->op_params[4];
+        if (!conv1d_fused_ok(IC, K, s, d, nullptr)) return;
+        if (kern->nb[0] != tts_type_size(kern->type)) return;
+        // the conv output may continue into a RESHAPE (ggml_conv_1d's reshape_3d), bias ADD, residual ADD
+        const tts_tensor * out = mm;
+        std::vector<int> absorbed = {i, (int)index[mm]};
+        const tts_tensor * r3 = sole_consumer(mm);
+        const tts_tensor * cur = mm;
+        if (r3 && r3->op == TTS_OP_RESHAPE && r3->ne[0] == OL && r3->ne[1] == OC) cur = r3;
+        Conv1dArgs a;
+        const tts_tensor * bias = nullptr;
+        const tts_tensor * res = nullptr;
+        const tts_tensor * nb = sole_consumer(cur);
+        if (nb && nb->op == TTS_OP_ADD && nb->src[0] == cur && nb->type == TTS_TYPE_F32 && contiguous(nb) && nb->ne[0] == OL &&
+            nb->ne[1] == OC && nb->ne[2] * nb->ne[3] == 1 && chan_vec(nb->src[1], OC) && nb->src[1]->ne[1] == OC) {
+            bias = nb->src[1];
+            out = nb;
+            absorbed.push_back(index[nb]);
+            const tts_tensor * nr = sole_consumer(nb);
+            if (nr && nr->op == TTS_OP_ADD && nr->type == TTS_TYPE_F32 && contiguous(nr) && nr->ne[0] == OL && nr->ne[1] == OC &&
+                nr->ne[2] * nr->ne[3] == 1) {
+                const tts_tensor * other = nr->src[0] == nb ? nr->src[1] : nr->src[0];
+                if (other && other != nb && other->type == TTS_TYPE_F32 && contiguous(other) && other->ne[0] == OL && other->ne[1] == OC &&
+                    other->ne[2] * other->ne[3] == 1 && (!overlap(nr, other) || nr->data == other->data)) {
+                    res = other;
+                    out = nr;
+                    absorbed.push_back(index[nr]);
+                }
+            }
+        }
+        // The kernel reads x windows across tiles while writing its output, so the output must
+        // not alias x.  ggml-alloc often hands a conv's output the memory of its input (freed
+        // after IM2COL); then the kernel writes the im2col buffer instead -- dead in the fused
+        // form, allocated while x was alive -- and a D2D copy moves the result into place.
+        if (overlap(out, kern) || (bias && overlap(out, bias))) return;
+        float * stage = nullptr;
+        if (overlap(out, x)) {
+            const size_t need = (size_t)OL * (size_t)OC * 4;
+            if (tbytes(col) < need || overlap(col, x) || overlap(col, out) || (res && overlap(col, res)) || overlap(col, kern) ||
+                (bias && overlap(col, bias)))
+                return;
+            stage = (float *)col->data;
+        }
+        a.x = make_td(x);
+        a.w = kern->data;
+        a.w16 = kern->type == TTS_TYPE_F16;
+        const size_t es = tts_type_size(kern->type);
+        a.wk = (int64_t)(kern->nb[0] / es), a.wic = (int64_t)(kern->nb[1] / es), a.woc = (int64_t)(kern->nb[2] / es);
+        a.y = (float *)out->data;
+        a.ycs = (int64_t)(out->nb[1] / 4);
+        if (stage) {
+            a.copy_dst = a.y;
+            a.y = stage;
+            a.ycs = OL;
+        }
+        if (bias) a.bias = (const float *)bias->data, a.bcs = bias->ne[1] == 1 ? 0 : (int64_t)(bias->nb[1] / 4);
+        if (res) a.res = (const float *)res->data, a.rcs = (int64_t)(res->nb[1] / 4);
+        a.L = L, a.IC = IC, a.OL = OL, a.OC = OC;
+        a.K = K, a.s = s, a.p = p, a.d = d;
+        const size_t xb = (size_t)((x->ne[0] - 1) * x->nb[0] + (x->ne[1] - 1) * x->nb[1]) + 4;
+        const size_t wb = tbytes(kern);
+        if (xb >= 0x80000000u || wb >= 0x80000000u) return;  // 32-bit buffer offsets
+        a.x_bytes = (uint32_t)xb, a.w_bytes = (uint32_t)wb;
+        Item it;
+        it.kind = Item::CONV;
+        it.conv = a;
+        it.dst = out;
+        for (size_t k = 0; k + 1 < absorbed.size(); ++k) act[absorbed[k]] = -1;
+        act[absorbed.back()] = add_item(std::move(it));
+    }
+
     // ADD chain over GET_ROWS terms (parler_build_inp_embd, model.cpp:387-410) -> one launch.
     // Linear chains only (each ADD has at most one ADD operand), evaluated innermost pair first.
     bool embed_terms(const tts_tensor * a, const tts_tensor * root, std::vector<const tts_tensor *> & terms, std::vector<int> & members) {
@@ -896,6 +990,9 @@ static int run_item(tts_hip_backend * be, const Item & it) {
             return 0;
         case Item::SNAKE:
             launch_snake(be, it.dst, it.x, it.w, it.b);
+            return 0;
+        case Item::CONV:
+            launch_conv1d_fused(be, it.conv);
             return 0;
         case Item::LSTM:
             if (it.lkind & 1) {

@@ -232,7 +232,7 @@ struct tts_hip_backend {
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
     bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
-    int fusion = 0x1FF;  // bitmask of TTS_FUSE_* patterns (all on)
+    int fusion = 0x3FF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -290,6 +290,43 @@ void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, cons
 bool audio_op_supported(const tts_tensor * n);
 int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);
 void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node);
+// conv_1d chain (IM2COL -> MUL_MAT [-> ADD bias] [-> ADD residual]) as one implicit-GEMM kernel
+constexpr int CONV1D_MAX_R = 128;
+struct Conv1dArgs {
+    TD x;                           // input [L, IC] f32 (any strides)
+    const void * w = nullptr;       // kernel [K, IC, OC], element strides wk / wic / woc
+    int w16 = 0;                    // kernel stored as F16 (else F32)
+    int64_t wk = 0, wic = 0, woc = 0;
+    float * y = nullptr;            // output [OL, OC]: y[ol + oc * ycs]
+    int64_t ycs = 0;
+    const float * bias = nullptr;   // bias[oc * bcs] or null
+    int64_t bcs = 0;
+    const float * res = nullptr;    // residual [OL, OC] (res[ol + oc * rcs]) or null
+    int64_t rcs = 0;
+    int64_t L = 0, IC = 0, OL = 0, OC = 0;
+    int K = 1, s = 1, p = 0, d = 1;
+    int icc = 0, xw = 0, rs = 0;    // set by the launcher
+    float * copy_dst = nullptr;     // non-null: y is a staging buffer, copied here (contiguous) after the kernel
+    uint32_t x_bytes = 0, w_bytes = 0;  // buffer-descriptor ranges (reads past them return 0)
+};
+constexpr int CONV1D_XN = 16, CONV1D_WN = 16;  // staged elements per thread (x window, kernel slice)
+inline int conv1d_icc(int64_t IC, int K, int xw) {  // input channels per LDS chunk
+    // the reduction (icc * K) is padded to whole batches of 32 and held to 64 (so the kernel
+    // slice is 64 x 64 floats, CONV1D_WN per thread); the x window (icc * xw floats) to
+    // CONV1D_XN per thread.  Pick the icc that wastes the least, preferring larger chunks.
+    int best = 0;
+    double best_eff = -1.0;
+    const int top = (int)(IC < 64 ? IC : 64);
+    for (int c = 1; c <= top; ++c) {
+        const int r = c * K, rp = (r + 31) & ~31;
+        if (rp > 64 || c * xw > 256 * CONV1D_XN) break;
+        const double eff = (double)r / rp + 1e-4 * c;
+        if (eff > best_eff) best_eff = eff, best = c;
+    }
+    return best;  // 0: the shape does not fit (K > 64 or a window too wide)
+}
+bool conv1d_fused_ok(int64_t IC, int K, int s, int d, size_t * lds);
+void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a);
 bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);
 // carve an ActQuant layout for weight type `wtype` out of `base` (no launch)

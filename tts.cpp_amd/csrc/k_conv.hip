@@ -231,6 +231,202 @@ bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node) {
 }
 
 // ------------------------------------------------------------------------------------------
+// conv_1d as an implicit GEMM (ggml_conv_1d = IM2COL(F16) -> MUL_MAT, general_neural_audio_codec
+// / Kokoro convs) with the conv's bias and residual ADDs as the epilogue; the im2col matrix is
+// never written.  Values are the ones the node chain sees: x and the kernel are rounded to f16
+// (im2col's dst type, MUL_MAT's vec_dot_type), products f16 x f16 are exact in f64 and summed
+// in f64 on the matrix cores (as k_gemm_f16_f64acc), the sum rounds to f32, then + bias (f32),
+// then + residual (f32) -- the same roundings as the three nodes.
+// Workgroup tile: 64 output channels (MFMA rows) x 64 output positions (MFMA columns, so 16
+// lanes store 16 consecutive positions); 4 waves of 32 x 32.  The reduction r = ic*K + k walks
+// input channels in chunks of `icc`: per chunk the x window (positions ol0*s - p ..
+// + 63*s + (K-1)*d, icc channels) and the kernel slice (64 channels x icc*K taps) are staged in
+// LDS as f16-rounded floats; a per-r offset table maps r to its x-window slot (r >= R points at
+// a zero slot) so the MFMA loop does no division.
+template <bool W16, bool BIAS, bool RES>
+__global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
+    extern __shared__ float sm[];
+    __shared__ int xoff[CONV1D_MAX_R];  // r -> x-window slot (ic*xw + k*d), zero slot past R
+    __shared__ int wofs[CONV1D_MAX_R];  // r -> kernel element offset (k*wk + ic*wic), -1 past R
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int c16 = lane & 15, kq = lane >> 4;
+    const int64_t ol0 = (int64_t)blockIdx.x * 64;
+    const int oc0 = blockIdx.y * 64;
+    const int K = a.K, s = a.s, icc = a.icc, xw = a.xw, rs = a.rs;
+    const int R = icc * K, Rp = (R + 31) & ~31;  // reduction padded to whole MFMA batches
+    float * xs = sm;                 // [icc][xw] + 1 zero slot
+    float * ws = sm + icc * xw + 1;  // [64 oc][rs]
+    const int zslot = icc * xw;
+    for (int r = threadIdx.x; r < Rp; r += 256) {
+        const int ic = r / K, k = r - ic * K;
+        xoff[r] = r < R ? ic * xw + k * a.d : zslot;
+        wofs[r] = r < R ? (int)(k * a.wk + ic * a.wic) : -1;
+    }
+    if (threadIdx.x == 0) xs[zslot] = 0.f;
+    __syncthreads();
+    const int wr0 = (wave >> 1) * 32, wc0 = (wave & 1) * 32;  // wave's oc / ol offsets in the tile
+    f64x4_t acc[2][2] = {};
+    const int64_t base = ol0 * s - a.p;
+    // Staging: thread t owns x-window elements e = t + 256u (u < CONV1D_XN) and kernel-slice
+    // elements t + 256u (u < CONV1D_WN); their byte offsets relative to the chunk's first channel
+    // are fixed for the whole kernel and computed once.  Loads go through buffer descriptors (an
+    // out-of-range offset -- padding, the channel tail -- reads 0) into registers one chunk
+    // ahead, so the next chunk's loads are in flight while the current one computes.
+    const int EX = icc * xw, EW = 64 * Rp;
+    constexpr int esz = W16 ? 2 : 4;
+    const uint32_t OOB = 0x80000000u;
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(a.x.data, 0, a.x_bytes, 0x00020000);
+    const auto wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(a.w), 0, a.w_bytes, 0x00020000);
+    uint32_t xrel[CONV1D_XN], wrel[CONV1D_WN];
+    int xic[CONV1D_XN], wic[CONV1D_WN];  // channel within the chunk (for the tail chunk), -1 = unused
+#pragma unroll
+    for (int u = 0; u < CONV1D_XN; ++u) {
+        const int e = (int)threadIdx.x + 256 * u;
+        const int ic = e / xw, q = e - ic * xw;
+        const int64_t pos = base + q;
+        const bool ok = e < EX && pos >= 0 && pos < a.L;
+        xrel[u] = ok ? (uint32_t)(pos * a.x.nb[0] + (int64_t)ic * a.x.nb[1]) : OOB;
+        xic[u] = e < EX ? ic : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < CONV1D_WN; ++u) {
+        const int e = (int)threadIdx.x + 256 * u;
+        const int oc = e / Rp, r = e - oc * Rp;
+        const int wo = e < EW ? wofs[r] : -1;
+        const bool ok = wo >= 0 && oc0 + oc < a.OC;
+        wrel[u] = ok ? (uint32_t)(((int64_t)(oc0 + oc) * a.woc + wo) * esz) : OOB;
+        wic[u] = e < EW ? (r < R ? r / K : icc) : -1;
+    }
+    float xv[CONV1D_XN], wv[CONV1D_WN];
+    auto fetch = [&](int ic0) {
+        const int nic = min(icc, (int)(a.IC - ic0));
+        const uint32_t xc = (uint32_t)((int64_t)ic0 * a.x.nb[1]);
+        const uint32_t wc = (uint32_t)((int64_t)ic0 * a.wic * esz);
+#pragma unroll
+        for (int u = 0; u < CONV1D_XN; ++u) {
+            const uint32_t off = (xrel[u] == OOB || xic[u] >= nic) ? OOB : xrel[u] + xc;
+            xv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(xr, off, 0, 0));
+        }
+#pragma unroll
+        for (int u = 0; u < CONV1D_WN; ++u) {
+            const uint32_t off = (wrel[u] == OOB || wic[u] >= nic) ? OOB : wrel[u] + wc;
+            if (W16) wv[u] = __half2float(__builtin_bit_cast(__half, __builtin_amdgcn_raw_buffer_load_b16(wr, off, 0, 0)));
+            else wv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
+        }
+    };
+    fetch(0);
+    for (int ic0 = 0; ic0 < a.IC; ic0 += icc) {
+        // f16 rounding (im2col's dst type / MUL_MAT's vec_dot_type) on the way into LDS
+#pragma unroll
+        for (int u = 0; u < CONV1D_XN; ++u)
+            if (xic[u] >= 0) xs[(int)threadIdx.x + 256 * u] = __half2float(__float2half_rn(xv[u]));
+#pragma unroll
+        for (int u = 0; u < CONV1D_WN; ++u)
+            if (wic[u] >= 0) {
+                const int e = (int)threadIdx.x + 256 * u;
+                const int oc = e / Rp;
+                ws[oc * rs + (e - oc * Rp)] = W16 ? wv[u] : __half2float(__float2half_rn(wv[u]));
+            }
+        __syncthreads();
+        if (ic0 + icc < a.IC) fetch(ic0 + icc);
+        // batches of 8 reduction quads: every operand of the batch is read from LDS first (the
+        // offset-table reads, then the dependent operand reads, all independent of each other),
+        // then 32 MFMAs issue back to back
+        for (int r0 = 0; r0 < Rp; r0 += 32) {
+            int xo[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) xo[u] = xoff[r0 + 4 * u + kq];
+            float af[8][2], bf[8][2];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int r = r0 + 4 * u + kq;
+                const bool z = xo[u] == zslot;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    af[u][t] = ws[(wr0 + 16 * t + c16) * rs + r];
+                    bf[u][t] = xs[z ? zslot : xo[u] + (wc0 + 16 * t + c16) * s];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int tj = 0; tj < 2; ++tj)
+                        acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)af[u][ti], (double)bf[u][tj], acc[ti][tj], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: bias and residual operands fetched for all 32 outputs first (clamped, branchless)
+    float bv[2][4], rv[2][2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int oc = min(oc0 + wr0 + 16 * ti + kq + 4 * e, (int)a.OC - 1);
+            bv[ti][e] = BIAS ? a.bias[(int64_t)oc * a.bcs] : 0.f;
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const int64_t ol = min(ol0 + wc0 + 16 * tj + c16, a.OL - 1);
+                rv[tj][ti][e] = RES ? a.res[ol + (int64_t)oc * a.rcs] : 0.f;
+            }
+        }
+#pragma unroll
+    for (int tj = 0; tj < 2; ++tj) {
+        const int64_t ol = ol0 + wc0 + 16 * tj + c16;
+        if (ol >= a.OL) continue;
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int oc = oc0 + wr0 + 16 * ti + kq + 4 * e;
+                if (oc >= a.OC) continue;
+                float v = (float)acc[ti][tj][e];
+                if (BIAS) v = v + bv[ti][e];
+                if (RES) v = rv[tj][ti][e] + v;
+                a.y[ol + (int64_t)oc * a.ycs] = v;
+            }
+    }
+}
+
+bool conv1d_fused_ok(int64_t IC, int K, int s, int d, size_t * lds) {
+    if (K < 1 || K > 64 || s < 1 || d < 1 || IC < 1) return false;
+    const int xw = 63 * s + (K - 1) * d + 1;
+    const int icc = conv1d_icc(IC, K, xw);
+    if (icc < 1) return false;
+    const int rs = ((icc * K + 31) & ~31) + 1;
+    const size_t bytes = ((size_t)icc * xw + 1 + 64 * (size_t)rs) * 4;
+    if (lds) *lds = bytes;
+    return bytes <= 64 * 1024;
+}
+
+void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a) {
+    a.xw = 63 * a.s + (a.K - 1) * a.d + 1;
+    a.icc = conv1d_icc(a.IC, a.K, a.xw);
+    a.rs = ((a.icc * a.K + 31) & ~31) + 1;
+    size_t lds = 0;
+    if (!conv1d_fused_ok(a.IC, a.K, a.s, a.d, &lds)) {
+        fprintf(stderr, "tts_hip: conv1d_fused shape unsupported\n");
+        abort();
+    }
+    const dim3 grid((unsigned)((a.OL + 63) / 64), (unsigned)((a.OC + 63) / 64));
+    const int sel = (a.w16 ? 4 : 0) | (a.bias ? 2 : 0) | (a.res ? 1 : 0);
+    switch (sel) {
+        case 0: hipLaunchKernelGGL((k_conv1d_f64<false, false, false>), grid, dim3(256), lds, be->stream, a); break;
+        case 1: hipLaunchKernelGGL((k_conv1d_f64<false, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 2: hipLaunchKernelGGL((k_conv1d_f64<false, true, false>), grid, dim3(256), lds, be->stream, a); break;
+        case 3: hipLaunchKernelGGL((k_conv1d_f64<false, true, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 4: hipLaunchKernelGGL((k_conv1d_f64<true, false, false>), grid, dim3(256), lds, be->stream, a); break;
+        case 5: hipLaunchKernelGGL((k_conv1d_f64<true, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 6: hipLaunchKernelGGL((k_conv1d_f64<true, true, false>), grid, dim3(256), lds, be->stream, a); break;
+        default: hipLaunchKernelGGL((k_conv1d_f64<true, true, true>), grid, dim3(256), lds, be->stream, a); break;
+    }
+    TTS_HIP_CHECK(hipGetLastError());
+    if (a.copy_dst)  // the output aliased the input: the kernel wrote a staging buffer
+        TTS_HIP_CHECK(hipMemcpyAsync(a.copy_dst, a.y, (size_t)a.OL * (size_t)a.OC * 4, hipMemcpyDeviceToDevice, be->stream));
+}
+
+// ------------------------------------------------------------------------------------------
 // y[oc][o] = sum over (k, i) with o = i*s - p + k*d, ic in oc's group: x[i][ic] * w[k][oc%OCg][ic]
 // One output position per lane; for d = 1 only taps k = r + j*s (r = (o+p) mod s) land on o.
 __global__ __launch_bounds__(256) void k_conv_transpose_1d(TD y, TD x, TD w, int s, int p, int d, int g) {
@@ -315,7 +511,7 @@ __global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w,
 // oracle (tests: rel 1e-5 per layer, PCM 1e-4 end to end).
 template <int S>
 __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p) {
-    constexpr int JM = 2, K = 2 * S;  // DAC / SNAC upsamplers: kernel = 2 * stride
+    constexpr int JM = 2, K = 2 * S;  // DAC / SNAC / Kokoro upsamplers: kernel = 2 * stride
     constexpr int QT = 64, OCT = 32, ICC = 16, XW = QT + JM - 1;
     constexpr int NX = ICC * XW, NW4 = ICC * K * OCT / 4;
     constexpr int XR = (NX + 255) / 256, WR = (NW4 + 255) / 256;
@@ -418,13 +614,16 @@ void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
     const int s = node->op_params[0], p = node->op_params[1], d = node->op_params[2], g = node->op_params[4];
     // the LDS kernel reads whole 4-tap float4 rows of the weight: contiguous taps (nb0 = 4), 16-B rows
     const bool wvec = w->nb[0] == 4 && w->nb[1] % 16 == 0 && w->nb[2] % 16 == 0 && ((uintptr_t)w->data % 16) == 0;
-    if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16 && (s == 2 || s == 4 || s == 8) && w->ne[0] == 2 * s && wvec && be->convt_lds) {
+    if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16 && (s == 2 || s == 4 || s == 6 || s == 8 || s == 10) && w->ne[0] == 2 * s && wvec &&
+        be->convt_lds) {
         const int64_t nq = (node->ne[0] + p) / s + 1;
         const dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((w->ne[1] + 31) / 32));
         const TD Y = make_td(node), X = make_td(x), W = make_td(w);
         if (s == 2) hipLaunchKernelGGL((k_convt_f64_lds<2>), grid, dim3(256), 0, be->stream, Y, X, W, p);
         else if (s == 4) hipLaunchKernelGGL((k_convt_f64_lds<4>), grid, dim3(256), 0, be->stream, Y, X, W, p);
-        else hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        else if (s == 6) hipLaunchKernelGGL((k_convt_f64_lds<6>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        else if (s == 8) hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        else hipLaunchKernelGGL((k_convt_f64_lds<10>), grid, dim3(256), 0, be->stream, Y, X, W, p);
         TTS_HIP_CHECK(hipGetLastError());
         return;
     }

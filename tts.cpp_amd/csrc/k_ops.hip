@@ -402,6 +402,31 @@ __global__ __launch_bounds__(256) void k_mul_mat_f32(TD dst, TD s0, TD s1, int64
     if (lane == 0) *(float *)(dst.data + i01 * dst.nb[0] + i11 * dst.nb[1] + i12 * dst.nb[2] + i13 * dst.nb[3]) = (float)acc;
 }
 
+// Short rows (K <= 32: Kokoro's harmonic merge Linear(9, 1), the 1-tap noise conv over 22 STFT
+// channels): one thread per output, the dot summed sequentially in f64 as the oracle does.
+__global__ __launch_bounds__(256) void k_mul_mat_smallk(TD dst, TD s0, TD s1, int64_t nout) {
+    const int64_t o = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (o >= nout) return;
+    const int64_t i01 = o % dst.ne[0];
+    int64_t rest = o / dst.ne[0];
+    const int64_t i11 = rest % dst.ne[1];
+    rest /= dst.ne[1];
+    const int64_t i12 = rest % dst.ne[2];
+    const int64_t i13 = rest / dst.ne[2];
+    const int64_t i02 = i12 / (s1.ne[2] / s0.ne[2]), i03 = i13 / (s1.ne[3] / s0.ne[3]);
+    const char * a = s0.data + i01 * s0.nb[1] + i02 * s0.nb[2] + i03 * s0.nb[3];
+    const char * b = s1.data + i11 * s1.nb[1] + i12 * s1.nb[2] + i13 * s1.nb[3];
+    double acc = 0.0;
+    const int64_t K = s0.ne[0];
+    for (int64_t k = 0; k < K; ++k) {
+        const float x = s0.type == TTS_TYPE_F16 ? __half2float(*(const __half *)(a + k * s0.nb[0])) : *(const float *)(a + k * s0.nb[0]);
+        float y = s1.type == TTS_TYPE_F16 ? __half2float(*(const __half *)(b + k * s1.nb[0])) : *(const float *)(b + k * s1.nb[0]);
+        if (s0.type == TTS_TYPE_F16) y = __half2float(__float2half_rn(y));
+        acc += (double)__fmul_rn(x, y);
+    }
+    *(float *)(dst.data + i01 * dst.nb[0] + i11 * dst.nb[1] + i12 * dst.nb[2] + i13 * dst.nb[3]) = (float)acc;
+}
+
 // ------------------------------------------------------------------------------------------
 
 static inline float op_f(const tts_tensor * t, int i) {
@@ -544,6 +569,10 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
             // float path (quantized weights go through the GEMV kernels)
             if (launch_gemm_f16(be, node)) return 0;
             const int64_t nout = nel(node);
+            if (s0->ne[0] <= 32) {
+                hipLaunchKernelGGL(k_mul_mat_smallk, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
+                break;
+            }
             hipLaunchKernelGGL(k_mul_mat_f32, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
         } break;
         case TTS_OP_IM2COL: launch_im2col(be, node); return 0;
