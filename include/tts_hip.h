@@ -178,6 +178,9 @@ int tts_hip_tensor_get(tts_hip_backend_t backend, void * dst_host, const void * 
 int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size); /* stream-ordered */
 /* ggml_backend_i::set_tensor_async: `src_host` is staged at once (reusable on return), the copy runs
  * in stream order after the work already queued. */
+/* Fusion coverage of a node list without a device: counts[0..14] = fused items per kind (GEMV, ATTN,
+ * LN, LSTM, SNAKE, EMBED, CONV, ADAIN), counts[15] = nodes still launched one by one. */
+int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int mask, int32_t * counts);
 int tts_hip_tensor_set_async(tts_hip_backend_t backend, void * dst_dev, const void * src_host, size_t size);
 int tts_hip_memset(tts_hip_backend_t backend, void * dst_dev, int value, size_t size);
 int tts_hip_synchronize(tts_hip_backend_t backend);
@@ -211,7 +214,8 @@ enum tts_fuse_bits {
     TTS_FUSE_LSTM = 64, /* Kokoro build_lstm_run's unrolled recurrence -> one kernel per step, no O(T^2) concat */
     TTS_FUSE_SNAKE = 128, /* snake_1d's five elementwise nodes -> one pass */
     TTS_FUSE_EMBED = 256, /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
-    TTS_FUSE_CONV = 512   /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
+    TTS_FUSE_CONV = 512,  /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
+    TTS_FUSE_ADAIN = 1024 /* Kokoro AdaIN1d (norm, transposes, affine) + snake_1d -> one pass per channel row */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

@@ -148,6 +148,8 @@ uint64_t tts_kokoro_gen_weight(tts_kokoro_gen * k, int32_t i, char * name, uint6
 uint64_t tts_kokoro_gen_get_node(tts_kokoro_gen * k, const char * name, void * dst, uint64_t cap);
 /* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
 uint64_t tts_kokoro_gen_node(tts_kokoro_gen * k, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap);
+/* The last graph's node list (valid until the next run), e.g. for tts_hip_plan_stats. */
+tts_tensor * const * tts_kokoro_gen_graph(const tts_kokoro_gen * k, int32_t * n_nodes);
 
 #ifdef __cplusplus
 }

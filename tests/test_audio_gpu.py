@@ -167,3 +167,47 @@ def test_row_broadcast_binary_bit_exact(hip, shape):
         return [g.node(op, F32, [T, C], [xl, bl]) for op in ("ADD", "SUB", "MUL", "DIV")]
     for gpu, ref in run_both(hip, build):
         assert np.array_equal(gpu, ref)
+
+
+def _adain_graph(g, x, gamma, beta, alpha, snake):
+    """One AdaIN1d half of build_kokoro_generator_res_block (kokoro/model.cpp:142-146), then
+    snake_1d: NORM over time, CONT(TRANSPOSE), x + x*gamma + beta, CONT(TRANSPOSE) back."""
+    C, T = x.shape
+    xl = g.leaf(x)
+    n = g.node("NORM", F32, [T, C], [xl], fparams={0: 1e-5})
+    c1 = g.node("CONT", F32, [C, T], [g.transpose(n)])
+    gl, bl = g.leaf(gamma.reshape(C, 1).T.copy()), g.leaf(beta.reshape(C, 1).T.copy())  # ne [C, 1]
+    m = g.node("MUL", F32, [C, T], [c1, gl])
+    a1 = g.node("ADD", F32, [C, T], [c1, m])
+    a2 = g.node("ADD", F32, [C, T], [a1, bl])
+    c2 = g.node("CONT", F32, [T, C], [g.transpose(a2)])
+    if not snake:
+        return c2
+    al = g.leaf(alpha.reshape(C, 1))
+    one = g.leaf(np.ones((1, 1), np.float32))
+    onev = g.view(one, [1, C, 1, 1], [4, 0, 0, 0])
+    recip = g.node("DIV", F32, [1, C], [onev, al])
+    m1 = g.node("MUL", F32, [T, C], [c2, al])
+    s = g.node("SIN", F32, [T, C], [m1])
+    q = g.node("SQR", F32, [T, C], [s])
+    m2 = g.node("MUL", F32, [T, C], [q, recip])
+    return g.node("ADD", F32, [T, C], [c2, m2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C,T", [(128, 4801), (256, 800), (7, 33), (16, 20000), (3, 65536)])
+@pytest.mark.parametrize("snake", [True, False])
+@pytest.mark.parametrize("fused", [True, False])
+def test_adain_snake_bit_exact(hip, C, T, snake, fused):
+    rng = np.random.default_rng(C * 7 + T)
+    x = (rng.standard_normal((C, T)) * 3 + 1).astype(np.float32)
+    gamma = (rng.standard_normal(C) * 0.2).astype(np.float32)
+    beta = (rng.standard_normal(C) * 0.2).astype(np.float32)
+    alpha = rng.uniform(0.5, 1.5, C).astype(np.float32)
+    if not fused:
+        hip.set_option(0, ttship.FUSE_ALL & ~ttship.FUSE["ADAIN"])
+    try:
+        (gpu, ref), = run_both(hip, lambda g: [_adain_graph(g, x, gamma, beta, alpha, snake)])
+    finally:
+        hip.set_option(0, ttship.FUSE_ALL)
+    assert np.array_equal(gpu, ref)

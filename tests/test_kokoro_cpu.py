@@ -77,3 +77,20 @@ def test_kokoro_generator_rejects_bad_config():
             k.run(x, f0, style)
     finally:
         k.close()
+
+
+def test_kokoro_generator_fusion_coverage():
+    """The HIP planner's view of the generator graph (no device needed): every AdaIN1d (+ snake)
+    and conv_1d chain collapses into one item (TTS_FUSE_ADAIN / TTS_FUSE_CONV)."""
+    cfg = ttship.kokoro_gen_config(in_channels=64, style_dim=16, max_frames=16)
+    k = ttship.KokoroGenerator(py_oracle.iface(4), cfg)
+    try:
+        k.run(*inputs(cfg, 4, 0))
+        st = k.plan_stats()
+        off = k.plan_stats(0)
+    finally:
+        k.close()
+    n_adain = cfg.n_ups * (1 + cfg.n_kernels) * 3 * 2  # (noise + res blocks) x 3 units x 2 halves
+    assert st["adain"] == n_adain
+    assert st["conv"] >= n_adain  # every res-block conv (+ noise / post convs when they fit)
+    assert st["unfused"] < off["unfused"] // 10

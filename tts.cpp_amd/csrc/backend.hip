@@ -24,6 +24,7 @@ static void build_gelu_table(uint16_t * t) {
 static const size_t kScratchBytes = 64u << 20;
 static const size_t kShadowBytes = 4u << 20;  // private copy of an attention output (decode: 32 KB per 8 prompts)
 static const size_t kLstmFloats = 4u << 20;
+static const size_t kVecScratchFloats = 1u << 18;  // per-channel vectors staged by fused items (AdaIN)
 static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tensor_async   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
 
 extern "C" {
@@ -50,6 +51,7 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     TTS_HIP_CHECK(hipMalloc((void **)&be->shadow, kShadowBytes));
     be->shadow_size = kShadowBytes;
     TTS_HIP_CHECK(hipMalloc((void **)&be->lstm_buf, kLstmFloats * sizeof(float)));
+    TTS_HIP_CHECK(hipMalloc((void **)&be->vec_scratch, kVecScratchFloats * sizeof(float)));
     be->lstm_floats = kLstmFloats;
     TTS_HIP_CHECK(hipHostMalloc((void **)&be->pin, kPinBytes, hipHostMallocDefault));
     be->pin_size = kPinBytes;
@@ -77,6 +79,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->lstm_buf);
+    hipFree(be->vec_scratch);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
     if (be->gexec) hipGraphExecDestroy(be->gexec);

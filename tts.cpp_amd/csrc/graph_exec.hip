@@ -14,6 +14,7 @@
 // A pattern fuses only when every intermediate tensor has a single consumer inside the group
 // and the fused output does not overlap an input it reads (the graph arrives already
 // allocated, so aliasing is checked on the real addresses).
+#include <algorithm>
 #include <cstring>
 #include <unordered_map>
 #include <vector>
@@ -98,7 +99,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -128,6 +129,8 @@ struct Item {
     int64_t lHd = 0, lT = 0;
     // CONV: implicit-GEMM conv_1d with its bias / residual ADDs
     Conv1dArgs conv{};
+    // ADAIN: per-channel norm + affine (+ snake)
+    AdainArgs adain{};
 };
 
 struct Planner {
@@ -140,6 +143,7 @@ struct Planner {
     std::vector<Item> items;
     int mask = 0xFF;
     float * lstm_buf = nullptr;  // backend scratch for fused LSTM chains (hidden history + cell)
+    size_t vec_cap = 0;          // floats of the backend's vector scratch (fused AdaIN staging)
     size_t lstm_cap = 0, lstm_used = 0;
 
     const tts_tensor * sole_consumer(const tts_tensor * t) {
@@ -180,6 +184,9 @@ struct Planner {
             const tts_tensor * t = nodes[i];
             switch (t->op) {
                 case TTS_OP_NORM:
+                    if ((mask & TTS_FUSE_ADAIN) && try_adain(i)) break;
+                    if (mask & TTS_FUSE_LN) try_ln(i);
+                    break;
                 case TTS_OP_RMS_NORM: if (mask & TTS_FUSE_LN) try_ln(i); break;
                 case TTS_OP_SOFT_MAX: if (mask & TTS_FUSE_ATTN) try_attn(i); break;
                 case TTS_OP_ADD: if (mask & TTS_FUSE_SNAKE) try_snake(i); break;
@@ -626,6 +633,158 @@ struct Planner {
         act[i] = add_item(std::move(it));
     }
 
+    // AdaIN1d as build_kokoro_generator_res_block emits it (kokoro/model.cpp:136-165):
+    //   n = NORM(x [T, C]); c1 = CONT(TRANSPOSE(n)); y = ADD(ADD(c1, MUL(c1, gamma)), beta);
+    //   c2 = CONT(TRANSPOSE(y)) [T, C]; optionally snake_1d(alpha, c2) (util.cpp:98-101)
+    // -> one pass per channel row (k_adain_snake).  The item runs where the last absorbed node
+    // ran, so the nodes executed in between (the recip DIV, ...) must not write over its inputs.
+    static bool vec_c(const tts_tensor * t, int64_t C) {  // [C] or [C, 1] f32, or [1, C] (stride 4)
+        if (!t || t->type != TTS_TYPE_F32 || t->ne[2] * t->ne[3] != 1 || t->nb[0] != 4) return false;
+        return (t->ne[0] == C && t->ne[1] == 1) || (t->ne[0] == 1 && t->ne[1] == C && t->nb[1] == 4);
+    }
+    static bool same_shape(const tts_tensor * a, int64_t n0, int64_t n1) {
+        return a->type == TTS_TYPE_F32 && a->ne[0] == n0 && a->ne[1] == n1 && a->ne[2] * a->ne[3] == 1;
+    }
+    // TTS_PLAN_DEBUG=1: report why a fusion pattern was not taken
+    static bool plan_debug() {
+        static const bool dbg = getenv("TTS_PLAN_DEBUG") != nullptr;
+        return dbg;
+    }
+    static void plan_reject(const char * what, int code) {
+        if (plan_debug()) fprintf(stderr, "plan: %s not fused (check %d)\n", what, code);
+    }
+    static bool adain_fail(int code) {
+        plan_reject("adain", code);
+        return false;
+    }
+    bool try_adain(int i) {
+        const tts_tensor * N = nodes[i];
+        const tts_tensor * X = N->src[0];
+        if (!X || X->type != TTS_TYPE_F32 || N->type != TTS_TYPE_F32 || X->nb[0] != 4 || N->ne[2] * N->ne[3] != 1) return adain_fail(1);
+        const int64_t T = N->ne[0], C = N->ne[1];
+        if (!adain_supported(T)) return adain_fail(2);
+        const tts_tensor * T1 = sole_consumer(N);
+        if (!T1 || T1->op != TTS_OP_TRANSPOSE) return adain_fail(3);
+        const tts_tensor * C1 = sole_consumer(T1);
+        if (!C1 || C1->op != TTS_OP_CONT || !same_shape(C1, C, T) || uses[C1] != 2) return adain_fail(4);
+        const auto & cc = consumers[C1];
+        if (cc.size() != 2) return adain_fail(5);
+        const tts_tensor *M = nodes[cc[0]], *A1 = nodes[cc[1]];
+        if (M->op != TTS_OP_MUL || M->src[0] != C1 || !vec_c(M->src[1], C) || sole_consumer(M) != A1) return adain_fail(6);
+        if (A1->op != TTS_OP_ADD || A1->src[0] != C1 || A1->src[1] != M || !same_shape(A1, C, T)) return adain_fail(7);
+        const tts_tensor * A2 = sole_consumer(A1);
+        if (!A2 || A2->op != TTS_OP_ADD || A2->src[0] != A1 || !vec_c(A2->src[1], C) || !same_shape(A2, C, T)) return adain_fail(8);
+        const tts_tensor * T2 = sole_consumer(A2);
+        if (!T2 || T2->op != TTS_OP_TRANSPOSE) return adain_fail(9);
+        const tts_tensor * C2 = sole_consumer(T2);
+        if (!C2 || C2->op != TTS_OP_CONT || !same_shape(C2, T, C) || !contiguous(C2)) return adain_fail(10);
+        const tts_tensor *gamma = M->src[1], *beta = A2->src[1];
+        std::vector<int> absorbed = {i, index[C1], index[M], index[A1], index[A2], index[C2]};
+        // gamma / beta = ADD(MUL_MAT(W [S, C] f32, style [S]), bias [C]) used only here: evaluated
+        // in the kernel, so neither their nodes nor their (aliasable) outputs are needed
+        auto affine_src = [&](const tts_tensor * v, const tts_tensor * user, const tts_tensor *& W, const tts_tensor *& B,
+                              const tts_tensor *& st) {
+            if (!v || v->op != TTS_OP_ADD || sole_consumer(v) != user) return false;
+            const tts_tensor * mm = v->src[0];
+            if (!mm || mm->op != TTS_OP_MUL_MAT || sole_consumer(mm) != v || !vec_c(v->src[1], C) || v->src[1]->ne[0] != C) return false;
+            W = mm->src[0], st = mm->src[1], B = v->src[1];
+            const int64_t S = W->ne[0];
+            return W->type == TTS_TYPE_F32 && contiguous(W) && W->ne[1] == C && W->ne[2] * W->ne[3] == 1 && S % 4 == 0 &&
+                   ((uintptr_t)W->data % 16) == 0 && st->type == TTS_TYPE_F32 && contiguous(st) && st->ne[0] == S &&
+                   st->ne[1] * st->ne[2] * st->ne[3] == 1 && ((uintptr_t)st->data % 16) == 0;
+        };
+        const tts_tensor *gW = nullptr, *gB = nullptr, *gS = nullptr, *bW = nullptr, *bB = nullptr, *bS = nullptr;
+        const bool inline_gb = affine_src(gamma, M, gW, gB, gS) && affine_src(beta, A2, bW, bB, bS) && gS == bS;
+        if (inline_gb) {
+            for (const tts_tensor * t : {gamma, (const tts_tensor *)gamma->src[0], beta, (const tts_tensor *)beta->src[0]}) absorbed.push_back(index[t]);
+            gamma = beta = nullptr;  // no longer read
+        }
+        const tts_tensor * out = C2;
+        const tts_tensor *alpha = nullptr, *recip = nullptr, *one = nullptr;
+        // snake_1d on C2: M1 = MUL(C2, alpha), S = SIN(M1), Q = SQR(S), M2 = MUL(Q, R), A = ADD(C2, M2)
+        if ((mask & TTS_FUSE_SNAKE) && uses[C2] == 2) {
+            const auto & sc = consumers[C2];
+            const tts_tensor *M1 = nodes[sc[0]], *SA = nodes[sc[1]];
+            const tts_tensor *S = sole_consumer(M1), *Q = S ? sole_consumer(S) : nullptr, *M2 = Q ? sole_consumer(Q) : nullptr;
+            // reciprocal() (util.cpp:86-94) = DIV(broadcast view of a scalar, alpha): when it feeds
+            // only this snake, the kernel evaluates it itself (same division) and the node is skipped
+            const tts_tensor * R = M2 ? M2->src[1] : nullptr;
+            const tts_tensor * O = R ? R->src[0] : nullptr;
+            const bool r_inline = R && R->op == TTS_OP_DIV && O && R->src[1] == M1->src[1] && sole_consumer(R) == M2 &&
+                                  O->type == TTS_TYPE_F32 && O->nb[1] == 0 && O->ne[0] == 1 && O->ne[2] * O->ne[3] == 1 &&
+                                  same_shape(R, 1, C);
+            if (M1->op == TTS_OP_MUL && M1->src[0] == C2 && S && S->op == TTS_OP_SIN && Q && Q->op == TTS_OP_SQR && M2 &&
+                M2->op == TTS_OP_MUL && M2->src[0] == Q && sole_consumer(M2) == SA && SA->op == TTS_OP_ADD && SA->src[0] == C2 &&
+                SA->src[1] == M2 && vec_c(M1->src[1], C) && vec_c(M2->src[1], C) && same_shape(SA, T, C) && contiguous(SA) &&
+                same_shape(M1, T, C) && same_shape(S, T, C) && same_shape(Q, T, C) && same_shape(M2, T, C)) {
+                alpha = M1->src[1];
+                recip = M2->src[1];
+                out = SA;
+                for (const tts_tensor * t : {M1, S, Q, M2, SA}) absorbed.push_back(index[t]);
+                if (r_inline) {
+                    absorbed.push_back(index[R]);
+                    recip = nullptr;
+                    one = O;
+                }
+            }
+        }
+        // rows are read whole before they are written, so out may be X itself (same rows), but
+        // no other aliasing with the inputs
+        const bool in_place = out->data == X->data && out->nb[1] == X->nb[1];
+        if (overlap(out, X) && !in_place) return adain_fail(11);
+        // ggml-alloc may place the output over gamma / beta (freed after their absorbed consumers):
+        // then the launch first copies the vectors to the backend's scratch
+        bool stage = false;
+        for (const tts_tensor * t : {gamma, beta, alpha, recip, one})
+            if (t && overlap(out, t)) stage = true;
+        if (inline_gb)
+            for (const tts_tensor * t : {gW, gB, bW, bB, gS})
+                if (overlap(out, t)) return adain_fail(14);
+        if (stage && 4 * C + 1 > (int64_t)vec_cap) return adain_fail(12);
+        const int last = *std::max_element(absorbed.begin(), absorbed.end());
+        std::vector<bool> is_abs(n, false);
+        for (int k : absorbed) is_abs[k] = true;
+        for (int k = i + 1; k < last; ++k) {  // nodes that still run between the NORM and the item
+            if (is_abs[k] || is_view(nodes[k]->op) || act[k] < 0) continue;
+            const tts_tensor * w = nodes[k];
+            for (const tts_tensor * t : {X, gamma, beta, alpha, recip, one, gW, gB, bW, bB, gS})
+                if (t && t != w && overlap(w, t)) {
+                    if (plan_debug()) fprintf(stderr, "plan: adain node %d (%s) between %d..%d overlaps an input\n", k, tts_op_name(w->op), i, last);
+                    return adain_fail(13);
+                }
+        }
+        AdainArgs a;
+        a.x = (const float *)X->data;
+        a.xcs = (int64_t)(X->nb[1] / 4);
+        a.y = (float *)out->data;
+        a.ycs = (int64_t)(out->nb[1] / 4);
+        auto vstride = [](const tts_tensor * t) { return t->ne[0] == 1 ? (int64_t)(t->nb[1] / 4) : (int64_t)1; };
+        if (inline_gb) {
+            a.gw = (const float *)gW->data, a.gb = (const float *)gB->data;
+            a.bw = (const float *)bW->data, a.bb = (const float *)bB->data;
+            a.style = (const float *)gS->data, a.S = gW->ne[0];
+        } else {
+            a.gamma = (const float *)gamma->data, a.gcs = vstride(gamma);
+            a.beta = (const float *)beta->data, a.bcs = vstride(beta);
+        }
+        if (alpha) {
+            a.alpha = (const float *)alpha->data, a.acs = vstride(alpha);
+            if (recip) a.recip = (const float *)recip->data, a.rcs = vstride(recip);
+            else a.one = (const float *)one->data;
+        }
+        a.T = T, a.C = C;
+        a.stage = stage;
+        memcpy(&a.eps, &N->op_params[0], 4);
+        Item it;
+        it.kind = Item::ADAIN;
+        it.adain = a;
+        it.dst = out;
+        for (int k : absorbed)
+            if (k != last) act[k] = -1;
+        act[last] = add_item(std::move(it));
+        return true;
+    }
+
     // ggml_conv_1d's IM2COL(F16) -> RESHAPE -> MUL_MAT -> RESHAPE, then optionally ADD of a
     // per-channel bias and ADD of a same-shape residual (build_residual_unit,
     // general_neural_audio_codec.cpp:133-149; build_kokoro_generator_res_block,
@@ -634,21 +793,21 @@ struct Planner {
     void try_conv(int i) {
         const tts_tensor * col = nodes[i];
         const tts_tensor *kern = col->src[0], *x = col->src[1];
-        if (col->type != TTS_TYPE_F16 || col->op_params[6] != 0 || col->ne[2] * col->ne[3] != 1) return;  // 1-D, one batch
-        if (!x || x->type != TTS_TYPE_F32 || x->ne[2] * x->ne[3] != 1) return;
-        if (!kern || (kern->type != TTS_TYPE_F32 && kern->type != TTS_TYPE_F16) || kern->ne[3] != 1) return;
+        if (col->type != TTS_TYPE_F16 || col->op_params[6] != 0 || col->ne[2] * col->ne[3] != 1) return plan_reject("conv", 1);  // 1-D, one batch
+        if (!x || x->type != TTS_TYPE_F32 || x->ne[2] * x->ne[3] != 1) return plan_reject("conv", 2);
+        if (!kern || (kern->type != TTS_TYPE_F32 && kern->type != TTS_TYPE_F16) || kern->ne[3] != 1) return plan_reject("conv", 3);
         const tts_tensor * cv = sole_consumer(col);
-        if (!cv || cv->op != TTS_OP_RESHAPE || !contiguous(col)) return;
+        if (!cv || cv->op != TTS_OP_RESHAPE || !contiguous(col)) return plan_reject("conv", 4);
         const tts_tensor * mm = sole_consumer(cv);
-        if (!mm || mm->op != TTS_OP_MUL_MAT || mm->src[0] != cv || mm->type != TTS_TYPE_F32) return;
+        if (!mm || mm->op != TTS_OP_MUL_MAT || mm->src[0] != cv || mm->type != TTS_TYPE_F32) return plan_reject("conv", 5);
         const tts_tensor * wv = mm->src[1];
-        if (!wv || through_view(wv) != kern) return;
+        if (!wv || through_view(wv) != kern) return plan_reject("conv", 6);
         const int K = (int)kern->ne[0];
         const int64_t IC = kern->ne[1], OC = kern->ne[2], L = x->ne[0], OL = col->ne[1];
-        if (x->ne[1] != IC || mm->ne[0] != OL || mm->ne[1] != OC || !contiguous(mm)) return;
+        if (x->ne[1] != IC || mm->ne[0] != OL || mm->ne[1] != OC || !contiguous(mm)) return plan_reject("conv", 7);
         const int s = col->op_params[0], p = col->op_params[2], d = col->op_params[4];
-        if (!conv1d_fused_ok(IC, K, s, d, nullptr)) return;
-        if (kern->nb[0] != tts_type_size(kern->type)) return;
+        if (!conv1d_fused_ok(IC, K, s, d, nullptr)) return plan_reject("conv", 8);
+        if (kern->nb[0] != tts_type_size(kern->type)) return plan_reject("conv", 9);
         // the conv output may continue into a RESHAPE (ggml_conv_1d's reshape_3d), bias ADD, residual ADD
         const tts_tensor * out = mm;
         std::vector<int> absorbed = {i, (int)index[mm]};
@@ -680,13 +839,13 @@ struct Planner {
         // not alias x.  ggml-alloc often hands a conv's output the memory of its input (freed
         // after IM2COL); then the kernel writes the im2col buffer instead -- dead in the fused
         // form, allocated while x was alive -- and a D2D copy moves the result into place.
-        if (overlap(out, kern) || (bias && overlap(out, bias))) return;
+        if (overlap(out, kern) || (bias && overlap(out, bias))) return plan_reject("conv", 10);
         float * stage = nullptr;
         if (overlap(out, x)) {
             const size_t need = (size_t)OL * (size_t)OC * 4;
             if (tbytes(col) < need || overlap(col, x) || overlap(col, out) || (res && overlap(col, res)) || overlap(col, kern) ||
                 (bias && overlap(col, bias)))
-                return;
+                return plan_reject("conv", 11);
             stage = (float *)col->data;
         }
         a.x = make_td(x);
@@ -707,7 +866,7 @@ struct Planner {
         a.K = K, a.s = s, a.p = p, a.d = d;
         const size_t xb = (size_t)((x->ne[0] - 1) * x->nb[0] + (x->ne[1] - 1) * x->nb[1]) + 4;
         const size_t wb = tbytes(kern);
-        if (xb >= 0x80000000u || wb >= 0x80000000u) return;  // 32-bit buffer offsets
+        if (xb >= 0x80000000u || wb >= 0x80000000u) return plan_reject("conv", 12);  // 32-bit buffer offsets
         a.x_bytes = (uint32_t)xb, a.w_bytes = (uint32_t)wb;
         Item it;
         it.kind = Item::CONV;
@@ -994,6 +1153,9 @@ static int run_item(tts_hip_backend * be, const Item & it) {
         case Item::CONV:
             launch_conv1d_fused(be, it.conv);
             return 0;
+        case Item::ADAIN:
+            launch_adain_snake(be, it.adain);
+            return 0;
         case Item::LSTM:
             if (it.lkind & 1) {
                 launch_lstm_step(be, it.ls);
@@ -1101,6 +1263,21 @@ extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
     return 0;
 }
 
+// Fusion coverage of a graph without a device (tests, tooling): counts[k] = items of kind k
+// (Item::Kind order), counts[15] = nodes still launched one by one.  Returns the item count.
+extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int mask, int32_t * counts) {
+    Planner pl;
+    pl.mask = mask;
+    pl.vec_cap = 1u << 18;
+    if (mask) pl.build(nodes, n_nodes);
+    else pl.act.assign(n_nodes, 0);
+    for (int k = 0; k < 16; ++k) counts[k] = 0;
+    for (const Item & it : pl.items) counts[(int)it.kind]++;
+    for (int i = 0; i < n_nodes; ++i)
+        if (pl.act[i] == 0 && !is_view(nodes[i]->op)) counts[15]++;
+    return (int)pl.items.size();
+}
+
 static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     be->graph_epoch++;
     be->aq.src = nullptr;
@@ -1109,6 +1286,7 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     pl.mask = be->fusion;
     pl.lstm_buf = be->lstm_buf;
     pl.lstm_cap = be->lstm_floats;
+    pl.vec_cap = be->vec_scratch ? (1u << 18) : 0;
     if (be->fusion) pl.build(nodes, n_nodes);
     for (int i = 0; i < n_nodes; ++i) {
         tts_tensor * n = nodes[i];

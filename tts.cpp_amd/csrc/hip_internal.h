@@ -227,12 +227,13 @@ struct tts_hip_backend {
     hipEvent_t plan_ev[2] = {nullptr, nullptr};
     bool plan_ev_pending[2] = {false, false};
     float * lstm_buf = nullptr;  // fused LSTM chains: per chain [Hd] cell state + [Hd, T] hidden history
+    float * vec_scratch = nullptr;  // 256K floats: per-channel vectors a fused item copies away from its output
     size_t lstm_floats = 0;
     tts::ActQuant aq;
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
     bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
-    int fusion = 0x3FF;  // bitmask of TTS_FUSE_* patterns (all on)
+    int fusion = 0x7FF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -326,6 +327,25 @@ inline int conv1d_icc(int64_t IC, int K, int xw) {  // input channels per LDS ch
     return best;  // 0: the shape does not fit (K > 64 or a window too wide)
 }
 bool conv1d_fused_ok(int64_t IC, int K, int s, int d, size_t * lds);
+// AdaIN (+ snake) per channel row: y[c][t] = snake((norm(x[c])[t] * (1 + g[c])...) -- see k_fused.hip
+struct AdainArgs {
+    const float * x = nullptr;   // NORM input rows: x[c * xcs + t], t < T
+    int64_t xcs = 0;
+    float * y = nullptr;         // output rows (the [T, C] tensor after the second transpose)
+    int64_t ycs = 0;
+    const float *gamma = nullptr, *beta = nullptr, *alpha = nullptr, *recip = nullptr;  // alpha null: no snake
+    const float * one = nullptr;  // recip null: recip[c] = one[0] / alpha[c] (reciprocal()'s DIV)
+    int stage = 0;  // 1: the output overlaps a vector's memory -> copy the vectors to be->vec_scratch first
+    // gamma / beta evaluated in the kernel (their MUL_MAT + bias ADD absorbed): gamma[c] =
+    // dot(gw[c * S ...], style) + gb[c], in k_gemv_float's exact order; gw null: read gamma / beta
+    const float *gw = nullptr, *gb = nullptr, *bw = nullptr, *bb = nullptr, *style = nullptr;
+    int64_t S = 0;
+    int64_t gcs = 1, bcs = 1, acs = 1, rcs = 1;
+    int64_t T = 0, C = 0;
+    float eps = 0.f;
+};
+bool adain_supported(int64_t T);
+void launch_adain_snake(tts_hip_backend * be, const AdainArgs & a);
 void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a);
 bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node);
 size_t act_quant_bytes(int wtype, int64_t K, int64_t M);

@@ -176,6 +176,130 @@ void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+// ---- AdaIN (+ snake) over one channel row (build_kokoro_generator_res_block, kokoro/model.cpp:
+// 136-165): NORM over time -> CONT(TRANSPOSE) -> x + x*gamma[c] -> + beta[c] -> CONT(TRANSPOSE)
+// [-> snake_1d with alpha[c], recip[c]] in one pass.  One 1024-thread workgroup per channel keeps
+// the row in registers (NPT elements per thread): one HBM read and one write instead of the
+// nine launches and the two transposes of the node chain.  Every f32 operation is the node's, in
+// the node's order; the two f64 sums are block reductions, as k_norm's. ----
+__device__ __forceinline__ double block_sum1024(double v, double * sh) {
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += sh[i];
+    return t;
+}
+
+template <int NPT, bool SNAKE>
+__global__ __launch_bounds__(1024) void k_adain_snake(AdainArgs a) {
+    __shared__ double sh[16];
+    const int64_t c = blockIdx.x;
+    const int64_t T = a.T;
+    const float * x = a.x + c * a.xcs;
+    float * y = a.y + c * a.ycs;
+    float v[NPT];
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+        const int64_t t = threadIdx.x + 1024 * u;
+        v[u] = t < T ? x[t] : 0.f;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) s += (double)v[u];  // padding adds 0
+    s = block_sum1024(s, sh);
+    const float mean = (float)(s / (double)T);
+    double s2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+        const int64_t t = threadIdx.x + 1024 * u;
+        const float d = __fsub_rn(v[u], mean);
+        if (t < T) s2 += (double)__fmul_rn(d, d);
+    }
+    s2 = block_sum1024(s2, sh);
+    const float variance = (float)(s2 / (double)T);
+    const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(variance, a.eps)));
+    float g, b;
+    if (a.gw) {
+        // waves 0 / 1: the gamma / beta GEMV rows, lane l summing k = 4l + 256j in k_gemv_float's
+        // order (f32 products, f64 sum, xor butterfly), then the bias ADD
+        __shared__ float gbv[2];
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+        if (w < 2) {
+            const float * wr = (w == 0 ? a.gw : a.bw) + c * a.S;
+            double acc = 0.0;
+            for (int64_t k = l * 4; k < a.S; k += 256) {
+                const float4 wv = *(const float4 *)(wr + k);
+                const float4 xv = *(const float4 *)(a.style + k);
+                acc += (double)__fmul_rn(wv.x, xv.x);
+                acc += (double)__fmul_rn(wv.y, xv.y);
+                acc += (double)__fmul_rn(wv.z, xv.z);
+                acc += (double)__fmul_rn(wv.w, xv.w);
+            }
+            for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+            if (l == 0) gbv[w] = __fadd_rn((float)acc, (w == 0 ? a.gb : a.bb)[c]);
+        }
+        __syncthreads();
+        g = gbv[0], b = gbv[1];
+    } else {
+        g = a.gamma[c * a.gcs], b = a.beta[c * a.bcs];
+    }
+    const float al = SNAKE ? a.alpha[c * a.acs] : 0.f;
+    const float rc = SNAKE ? (a.recip ? a.recip[c * a.rcs] : cr_divf(a.one[0], al)) : 0.f;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+        const int64_t t = threadIdx.x + 1024 * u;
+        if (t >= T) continue;
+        const float n = __fmul_rn(__fsub_rn(v[u], mean), scale);
+        float o = __fadd_rn(__fadd_rn(n, __fmul_rn(n, g)), b);
+        if (SNAKE) {
+            const float sn = cr_sinf(__fmul_rn(o, al));
+            o = __fadd_rn(o, __fmul_rn(__fmul_rn(sn, sn), rc));
+        }
+        y[t] = o;
+    }
+}
+
+bool adain_supported(int64_t T) { return T >= 1 && T <= 1024 * 64; }
+
+__global__ void k_stage_vecs(float * __restrict__ dst, AdainArgs a) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.C) return;
+    if (!a.gw) {
+        dst[c] = a.gamma[c * a.gcs];
+        dst[a.C + c] = a.beta[c * a.bcs];
+    }
+    if (a.alpha) dst[2 * a.C + c] = a.alpha[c * a.acs];
+    if (a.alpha && a.recip) dst[3 * a.C + c] = a.recip[c * a.rcs];
+    if (c == 0 && a.one) dst[4 * a.C] = a.one[0];
+}
+
+void launch_adain_snake(tts_hip_backend * be, const AdainArgs & args) {
+    AdainArgs a = args;
+    if (a.stage) {
+        float * v = be->vec_scratch;
+        hipLaunchKernelGGL(k_stage_vecs, dim3((unsigned)((a.C + 255) / 256)), dim3(256), 0, be->stream, v, args);
+        if (!a.gw) a.gamma = v, a.gcs = 1, a.beta = v + a.C, a.bcs = 1;
+        if (a.alpha) a.alpha = v + 2 * a.C, a.acs = 1;
+        if (a.alpha && a.recip) a.recip = v + 3 * a.C, a.rcs = 1;
+        if (a.one) a.one = v + 4 * a.C;
+    }
+    const bool sn = a.alpha != nullptr;
+    const int npt = a.T <= 8192 ? 8 : a.T <= 16384 ? 16 : a.T <= 32768 ? 32 : 64;
+    const dim3 grid((unsigned)a.C), block(1024);
+#define TTS_ADAIN(N)                                                                                       \
+    if (npt == N) {                                                                                        \
+        if (sn) hipLaunchKernelGGL((k_adain_snake<N, true>), grid, block, 0, be->stream, a);               \
+        else hipLaunchKernelGGL((k_adain_snake<N, false>), grid, block, 0, be->stream, a);                 \
+    }
+    TTS_ADAIN(8) TTS_ADAIN(16) TTS_ADAIN(32) TTS_ADAIN(64)
+#undef TTS_ADAIN
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 // ---- greedy sampling step (sampler::max, src/sampler.cpp:185-204) --------------------------------
 // One wave per (prompt b, head h) row of the step's logits [B][NH][V]: each lane scans its strided
 // slice keeping the first strict maximum (indices ascend within a lane), then the lanes combine by

@@ -444,3 +444,9 @@ extern "C" uint64_t tts_kokoro_gen_node(tts_kokoro_gen * k, int32_t i, int32_t *
     if (n > cap || k->be.get(k->be.ctx, dst, t->data, n) != 0) return 0;
     return n;
 }
+
+// The last graph's node list (valid until the next run), e.g. for tts_hip_plan_stats.
+extern "C" tts_tensor * const * tts_kokoro_gen_graph(const tts_kokoro_gen * k, int32_t * n_nodes) {
+    if (n_nodes) *n_nodes = k ? (int32_t)k->gctx.nodes.size() : 0;
+    return k ? k->gctx.nodes.data() : nullptr;
+}

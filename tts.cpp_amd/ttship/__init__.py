@@ -21,7 +21,7 @@ OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "
        "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
-FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512}
+FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024}
 FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
@@ -210,6 +210,8 @@ def lib():
         "tts_kokoro_gen_n_weights": (i32, [vp]),
         "tts_kokoro_gen_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
         "tts_kokoro_gen_node": (u64, [vp, i32, vp, vp, vp, vp, u64]),
+        "tts_kokoro_gen_graph": (vp, [vp, ctypes.POINTER(i32)]),
+        "tts_hip_plan_stats": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i32)]),
         "tts_kokoro_gen_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
     }
     for name, (res, args) in sig.items():
@@ -493,6 +495,15 @@ class KokoroGenerator:
         n = self.L.tts_kokoro_gen_node(self.ptr, i, ctypes.byref(op), ctypes.byref(ty), ne, buf.ctypes.data, cap)
         return OPS[op.value], ty.value, tuple(ne), (buf[: n // 4].copy() if n else None)
 
+    def plan_stats(self, mask=None):
+        """Fusion coverage of the last graph (no device needed): {item kind: count, "unfused": n}."""
+        return plan_stats(*self._graph(), FUSE_ALL if mask is None else mask)
+
+    def _graph(self):
+        n = ctypes.c_int32()
+        p = self.L.tts_kokoro_gen_graph(self.ptr, ctypes.byref(n))
+        return p, n.value
+
     def node(self, name):
         """float32 values of a named node of the last run (flat), or None."""
         import numpy as np
@@ -510,3 +521,15 @@ class KokoroGenerator:
         if self.ptr:
             self.L.tts_kokoro_gen_free(self.ptr)
             self.ptr = None
+
+
+PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain"]
+
+
+def plan_stats(nodes_ptr, n_nodes, mask):
+    """tts_hip_plan_stats over a node array: {kind: items, "unfused": nodes launched one by one}."""
+    counts = (ctypes.c_int32 * 16)()
+    lib().tts_hip_plan_stats(nodes_ptr, n_nodes, mask, counts)
+    out = {k: int(counts[i]) for i, k in enumerate(PLAN_KINDS)}
+    out["unfused"] = int(counts[15])
+    return out
