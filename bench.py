@@ -171,6 +171,29 @@ def gemv_roofline(be, runner, steps):
             "launches_sampled": launches}
 
 
+def run_replicas(fn, n):
+    """fn(0..n-1) concurrently on host threads (the ctypes calls release the GIL), re-raising errors."""
+    if n == 1:
+        fn(0)
+        return
+    import threading
+    errs = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+
+
 def kokoro_inputs(cfg, T, rank):
     """Synthetic generator inputs: decoder features, a voiced F0 contour with unvoiced gaps, a
     style vector and the uniform noise draws (seeded per rank)."""
@@ -195,24 +218,45 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=400)
     ap.add_argument("--no-fusion", action="store_true")
     ap.add_argument("--no-dac", action="store_true", help="AR decode only")
+    ap.add_argument("--attn-split", type=int, default=None, help="TTS_HIP_OPT_ATTN_SPLIT: min KV length for split attention (0 = off)")
+    ap.add_argument("--replicas", type=int, default=2, help="concurrent runner replicas per GPU, each on its own "
+                    "backend/stream with batch/replicas prompts (the server's worker model)")
+    ap.add_argument("--kv-prefetch", type=int, default=None, help="TTS_HIP_OPT_KV_PREFETCH: min KV length (0 = off)")
+    ap.add_argument("--kv-prefetch-blocks", type=int, default=None)
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
     ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
-    be = ttship.HipBackend(local)
-    if args.no_fusion:
-        be.set_option(0, 0)
-    be.set_option(2, args.graphs)
-    cfg = ttship.parler_config(batch=args.batch, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
+    R = args.replicas
+    if R < 1 or args.batch % R:
+        raise SystemExit(f"--replicas {R} must divide --batch {args.batch}")
+    bl = args.batch // R  # prompts per replica
+    cfg = ttship.parler_config(batch=bl, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
                                arena_bytes=4 << 30)
-    runner = ttship.Parler(be.iface(), cfg)
-    dac = None
-    if not args.no_dac:
-        dcfg = ttship.dac_config(max_frames=args.steps)
-        dac = ttship.Dac(be.iface(), dcfg)
-        dac.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+    reps = []
+    for r in range(R):
+        # a replica = one backend (its own HIP stream) + its own runners, as a server worker owns its
+        # runners (examples/server/server.cpp:316-321); replicas run concurrently from host threads
+        rb = ttship.HipBackend(local)
+        if args.no_fusion:
+            rb.set_option(0, 0)
+        rb.set_option(2, args.graphs)
+        if args.attn_split is not None:
+            rb.set_option(ttship.OPT["ATTN_SPLIT"], args.attn_split)
+        if args.kv_prefetch is not None:
+            rb.set_option(ttship.OPT["KV_PREFETCH"], args.kv_prefetch)
+        if args.kv_prefetch_blocks is not None:
+            rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
+        rr = ttship.Parler(rb.iface(), cfg)
+        rd = None
+        if not args.no_dac:
+            dcfg = ttship.dac_config(max_frames=args.steps)
+            rd = ttship.Dac(rb.iface(), dcfg)
+            rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+        reps.append((rb, rr, rd))
+    be, runner, dac = reps[0]
     kok = None
     if args.kokoro_calls > 0:
         kcfg = ttship.kokoro_gen_config(max_frames=args.kokoro_frames)
@@ -221,21 +265,41 @@ def main():
         kpcm = np.empty(300 * args.kokoro_frames, dtype=np.float32)
         kok.run(*kin, out=kpcm)  # warm (code objects, arena)
     # text-prompt pass to reach the measured KV length
-    runner.prefill(prompt_tokens(args.batch, args.ctx, cfg.prompt_vocab, offset=rank * args.batch))
-    runner.generate(args.warmup)
+    for r, (rb, rr, rd) in enumerate(reps):
+        rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * args.batch + r * bl))
+        rr.generate(args.warmup)
+        rb.sync()
     barrier_sync(dist, be)
 
     runner.host_stats(reset=True)
+    c0 = be.counters()
+    toks_r = [None] * R
+
+    def ar_leg(r):
+        rb, rr, _ = reps[r]
+        toks_r[r] = rr.generate(args.steps)
+        rb.sync()
+
+    def dac_leg(r):
+        rb, _, rd = reps[r]
+        for b in range(bl):
+            rd.decode(dac_codes(toks_r[r][b], dcfg.codebook_size))
+        rb.sync()
+
     t0 = time.perf_counter()
-    toks = runner.generate(args.steps)
-    be.sync()
+    run_replicas(ar_leg, R)
     t1 = time.perf_counter()
+    c1 = be.counters()
+    cdelta = {k: (c1.get(k, 0) - c0.get(k, 0)) / 1e3 / max(1, args.steps) for k in ("plan_wait_ns", "cap_plan_ns", "cap_launch_ns", "cap_update_ns")}
     if dac is not None:
-        for b in range(args.batch):
-            dac.decode(dac_codes(toks[b], dcfg.codebook_size))
+        run_replicas(dac_leg, R)
     barrier_sync(dist, be)
     t2 = time.perf_counter()
+    toks = np.concatenate(toks_r, axis=0)
     host = runner.host_stats(reset=True)
+    # parts of compute_enqueue: waiting on the device for the plan slot, planner, launches under
+    # capture (incl. planner), exec update
+    host.update({k.replace("_ns", "_us"): round(v, 1) for k, v in cdelta.items()})
     kres = None
     if kok is not None:
         # BASELINE configs[1]: the Kokoro-82M iSTFTNet vocoder path, timed on its own
@@ -283,7 +347,7 @@ def main():
             "config": {"workload": f"Parler-TTS-mini-v1 Q4_K, greedy AR decode + DAC-44k (BASELINE configs[2])",
                        "model": "parler-tts-mini-v1", "prompts_per_gpu": args.batch, "global_batch": total_prompts,
                        "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
-                       "parallelism": f"dp{world} (prompt shards)", "graph_nodes_per_step": runner.last_graph_nodes(),
+                       "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} prompts per GPU", "graph_nodes_per_step": runner.last_graph_nodes(),
                        "dac_graph_nodes": dac.last_graph_nodes() if dac is not None else None},
             "ar_audio_sec_per_s": round(audio_s / dt_ar, 3),
             "ar_ms_per_step": round(1000.0 * dt_ar / args.steps, 4),
@@ -295,12 +359,13 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if dac is not None:
-        dac.close()
     if kok is not None:
         kok.close()
-    runner.close()
-    be.close()
+    for rb, rr, rd in reps:
+        if rd is not None:
+            rd.close()
+        rr.close()
+        rb.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

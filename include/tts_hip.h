@@ -207,7 +207,12 @@ enum tts_hip_option {
     TTS_HIP_OPT_PROFILE_GEMV = 1, /* 1 = time quantized GEMV launches with HIP events */
     TTS_HIP_OPT_GRAPHS = 2,       /* 1 = replay each graph_compute as a HIP graph (capture + exec update) */
     TTS_HIP_OPT_CONV_F32ACC = 3,  /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
-    TTS_HIP_OPT_CONVT_LDS = 4     /* 1 (default) = conv_transpose_1d on the LDS-staged f64 MFMA kernel, 0 = per-wave kernel */
+    TTS_HIP_OPT_CONVT_LDS = 4,    /* 1 (default) = conv_transpose_1d on the LDS-staged f64 MFMA kernel, 0 = per-wave kernel */
+    TTS_HIP_OPT_ATTN_SPLIT = 5,   /* decode attention over P >= value keys runs as two position/dim-split kernels
+                                     (scores, then softmax + P.V); 0 = always the one-workgroup-per-head kernel */
+    TTS_HIP_OPT_KV_PREFETCH = 6,  /* prefetch the next decode attention's K/V (KV length >= value) into the
+                                     Infinity Cache on a side stream during the GEMVs before it; 0 = off */
+    TTS_HIP_OPT_KV_PREFETCH_BLOCKS = 7 /* workgroups of the prefetch kernel (default 128) */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
@@ -215,7 +220,8 @@ enum tts_fuse_bits {
     TTS_FUSE_SNAKE = 128, /* snake_1d's five elementwise nodes -> one pass */
     TTS_FUSE_EMBED = 256, /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
     TTS_FUSE_CONV = 512,  /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
-    TTS_FUSE_ADAIN = 1024 /* Kokoro AdaIN1d (norm, transposes, affine) + snake_1d -> one pass per channel row */
+    TTS_FUSE_ADAIN = 1024, /* Kokoro AdaIN1d (norm, transposes, affine) + snake_1d -> one pass per channel row */
+    TTS_FUSE_XATTN = 2048  /* short-context attention (P <= 64) folded into the Q4_K GEMV producing its query */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

@@ -64,6 +64,8 @@ int32_t tts_parler_position(const tts_parler * p);
 int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset);
 /* Nodes in the last step graph and bytes of the compute arena it used. */
 int32_t tts_parler_last_graph_nodes(const tts_parler * p);
+/* The last step graph's node list (valid until the next step is prepared). */
+tts_tensor * const * tts_parler_graph(const tts_parler * p, int32_t * n_nodes);
 uint64_t tts_parler_weight_bytes(const tts_parler * p);
 /* Debug: copy a named node of the last graph to host (returns bytes, 0 if not found). */
 uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap);

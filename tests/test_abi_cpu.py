@@ -123,6 +123,12 @@ def test_supports_op_host_logic():
     w_bad.ne[0] = 1000
     mm_bad = _t(ttship.F32, [4, 1], op=ttship.OP["MUL_MAT"], srcs=(w_bad, x))
     assert L.tts_hip_supports_op(ctypes.byref(mm_bad)) == 0
+    # ggml_can_mul_mat: src1 must broadcast over src0 (dims 2, 3); H = 24 probabilities x 8 V heads is invalid
+    kq = _t(ttship.F32, [300, 1, 24, 1])
+    v8 = _t(ttship.F32, [300, 64, 8, 1])
+    assert L.tts_hip_supports_op(ctypes.byref(_t(ttship.F32, [1, 64, 24, 1], op=ttship.OP["MUL_MAT"], srcs=(kq, v8)))) == 0
+    v24 = _t(ttship.F32, [300, 64, 24, 1])
+    assert L.tts_hip_supports_op(ctypes.byref(_t(ttship.F32, [1, 64, 24, 1], op=ttship.OP["MUL_MAT"], srcs=(kq, v24)))) == 1
     # buffer-less host leaf (src/util.cpp:86-94 reciprocal) must stay on the CPU backend
     host_leaf = _t(ttship.F32, [1024, 1], flags=2)
     div = _t(ttship.F32, [1024, 1], op=ttship.OP["DIV"], srcs=(x, host_leaf))

@@ -3,8 +3,9 @@
 mul_mat(kq, V view) -> permute(2, 0, 1, 3) -> cont, with K / V read from cache layouts.
 
 Kernel choice depends on the context length (k_attn.hip): P <= 64 -> k_attn_small (sequential
-sums, bit-exact), P <= 512 / 1024 -> k_attn_decode_rows with V prefetched (8 / 16 chunks per lane),
-longer -> streamed V; hd 128 (Dia / Orpheus head size).  The row kernel reassociates
+sums, bit-exact); P >= TTS_HIP_OPT_ATTN_SPLIT (default 128) -> k_attn_scores + k_attn_pv (split over
+positions, then over output dims); otherwise k_attn_decode_rows with V prefetched (P <= 512) or
+streamed; hd 128 (Dia / Orpheus head size).  `split` runs every case both ways.  The row kernel reassociates
 the f64 sums (quad / row DPP reductions), so it is held to <= 1 ulp with almost all elements exact.
 """
 import numpy as np
@@ -38,8 +39,12 @@ def build(g, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx):
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,hd,H,Hk,B", [(3, 64, 16, 16, 2), (64, 64, 16, 16, 1), (65, 64, 4, 4, 1), (500, 64, 16, 16, 2),
                                          (700, 64, 16, 16, 1), (1024, 64, 4, 4, 1), (1500, 64, 4, 4, 1),
-                                         (37, 128, 16, 16, 2), (430, 128, 8, 8, 1), (1, 64, 4, 4, 1)])
-def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B):
+                                         (37, 128, 16, 16, 2), (430, 128, 8, 8, 1), (1, 64, 4, 4, 1),
+                                         (1309, 64, 16, 16, 8), (2100, 128, 24, 24, 1), (128, 64, 16, 16, 3),
+                                         (257, 128, 16, 16, 2), (4096, 64, 16, 16, 2)])
+@pytest.mark.parametrize("split", [True, False])
+def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, split):
+    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
     rng = np.random.default_rng(P * 7 + hd)
     max_ctx = P + 40
     q = rng.standard_normal((B, H, hd)).astype(np.float32)
@@ -53,6 +58,7 @@ def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B):
     o2 = build(g2, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx)
     g1.run_hip(hip)
     g2.run_oracle(n_threads=8)
+    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT)
     gpu, ref = g1.node_array(o1), g2.node_array(o2)
     if P <= 64:
         assert np.array_equal(gpu, ref)

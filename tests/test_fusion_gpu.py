@@ -9,7 +9,8 @@ import ttship
 
 TINY = dict(n_layers=2, hidden_size=256, n_attn_heads=4, ffn_size=1024, output_vocab=1088, max_ctx=96,
             prompt_vocab=512, max_positions=128)
-MASKS = {"off": 0, "ln": 1, "group": 2, "kv": 2 | 4, "epi": 8, "heads": 16, "attn": 32, "embed": 256, "all": ttship.FUSE_ALL}
+MASKS = {"off": 0, "ln": 1, "group": 2, "kv": 2 | 4, "epi": 8, "heads": 16, "attn": 32, "embed": 256,
+         "xattn": 32 | 2048, "ln_xattn": 1 | 32 | 2048, "all_but_xattn": ttship.FUSE_ALL & ~2048, "all": ttship.FUSE_ALL}
 
 
 @pytest.fixture(scope="module")

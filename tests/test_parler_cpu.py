@@ -1,0 +1,31 @@
+"""Host-side planning of the Parler decode step (no device): the fusion planner's coverage of the
+reference node list (build_parler_graph, src/models/parler/model.cpp:520-614) built by the runner on
+the oracle backend.  Every layer's cross-attention (n_enc <= 64 positions) must fold into the Q4_K
+GEMV producing its query (TTS_FUSE_XATTN), the self-attention must be one fused item per layer."""
+import numpy as np
+
+import py_oracle
+import ttship
+
+TINY = dict(n_layers=3, hidden_size=256, n_attn_heads=4, ffn_size=1024, output_vocab=1088, max_ctx=96,
+            prompt_vocab=512, max_positions=128)
+
+
+def _decoded(batch):
+    c = ttship.Parler(py_oracle.iface(2), ttship.parler_config(batch=batch, **TINY))
+    prompt = (np.arange(6 * batch, dtype=np.int32).reshape(batch, 6) * 41) % 512
+    c.prefill(prompt)
+    c.decode(np.full((batch, 9), 7, dtype=np.int32))
+    return c
+
+
+def test_parler_step_plan_coverage():
+    for batch in (1, 3):
+        c = _decoded(batch)
+        st = c.plan_stats()
+        L = TINY["n_layers"]
+        assert st["attn"] == 2 * L, st          # self + cross per layer
+        assert st["xattn"] == L, st             # every cross-attention rides its query GEMV
+        without = c.plan_stats(ttship.FUSE_ALL & ~ttship.FUSE["XATTN"])
+        assert without["xattn"] == 0 and without["attn"] == 2 * L
+        c.close()

@@ -24,6 +24,7 @@ static void build_gelu_table(uint16_t * t) {
 static const size_t kScratchBytes = 64u << 20;
 static const size_t kShadowBytes = 4u << 20;  // private copy of an attention output (decode: 32 KB per 8 prompts)
 static const size_t kLstmFloats = 4u << 20;
+static const size_t kAttnFloats = 4u << 20;  // split attention scores: e.g. B 8 x H 16 x P 4096 = 512K floats
 static const size_t kVecScratchFloats = 1u << 18;  // per-channel vectors staged by fused items (AdaIN)
 static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tensor_async   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
 
@@ -43,6 +44,9 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     be->device = device;
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->stream, hipStreamNonBlocking));
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->cap_stream, hipStreamNonBlocking));
+    TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->pf_stream, hipStreamNonBlocking));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&be->pf_fork, hipEventDisableTiming));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&be->pf_join, hipEventDisableTiming));
     hipDeviceProp_t prop;
     TTS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     snprintf(be->name, sizeof(be->name), "HIP%d(%s)", device, prop.gcnArchName);
@@ -51,6 +55,8 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     TTS_HIP_CHECK(hipMalloc((void **)&be->shadow, kShadowBytes));
     be->shadow_size = kShadowBytes;
     TTS_HIP_CHECK(hipMalloc((void **)&be->lstm_buf, kLstmFloats * sizeof(float)));
+    TTS_HIP_CHECK(hipMalloc((void **)&be->attn_buf, kAttnFloats * sizeof(float)));
+    be->attn_floats = kAttnFloats;
     TTS_HIP_CHECK(hipMalloc((void **)&be->vec_scratch, kVecScratchFloats * sizeof(float)));
     be->lstm_floats = kLstmFloats;
     TTS_HIP_CHECK(hipHostMalloc((void **)&be->pin, kPinBytes, hipHostMallocDefault));
@@ -79,6 +85,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->lstm_buf);
+    hipFree(be->attn_buf);
     hipFree(be->vec_scratch);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
@@ -87,6 +94,9 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
         if (ex) hipGraphExecDestroy(ex);
     hipStreamDestroy(be->stream);
     hipStreamDestroy(be->cap_stream);
+    hipStreamDestroy(be->pf_stream);
+    hipEventDestroy(be->pf_fork);
+    hipEventDestroy(be->pf_join);
     delete be;
 }
 
@@ -282,6 +292,8 @@ int tts_hip_supports_op(const tts_tensor * n) {
             const tts_tensor * a = n->src[0];
             const tts_tensor * b = n->src[1];
             if (!is_f32(b)) return 0;
+            // ggml_can_mul_mat: src1 broadcasts over src0 in dims 2 and 3
+            if (a->ne[0] != b->ne[0] || b->ne[2] % a->ne[2] || b->ne[3] % a->ne[3]) return 0;
             if (a->type == TTS_TYPE_F32 || a->type == TTS_TYPE_F16) return 1;
             if (a->type == TTS_TYPE_Q4_K) return a->ne[0] % 256 == 0;
             if (a->type == TTS_TYPE_Q8_0) return a->ne[0] % 32 == 0;
@@ -302,15 +314,19 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
         case TTS_HIP_OPT_CONV_F32ACC: be->conv_f32acc = value != 0; return 0;
+        case TTS_HIP_OPT_ATTN_SPLIT: be->attn_split_minp = value; return 0;
+        case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
+        case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }
 }
 
 extern "C" int tts_hip_counters(tts_hip_backend_t be, int64_t * out, int n) {
     if (!be || !out) return TTS_STATUS_BAD_ARG;
-    const int64_t v[4] = {be->graph_updates, be->graph_instantiations, be->lstm_chains, be->lstm_steps};
+    const int64_t v[8] = {be->graph_updates, be->graph_instantiations, be->lstm_chains, be->lstm_steps, be->plan_wait_ns,
+                          be->cap_plan_ns, be->cap_launch_ns, be->cap_update_ns};
     int k = 0;
-    for (; k < n && k < 4; ++k) out[k] = v[k];
+    for (; k < n && k < 8; ++k) out[k] = v[k];
     return k;
 }
 

@@ -20,10 +20,13 @@
 #include <vector>
 
 #include "hip_internal.h"
+#include <chrono>
 
 using namespace tts;
 
 namespace tts {
+void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int pdim, int blocks);
+void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnArgs & a);
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
                         float * out, int hd, int P, int H, int n, int B, float * out2);
 void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
@@ -112,6 +115,8 @@ struct Item {
     bool lnrms = false;
     bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
     bool shadow = false;    // ATTN: also write the private copy (be->shadow)
+    int xattn = -1;         // GEMV: index of the short-context ATTN item whose query it produces (one launch)
+    bool fused = false;     // ATTN: launched by the GEMV item that produces its query
     // ATTN
     const tts_tensor *q = nullptr, *k = nullptr, *v = nullptr, *mask = nullptr, *out = nullptr;
     float scale = 1.f;
@@ -199,6 +204,7 @@ struct Planner {
         }
         if (mask & TTS_FUSE_LN) fuse_ln_into_gemv();
         link_attn_shadow();
+        if (mask & TTS_FUSE_XATTN) fuse_xattn();
     }
 
     // attention output -> [views] -> Q4_K GEMV: the attention kernel also writes a private copy
@@ -216,6 +222,44 @@ struct Planner {
             const tts_tensor * x = G.mms[0]->src[1];
             if (x->data != A.out->data || !contiguous(x) || tbytes(x) != tbytes(A.out)) continue;
             A.shadow = G.x_shadow = true;
+        }
+    }
+
+    // Short-context attention (P <= 64, hd 64, one query: Parler's cross-attention over the T5
+    // encoding) whose query is the output of a single-matrix Q4_K GEMV item, through reshape /
+    // permute views only: both run as one k_gemv_q4K_xattn launch at the GEMV's position.  Nothing
+    // may run between the two (the attention output is written early).
+    void fuse_xattn() {
+        for (size_t ai = 0; ai < items.size(); ++ai) {
+            Item & A = items[ai];
+            if (A.kind != Item::ATTN || A.k->ne[1] > 64 || A.q->ne[0] != 64 || A.q->ne[1] != 1) continue;
+            const tts_tensor * Q = A.q;
+            const tts_tensor * t = Q;
+            int hops = 0;
+            while (t && is_view(t->op) && t->src[0] && hops < 4) {
+                if (uses[t->src[0]] != 1) break;
+                t = t->src[0];
+                ++hops;
+            }
+            if (!t || t->op != TTS_OP_MUL_MAT || uses[t] != 1) continue;
+            const int gi = act[index[t]];
+            if (gi <= 0) continue;
+            Item & G = items[gi - 1];
+            if (G.kind != Item::GEMV || G.mms.size() != 1 || G.mms[0] != t || G.epi != EPI_NONE || G.res || G.xattn >= 0) continue;
+            const tts_tensor * W = t->src[0];
+            const int64_t H = Q->ne[2], B = Q->ne[3];
+            if (W->type != TTS_TYPE_Q4_K || W->ne[0] > 1024 || W->ne[1] != 64 * H || t->ne[1] * t->ne[2] * t->ne[3] != B) continue;
+            if (G.tgt[0].y != (float *)t->data || G.tgt[0].ycs != W->ne[1] || G.tgt[0].yrs != 1) continue;
+            if (Q->data != t->data || Q->nb[0] != 4 || Q->nb[2] != 256 || (int64_t)Q->nb[3] != 4 * W->ne[1]) continue;
+            if (A.k->ne[2] != H || A.v->ne[2] != H || B % A.k->ne[3] || B % A.v->ne[3]) continue;  // K/V may be shared by all prompts
+            if (A.mask && A.mask->ne[0] != A.k->ne[1]) continue;
+            const int g_node = index[t], o_node = index[A.out];
+            bool clear = g_node < o_node;
+            for (int i = g_node + 1; clear && i < o_node; ++i)
+                if (act[i] > 0 || (act[i] == 0 && !is_view(nodes[i]->op))) clear = false;
+            if (!clear) continue;
+            G.xattn = (int)ai;
+            A.fused = true;
         }
     }
 
@@ -1028,7 +1072,15 @@ static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a) {
     return be->repack_tmp;
 }
 
-static int run_gemv_item(tts_hip_backend * be, const Item & it) {
+static int run_attn_item(tts_hip_backend * be, const Item & it) {
+    const TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
+    float * out2 = it.shadow && tbytes(it.out) <= be->shadow_size ? be->shadow : nullptr;
+    launch_attn_decode(be, q, k, v, it.mask ? (const float *)it.mask->data : nullptr, it.scale, (float *)it.out->data,
+                       (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3], out2);
+    return 0;
+}
+
+static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xattn = nullptr) {
     const tts_tensor * mm0 = it.mms[0];
     const tts_tensor * a0 = mm0->src[0];
     const tts_tensor * b = mm0->src[1];
@@ -1097,6 +1149,40 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it) {
     }
     // a Q4_K matrix in native layout goes through the one-matrix repack temp: launch it alone
     const bool tmp = a0->type == TTS_TYPE_Q4_K && !(a0->flags & TTS_FLAG_REPACKED);
+    if (xattn) {
+        const Item & A = *xattn;
+        const TD k = make_td(A.k), v = make_td(A.v);
+        const char * o0 = (const char *)A.out->data;
+        const char * o1 = o0 + tbytes(A.out);
+        const char * x0 = (const char *)j.x;
+        const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
+        const bool ok = !tmp && j.wtype == TTS_TYPE_Q4_K && j.K <= 1024 && j.N == 64 * A.q->ne[2] && k.nb[0] == 4 &&
+                        (k.nb[1] % 16) == 0 && (k.nb[2] % 16) == 0 && (k.nb[3] % 16) == 0 && ((uintptr_t)k.data % 16) == 0 &&
+                        A.k->ne[1] >= 1 && A.k->ne[1] <= 64 && !(o0 < x1 && x0 < o1) && contiguous(A.out);
+        if (ok) {
+            GemvJob jj = j;
+            jj.nmat = 1;
+            jj.W[0] = (const uint8_t *)weight_ptr(be, a0);
+            jj.Y[0] = nullptr;
+            if (jj.lnout) {  // the LN output may already be dead and its memory the attention output
+                const char * l0 = (const char *)jj.lnout;
+                const char * l1 = l0 + 4 * (size_t)((j.M - 1) * j.locs + j.K);
+                if (l0 < o1 && o0 < l1) jj.lnout = nullptr;
+            }
+            XAttnArgs xa;
+            xa.k = k;
+            xa.v = v;
+            xa.mask = A.mask ? (const float *)A.mask->data : nullptr;
+            xa.scale = A.scale;
+            xa.out = (float *)A.out->data;
+            xa.out2 = A.shadow && tbytes(A.out) <= be->shadow_size ? be->shadow : nullptr;
+            xa.P = (int)A.k->ne[1];
+            xa.H = (int)A.q->ne[2];
+            xa.B = (int)A.q->ne[3];
+            launch_gemv_q4K_xattn(be, jj, xa);
+            return 0;
+        }
+    }
     size_t k = 0;
     while (k < it.mms.size()) {
         GemvJob jj = j;
@@ -1112,11 +1198,14 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it) {
         }
         launch_gemv_job(be, jj);
     }
+    if (xattn) return run_attn_item(be, *xattn);  // unfused fallback: the attention right after its query
     return 0;
 }
 
 static int run_node(tts_hip_backend * be, const tts_tensor * n) {
     if (n->op == TTS_OP_MUL_MAT) {
+        const tts_tensor * a = n->src[0], * b = n->src[1];
+        if (a->ne[0] != b->ne[0] || b->ne[2] % a->ne[2] || b->ne[3] % a->ne[3]) return TTS_STATUS_UNSUPPORTED;  // ggml_can_mul_mat
         if (is_gemv(n)) {
             Item it;
             it.kind = Item::GEMV;
@@ -1131,16 +1220,12 @@ static int run_node(tts_hip_backend * be, const tts_tensor * n) {
     return launch_op(be, n);
 }
 
-static int run_item(tts_hip_backend * be, const Item & it) {
+static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Item> & items) {
     switch (it.kind) {
-        case Item::GEMV: return run_gemv_item(be, it);
-        case Item::ATTN: {
-            const TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
-            float * out2 = it.shadow && tbytes(it.out) <= be->shadow_size ? be->shadow : nullptr;
-            launch_attn_decode(be, q, k, v, it.mask ? (const float *)it.mask->data : nullptr, it.scale, (float *)it.out->data,
-                               (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3], out2);
-            return 0;
-        }
+        case Item::GEMV: return run_gemv_item(be, it, it.xattn >= 0 ? &items[it.xattn] : nullptr);
+        case Item::ATTN:
+            if (it.fused) return 0;  // launched with its query GEMV
+            return run_attn_item(be, it);
         case Item::LN:
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
             return 0;
@@ -1178,7 +1263,9 @@ static bool capture_worthy(tts_hip_backend * be, tts_tensor * const * nodes, int
     if (!be->use_graphs || be->profile_gemv) return false;
     for (int i = 0; i < n_nodes; ++i) {
         const tts_tensor * t = nodes[i];
-        if (t->op == TTS_OP_MUL_MAT && t->src[1] && t->src[1]->ne[1] * t->src[1]->ne[2] * t->src[1]->ne[3] > 64) return false;
+        // prefill-sized products (more than 64 columns per matrix) run once: not worth recording.
+        // Decode attention's batched q.K / p.V products have one column per (head, prompt).
+        if (t->op == TTS_OP_MUL_MAT && t->src[1] && t->src[1]->ne[1] > 64) return false;
     }
     return true;
 }
@@ -1191,11 +1278,14 @@ static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_
     // for the step still running there, and the whole point of a prepared plan is to overlap it
     hipStream_t run = be->stream;
     be->stream = be->cap_stream;
+    const auto t0 = std::chrono::steady_clock::now();
     TTS_HIP_CHECK(hipStreamBeginCapture(be->stream, hipStreamCaptureModeThreadLocal));
     const int st = graph_compute_launches(be, nodes, n_nodes);
     hipGraph_t graph = nullptr;
     TTS_HIP_CHECK(hipStreamEndCapture(be->stream, &graph));
     be->stream = run;
+    const auto t1 = std::chrono::steady_clock::now();
+    be->cap_launch_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
     if (st != 0) {
         if (graph) hipGraphDestroy(graph);
         return st;
@@ -1217,6 +1307,7 @@ static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_
         be->graph_instantiations++;
     }
     TTS_HIP_CHECK(hipGraphDestroy(graph));
+    be->cap_update_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t1).count();
     return 0;
 }
 
@@ -1238,7 +1329,9 @@ extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * 
     if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
     if (be->plan_ev_pending[slot]) {  // the slot's previous launch must have run before it is re-recorded
+        const auto t0 = std::chrono::steady_clock::now();
         TTS_HIP_CHECK(hipEventSynchronize(be->plan_ev[slot]));
+        be->plan_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
         be->plan_ev_pending[slot] = false;
     }
     be->plan_nodes[slot] = nodes;
@@ -1264,7 +1357,8 @@ extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
 }
 
 // Fusion coverage of a graph without a device (tests, tooling): counts[k] = items of kind k
-// (Item::Kind order), counts[15] = nodes still launched one by one.  Returns the item count.
+// (Item::Kind order), counts[14] = attention items folded into their query GEMV (TTS_FUSE_XATTN),
+// counts[15] = nodes still launched one by one.  Returns the item count.
 extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int mask, int32_t * counts) {
     Planner pl;
     pl.mask = mask;
@@ -1272,7 +1366,10 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     if (mask) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
     for (int k = 0; k < 16; ++k) counts[k] = 0;
-    for (const Item & it : pl.items) counts[(int)it.kind]++;
+    for (const Item & it : pl.items) {
+        counts[(int)it.kind]++;
+        if (it.xattn >= 0) counts[14]++;
+    }
     for (int i = 0; i < n_nodes; ++i)
         if (pl.act[i] == 0 && !is_view(nodes[i]->op)) counts[15]++;
     return (int)pl.items.size();
@@ -1282,20 +1379,54 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     be->graph_epoch++;
     be->aq.src = nullptr;
     if (be->profile_gemv) launch_profile_spin(be, 4000.0);  // see launch_profile_spin (k_gemv.hip)
+    const auto tp0 = std::chrono::steady_clock::now();
     Planner pl;
     pl.mask = be->fusion;
     pl.lstm_buf = be->lstm_buf;
     pl.lstm_cap = be->lstm_floats;
     pl.vec_cap = be->vec_scratch ? (1u << 18) : 0;
     if (be->fusion) pl.build(nodes, n_nodes);
+    be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
+    // long-context attention items in launch order: each one's K/V is prefetched into MALL on the
+    // side stream right after the previous one ran (fork), and joined just before it runs
+    std::vector<int> pf_items;
+    if (be->fusion && be->kv_prefetch_minp > 0) {
+        for (int i = 0; i < n_nodes; ++i) {
+            const int a = pl.act[i];
+            if (a > 0 && pl.items[a - 1].kind == Item::ATTN && pl.items[a - 1].k->ne[1] >= be->kv_prefetch_minp) pf_items.push_back(a - 1);
+        }
+    }
+    size_t pf_next = 0;
+    int pf_pending = -1;  // item whose prefetch was forked and not yet joined
+    auto pf_fork = [&]() {
+        if (pf_next >= pf_items.size()) return;
+        const Item & t = pl.items[pf_items[pf_next]];
+        TTS_HIP_CHECK(hipEventRecord(be->pf_fork, be->stream));
+        TTS_HIP_CHECK(hipStreamWaitEvent(be->pf_stream, be->pf_fork, 0));
+        launch_kv_prefetch(be, be->pf_stream, make_td(t.k), 1, be->kv_prefetch_blocks);
+        launch_kv_prefetch(be, be->pf_stream, make_td(t.v), 0, be->kv_prefetch_blocks);
+        TTS_HIP_CHECK(hipEventRecord(be->pf_join, be->pf_stream));
+        pf_pending = pf_items[pf_next];
+    };
+    pf_fork();
     for (int i = 0; i < n_nodes; ++i) {
         tts_tensor * n = nodes[i];
         const int a = be->fusion ? pl.act[i] : 0;
         if (a < 0) continue;
         if (a == 0 && is_view(n->op)) continue;
-        const int st = a > 0 ? run_item(be, pl.items[a - 1]) : run_node(be, n);
+        const bool is_pf = a > 0 && pf_pending == a - 1;
+        if (is_pf) {
+            TTS_HIP_CHECK(hipStreamWaitEvent(be->stream, be->pf_join, 0));
+            pf_pending = -1;
+        }
+        const int st = a > 0 ? run_item(be, pl.items[a - 1], pl.items) : run_node(be, n);
+        if (is_pf) {
+            ++pf_next;
+            pf_fork();
+        }
         if (st != 0) {
             fprintf(stderr, "tts_hip_graph_compute: node %d (%s, %s) failed: %d\n", i, n->name, tts_op_name(n->op), st);
+            if (pf_pending >= 0) (void)hipStreamWaitEvent(be->stream, be->pf_join, 0);
             return st;
         }
         // The Q8_K activation cache is keyed by address and the graph reuses freed memory, so it
@@ -1324,6 +1455,7 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
             if (!keep) be->aq.src = nullptr;
         }
     }
+    if (pf_pending >= 0) TTS_HIP_CHECK(hipStreamWaitEvent(be->stream, be->pf_join, 0));  // every fork rejoins
     return 0;
 }
 

@@ -198,6 +198,16 @@ struct GemvJob {
     } while (0)
 #endif
 enum { PRO_QUANT = 1, PRO_LN = 2 };
+// Cross-attention over a short context folded into the Q4_K GEMV that produces its query
+// (k_gemv_q4K_xattn): K view [hd, P, H, B], V view [P, hd, H, B] (f32), out [hd, H, 1, B].
+struct XAttnArgs {
+    TD k, v;
+    const float * mask = nullptr;  // [P] row 0 (n = 1), or null
+    float scale = 1.f;
+    float * out = nullptr;
+    float * out2 = nullptr;        // optional private copy (the next GEMV's input, be->shadow)
+    int P = 0, H = 0, B = 0;
+};
 
 }  // namespace tts
 
@@ -212,6 +222,16 @@ struct tts_hip_backend {
     // allocator has placed that GEMV's output on the attention output's memory
     float * shadow = nullptr;
     size_t shadow_size = 0;
+    // split decode attention: masked, scaled scores [B][n][H][P] and per-chunk maxima between the
+    // scores kernel and the softmax + P.V kernel (consumed by the very next launch on the stream)
+    float * attn_buf = nullptr;
+    size_t attn_floats = 0;
+    int attn_split_minp = 128;
+    // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
+    int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
+    int kv_prefetch_blocks = 128;
+    hipStream_t pf_stream = nullptr;
+    hipEvent_t pf_fork = nullptr, pf_join = nullptr;
     // tts_hip_tensor_set_async staging: a pinned ring; a region is reused once the event recorded
     // after its copy has completed (ggml_backend_i::set_tensor_async semantics: the caller may
     // reuse its buffer at once, the copy is ordered on the compute stream)
@@ -233,7 +253,7 @@ struct tts_hip_backend {
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
     bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
-    int fusion = 0x7FF;  // bitmask of TTS_FUSE_* patterns (all on)
+    int fusion = 0xFFF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -250,7 +270,9 @@ struct tts_hip_backend {
     hipGraphExec_t gexec = nullptr;
     hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;
-    int64_t lstm_chains = 0, lstm_steps = 0;  // fused LSTM recurrences launched (tts_hip_counters)
+    int64_t lstm_chains = 0, lstm_steps = 0;
+    int64_t plan_wait_ns = 0;
+    int64_t cap_plan_ns = 0, cap_launch_ns = 0, cap_update_ns = 0;  // capture_into phases (host)  // host time spent in graph_prepare waiting for the slot's previous launch  // fused LSTM recurrences launched (tts_hip_counters)
     // two prepared plans (tts_hip_graph_prepare / _launch): step n+1 is recorded while step n runs
     hipGraphExec_t pexec[2] = {nullptr, nullptr};
     tts_tensor * const * plan_nodes[2] = {nullptr, nullptr};

@@ -379,6 +379,170 @@ static void launch_attn_rows(tts_hip_backend * be, const AttnArgs & a, bool vvec
 }
 
 // ------------------------------------------------------------------------------------------
+// Split decode attention for long contexts (P >= be->attn_split_minp).  One workgroup per head
+// leaves most of the chip idle at decode batch sizes (Parler B = 8: 128 workgroups on 256 CUs) and
+// keeps too few bytes in flight per CU; the split runs the same arithmetic as k_attn_decode_rows
+// over many more workgroups, in two launches whose boundary is the softmax's global max:
+//   k_attn_scores: grid (P chunks, H, n*B): the masked, scaled scores w_i = f32(f32(q.K_i)*scale)
+//                  (+ mask) of 128*KS positions -> attn_buf, and the chunk's max;
+//   k_attn_pv:     grid (hd/16, H, n*B): every workgroup takes the global max from the chunk maxima,
+//                  recomputes e_i = expf(w_i - max) and the f64 sum over all P (cheap, L2-resident),
+//                  p_i = e_i * (1/sum), then 16 output dims of sum_i f32(p_i * V[d,i]) in f64.
+// Each output dim is still one workgroup's sum in one fixed order, and the V stream for that
+// workgroup is requested at kernel entry, before the softmax, so its latency hides under it.
+template <int DPR, int KS>
+__global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float * __restrict__ sbuf, int pstride,
+                                                             float * __restrict__ mxbuf, int nch) {
+    __shared__ float s_wf[ATTN_THREADS / 64];
+    constexpr int F = 4 * DPR;
+    const int c = blockIdx.x, h = blockIdx.y, z = blockIdx.z;
+    const int b = z / a.n, tq = z - b * a.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = lane & 3;
+    const int P = a.P;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const int64_t knb1 = a.k.nb[1];
+    const int i0 = c * 128 * KS + wave * 16 + (lane >> 2);
+    float4 kv[KS][F];
+#pragma unroll
+    for (int u = 0; u < KS; ++u) {
+        const int i = min(i0 + 128 * u, P - 1);
+#pragma unroll
+        for (int f = 0; f < F; ++f) kv[u][f] = *(const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + f));
+    }
+    float qv[F][4];
+#pragma unroll
+    for (int f = 0; f < F; ++f)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qv[f][e] = ((const float *)qbase)[16 * DPR * qd + 4 * f + e];
+    TTS_PIN_LOADS();
+    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < KS; ++u) {
+        double s = 0.0;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+            s += (double)__fmul_rn(kv[u][f].x, qv[f][0]);
+            s += (double)__fmul_rn(kv[u][f].y, qv[f][1]);
+            s += (double)__fmul_rn(kv[u][f].z, qv[f][2]);
+            s += (double)__fmul_rn(kv[u][f].w, qv[f][3]);
+        }
+        s += dpp_f64<DPP_XOR1>(s);
+        s += dpp_f64<DPP_XOR2>(s);
+        const int i = i0 + 128 * u;
+        if (i < P) {
+            float w = __fmul_rn((float)s, a.scale);
+            if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+            if (qd == 0) srow[i] = w;
+            mx = fmaxf(mx, w);
+        }
+    }
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    if (lane == 0) s_wf[wave] = mx;
+    __syncthreads();
+    if (tid == 0) {
+        float m = s_wf[0];
+#pragma unroll
+        for (int w = 1; w < ATTN_THREADS / 64; ++w) m = fmaxf(m, s_wf[w]);
+        mxbuf[((int64_t)z * a.H + h) * nch + c] = m;
+    }
+}
+
+constexpr int PV_THREADS = 256;
+
+template <bool VVEC, int UV>
+__global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float * __restrict__ sbuf, int pstride,
+                                                       const float * __restrict__ mxbuf, int nch) {
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    __shared__ double s_wd[PV_THREADS / 64];
+    constexpr int NW = PV_THREADS / 64;
+    const int h = blockIdx.y, z = blockIdx.z;
+    const int b = z / a.n, tq = z - b * a.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane >> 4, t = lane & 15;
+    const int P = a.P;
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const int64_t vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
+    const int d = blockIdx.x * 16 + wave * 4 + r;
+    const char * vrow = vbase + (int64_t)min(d, a.hd - 1) * vnb1;
+    const int ilast = ((P - 1) >> 2) << 2;
+    float4 w4[VVEC ? UV : 1];
+    float w1[VVEC ? 1 : UV];
+    auto load_v = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+            if (VVEC) w4[VVEC ? u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast));
+            else w1[VVEC ? 0 : u] = *(const float *)(vrow + (int64_t)min(k0 + 16 * u + t, P - 1) * vnb0);
+        }
+    };
+    load_v(0);  // in flight during the softmax
+    const float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
+    const float * mrow = mxbuf + ((int64_t)z * a.H + h) * nch;
+    float mx = -INFINITY;
+    for (int k = 0; k < nch; ++k) mx = fmaxf(mx, mrow[k]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += PV_THREADS) {
+        const float e = cr_expf(__fsub_rn(srow[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_f64(sum);
+    if (lane == 0) s_wd[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += s_wd[w];
+    const float inv = (float)(1.0 / sum);
+    const int P64 = (P + 63) & ~63;
+    for (int i = tid; i < P64; i += PV_THREADS) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    __syncthreads();
+
+    double acc = 0.0;
+    const int kstep = VVEC ? 64 * UV : 16 * UV;
+    for (int k0 = 0; k0 < P; k0 += kstep) {
+        if (k0 > 0) {
+            load_v(k0);
+            TTS_PIN_LOADS();
+        }
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+            if (VVEC) {
+                const int i = k0 + 64 * u + 4 * t;
+                const float4 pp = *(const float4 *)(s_p + min(i, P64 - 4));
+                const float4 vq = w4[VVEC ? u : 0];
+                acc += i + 0 < P ? (double)__fmul_rn(pp.x, vq.x) : 0.0;
+                acc += i + 1 < P ? (double)__fmul_rn(pp.y, vq.y) : 0.0;
+                acc += i + 2 < P ? (double)__fmul_rn(pp.z, vq.z) : 0.0;
+                acc += i + 3 < P ? (double)__fmul_rn(pp.w, vq.w) : 0.0;
+            } else {
+                const int i = k0 + 16 * u + t;
+                acc += i < P ? (double)__fmul_rn(s_p[min(i, P - 1)], w1[VVEC ? 0 : u]) : 0.0;
+            }
+        }
+    }
+    acc += dpp_f64<DPP_XOR1>(acc);
+    acc += dpp_f64<DPP_XOR2>(acc);
+    acc += dpp_f64<DPP_HALF_MIRROR>(acc);
+    acc += dpp_f64<DPP_MIRROR>(acc);
+    if (t == 0 && d < a.hd) {
+        const int64_t o = (((int64_t)b * a.n + tq) * a.H + h) * a.hd + d;
+        a.out[o] = (float)acc;
+        if (a.out2) a.out2[o] = (float)acc;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Short contexts (P <= 64: Parler's cross-attention over the T5 prompt encoding, n_enc = 3; the
 // first decode steps): one wave per (head, query, sequence), lane = key position, every sum in the
 // oracle's sequential order -- the q.K dot over d, the soft_max denominator over positions (lane 0
@@ -461,6 +625,49 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// KV prefetch into the memory-side Infinity Cache (MALL).  Decode attention streams the whole KV
+// cache of a layer once per step (Parler B = 8, P = 900: 59 MB); cold from HBM the row kernel
+// reaches about half the bandwidth it gets from MALL-resident data, while the GEMVs between two
+// attentions are latency-bound and leave HBM idle.  This kernel reads the K or V view of the NEXT
+// attention on a side stream during those GEMVs; the attention then hits the 256 MB MALL.  The
+// position written in this step (index P-1 along `pdim`) is never touched, so no cache level can
+// hold a stale copy of it; the rest of the cache was written by earlier steps.
+__global__ __launch_bounds__(256) void k_kv_prefetch(const char * __restrict__ base, int64_t n1, int64_t nb1, int64_t n2, int64_t nb2,
+                                                    int64_t n3, int64_t nb3, int cpr, unsigned * sink) {
+    const int64_t total = n1 * n2 * n3 * cpr;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    unsigned acc = 0;
+    for (int64_t c0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c0 < total; c0 += 4 * gs) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t c = min(c0 + u * gs, total - 1);
+            const int64_t r = c / cpr, k = c - r * cpr;
+            const int64_t i1 = r % n1, t = r / n1;
+            const int64_t i2 = t % n2, i3 = t / n2;
+            v[u] = *(const uint4 *)(base + i1 * nb1 + i2 * nb2 + i3 * nb3 + 16 * k);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x9E3779B9u && sink) *sink = acc;  // keeps the loads; practically never stores
+}
+
+// K view [hd, P, Hk, Bk] (pdim 1) or V view [P, hd, Hv, Bv] (pdim 0), f32, nb[0] == 4.
+void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int pdim, int blocks) {
+    if (t.nb[0] != 4 || ((uintptr_t)t.data) % 16) return;
+    const int64_t P = t.ne[pdim];
+    if (P < 2) return;
+    int64_t n1 = t.ne[1], row_bytes = t.ne[0] * 4;
+    if (pdim == 1) n1 = P - 1;
+    else row_bytes = (P - 1) * 4;
+    const int cpr = (int)(row_bytes / 16);  // whole 16-B chunks only (never the chunk holding P-1)
+    if (cpr <= 0 || (t.nb[1] % 16) || (t.nb[2] % 16) || (t.nb[3] % 16)) return;
+    hipLaunchKernelGGL(k_kv_prefetch, dim3((unsigned)blocks), dim3(256), 0, st, (const char *)t.data, n1, (int64_t)t.nb[1],
+                       t.ne[2], (int64_t)t.nb[2], t.ne[3], (int64_t)t.nb[3], cpr, (unsigned *)nullptr);
+}
+
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
                         float * out, int hd, int P, int H, int n, int B, float * out2) {
     AttnArgs a;
@@ -486,6 +693,27 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
         else hipLaunchKernelGGL(k_attn_small<128>, grid, dim3(64), 0, be->stream, a);
         TTS_HIP_CHECK(hipGetLastError());
         return;
+    }
+    if (krows && be->attn_split_minp > 0 && P >= be->attn_split_minp && P <= ATTN_MAXP && hd % 16 == 0) {
+        constexpr int KS = 2;
+        const int nch = (P + 128 * KS - 1) / (128 * KS);
+        const int pstride = (P + 63) & ~63;
+        const size_t rows = (size_t)H * n * B;
+        if (rows * ((size_t)pstride + nch) <= be->attn_floats) {
+            float * sbuf = be->attn_buf;
+            float * mxbuf = be->attn_buf + rows * pstride;
+            const dim3 g1((unsigned)nch, (unsigned)H, (unsigned)(n * B));
+            if (hd == 64) hipLaunchKernelGGL((k_attn_scores<1, KS>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            else hipLaunchKernelGGL((k_attn_scores<2, KS>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            TTS_HIP_CHECK(hipGetLastError());
+            const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
+                              (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
+            const dim3 g2((unsigned)(hd / 16), (unsigned)H, (unsigned)(n * B));
+            if (vvec) hipLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            else hipLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            TTS_HIP_CHECK(hipGetLastError());
+            return;
+        }
     }
     if (krows) {
         const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&

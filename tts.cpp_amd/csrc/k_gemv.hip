@@ -250,7 +250,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         constexpr int NP = (NCH + 3) / 4;
         constexpr bool PRE = NCH <= 4;
         const double Kd = (double)j.K;
-        const bool write = j.lnout && blockIdx.x == 0 && blockIdx.y == 0;
+        const bool write = j.lnout && blockIdx.x == 0;
         const float * lnb = j.lnb ? j.lnb : j.lnw;
         float wp[PRE ? NP : 1][16], bp[PRE ? NP : 1][16];
         if (PRE) {
@@ -335,6 +335,61 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
     }
 }
 
+// One Q4_K block of one (row, column) for lane l of an octet: aux32[l] from eight sdot4 with the
+// 6-bit scales, sumi from the mins and the per-32 Q8_K sums, then ggml's f32 combine
+// sums[l] += d*yd*aux32[l], sumf -= dmin*yd*sumi (vec_dot_q4_K_q8_K generic order).  `xb` is the
+// Q8_K block index in LDS; an invalid (padding) block leaves the accumulators unchanged.
+__device__ __forceinline__ void q4k_block(const u32x4 & h, const u32x4 & qw, const int8_t * xq_s, const int16_t * xs_s,
+                                          const float * xd_s, int xb, int l, bool valid, float & sums, float & sumf) {
+    const uint32_t A = h.y, B = h.z, C = h.w;
+    // 6-bit scales / mins of the eight 32-element sub-blocks, four per word (get_scale_min_k4)
+    const uint32_t sc_lo = A & 0x3F3F3F3Fu, mn_lo = B & 0x3F3F3F3Fu;
+    const uint32_t sc_hi = (C & 0x0F0F0F0Fu) | ((A >> 2) & 0x30303030u);
+    const uint32_t mn_hi = ((C >> 4) & 0x0F0F0F0Fu) | ((B >> 2) & 0x30303030u);
+    const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
+    const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
+    const uint32_t w0 = qw.x, w1 = qw.y, w2 = qw.z, w3 = qw.w;
+    // aux32[l] = sum_j scale_j * dot4_j; |dot4| <= 7620 and scale <= 63 fit the 24-bit multiplier
+    int aux = __mul24((int)(sc_lo & 0xFF), __builtin_amdgcn_sdot4((int)(w0 & 0x0F0F0F0Fu), xl.x, 0, false));
+    aux += __mul24((int)((sc_lo >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w0 >> 4) & 0x0F0F0F0Fu), xh.x, 0, false));
+    aux += __mul24((int)((sc_lo >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w1 & 0x0F0F0F0Fu), xl.y, 0, false));
+    aux += __mul24((int)(sc_lo >> 24), __builtin_amdgcn_sdot4((int)((w1 >> 4) & 0x0F0F0F0Fu), xh.y, 0, false));
+    aux += __mul24((int)(sc_hi & 0xFF), __builtin_amdgcn_sdot4((int)(w2 & 0x0F0F0F0Fu), xl.z, 0, false));
+    aux += __mul24((int)((sc_hi >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w2 >> 4) & 0x0F0F0F0Fu), xh.z, 0, false));
+    aux += __mul24((int)((sc_hi >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w3 & 0x0F0F0F0Fu), xl.w, 0, false));
+    aux += __mul24((int)(sc_hi >> 24), __builtin_amdgcn_sdot4((int)((w3 >> 4) & 0x0F0F0F0Fu), xh.w, 0, false));
+    // sumi = sum_j mins[j] * bsum32[j] (int16 pairs, v_dot2)
+    const int4 bs = *(const int4 *)(xs_s + xb * 8);
+    const int mn01 = (int)((mn_lo & 0xFF) | ((mn_lo & 0xFF00) << 8));
+    const int mn23 = (int)(((mn_lo >> 16) & 0xFF) | ((mn_lo >> 8) & 0xFF0000));
+    const int mn45 = (int)((mn_hi & 0xFF) | ((mn_hi & 0xFF00) << 8));
+    const int mn67 = (int)(((mn_hi >> 16) & 0xFF) | ((mn_hi >> 8) & 0xFF0000));
+    int sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn01), __builtin_bit_cast(short2_t, bs.x), 0, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn23), __builtin_bit_cast(short2_t, bs.y), sumi, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn45), __builtin_bit_cast(short2_t, bs.z), sumi, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn67), __builtin_bit_cast(short2_t, bs.w), sumi, false);
+    const float yd = xd_s[xb];
+    const float dw = dev_fp16_to_fp32((uint16_t)(h.x & 0xFFFF));
+    const float dmw = dev_fp16_to_fp32((uint16_t)(h.x >> 16));
+    const float ns = __fadd_rn(sums, __fmul_rn(__fmul_rn(dw, yd), (float)aux));
+    const float nf = __fsub_rn(sumf, __fmul_rn(__fmul_rn(dmw, yd), (float)sumi));
+    sums = valid ? ns : sums;
+    sumf = valid ? nf : sumf;
+}
+
+// sumf += sums[0..7] in order; lane l = 0 of the octet reads lane l = k by row_shl:k
+__device__ __forceinline__ float q4k_octet_total(float sumf, float sums) {
+    float tot = __fadd_rn(sumf, sums);
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 1>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 2>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 3>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 4>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 5>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 6>(sums));
+    tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 7>(sums));
+    return tot;
+}
+
 // ------------------------------------------------------------------------------------------
 // Q4_K x Q8_K GEMV on repacked weights, reproducing ggml_vec_dot_q4_K_q8_K's generic f32 order
 // exactly: per (row, column), blocks in ascending order, sums[l] += d*aux32[l] (l = 0..7),
@@ -406,52 +461,10 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
             for (int u = 0; u < NBMAX; ++u) {  // branch-free: padding blocks compute and are discarded
                 const bool valid = b0 + u < nb;
                 const int b = min(b0 + u, nb - 1);
-                const uint32_t A = hdr[u].y, B = hdr[u].z, C = hdr[u].w;
-                // 6-bit scales / mins of the eight 32-element sub-blocks, four per word (get_scale_min_k4)
-                const uint32_t sc_lo = A & 0x3F3F3F3Fu, mn_lo = B & 0x3F3F3F3Fu;
-                const uint32_t sc_hi = (C & 0x0F0F0F0Fu) | ((A >> 2) & 0x30303030u);
-                const uint32_t mn_hi = ((C >> 4) & 0x0F0F0F0Fu) | ((B >> 2) & 0x30303030u);
-                const int xb = m * nb + b;
-                const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
-                const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
-                const uint32_t w0 = q[u].x, w1 = q[u].y, w2 = q[u].z, w3 = q[u].w;
-                // aux32[l] = sum_j scale_j * dot4_j; |dot4| <= 7620 and scale <= 63 fit the 24-bit multiplier
-                int aux = __mul24((int)(sc_lo & 0xFF), __builtin_amdgcn_sdot4((int)(w0 & 0x0F0F0F0Fu), xl.x, 0, false));
-                aux += __mul24((int)((sc_lo >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w0 >> 4) & 0x0F0F0F0Fu), xh.x, 0, false));
-                aux += __mul24((int)((sc_lo >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w1 & 0x0F0F0F0Fu), xl.y, 0, false));
-                aux += __mul24((int)(sc_lo >> 24), __builtin_amdgcn_sdot4((int)((w1 >> 4) & 0x0F0F0F0Fu), xh.y, 0, false));
-                aux += __mul24((int)(sc_hi & 0xFF), __builtin_amdgcn_sdot4((int)(w2 & 0x0F0F0F0Fu), xl.z, 0, false));
-                aux += __mul24((int)((sc_hi >> 8) & 0xFF), __builtin_amdgcn_sdot4((int)((w2 >> 4) & 0x0F0F0F0Fu), xh.z, 0, false));
-                aux += __mul24((int)((sc_hi >> 16) & 0xFF), __builtin_amdgcn_sdot4((int)(w3 & 0x0F0F0F0Fu), xl.w, 0, false));
-                aux += __mul24((int)(sc_hi >> 24), __builtin_amdgcn_sdot4((int)((w3 >> 4) & 0x0F0F0F0Fu), xh.w, 0, false));
-                // sumi = sum_j mins[j] * bsum32[j] (int16 pairs, v_dot2)
-                const int4 bs = *(const int4 *)(xs_s + xb * 8);
-                const int mn01 = (int)((mn_lo & 0xFF) | ((mn_lo & 0xFF00) << 8));
-                const int mn23 = (int)(((mn_lo >> 16) & 0xFF) | ((mn_lo >> 8) & 0xFF0000));
-                const int mn45 = (int)((mn_hi & 0xFF) | ((mn_hi & 0xFF00) << 8));
-                const int mn67 = (int)(((mn_hi >> 16) & 0xFF) | ((mn_hi >> 8) & 0xFF0000));
-                int sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn01), __builtin_bit_cast(short2_t, bs.x), 0, false);
-                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn23), __builtin_bit_cast(short2_t, bs.y), sumi, false);
-                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn45), __builtin_bit_cast(short2_t, bs.z), sumi, false);
-                sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, mn67), __builtin_bit_cast(short2_t, bs.w), sumi, false);
-                const float yd = xd_s[xb];
-                const float dw = dev_fp16_to_fp32((uint16_t)(hdr[u].x & 0xFFFF));
-                const float dmw = dev_fp16_to_fp32((uint16_t)(hdr[u].x >> 16));
-                const float ns = __fadd_rn(sums, __fmul_rn(__fmul_rn(dw, yd), (float)aux));
-                const float nf = __fsub_rn(sumf, __fmul_rn(__fmul_rn(dmw, yd), (float)sumi));
-                sums = valid ? ns : sums;
-                sumf = valid ? nf : sumf;
+                q4k_block(hdr[u], q[u], xq_s, xs_s, xd_s, m * nb + b, l, valid, sums, sumf);
             }
         }
-        // sumf += sums[0..7] in order; lane l = 0 of the octet reads lane l = k by row_shl:k
-        float tot = __fadd_rn(sumf, sums);
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 1>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 2>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 3>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 4>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 5>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 6>(sums));
-        tot = __fadd_rn(tot, dpp_f32<DPP_ROW_SHL0 + 7>(sums));
+        const float tot = q4k_octet_total(sumf, sums);
         const int64_t flat0 = g * S;
         const int mat = mat_of(flat0);
         const int64_t row = flat0 - (int64_t)mat * j.N + s;
@@ -460,6 +473,117 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
         if (g + gstride < G) load_row(g + gstride, 0);
     }
     TTS_TS(j, 5);
+}
+
+// Cross-attention query GEMV + attention in one launch (Parler model.cpp:583-594: q = W_q
+// LN(x), then cont(K) -> mul_mat -> soft_max_ext -> mul_mat(V) -> permute -> cont over the n_enc
+// encoder positions).  Workgroup (h, b) owns head h of prompt b: 8 waves x 8 rows = the head's 64
+// query rows for column b alone (MC = 1 lane mapping: row slot s = lane >> 3, residue l = lane & 7),
+// with the LN / Q8_K prologue of that one column.  The 64 query values go to LDS and the last wave
+// runs the short-context attention of k_attn_small<64> on them (lane = key position, every sum in
+// the oracle's sequential order).  Each value is computed exactly as by the two separate launches
+// (same per-(row, column) Q4_K order, same attention arithmetic), so the result is bit-identical;
+// the launch and the attention kernel's whole latency chain disappear.  The attention's K, V and
+// mask are requested at kernel entry, next to the weight rows.
+template <int PRO>
+__global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) {
+    constexpr int HD = 64, NW = 8, F = HD / 4, VB = 8;
+    __shared__ __attribute__((aligned(16))) int8_t xq_s[5 * QK_K];  // nb <= 4 blocks + trash slot
+    __shared__ float xd_s[8];
+    __shared__ __attribute__((aligned(16))) int16_t xs_s[5 * 8];
+    __shared__ float s_q[HD];
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l = lane & 7, s = lane >> 3;
+    const int nb = (int)(j.K / QK_K);
+    GemvJob jb = j;  // this workgroup's column
+    jb.M = 1;
+    jb.x = j.x + (int64_t)b * j.xcs;
+    jb.lnout = j.lnout && h == 0 ? j.lnout + (int64_t)b * j.locs : nullptr;
+    const int64_t row = (int64_t)h * HD + wave * 8 + s;
+    const uint8_t * wr = j.W[0] + row * j.w_row_bytes;
+    u32x4 hdr[4], q[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t bo = (int64_t)min(u, nb - 1) * 144;
+        hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
+        q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
+    }
+    // attention operands for the last wave (position p = lane)
+    const int P = a.P;
+    const int p = min(lane, P - 1);
+    float4 kr[F];
+    float vv[VB];
+    float mk = 0.f;
+    const int bk = b / (a.B / (int)a.k.ne[3]), bv = b / (a.B / (int)a.v.ne[3]);  // K/V shared across prompts or not
+    const char * kbase = a.k.data + (int64_t)h * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * vbase = a.v.data + (int64_t)h * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    if (wave == NW - 1) {
+#pragma unroll
+        for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+#pragma unroll
+        for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
+        if (a.mask) mk = a.mask[p];
+    }
+    TTS_PIN_LOADS();
+    q4k_prologue<PRO, 4>(jb, nb, xq_s, xd_s, xs_s);
+    __syncthreads();
+    float sums = 0.f, sumf = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q4k_block(hdr[u], q[u], xq_s, xs_s, xd_s, min(u, nb - 1), l, u < nb, sums, sumf);
+    const float tot = q4k_octet_total(sumf, sums);
+    if (l == 0) s_q[wave * 8 + s] = tot;
+    __syncthreads();
+    if (wave != NW - 1) return;
+    // ---- k_attn_small<64> on (h, b) with q from LDS ----
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < F; ++c) {
+        acc += (double)__fmul_rn(kr[c].x, s_q[4 * c + 0]);
+        acc += (double)__fmul_rn(kr[c].y, s_q[4 * c + 1]);
+        acc += (double)__fmul_rn(kr[c].z, s_q[4 * c + 2]);
+        acc += (double)__fmul_rn(kr[c].w, s_q[4 * c + 3]);
+    }
+    float w = __fmul_rn((float)acc, a.scale);
+    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, mk));
+    if (lane >= P) w = -INFINITY;
+    float mx = w;
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    const float e = lane < P ? cr_expf(__fsub_rn(w, mx)) : 0.f;
+    double sum = 0.0;
+    for (int i = 0; i < P; ++i) sum += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), i));
+    const float pr = __fmul_rn(e, (float)(1.0 / sum));
+    double o = 0.0;
+    for (int i0 = 0; i0 < P; i0 += VB) {
+        if (i0 > 0) {
+#pragma unroll
+            for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(i0 + u, P - 1) * a.v.nb[0]);
+            TTS_PIN_LOADS();
+        }
+#pragma unroll
+        for (int u = 0; u < VB; ++u) {
+            if (i0 + u >= P) break;
+            const float pi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), i0 + u));
+            o += (double)__fmul_rn(pi, vv[u]);
+        }
+    }
+    const int64_t orow = ((int64_t)b * a.H + h) * HD;
+    a.out[orow + lane] = (float)o;
+    if (a.out2) a.out2[orow + lane] = (float)o;
+}
+
+// Host checks (caller): Q4_K repacked weights, one matrix of N = H * 64 rows, K <= 1024, M = B
+// columns with 16-B aligned, 16-B strided x; K rows 16-B vectors; P <= 64.
+void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnArgs & a) {
+    const dim3 grid((unsigned)a.H, (unsigned)a.B);
+    if (j.pro == PRO_LN) hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_LN>, grid, dim3(512), 0, be->stream, j, a);
+    else hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_QUANT>, grid, dim3(512), 0, be->stream, j, a);
+    TTS_HIP_CHECK(hipGetLastError());
 }
 
 // Q8_0 x Q8_0 GEMV reproducing ggml_vec_dot_q8_0_q8_0's generic order: per (row, column),

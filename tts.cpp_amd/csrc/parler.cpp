@@ -671,6 +671,12 @@ extern "C" int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset
 extern "C" int32_t tts_parler_last_graph_nodes(const tts_parler * p) { return p->last_nodes; }
 extern "C" uint64_t tts_parler_weight_bytes(const tts_parler * p) { return p->wbytes; }
 
+// The last step graph's node list (valid until the next step is prepared), e.g. for tts_hip_plan_stats.
+extern "C" tts_tensor * const * tts_parler_graph(const tts_parler * p, int32_t * n_nodes) {
+    if (n_nodes) *n_nodes = p ? (int32_t)p->gctx.nodes.size() : 0;
+    return p ? p->gctx.nodes.data() : nullptr;
+}
+
 // Debug: node i of the last step graph -> op, type, ne[4]; copies its bytes if contiguous and cap fits.
 extern "C" uint64_t tts_parler_node(tts_parler * p, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap) {
     if (i < 0 || i >= (int32_t)p->gctx.nodes.size()) return 0;

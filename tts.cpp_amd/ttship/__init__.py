@@ -21,9 +21,13 @@ OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "
        "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
-FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024}
+FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048}
 FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
+
+# tts_hip_option ids (include/tts_hip.h)
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7}
+ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 
 TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
 BLCK_SIZE = {F32: 1, F16: 1, Q4_K: 256, Q8_0: 32, I32: 1}
@@ -192,6 +196,7 @@ def lib():
         "tts_parler_position": (i32, [vp]),
         "tts_parler_host_stats": (i64, [vp, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "tts_parler_last_graph_nodes": (i32, [vp]),
+        "tts_parler_graph": (vp, [vp, ctypes.POINTER(i32)]),
         "tts_parler_weight_bytes": (u64, [vp]),
         "tts_parler_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
         "tts_parler_node": (u64, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i64), vp, u64]),
@@ -275,10 +280,11 @@ class HipBackend:
         return ms.value, n.value, b.value
 
     def counters(self):
-        """{graph_updates, graph_instantiations, lstm_chains, lstm_steps} since creation."""
-        out = (ctypes.c_int64 * 4)()
-        n = self.L.tts_hip_counters(self.ptr, out, 4)
-        keys = ("graph_updates", "graph_instantiations", "lstm_chains", "lstm_steps")
+        """{graph_updates, graph_instantiations, lstm_chains, lstm_steps, plan_wait_ns} since creation."""
+        out = (ctypes.c_int64 * 8)()
+        n = self.L.tts_hip_counters(self.ptr, out, 8)
+        keys = ("graph_updates", "graph_instantiations", "lstm_chains", "lstm_steps", "plan_wait_ns",
+                "cap_plan_ns", "cap_launch_ns", "cap_update_ns")
         return {keys[i]: int(out[i]) for i in range(n)}
 
     def close(self):
@@ -347,6 +353,12 @@ class Parler:
 
     def last_graph_nodes(self):
         return self.L.tts_parler_last_graph_nodes(self.ptr)
+
+    def plan_stats(self, mask=None):
+        """Fusion coverage of the last step graph (no device needed)."""
+        n = ctypes.c_int32()
+        p = self.L.tts_parler_graph(self.ptr, ctypes.byref(n))
+        return plan_stats(p, n.value, FUSE_ALL if mask is None else mask)
 
     def host_stats(self, reset=True):
         """Mean host microseconds per step: build, alloc, set_inputs, compute enqueue, logits wait."""
@@ -531,5 +543,6 @@ def plan_stats(nodes_ptr, n_nodes, mask):
     counts = (ctypes.c_int32 * 16)()
     lib().tts_hip_plan_stats(nodes_ptr, n_nodes, mask, counts)
     out = {k: int(counts[i]) for i, k in enumerate(PLAN_KINDS)}
+    out["xattn"] = int(counts[14])
     out["unfused"] = int(counts[15])
     return out
