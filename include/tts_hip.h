@@ -135,6 +135,8 @@ enum tts_status {
 #define TTS_FLAG_OUTPUT 4
 #define TTS_FLAG_PERSIST 8
 #define TTS_FLAG_REPACKED 16 /* set by the HIP backend: the tensor is stored in its Q4_K lane layout */
+#define TTS_FLAG_TILED 32    /* set by the HIP backend: Q4_K stored in its 4-row tile layout (tts_repack_q4_K_tiled),
+                                read by the matrix-core GEMV (large matrices, tts_hip_weight_set) */
 
 /* Plain mirror of the ggml_tensor fields a backend reads.  `data` is a device pointer for
  * tensors handed to tts_hip_* (a host pointer for the CPU oracle in oracle/).  op_params hold
@@ -192,6 +194,11 @@ int tts_hip_weight_set(tts_hip_backend_t backend, tts_tensor * t, const void * s
 int tts_hip_weight_get(tts_hip_backend_t backend, const tts_tensor * t, void * dst_host);
 /* Host helper: (inverse = 0) ggml Q4_K blocks -> backend lane layout, (1) the reverse. */
 void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse);
+/* The 4-row tile layout of a Q4_K matrix [nrows][nb blocks] (nrows % 4 == 0): per (tile t of rows
+ * 4t..4t+3, block b) 576 bytes at (t*nb + b)*576: the four 16-B block headers (d, dmin, scales),
+ * then for chunk c = 0..3, half h = 0..1, row i = 0..3 a 16-B piece whose dword l' holds the bytes
+ * qs[32c + 8kk + 4h + l'] (kk = 0..3) -- one lane's MFMA operand for residues 4h..4h+3. */
+void tts_repack_q4_K_tiled(const void * src, void * dst, int64_t nrows, int64_t nb, int inverse);
 
 int tts_hip_supports_op(const tts_tensor * node);
 int tts_hip_graph_compute(tts_hip_backend_t backend, tts_tensor * const * nodes, int n_nodes);
@@ -212,7 +219,10 @@ enum tts_hip_option {
                                      (scores, then softmax + P.V); 0 = always the one-workgroup-per-head kernel */
     TTS_HIP_OPT_KV_PREFETCH = 6,  /* prefetch the next decode attention's K/V (KV length >= value) into the
                                      Infinity Cache on a side stream during the GEMVs before it; 0 = off */
-    TTS_HIP_OPT_KV_PREFETCH_BLOCKS = 7 /* workgroups of the prefetch kernel (default 128) */
+    TTS_HIP_OPT_KV_PREFETCH_BLOCKS = 7, /* workgroups of the prefetch kernel (default 128) */
+    TTS_HIP_OPT_Q4K_TILE_BYTES = 8 /* tts_hip_weight_set stores Q4_K matrices of >= value bytes (ne1 % 4 == 0) in the
+                                     4-row tile layout; their GEMVs run on the matrix-core kernel (exact integer f16
+                                     MFMAs, bit-identical).  Default 4 MiB; 0 = never */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
@@ -243,6 +253,9 @@ int tts_hip_counters(tts_hip_backend_t backend, int64_t * out, int n);
  * Q4_K weights must already be in the backend lane layout (tts_repack_q4_K). */
 int tts_hip_gemv(tts_hip_backend_t backend, int type, const void * w, const float * x, float * y,
                  int64_t K, int64_t N, int64_t M);
+/* As tts_hip_gemv for a weight stored with tts_tensor flags `wflags` (TTS_FLAG_TILED: the tile layout). */
+int tts_hip_gemv_ex(tts_hip_backend_t backend, int type, const void * w, const float * x, float * y,
+                    int64_t K, int64_t N, int64_t M, int32_t wflags);
 
 /* ---- generic backend vtable: lets the same C++ runners target the HIP backend or the CPU oracle
  * (the latter lives in oracle/ and is only linked by tests and bench.py's cpu_baseline leg). ---- */

@@ -72,6 +72,48 @@ uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint
 /* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
 uint64_t tts_parler_node(tts_parler * p, int32_t i, int32_t * op, int32_t * type, int64_t * ne, void * dst, uint64_t cap);
 
+/* Orpheus-3B decoder config (defaults = orpheus_model, src/models/orpheus/model.h:31-46; rope
+ * factors from Llama-3.2 rope scaling as py-gguf/tts_encoders/orpheus_gguf_encoder.py:144-173). */
+typedef struct tts_orpheus_config {
+    int32_t n_layers;         /* 28 */
+    int32_t hidden_size;      /* 3072 */
+    int32_t n_attn_heads;     /* 24 */
+    int32_t n_kv_attn_heads;  /* 8 (K/V stored repeat-interleaved x3, orpheus_build_kv_store) */
+    int32_t head_size;        /* 128 */
+    int32_t ffn_size;         /* 8192 */
+    int32_t vocab_size;       /* 156940 */
+    int32_t max_ctx;          /* 1024 + 2100 (KV capacity) */
+    int32_t weight_type;      /* TTS_TYPE_Q4_K for config 5 (all matrices incl. embedding and head) */
+    int32_t batch;            /* independent prompts stepped in lockstep (1 = reference graph) */
+    uint64_t seed;            /* synthetic weight seed base (0x5EED) */
+    uint64_t arena_bytes;     /* compute arena (0 = default 512 MiB) */
+    float rope_theta;         /* 500000 */
+    float rope_factor;        /* 32 */
+    float rope_low_freq_factor;   /* 1 */
+    float rope_high_freq_factor;  /* 4 */
+    int32_t rope_original_ctx;    /* 8192 */
+    int32_t pad_;
+} tts_orpheus_config;
+
+typedef struct tts_orpheus tts_orpheus;
+
+void tts_orpheus_default_config(tts_orpheus_config * cfg);
+tts_orpheus * tts_orpheus_create(const tts_backend_iface * be, const tts_orpheus_config * cfg);
+void tts_orpheus_free(tts_orpheus * p);
+void tts_orpheus_reset(tts_orpheus * p);
+/* Prompt pass (orpheus_runner::decode over batch_from_sentence): tokens [batch][n]; logits of the last
+ * token [batch][vocab] when `logits` is not NULL. */
+int tts_orpheus_prefill(tts_orpheus * p, const int32_t * tokens, int32_t n, float * logits);
+/* One AR step: tokens [batch] -> logits [batch][vocab]. */
+int tts_orpheus_decode(tts_orpheus * p, const int32_t * tokens, float * logits);
+/* Greedy loop (generate_from_batch, sampler::max): feeds first_tokens [batch], then each step's samples;
+ * writes tokens [batch][n_steps].  Samples stay on the device when the backend offers greedy_step. */
+int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_tokens, int32_t n_steps, int32_t * tokens_out);
+int32_t tts_orpheus_position(const tts_orpheus * p);
+int32_t tts_orpheus_last_graph_nodes(const tts_orpheus * p);
+uint64_t tts_orpheus_weight_bytes(const tts_orpheus * p);
+tts_tensor * const * tts_orpheus_graph(const tts_orpheus * p, int32_t * n_nodes);
+
 /* DAC decoder (codec tokens -> PCM): dac_runner::run / build_dac_graph,
  * /root/reference/src/decoder/dac_model.cpp:139-212.  Defaults = DAC 44.1 kHz as used by
  * Parler-TTS mini v1 (9 codebooks x 1024 x 8, latent 1024, decoder 1536, rates 8,8,4,2: 512

@@ -27,10 +27,15 @@ SHAPES = [  # (name, type, K, N)
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    mlist = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 8]
+    tiled = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # 1: Q4_K in the tile layout (matrix-core kernel)
+    only = sys.argv[4].split(",") if len(sys.argv) > 4 else None
     hip = ttship.HipBackend(0)
     L = ttship.lib()
     rng = np.random.default_rng(0)
     for name, wt, K, N in SHAPES:
+        if only and name not in only:
+            continue
         wbytes = ttship.row_size(wt, K) * N
         w = rng.integers(0, 256, size=wbytes, dtype=np.uint8)
         if wt == ttship.Q4_K:  # keep d/dmin finite: small fp16 in the block headers
@@ -42,25 +47,30 @@ def main():
             blk[:, 0:2] = np.frombuffer(np.float16(1e-3).tobytes(), dtype=np.uint8)
         else:
             w = (rng.standard_normal(K * N).astype(np.float32) * 0.02).view(np.uint8)
+        flags = 0
+        if tiled and wt == ttship.Q4_K:  # random bytes are valid in any layout; only the flag matters
+            flags = 32
+            if N % 4:
+                continue
         dw = hip.alloc(w.nbytes)
         hip.set(dw, w)
-        for M in (1, 8):
+        for M in mlist:
             x = rng.standard_normal((M, K)).astype(np.float32)
             dx = hip.alloc(x.nbytes)
             dy = hip.alloc(4 * M * N)
             hip.set(dx, x)
             for _ in range(3):
-                L.tts_hip_gemv(hip.ptr, wt, dw, dx, dy, K, N, M)
+                L.tts_hip_gemv_ex(hip.ptr, wt, dw, dx, dy, K, N, M, flags)
             hip.sync()
             hip.set_option(1, 1)
             hip.gemv_stats(-1, reset=True)
             for _ in range(reps):
-                L.tts_hip_gemv(hip.ptr, wt, dw, dx, dy, K, N, M)
+                L.tts_hip_gemv_ex(hip.ptr, wt, dw, dx, dy, K, N, M, flags)
             ms, n, nbytes = hip.gemv_stats(wt, reset=True)
             hip.set_option(1, 0)
             us = 1000.0 * ms / n
             print(json.dumps({"shape": name, "type": ttship.lib().tts_type_name(wt).decode(), "K": K, "N": N, "M": M,
-                              "weight_MB": round(wbytes / 1e6, 3), "avg_us": round(us, 2),
+                              "weight_MB": round(wbytes / 1e6, 3), "tiled": bool(tiled and wt == ttship.Q4_K), "avg_us": round(us, 2),
                               "GBps": round(nbytes / n / (us * 1e-6) / 1e9, 1)}), flush=True)
             hip.free(dx)
             hip.free(dy)

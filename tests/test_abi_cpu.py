@@ -144,3 +144,29 @@ def test_no_device_is_reported_not_faked():
         pytest.skip("a HIP device is visible")
     with pytest.raises(RuntimeError):
         ttship.HipBackend(0)
+
+
+def test_repack_q4_K_tiled_roundtrip_and_layout():
+    """4-row tile layout (include/tts_hip.h): per (tile, block) 576 B = 4 headers, then 16-B pieces
+    (chunk c, half h, row i) whose dword l' holds qs[32c + 8kk + 4h + l'], kk = 0..3."""
+    L = ttship.lib()
+    rng = np.random.default_rng(11)
+    N, nb = 12, 3
+    src = rng.integers(0, 256, size=N * nb * 144, dtype=np.uint8)
+    til = np.empty_like(src)
+    back = np.empty_like(src)
+    L.tts_repack_q4_K_tiled(src.ctypes.data, til.ctypes.data, N, nb, 0)
+    L.tts_repack_q4_K_tiled(til.ctypes.data, back.ctypes.data, N, nb, 1)
+    assert np.array_equal(back, src)
+    s = src.reshape(N, nb, 144)
+    t = til.reshape(N // 4, nb, 576)
+    for row in range(N):
+        for b in range(nb):
+            g, i = t[row // 4, b], row % 4
+            assert np.array_equal(g[i * 16:i * 16 + 16], s[row, b, :16])
+            for c in range(4):
+                for h in range(2):
+                    piece = g[64 + ((c * 2 + h) * 4 + i) * 16:][:16]
+                    for lp in range(4):
+                        for kk in range(4):
+                            assert piece[lp * 4 + kk] == s[row, b, 16 + 32 * c + 8 * kk + 4 * h + lp]

@@ -85,3 +85,61 @@ def test_float(hip, wtype, K, N, M):
     got = run_gpu(hip, wtype, w.view(np.uint8), x, N)
     # f64 accumulation on both sides: agreement to the final f32 rounding
     helpers.assert_close_scaled(got, ref, magnitude(w.astype(np.float32), x), 1e-7, "float")
+
+
+MF_SHAPES = [(1024, 1024), (256, 4), (1024, 1000), (3072, 2048), (8192, 512), (4096, 1024), (3072, 8192)]
+
+
+def run_gpu_tiled(hip, w, x, N):
+    """Raw GEMV on a weight in the backend's 4-row tile layout (the matrix-core kernel)."""
+    M, K = x.shape
+    w = np.ascontiguousarray(w, dtype=np.uint8)
+    tl = np.empty_like(w)
+    ttship.lib().tts_repack_q4_K_tiled(w.ctypes.data, tl.ctypes.data, N, K // 256, 0)
+    dw = hip.alloc(tl.nbytes)
+    dx = hip.alloc(x.nbytes)
+    dy = hip.alloc(4 * M * N)
+    try:
+        hip.set(dw, tl)
+        hip.set(dx, x)
+        assert ttship.lib().tts_hip_gemv_ex(hip.ptr, ttship.Q4_K, dw, dx, dy, K, N, M, 32) == 0  # TTS_FLAG_TILED
+        y = np.empty((M, N), dtype=np.float32)
+        hip.get(y, dy)
+        return y
+    finally:
+        hip.free(dw)
+        hip.free(dx)
+        hip.free(dy)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N", MF_SHAPES)
+@pytest.mark.parametrize("M", [1, 2, 5, 8, 16, 19])
+def test_q4_K_mfma(hip, K, N, M):
+    """Matrix-core Q4_K path (k_gemv_q4K_mf on the tile layout): the integer block dots run as f16
+    MFMAs whose sums are exact integers, so the result is bit-identical to ggml's order."""
+    rng = np.random.default_rng(K * 5 + N + 3 * M)
+    w = helpers.rand_q4_K(rng, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+    got = run_gpu_tiled(hip, w, x, N)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+
+
+@pytest.mark.gpu
+def test_q4_K_mfma_extreme_blocks(hip):
+    """Largest integer sums the MFMA path must keep exact: all scales / mins 63, nibbles 15, and
+    activations quantized to +-127 (|aux32| up to 3.84e6, bsum up to 4064)."""
+    K, N, M = 1024, 64, 4
+    rng = np.random.default_rng(7)
+    w = helpers.rand_q4_K(rng, N, K)
+    blk = w.reshape(-1, 144)
+    blk[:, 4:16] = 0xFF               # every 6-bit scale and min = 63
+    blk[: len(blk) // 2, 16:] = 0xFF  # nibbles 15
+    x = np.full((M, K), 3.0, dtype=np.float32)
+    x[1] = -3.0
+    x[2, ::2] = -1.0
+    x[3] = rng.standard_normal(K).astype(np.float32)
+    ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+    got = run_gpu_tiled(hip, w, x, N)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()

@@ -1,0 +1,59 @@
+"""Orpheus-3B decoder parity: the HIP backend vs the CPU oracle on the same graph
+(build_orpheus_graph, src/models/orpheus/model.cpp:230-311).
+
+Bars (BASELINE.json north_star): greedy (sampler::max) token ids bit-exact; logits within
+1e-4 * max|logit| + 1e-4 (the only f32 differences are reduction orders outside ggml's exact paths).
+"""
+import numpy as np
+import pytest
+
+import py_oracle
+import ttship
+
+TINY = dict(n_layers=2, hidden_size=256, n_attn_heads=4, n_kv_attn_heads=2, head_size=64, ffn_size=512,
+            vocab_size=1000, max_ctx=48)
+# real Orpheus widths (3072 / 24 x 128 / 8 KV heads / 8192 / 156 940 vocab), two layers
+WIDE = dict(n_layers=2, max_ctx=32)
+
+
+def run_pair(hip, cfg_kw, batch, n_prompt, n_gen, tile_bytes=None):
+    if tile_bytes is not None:
+        hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], tile_bytes)
+    try:
+        g = ttship.Orpheus(hip.iface(), ttship.orpheus_config(batch=batch, **cfg_kw))
+    finally:
+        hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], 4 << 20)
+    c = ttship.Orpheus(py_oracle.iface(16), ttship.orpheus_config(batch=batch, **cfg_kw))
+    try:
+        V = c.cfg.vocab_size
+        prompt = (np.arange(n_prompt * batch, dtype=np.int32).reshape(batch, n_prompt) * 7919 + 3) % V
+        lg, lc = g.prefill(prompt), c.prefill(prompt)
+        tol = 1e-4 * np.abs(lc).max() + 1e-4
+        assert np.abs(lg - lc).max() <= tol, np.abs(lg - lc).max()
+        first = lc.argmax(axis=1).astype(np.int32)
+        assert np.array_equal(lg.argmax(axis=1), first)
+        tg, tc = g.generate(first, n_gen), c.generate(first, n_gen)
+        assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
+        dg, dc = g.decode(tg[:, -1]), c.decode(tc[:, -1])
+        assert np.abs(dg - dc).max() <= 1e-4 * np.abs(dc).max() + 1e-4
+    finally:
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 3])
+def test_orpheus_tiny(hip, batch):
+    run_pair(hip, TINY, batch, 6, 10)
+
+
+@pytest.mark.gpu
+def test_orpheus_tiny_all_tiled(hip):
+    """Every Q4_K matrix (embedding and head included) in the tile layout: matrix-core GEMVs."""
+    run_pair(hip, TINY, 2, 5, 8, tile_bytes=1)
+
+
+@pytest.mark.gpu
+def test_orpheus_wide_two_layers(hip):
+    """Full Orpheus widths (tile-layout GEMVs for q/o/gate/up/down and the 156 940-row head)."""
+    run_pair(hip, WIDE, 2, 4, 3)

@@ -58,6 +58,28 @@ def test_full_parler_mini_q4k_tokens(hip):
 
 
 @pytest.mark.gpu
+def test_full_parler_mini_q4k_tokens_mfma(hip):
+    """Full Parler-mini at batch 3 with every Q4_K matrix in the tile layout: all GEMVs (LN /
+    quantize prologues, grouped q/k/v with KV-store epilogues, GELU / residual epilogues) on the
+    matrix-core kernel, cross-attention unfused, embeddings gathered from tiled tables."""
+    hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], 1)  # every Q4_K matrix (and embedding table) tiled
+    try:
+        g, c = make_pair(hip, batch=3)
+    finally:
+        hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], 4 << 20)
+    try:
+        prompt = np.array([[11, 29, 400, 7, 1, 3000, 16], [5, 6, 7, 8, 9, 10, 11], [1, 1, 2, 3, 5, 8, 13]], dtype=np.int32)
+        g.prefill(prompt)
+        c.prefill(prompt)
+        tg = g.generate(6)
+        tc = c.generate(6)
+        assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
+    finally:
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("device_sampling", [True, False])
 def test_generate_in_chunks_and_sampling_paths(hip, device_sampling):
     """generate(5) + generate(7) on the HIP runner (device-resident greedy loop or host sampling)

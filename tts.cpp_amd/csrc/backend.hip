@@ -222,6 +222,32 @@ void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse)
     }
 }
 
+void tts_repack_q4_K_tiled(const void * src, void * dst, int64_t nrows, int64_t nb, int inverse) {
+    const uint8_t * s = (const uint8_t *)src;
+    uint8_t * d = (uint8_t *)dst;
+    const int64_t rb = nb * 144;
+    for (int64_t row = 0; row < nrows; ++row) {
+        const int64_t t = row >> 2, i = row & 3;
+        for (int64_t b = 0; b < nb; ++b) {
+            const int64_t nat = row * rb + b * 144;           // native block
+            const int64_t til = (t * nb + b) * 576;           // tile-layout block group
+            const uint8_t * a = inverse ? s + til : s + nat;  // source side
+            uint8_t * o = inverse ? d + nat : d + til;
+            if (!inverse) memcpy(o + i * 16, a, 16);
+            else memcpy(o, a + i * 16, 16);
+            for (int c = 0; c < 4; ++c)
+                for (int h = 0; h < 2; ++h)
+                    for (int lp = 0; lp < 4; ++lp)
+                        for (int kk = 0; kk < 4; ++kk) {
+                            const int64_t tpos = 64 + ((c * 2 + h) * 4 + i) * 16 + lp * 4 + kk;
+                            const int64_t npos = 16 + 32 * c + 8 * kk + 4 * h + lp;
+                            if (!inverse) o[tpos] = a[npos];
+                            else o[npos] = a[tpos];
+                        }
+        }
+    }
+}
+
 static size_t tensor_bytes(const tts_tensor * t) {
     size_t n = tts_row_size(t->type, t->ne[0]);
     for (int i = 1; i < 4; ++i) n *= (size_t)t->ne[i];
@@ -231,6 +257,15 @@ static size_t tensor_bytes(const tts_tensor * t) {
 int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
     if (!be || !t) return TTS_STATUS_BAD_ARG;
     const size_t n = tensor_bytes(t);
+    if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0 && t->ne[1] % 4 == 0 && t->ne[2] == 1 && t->ne[3] == 1 &&
+        be->q4k_tile_bytes > 0 && (int64_t)n >= be->q4k_tile_bytes) {
+        // large matrix: the matrix-core GEMV's tile layout
+        std::vector<uint8_t> tmp(n);
+        tts_repack_q4_K_tiled(src, tmp.data(), t->ne[1], t->ne[0] / 256, 0);
+        int st = tts_hip_tensor_set(be, t->data, tmp.data(), n);
+        if (st == 0) t->flags |= TTS_FLAG_REPACKED | TTS_FLAG_TILED;
+        return st;
+    }
     if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0) {
         std::vector<uint8_t> tmp(n);
         tts_repack_q4_K(src, tmp.data(), (int64_t)(n / 144), 0);
@@ -244,6 +279,12 @@ int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
 int tts_hip_weight_get(tts_hip_backend_t be, const tts_tensor * t, void * dst) {
     if (!be || !t) return TTS_STATUS_BAD_ARG;
     const size_t n = tensor_bytes(t);
+    if (t->type == TTS_TYPE_Q4_K && (t->flags & TTS_FLAG_TILED)) {
+        std::vector<uint8_t> tmp(n);
+        int st = tts_hip_tensor_get(be, tmp.data(), t->data, n);
+        if (st == 0) tts_repack_q4_K_tiled(tmp.data(), dst, t->ne[1], t->ne[0] / 256, 1);
+        return st;
+    }
     if (t->type == TTS_TYPE_Q4_K && (t->flags & TTS_FLAG_REPACKED)) {
         std::vector<uint8_t> tmp(n);
         int st = tts_hip_tensor_get(be, tmp.data(), t->data, n);
@@ -316,6 +357,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_CONV_F32ACC: be->conv_f32acc = value != 0; return 0;
         case TTS_HIP_OPT_ATTN_SPLIT: be->attn_split_minp = value; return 0;
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
+        case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
         case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }

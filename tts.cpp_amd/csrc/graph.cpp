@@ -212,6 +212,12 @@ tts_tensor * cont_3d(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int6
     return new_op(c, TTS_OP_CONT, a->type, ne, a);
 }
 
+tts_tensor * cont_4d(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int64_t ne2, int64_t ne3) {
+    if (ne0 * ne1 * ne2 * ne3 != nelements(a)) fail("cont_4d: element count mismatch");
+    int64_t ne[4] = {ne0, ne1, ne2, ne3};
+    return new_op(c, TTS_OP_CONT, a->type, ne, a);
+}
+
 tts_tensor * cpy(context & c, tts_tensor * a, tts_tensor * b) {
     if (nelements(a) != nelements(b)) fail("cpy: element count mismatch");
     tts_tensor * t = make_view(c, b, TTS_OP_CPY, 0);

@@ -60,6 +60,7 @@ tts_tensor * transpose(context & c, tts_tensor * a);
 tts_tensor * cont(context & c, tts_tensor * a);
 tts_tensor * cont_2d(context & c, tts_tensor * a, int64_t ne0, int64_t ne1);
 tts_tensor * cont_3d(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int64_t ne2);
+tts_tensor * cont_4d(context & c, tts_tensor * a, int64_t ne0, int64_t ne1, int64_t ne2, int64_t ne3);
 tts_tensor * cpy(context & c, tts_tensor * a, tts_tensor * b);
 
 tts_tensor * add(context & c, tts_tensor * a, tts_tensor * b);

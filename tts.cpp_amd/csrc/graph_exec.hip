@@ -248,7 +248,8 @@ struct Planner {
             if (G.kind != Item::GEMV || G.mms.size() != 1 || G.mms[0] != t || G.epi != EPI_NONE || G.res || G.xattn >= 0) continue;
             const tts_tensor * W = t->src[0];
             const int64_t H = Q->ne[2], B = Q->ne[3];
-            if (W->type != TTS_TYPE_Q4_K || W->ne[0] > 1024 || W->ne[1] != 64 * H || t->ne[1] * t->ne[2] * t->ne[3] != B) continue;
+            if (W->type != TTS_TYPE_Q4_K || (W->flags & TTS_FLAG_TILED) || W->ne[0] > 1024 || W->ne[1] != 64 * H ||
+                t->ne[1] * t->ne[2] * t->ne[3] != B) continue;
             if (G.tgt[0].y != (float *)t->data || G.tgt[0].ycs != W->ne[1] || G.tgt[0].yrs != 1) continue;
             if (Q->data != t->data || Q->nb[0] != 4 || Q->nb[2] != 256 || (int64_t)Q->nb[3] != 4 * W->ne[1]) continue;
             if (A.k->ne[2] != H || A.v->ne[2] != H || B % A.k->ne[3] || B % A.v->ne[3]) continue;  // K/V may be shared by all prompts
@@ -381,7 +382,7 @@ struct Planner {
             if (mm->op != TTS_OP_MUL_MAT || mm->src[1] != x || !is_gemv(mm)) break;
             const tts_tensor * a = mm->src[0];
             if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->ne[1] != a0->ne[1] || a->nb[1] != a0->nb[1]) break;
-            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & TTS_FLAG_REPACKED)) break;
+            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED))) break;
             GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
             GemvTarget kt;
             std::vector<int> ks;
@@ -1101,6 +1102,7 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
     if (j.wtype == TTS_TYPE_Q4_K) {
         // the kernel quantizes (and normalizes) src1 itself in every workgroup
         j.pro = it.ln ? PRO_LN : PRO_QUANT;
+        j.tiled = (a0->flags & TTS_FLAG_TILED) ? 1 : 0;
         if (it.ln) {
             j.x = (const float *)it.lnx->data;
             j.xcs = (int64_t)(it.lnx->nb[1] / 4);
@@ -1461,7 +1463,13 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
 
 extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
                             int64_t M) {
+    return tts_hip_gemv_ex(be, type, w, x, y, K, N, M, 0);
+}
+
+extern "C" int tts_hip_gemv_ex(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
+                               int64_t M, int32_t wflags) {
     if (!be) return TTS_STATUS_BAD_ARG;
+    if ((wflags & TTS_FLAG_TILED) && (type != TTS_TYPE_Q4_K || N % 4)) return TTS_STATUS_BAD_ARG;
     if (type == TTS_TYPE_Q4_K && K % 256) return TTS_STATUS_BAD_ARG;
     if (type == TTS_TYPE_Q8_0 && K % 32) return TTS_STATUS_BAD_ARG;
     if (type != TTS_TYPE_Q4_K && type != TTS_TYPE_Q8_0 && type != TTS_TYPE_F16 && type != TTS_TYPE_F32) return TTS_STATUS_UNSUPPORTED;
@@ -1481,6 +1489,7 @@ extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, cons
     j.xcs = K;
     if (type == TTS_TYPE_Q4_K) {
         j.pro = PRO_QUANT;
+        j.tiled = (wflags & TTS_FLAG_TILED) ? 1 : 0;
         if ((uintptr_t)x & 15) {  // the prologue reads 16-B vectors
             if ((size_t)(4 * K * M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
             launch_copy_cols(be, (float *)be->scratch, x, K, K, M);

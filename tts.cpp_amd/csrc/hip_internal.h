@@ -174,6 +174,7 @@ struct GemvJob {
     // Q4_K prologue: PRO_QUANT = quantize x to Q8_K in LDS; PRO_LN = first x <- norm(x)*w (+b)
     // (NORM/RMS_NORM -> MUL -> ADD, parler_build_layer_norm), written to lnout by workgroup 0.
     int pro = 0;
+    int tiled = 0;  // W in the 4-row tile layout (TTS_FLAG_TILED): k_gemv_q4K_mf
     const float * lnw = nullptr;
     const float * lnb = nullptr;
     float eps = 0.f;
@@ -228,6 +229,7 @@ struct tts_hip_backend {
     size_t attn_floats = 0;
     int attn_split_minp = 128;
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
+    int64_t q4k_tile_bytes = 4 << 20;  // weight_set: Q4_K matrices >= this size use the tile layout + MFMA GEMV (0 = never)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;
     hipStream_t pf_stream = nullptr;

@@ -14,6 +14,8 @@
 #include "hip_internal.h"
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 namespace tts {
 
 __device__ __forceinline__ float dev_fp16_to_fp32(uint16_t h) {
@@ -164,8 +166,7 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
 // elements 16t+e and 16t+e+8 are adjacent bytes), d and the eight per-32 sums as int16.  All
 // reductions stay inside the row (DPP); the code is branch-free so the compiler can interleave it
 // with neighbouring work.
-__device__ __forceinline__ void q8k_row_block(const float (&v)[16], int lane, int8_t * xq, float * xd, int16_t * xs) {
-    const int t = lane & 15;
+__device__ __forceinline__ void q8k_quant16(const float (&v)[16], int lane, int (&q)[16], float & d, int & s) {
     float lax = 0.f, lval = 0.f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
@@ -185,19 +186,51 @@ __device__ __forceinline__ void q8k_row_block(const float (&v)[16], int lane, in
     const float val = __shfl(lval, (lane & 48) + (rowbits ? __ffs(rowbits) - 1 : 0));
     const bool nz = ax != 0.f;
     const float iscale = nz ? cr_divf(-127.f, val) : 0.f;  // iscale 0 quantizes everything to 0
-    const float d = nz ? cr_divf(1.f, iscale) : 0.f;
-    int q[16];
+    d = nz ? cr_divf(1.f, iscale) : 0.f;
 #pragma unroll
     for (int e = 0; e < 16; ++e) q[e] = min(dev_nearest_int(__fmul_rn(iscale, v[e])), 127);
+    s = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += q[e];
+    s += dpp_i32<DPP_XOR1>(s);  // elements 32j..32j+31 = lanes 2j, 2j+1
+}
+
+__device__ __forceinline__ void q8k_row_block(const float (&v)[16], int lane, int8_t * xq, float * xd, int16_t * xs) {
+    const int t = lane & 15;
+    int q[16], s;
+    float d;
+    q8k_quant16(v, lane, q, d, s);
     const int base = ((t >> 1) & 1) * 16 + (t >> 2) * 4 + ((2 * t) & 3);
 #pragma unroll
     for (int e = 0; e < 8; ++e)
         *(int16_t *)(xq + e * 32 + base) = (int16_t)((q[e] & 0xFF) | ((q[e + 8] & 0xFF) << 8));
-    int s = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) s += q[e];
-    s += dpp_i32<DPP_XOR1>(s);  // elements 32j..32j+31 = lanes 2j, 2j+1
     if ((t & 1) == 0) xs[t >> 1] = (int16_t)s;
+    if (t == 0) *xd = d;
+}
+
+// The same Q8_K block written as the MFMA kernel's B operands (k_gemv_q4K_mf): f16 values (exact:
+// |q| <= 127) at b16[(l*4 + c)*8 + 4h + kk] for element 64c + 32h + 8kk + l, and the per-32 sums
+// split as bsum = 64*hi + lo (lo in [0, 63], both exact in f16) at sb[e] = lo_e, sb[8 + e] = hi_e.
+__device__ __forceinline__ void q8k_row_block_mf(const float (&v)[16], int lane, _Float16 * b16, _Float16 * sb, float * xd) {
+    const int t = lane & 15;
+    int q[16], s;
+    float d;
+    q8k_quant16(v, lane, q, d, s);
+    // lane t holds elements 16t + e: c = t >> 2, h = (t >> 1) & 1, kk = 2(t & 1) + (e >> 3), l = e & 7
+    const int base = (t >> 2) * 8 + ((t >> 1) & 1) * 4 + 2 * (t & 1);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        h2 pr;
+        pr.x = (_Float16)q[l];
+        pr.y = (_Float16)q[l + 8];
+        *(h2 *)(b16 + l * 32 + base) = pr;
+    }
+    if ((t & 1) == 0) {
+        const int hi = s >> 6, lo = s - 64 * hi;  // arithmetic shift: floor(s / 64)
+        sb[t >> 1] = (_Float16)lo;
+        sb[8 + (t >> 1)] = (_Float16)hi;
+    }
     if (t == 0) *xd = d;
 }
 
@@ -213,8 +246,14 @@ __device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
 // Prologue: the Q8_K activation of all M columns into LDS, optionally after LayerNorm / RMSNorm
 // with affine (ggml_compute_forward_norm_f32 / rms_norm_f32: f64 sums, mean and variance rounded
 // to f32, scale = 1/sqrtf(var + eps), then MUL(w) and ADD(b) each rounded).
-template <int PRO, int NCH>
-__device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s) {
+// MF: write the MFMA kernel's f16 operand layout (q8k_row_block_mf into mf_b16 / mf_sb) instead.
+template <int PRO, int NCH, bool MF = false>
+__device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s,
+                                             _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr) {
+    auto put = [&](const float (&v)[16], int lane, int slot) {
+        if constexpr (MF) q8k_row_block_mf(v, lane, mf_b16 + (int64_t)slot * QK_K, mf_sb + slot * 16, xd_s + slot);
+        else q8k_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
+    };
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int r = lane >> 4, t = lane & 15;
     const int M = (int)j.M;
@@ -237,7 +276,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
             for (int u = 0; u < QP; ++u) {
                 const int p = p0 + u * nw, qb = 4 * p + r;
                 const int slot = (p < npass && qb < nq) ? qb : trash;
-                q8k_row_block(v[u], lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
+                put(v[u], lane, slot);
             }
         };
         // the first batch is peeled out of the loop: a loop header makes the compiler wait for every
@@ -327,7 +366,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
                     for (int k = 0; k < 4; ++k) *(float4 *)(o + 4 * k) = make_float4(v[p][4 * k], v[p][4 * k + 1], v[p][4 * k + 2], v[p][4 * k + 3]);
                 }
                 const int slot = valid ? m * nb + 4 * p + r : trash;
-                q8k_row_block(v[p], lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
+                put(v[p], lane, slot);
             }
         };
         if (wave < M) column(wave);  // peeled, as above
@@ -473,6 +512,175 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
         if (g + gstride < G) load_row(g + gstride, 0);
     }
     TTS_TS(j, 5);
+}
+
+// ------------------------------------------------------------------------------------------
+// Q4_K x Q8_K GEMV on the matrix cores, for large matrices at 2..16 columns (Orpheus / Dia-sized
+// decode GEMVs at batch > 1).  The VALU kernel above spends ~45 instructions per (row, column,
+// block) on integer dots; here the integer part of ggml's vec_dot_q4_K_q8_K runs as f16 MFMAs
+// whose results are EXACT integers, so the f32 combine is unchanged and the output bit-identical:
+//   aux32[l] (row, col) = sum_{j,kk} (sc_j * q4[32j + 8kk + l]) * q8[32j + 8kk + l]
+// is one v_mfma_f32_16x16x32_f16 per residue l over K = 32 = (j, kk): A = sc_j * q4 <= 945 and
+// B = q8 (|q8| <= 127) are exact in f16, the products (<= 120015) exact in f32, and every partial
+// sum of a residue stays below 2^24 (<= 8 * 63 * 4 * 15 * 127 = 3.84e6), so the f32 accumulation
+// is exact in any order.  sumi = sum_j mins_j * bsum_j is a 9th MFMA with bsum = 64*hi + lo split
+// (A = [mins, 64*mins, 0, 0], B = [lo, hi, -, -]).
+// Tile: 16 weight rows x 16 columns per wave, K index k = 8*kg + 4h + kk for lane group kg = c:
+// lane (row r, kg) holds for each residue l the dword of bytes qs[32c + 8kk + l] (kk = 0..3; low
+// nibble sub-block 2c, high 2c+1), read from the tile layout (tts_repack_q4_K_tiled) as two 16-B
+// pieces; B comes from LDS in the matching order
+// (q8k_row_block_mf).  C: column = lane & 15, rows 4*kg + reg.  Per (row, col) the lane then does
+// ggml's f32 combine in block order: sums[l] += (d*yd)*aux32[l], sumf -= (dmin*yd)*sumi.
+// Loads: 4-block batches, double-buffered across batches and tiles, the first issued before the
+// prologue.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// bytes 0,1 (SEL 0x0C010C00) or 2,3 (0x0C030C02) of w (each <= 63) as u16 lanes of 1024 + n
+__device__ __forceinline__ f16x2 byte2_f16_biased(uint32_t w, uint32_t sel) {
+    return __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(0u, w, sel) | 0x64006400u);
+}
+
+template <int PRO, int NCH>
+__global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK_K);
+    const int M = (int)j.M;
+    const int nslot = M * nb + 1;  // + the prologue's trash slot
+    _Float16 * b16 = (_Float16 *)smem;                     // [nslot][256] B operands per residue
+    _Float16 * sbs = b16 + (size_t)nslot * QK_K;           // [nslot][16]  bsum lo / hi
+    float * xd_s = (float *)(sbs + (size_t)nslot * 16);    // [nslot]      Q8_K d
+
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int r = lane & 15, kg = lane >> 4;
+    const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
+    constexpr int CH = 4;
+    const int nch = (nb + CH - 1) / CH;
+    const int64_t NR = (int64_t)j.nmat * j.N;
+    const int64_t T = (NR + 15) / 16;
+    // tile t0 + k * tstride; consecutive tiles go to different workgroups, so a small matrix still
+    // spreads over every CU
+    const int64_t t0 = (int64_t)wave * gridDim.x + blockIdx.x, tstride = (int64_t)gridDim.x * nw;
+    const int64_t nmine = t0 < T ? ((T - 1 - t0) / tstride + 1) * nch : 0;
+    auto mat_of = [&](int64_t flat) {
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        return mt;
+    };
+
+    // tile layout (tts_repack_q4_K_tiled): lane (r, kg) reads its row's header and the two 16-B
+    // pieces of chunk c = kg (residues 0..3, 4..7); a quarter wave covers four 64-B runs
+    u32x4 hd[2][CH], qa[2][CH], qb[2][CH];
+    auto load = [&](auto BS, int64_t i) {
+        constexpr int bs = decltype(BS)::value;
+        const int64_t t = t0 + (i / nch) * tstride;
+        const int c = (int)(i % nch);
+        int64_t flat = t * 16 + r;
+        flat = flat < NR ? flat : NR - 1;
+        const int mat = mat_of(flat);
+        const int64_t row = flat - (int64_t)mat * j.N;
+        const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
+        const int ri = (int)(row & 3);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const uint8_t * bp = wt + (int64_t)min(c * CH + u, nb - 1) * 576;
+            hd[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
+            qa[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+            qb[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+        }
+        TTS_PIN_LOADS();
+    };
+
+    float sums[8][4], sumf[4];
+    auto compute = [&](auto BS, int64_t i) {
+        constexpr int bs = decltype(BS)::value;
+        const int64_t t = t0 + (i / nch) * tstride;
+        const int c = (int)(i % nch);
+        if (c == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                sumf[q] = 0.f;
+#pragma unroll
+                for (int l = 0; l < 8; ++l) sums[l][q] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int b = c * CH + u;
+            if (b >= nb) break;  // wave-uniform
+            const u32x4 h = hd[bs][u];
+            const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
+            const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+            const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+            // A side: scales of sub-blocks 2kg (low nibbles) and 2kg + 1 (high nibbles)
+            const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
+            const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
+            const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
+            const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
+            const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
+            const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8;
+            f32x4 acc[8];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) {
+                const uint32_t D = l < 4 ? qa[bs][u][l] : qb[bs][u][l - 4];
+                const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+                // fma(1024 + n, s, -1024 s) = s * n exactly (single rounding of an exact value)
+                const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
+                const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
+                const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
+                const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
+                const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+                const f16x8 B = *(const f16x8 *)(bsl + l * 32);
+                acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+            // sumi: lane group 0 holds the 8 mins, group 1 the mins times 64, groups 2, 3 zero
+            const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
+            const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
+            const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
+            const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
+            const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+            const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
+            const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            const float yd = xd_s[cc * nb + b];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
+                const float dy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+                const float dmy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+#pragma unroll
+                for (int l = 0; l < 8; ++l) sums[l][q] = __fadd_rn(sums[l][q], __fmul_rn(dy, acc[l][q]));
+                sumf[q] = __fsub_rn(sumf[q], __fmul_rn(dmy, si[q]));
+            }
+        }
+        if (c == nch - 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float tot = sumf[q];
+#pragma unroll
+                for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[l][q]);
+                const int64_t flat = t * 16 + 4 * kg + q;
+                if (r < M && flat < NR) {
+                    const int mat = mat_of(flat);
+                    gemv_store<8>(j, mat, flat - (int64_t)mat * j.N, r, tot);
+                }
+            }
+        }
+    };
+
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    if (nmine > 0) load(I0{}, 0);
+    q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs);
+    __syncthreads();
+    for (int64_t i = 0; i < nmine; i += 2) {
+        load(I1{}, min(i + 1, nmine - 1));
+        compute(I0{}, i);
+        if (i + 1 >= nmine) break;
+        load(I0{}, min(i + 2, nmine - 1));
+        compute(I1{}, i + 1);
+    }
 }
 
 // Cross-attention query GEMV + attention in one launch (Parler model.cpp:583-594: q = W_q
@@ -867,6 +1075,51 @@ static size_t q80_lds(int MC, int64_t K, int RW) {
     return a((size_t)MC * K) + a(4 * MC * nb) + a(4 * (size_t)RW * nb * MC) + 4 * (size_t)RW * nb * MC;
 }
 
+// ---- MFMA path (k_gemv_q4K_mf) ----
+static size_t q4k_mf_lds(int64_t M, int64_t K) { return (size_t)(M * (K / QK_K) + 1) * (2 * QK_K + 32 + 4); }
+static int64_t q4k_mf_max_cols(int64_t K) {
+    const int64_t c = ((int64_t)(160 * 1024) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
+    return c >= 16 ? 16 : c >= 8 ? 8 : c;
+}
+static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
+    (void)be;
+    return j.wtype == TTS_TYPE_Q4_K && j.tiled;
+}
+template <int PRO, int NCH>
+static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        TTS_HIP_CHECK(hipFuncSetAttribute((const void *)k_gemv_q4K_mf<PRO, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_set = true;
+    }
+    const int64_t T = (j.nmat * j.N + 15) / 16;
+    const unsigned gx = (unsigned)(T < 256 ? T : 256);
+    const size_t lds = q4k_mf_lds(j.M, j.K);
+    if (be->profile_gemv) {
+        hipEvent_t e0, e1;
+        profile_pair(be, e0, e1);
+        hipExtLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
+        return;
+    }
+    hipLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH>), dim3(gx), dim3(512), lds, be->stream, j);
+}
+static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
+    const int64_t cmax = q4k_mf_max_cols(job.K);
+    for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {
+        GemvJob j = job;
+        j.M = job.M - m0 < cmax ? job.M - m0 : cmax;
+        if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
+        j.x = job.x + m0 * job.xcs;
+        for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+        if (job.res) j.res = job.res + m0 * job.rcs;
+        // the LN prologue holds one column's K / 256 chunks in registers: 16 (K <= 4096) or 32
+        if (j.pro == PRO_LN && j.K <= 4 * 1024) launch_q4k_mf_pro<PRO_LN, 16>(be, j);
+        else if (j.pro == PRO_LN) launch_q4k_mf_pro<PRO_LN, 32>(be, j);
+        else launch_q4k_mf_pro<PRO_QUANT, 16>(be, j);
+    }
+}
+
 template <int MC>
 static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
     const unsigned nmat = (unsigned)j.nmat;
@@ -913,6 +1166,11 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
         TTS_HIP_CHECK(hipEventRecord(e0, be->stream));
     }
     const int64_t K = job.K;
+    if (q4k_mf_eligible(be, job)) {
+        launch_q4k_mf(be, job);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     const int64_t cmax = job.wtype == TTS_TYPE_Q4_K ? q4k_max_cols(K) : 8;
     for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {
         const int64_t mc = job.M - m0 < cmax ? job.M - m0 : cmax;

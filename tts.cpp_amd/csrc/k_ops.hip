@@ -252,6 +252,30 @@ __device__ __forceinline__ float table_elem(const TD & s0, const char * src, int
     return __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
 }
 
+// element k of row `row` of a Q4_K table in the 4-row tile layout (tts_repack_q4_K_tiled)
+__device__ __forceinline__ float table_elem_q4K_tiled(const char * base, int64_t row, int64_t nb, int64_t k) {
+    const uint8_t * g = (const uint8_t *)base + ((row >> 2) * nb + k / QK_K) * 576;
+    const int i = (int)(row & 3);
+    const uint8_t * hdr = g + i * 16;
+    const int e = (int)(k % QK_K);
+    const int c = e / 64, w = e % 64, hi = w >= 32, l = w % 32 % 8, kk = w % 32 / 8;
+    const int sb = 2 * c + hi;
+    const uint8_t * q = hdr + 4;
+    int sc, mn;
+    if (sb < 4) {
+        sc = q[sb] & 63;
+        mn = q[sb + 4] & 63;
+    } else {
+        sc = (q[sb + 4] & 0xF) | ((q[sb - 4] >> 6) << 4);
+        mn = (q[sb + 4] >> 4) | ((q[sb] >> 6) << 4);
+    }
+    const float d = __half2float(__ushort_as_half(*(const uint16_t *)hdr));
+    const float dm = __half2float(__ushort_as_half(*(const uint16_t *)(hdr + 2)));
+    const uint8_t qb = g[64 + ((c * 2 + (l >> 2)) * 4 + i) * 16 + (l & 3) * 4 + kk];
+    const int qv = hi ? (qb >> 4) : (qb & 0xF);
+    return __fsub_rn(__fmul_rn(__fmul_rn(d, (float)sc), (float)qv), __fmul_rn(dm, (float)mn));
+}
+
 __global__ void k_get_rows(TD dst, TD s0, TD s1) {
     const int64_t i = blockIdx.x;  // index into flattened s1
     const int64_t i10 = i % s1.ne[0], i11 = (i / s1.ne[0]) % s1.ne[1], i12 = i / (s1.ne[0] * s1.ne[1]);
@@ -259,6 +283,10 @@ __global__ void k_get_rows(TD dst, TD s0, TD s1) {
     const char * src = s0.data + i01 * s0.nb[1] + i11 * s0.nb[2] + i12 * s0.nb[3];
     float * out = (float *)(dst.data + i10 * dst.nb[1] + i11 * dst.nb[2] + i12 * dst.nb[3]);
     const int64_t nc = s0.ne[0];
+    if (s0.type == TTS_TYPE_Q4_K && (s0.pad & TTS_FLAG_TILED)) {  // 2-D tables only (weight_set)
+        for (int64_t k = threadIdx.x; k < nc; k += blockDim.x) out[k] = table_elem_q4K_tiled(s0.data, i01, nc / QK_K, k);
+        return;
+    }
     for (int64_t k = threadIdx.x; k < nc; k += blockDim.x) out[k] = table_elem(s0, src, k);
 }
 
@@ -287,7 +315,9 @@ __global__ void k_embed_sum(EmbedArgs a) {
     for (int t = 0; t < a.n; ++t) {
         const EmbedTerm & T = a.t[t];
         const int64_t r = T.idx[(T.rows == 1 ? 0 : m) * T.idx_stride];
-        const float v = table_elem(T.table, T.table.data + r * T.table.nb[1], h);
+        const float v = (T.table.type == TTS_TYPE_Q4_K && (T.table.pad & TTS_FLAG_TILED))
+                            ? table_elem_q4K_tiled(T.table.data, r, T.table.ne[0] / QK_K, h)
+                            : table_elem(T.table, T.table.data + r * T.table.nb[1], h);
         acc = t == 0 ? v : __fadd_rn(acc, v);
     }
     a.out[m * a.H + h] = acc;

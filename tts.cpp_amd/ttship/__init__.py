@@ -26,7 +26,7 @@ FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 
 TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
@@ -95,6 +95,29 @@ class ParlerConfig(ctypes.Structure):
         ("seed", ctypes.c_uint64),
         ("arena_bytes", ctypes.c_uint64),
         ("debug_no_reuse", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+    ]
+
+
+class OrpheusConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", ctypes.c_int32),
+        ("hidden_size", ctypes.c_int32),
+        ("n_attn_heads", ctypes.c_int32),
+        ("n_kv_attn_heads", ctypes.c_int32),
+        ("head_size", ctypes.c_int32),
+        ("ffn_size", ctypes.c_int32),
+        ("vocab_size", ctypes.c_int32),
+        ("max_ctx", ctypes.c_int32),
+        ("weight_type", ctypes.c_int32),
+        ("batch", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+        ("rope_theta", ctypes.c_float),
+        ("rope_factor", ctypes.c_float),
+        ("rope_low_freq_factor", ctypes.c_float),
+        ("rope_high_freq_factor", ctypes.c_float),
+        ("rope_original_ctx", ctypes.c_int32),
         ("pad_", ctypes.c_int32),
     ]
 
@@ -180,11 +203,24 @@ def lib():
         "tts_hip_gemv_stats": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
         "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
+        "tts_hip_gemv_ex": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64, i32]),
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
         "tts_hip_weight_set": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_hip_weight_get": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_repack_q4_K": (None, [vp, vp, i64, ctypes.c_int]),
+        "tts_repack_q4_K_tiled": (None, [vp, vp, i64, i64, ctypes.c_int]),
+        "tts_orpheus_default_config": (None, [ctypes.POINTER(OrpheusConfig)]),
+        "tts_orpheus_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(OrpheusConfig)]),
+        "tts_orpheus_free": (None, [vp]),
+        "tts_orpheus_reset": (None, [vp]),
+        "tts_orpheus_prefill": (ctypes.c_int, [vp, vp, i32, vp]),
+        "tts_orpheus_decode": (ctypes.c_int, [vp, vp, vp]),
+        "tts_orpheus_generate": (ctypes.c_int, [vp, vp, i32, vp]),
+        "tts_orpheus_position": (i32, [vp]),
+        "tts_orpheus_last_graph_nodes": (i32, [vp]),
+        "tts_orpheus_weight_bytes": (u64, [vp]),
+        "tts_orpheus_graph": (vp, [vp, ctypes.POINTER(i32)]),
         "tts_parler_default_config": (None, [ctypes.POINTER(ParlerConfig)]),
         "tts_parler_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(ParlerConfig)]),
         "tts_parler_free": (None, [vp]),
@@ -290,6 +326,67 @@ class HipBackend:
     def close(self):
         if self.ptr:
             self.L.tts_hip_backend_free(self.ptr)
+            self.ptr = None
+
+
+def orpheus_config(**kw):
+    cfg = OrpheusConfig()
+    lib().tts_orpheus_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Orpheus:
+    """Orpheus-3B decoder runner over a backend vtable (HIP, or the oracle in tests)."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_orpheus_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_orpheus_create failed")
+
+    def prefill(self, tokens, want_logits=True):
+        import numpy as np
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.empty((self.cfg.batch, self.cfg.vocab_size), dtype=np.float32) if want_logits else None
+        st = self.L.tts_orpheus_prefill(self.ptr, tok.ctypes.data, tok.shape[-1], out.ctypes.data if out is not None else None)
+        if st != 0:
+            raise RuntimeError(f"prefill failed {st}")
+        return out
+
+    def decode(self, tokens):
+        import numpy as np
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        out = np.empty((self.cfg.batch, self.cfg.vocab_size), dtype=np.float32)
+        st = self.L.tts_orpheus_decode(self.ptr, tok.ctypes.data, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"decode failed {st}")
+        return out
+
+    def generate(self, first_tokens, n_steps):
+        import numpy as np
+        ft = np.ascontiguousarray(first_tokens, dtype=np.int32)
+        out = np.empty((self.cfg.batch, n_steps), dtype=np.int32)
+        st = self.L.tts_orpheus_generate(self.ptr, ft.ctypes.data, n_steps, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"generate failed {st}")
+        return out
+
+    def position(self):
+        return self.L.tts_orpheus_position(self.ptr)
+
+    def last_graph_nodes(self):
+        return self.L.tts_orpheus_last_graph_nodes(self.ptr)
+
+    def weight_bytes(self):
+        return self.L.tts_orpheus_weight_bytes(self.ptr)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_orpheus_free(self.ptr)
             self.ptr = None
 
 
