@@ -220,9 +220,11 @@ enum tts_hip_option {
     TTS_HIP_OPT_KV_PREFETCH = 6,  /* prefetch the next decode attention's K/V (KV length >= value) into the
                                      Infinity Cache on a side stream during the GEMVs before it; 0 = off */
     TTS_HIP_OPT_KV_PREFETCH_BLOCKS = 7, /* workgroups of the prefetch kernel (default 128) */
-    TTS_HIP_OPT_Q4K_TILE_BYTES = 8 /* tts_hip_weight_set stores Q4_K matrices of >= value bytes (ne1 % 4 == 0) in the
+    TTS_HIP_OPT_Q4K_TILE_BYTES = 8, /* tts_hip_weight_set stores Q4_K matrices of >= value bytes (ne1 % 4 == 0) in the
                                      4-row tile layout; their GEMVs run on the matrix-core kernel (exact integer f16
                                      MFMAs, bit-identical).  Default 4 MiB; 0 = never */
+    TTS_HIP_OPT_GEMV_DEBUG = 10, /* matrix-core GEMV phase study: 1 = skip the row phase, 2 = skip the prologue
+                                     (results invalid; micro-benchmarks only) */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
@@ -231,7 +233,8 @@ enum tts_fuse_bits {
     TTS_FUSE_EMBED = 256, /* an ADD chain over GET_ROWS terms (codebook + positional embeddings) -> one launch */
     TTS_FUSE_CONV = 512,  /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
     TTS_FUSE_ADAIN = 1024, /* Kokoro AdaIN1d (norm, transposes, affine) + snake_1d -> one pass per channel row */
-    TTS_FUSE_XATTN = 2048  /* short-context attention (P <= 64) folded into the Q4_K GEMV producing its query */
+    TTS_FUSE_XATTN = 2048, /* short-context attention (P <= 64) folded into the Q4_K GEMV producing its query */
+    TTS_FUSE_MCPY = 4096   /* CPYs of one source into several views (Orpheus' repeat-interleaved KV store) -> one pass */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

@@ -30,7 +30,10 @@ def main():
     mlist = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 8]
     tiled = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # 1: Q4_K in the tile layout (matrix-core kernel)
     only = sys.argv[4].split(",") if len(sys.argv) > 4 else None
+    mr_tiles = None
     hip = ttship.HipBackend(0)
+    dbg = int(sys.argv[6]) if len(sys.argv) > 6 else 0  # TTS_HIP_OPT_GEMV_DEBUG phase study
+    hip.set_option(ttship.OPT["GEMV_DEBUG"], dbg)
     L = ttship.lib()
     rng = np.random.default_rng(0)
     for name, wt, K, N in SHAPES:
@@ -70,7 +73,7 @@ def main():
             hip.set_option(1, 0)
             us = 1000.0 * ms / n
             print(json.dumps({"shape": name, "type": ttship.lib().tts_type_name(wt).decode(), "K": K, "N": N, "M": M,
-                              "weight_MB": round(wbytes / 1e6, 3), "tiled": bool(tiled and wt == ttship.Q4_K), "avg_us": round(us, 2),
+                              "weight_MB": round(wbytes / 1e6, 3), "tiled": bool(tiled and wt == ttship.Q4_K), "dbg": dbg, "avg_us": round(us, 2),
                               "GBps": round(nbytes / n / (us * 1e-6) / 1e9, 1)}), flush=True)
             hip.free(dx)
             hip.free(dy)

@@ -64,5 +64,10 @@ def test_orpheus_step_plan():
         c.prefill(np.arange(4, dtype=np.int32)[None])
         c.decode(np.array([7], dtype=np.int32))
         assert c.last_graph_nodes() > 20 * TINY["n_layers"]
+        st = c.plan_stats()
+        L = TINY["n_layers"]
+        assert st["attn"] == L, st   # transposed-V cont folded: one fused attention per layer
+        assert st["mcpy"] == 2 * L, st  # K and V repeat-interleave copies: one pass each
+        assert st["ln"] + st["gemv"] >= 5 * L, st
     finally:
         c.close()

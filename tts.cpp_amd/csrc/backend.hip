@@ -3,6 +3,7 @@
 // /root/reference/examples/server/server.cpp:316-321).
 #include <cmath>
 #include <cstring>
+#include <thread>
 
 #include "hip_internal.h"
 
@@ -59,6 +60,10 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     be->attn_floats = kAttnFloats;
     TTS_HIP_CHECK(hipMalloc((void **)&be->vec_scratch, kVecScratchFloats * sizeof(float)));
     be->lstm_floats = kLstmFloats;
+    TTS_HIP_CHECK(hipMalloc((void **)&be->argmax_keys, kArgmaxRows * sizeof(unsigned long long)));
+    TTS_HIP_CHECK(hipMalloc((void **)&be->argmax_counts, kArgmaxRows * sizeof(unsigned)));
+    TTS_HIP_CHECK(hipMemset(be->argmax_keys, 0, kArgmaxRows * sizeof(unsigned long long)));
+    TTS_HIP_CHECK(hipMemset(be->argmax_counts, 0, kArgmaxRows * sizeof(unsigned)));
     TTS_HIP_CHECK(hipHostMalloc((void **)&be->pin, kPinBytes, hipHostMallocDefault));
     be->pin_size = kPinBytes;
     for (auto & e : be->plan_ev) TTS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -84,6 +89,8 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipHostFree(be->pin);
     hipFree(be->scratch);
     hipFree(be->shadow);
+    hipFree(be->argmax_keys);
+    hipFree(be->argmax_counts);
     hipFree(be->lstm_buf);
     hipFree(be->attn_buf);
     hipFree(be->vec_scratch);
@@ -222,11 +229,9 @@ void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse)
     }
 }
 
-void tts_repack_q4_K_tiled(const void * src, void * dst, int64_t nrows, int64_t nb, int inverse) {
-    const uint8_t * s = (const uint8_t *)src;
-    uint8_t * d = (uint8_t *)dst;
+static void repack_tiled_rows(const uint8_t * s, uint8_t * d, int64_t r0, int64_t r1, int64_t nb, int inverse) {
     const int64_t rb = nb * 144;
-    for (int64_t row = 0; row < nrows; ++row) {
+    for (int64_t row = r0; row < r1; ++row) {
         const int64_t t = row >> 2, i = row & 3;
         for (int64_t b = 0; b < nb; ++b) {
             const int64_t nat = row * rb + b * 144;           // native block
@@ -246,6 +251,22 @@ void tts_repack_q4_K_tiled(const void * src, void * dst, int64_t nrows, int64_t 
                         }
         }
     }
+}
+
+void tts_repack_q4_K_tiled(const void * src, void * dst, int64_t nrows, int64_t nb, int inverse) {
+    const uint8_t * s = (const uint8_t *)src;
+    uint8_t * d = (uint8_t *)dst;
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+    if (nrows * nb < 4096 || nt == 1) {
+        repack_tiled_rows(s, d, 0, nrows, nb, inverse);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = ((nrows + nt - 1) / nt + 3) & ~(int64_t)3;  // whole 4-row tiles per thread
+    for (int64_t r0 = 0; r0 < nrows; r0 += chunk)
+        th.emplace_back(repack_tiled_rows, s, d, r0, r0 + chunk < nrows ? r0 + chunk : nrows, nb, inverse);
+    for (auto & t : th) t.join();
 }
 
 static size_t tensor_bytes(const tts_tensor * t) {
@@ -358,6 +379,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_ATTN_SPLIT: be->attn_split_minp = value; return 0;
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
+        case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }

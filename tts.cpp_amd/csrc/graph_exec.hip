@@ -16,6 +16,7 @@
 // allocated, so aliasing is checked on the real addresses).
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <unordered_map>
 #include <vector>
 
@@ -102,7 +103,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -136,6 +137,7 @@ struct Item {
     Conv1dArgs conv{};
     // ADAIN: per-channel norm + affine (+ snake)
     AdainArgs adain{};
+    // MCPY: src (x) copied into every view in `terms`
 };
 
 struct Planner {
@@ -146,6 +148,7 @@ struct Planner {
     std::unordered_map<const tts_tensor *, std::vector<int>> consumers;
     std::vector<int> act;  // -1 skip, 0 run node, k>0 run items[k-1]
     std::vector<Item> items;
+    std::deque<tts_tensor> derived;  // strided stand-ins for folded CONT nodes (stable addresses)
     int mask = 0xFF;
     float * lstm_buf = nullptr;  // backend scratch for fused LSTM chains (hidden history + cell)
     size_t vec_cap = 0;          // floats of the backend's vector scratch (fused AdaIN staging)
@@ -196,6 +199,7 @@ struct Planner {
                 case TTS_OP_SOFT_MAX: if (mask & TTS_FUSE_ATTN) try_attn(i); break;
                 case TTS_OP_ADD: if (mask & TTS_FUSE_SNAKE) try_snake(i); break;
                 case TTS_OP_IM2COL: if (mask & TTS_FUSE_CONV) try_conv(i); break;
+                case TTS_OP_CPY: if (mask & TTS_FUSE_MCPY) try_mcpy(i); break;
                 case TTS_OP_MUL_MAT:
                     if (!((mask & TTS_FUSE_HEADS) && try_heads(i)) && (mask & (TTS_FUSE_GROUP | TTS_FUSE_KV | TTS_FUSE_EPI))) try_gemv(i);
                     break;
@@ -975,6 +979,54 @@ struct Planner {
         act[i] = add_item(std::move(it));
     }
 
+    // orpheus_build_kv_store (Orpheus model.cpp:194-228): `repeat` CPYs of one source into strided
+    // cache views, K's and V's interleaved.  All CPY consumers of the source run as one pass when
+    // nothing but CPYs and views sits between the first and the last (the destinations are disjoint
+    // cache views nobody reads in between).
+    void try_mcpy(int i) {
+        const tts_tensor * C = nodes[i];
+        const tts_tensor * src = C->src[0];
+        if (!src || src->type != TTS_TYPE_F32 || C->type != TTS_TYPE_F32) return;
+        auto it = consumers.find(src);
+        if (it == consumers.end() || it->second.size() < 2 || it->second.size() > 4) return;
+        std::vector<int> idx = it->second;
+        std::sort(idx.begin(), idx.end());
+        if (idx[0] != i) return;
+        for (int j : idx) {
+            const tts_tensor * D = nodes[j];
+            if (D->op != TTS_OP_CPY || D->src[0] != src || act[j] != 0 || D->type != TTS_TYPE_F32) return;
+            for (int k = 0; k < 4; ++k)
+                if (D->ne[k] != C->ne[k]) return;
+        }
+        // destinations: same shape and strides, bases interleaved inside one dim-1 period (the
+        // repeat copies), so their element sets are disjoint although their byte spans overlap
+        auto interleaved = [](const tts_tensor * a, const tts_tensor * b) {
+            for (int k = 0; k < 4; ++k)
+                if (a->nb[k] != b->nb[k]) return false;
+            const int64_t d = std::llabs((const char *)a->data - (const char *)b->data);
+            const int64_t run = a->ne[0] * (int64_t)a->nb[0], p1 = (int64_t)a->nb[1];
+            if (a->nb[0] != 4 || d < run || d + run > p1) return false;
+            for (int k = 2; k < 4; ++k)
+                if (a->ne[k] > 1 && a->nb[k] % p1) return false;
+            return true;
+        };
+        for (size_t a = 0; a < idx.size(); ++a) {
+            if (overlap(nodes[idx[a]], src)) return;
+            for (size_t b = a + 1; b < idx.size(); ++b)
+                if (overlap(nodes[idx[a]], nodes[idx[b]]) && !interleaved(nodes[idx[a]], nodes[idx[b]])) return;
+        }
+        for (int j = idx.front() + 1; j < idx.back(); ++j)
+            if (!is_view(nodes[j]->op) && nodes[j]->op != TTS_OP_CPY) return;
+        Item m;
+        m.kind = Item::MCPY;
+        m.x = src;
+        for (int j : idx) {
+            m.terms.push_back(nodes[j]);
+            act[j] = -1;
+        }
+        act[i] = add_item(std::move(m));
+    }
+
     void try_attn(int i) {
         const tts_tensor * S = nodes[i];
         const tts_tensor * KQ = S->src[0];
@@ -993,7 +1045,26 @@ struct Planner {
         const tts_tensor * Qa = KQ->src[1];
         const tts_tensor * V = KQV->src[1];
         const tts_tensor * K = Ka;
-        int skip_k = -1, skip_q = -1;
+        int skip_k = -1, skip_q = -1, skip_v = -1;
+        // V = cont_{3,4}d(transpose(view of a [dims, positions] cache)) (Orpheus model.cpp:265-272): read the
+        // transposed cache in place, V'(p, d, h, b) = T(p, d + hd*h, b); the per-step transpose copy disappears
+        if (V->op == TTS_OP_CONT && uses[V] == 1 && V->src[0] && V->src[0]->data) {
+            const tts_tensor * T = V->src[0];
+            if (T->ne[3] == 1 && V->ne[0] == T->ne[0] && V->ne[1] * V->ne[2] == T->ne[1] && V->ne[3] == T->ne[2] &&
+                T->type == TTS_TYPE_F32 && V->type == TTS_TYPE_F32) {
+                tts_tensor & d = derived.emplace_back(*V);
+                d.op = TTS_OP_VIEW;
+                d.data = T->data;
+                d.nb[0] = T->nb[0];
+                d.nb[1] = T->nb[1];
+                d.nb[2] = T->nb[1] * V->ne[1];
+                d.nb[3] = T->nb[2];
+                d.view_src = T->view_src ? T->view_src : const_cast<tts_tensor *>(T);
+                for (int k = 0; k < TTS_MAX_SRC; ++k) d.src[k] = nullptr;
+                skip_v = index[V];
+                V = &d;
+            }
+        }
         if (Ka->op == TTS_OP_CONT && uses[Ka] == 1) {
             K = Ka->src[0];
             skip_k = index[Ka];
@@ -1006,7 +1077,7 @@ struct Planner {
         if (K->type != TTS_TYPE_F32 || Q->type != TTS_TYPE_F32 || V->type != TTS_TYPE_F32) return;
         const int64_t hd = Q->ne[0], P = K->ne[1];
         if (K->ne[0] != hd || hd % 4 || hd > 256 || P > 8192 || S->ne[0] != P || V->ne[0] != P || V->ne[1] != hd) return;
-        if (Q->nb[0] != 4 || K->nb[0] != 4 || V->nb[0] != 4) return;
+        if (Q->nb[0] != 4 || K->nb[0] != 4 || V->nb[0] % 4 || (skip_v < 0 && V->nb[0] != 4)) return;
         const int64_t H = Q->ne[2], nq = Q->ne[1], B = Q->ne[3];
         if (H % K->ne[2] || B % K->ne[3] || H % V->ne[2] || B % V->ne[3]) return;
         if (V->ne[2] != H || V->ne[3] != B) return;  // kqv = mul_mat(kq, V): V carries the batch dims
@@ -1030,6 +1101,7 @@ struct Planner {
         act[index[KQV]] = -1;
         if (skip_k >= 0) act[skip_k] = -1;
         if (skip_q >= 0) act[skip_q] = -1;
+        if (skip_v >= 0) act[skip_v] = -1;
         act[index[O]] = add_item(std::move(it));
     }
 };
@@ -1242,6 +1314,9 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             return 0;
         case Item::ADAIN:
             launch_adain_snake(be, it.adain);
+            return 0;
+        case Item::MCPY:
+            launch_cpy_multi(be, it.x, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::LSTM:
             if (it.lkind & 1) {

@@ -22,6 +22,8 @@
 
 namespace tts {
 
+constexpr int kArgmaxRows = 4096;
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short short2_t __attribute__((ext_vector_type(2)));
@@ -175,6 +177,7 @@ struct GemvJob {
     // (NORM/RMS_NORM -> MUL -> ADD, parler_build_layer_norm), written to lnout by workgroup 0.
     int pro = 0;
     int tiled = 0;  // W in the 4-row tile layout (TTS_FLAG_TILED): k_gemv_q4K_mf
+    int dbg = 0;    // phase study (TTS_HIP_OPT_GEMV_DEBUG): 1 = skip the row phase, 2 = skip the prologue
     const float * lnw = nullptr;
     const float * lnb = nullptr;
     float eps = 0.f;
@@ -229,7 +232,10 @@ struct tts_hip_backend {
     size_t attn_floats = 0;
     int attn_split_minp = 128;
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
-    int64_t q4k_tile_bytes = 4 << 20;  // weight_set: Q4_K matrices >= this size use the tile layout + MFMA GEMV (0 = never)
+    unsigned long long * argmax_keys = nullptr;  // k_greedy_step_wide: per-row keys / arrival counts (self-clearing)
+    unsigned * argmax_counts = nullptr;
+    int64_t q4k_tile_bytes = 4 << 20;
+    int gemv_dbg = 0;  // tiled GEMVs with <= this many 16-row tiles: residue-split kernel  // weight_set: Q4_K matrices >= this size use the tile layout + MFMA GEMV (0 = never)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;
     hipStream_t pf_stream = nullptr;
@@ -255,7 +261,7 @@ struct tts_hip_backend {
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
     bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
-    int fusion = 0xFFF;  // bitmask of TTS_FUSE_* patterns (all on)
+    int fusion = 0x1FFF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};
@@ -306,6 +312,7 @@ struct LstmStepArgs {
     int Hd, K, wtype;
 };
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
+void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                         int32_t * hist, int32_t * next);
 constexpr int EMBED_MAX_TERMS = 16;

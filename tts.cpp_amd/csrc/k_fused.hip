@@ -337,8 +337,61 @@ __global__ __launch_bounds__(256) void k_greedy_step(const float * __restrict__ 
     next[h * B + b] = step + 1 > h ? (seen ? eos : tok) : bos;
 }
 
+// Large vocabularies (Orpheus: 156 940 logits per prompt): the row is split over `gridDim.x`
+// workgroups; each folds its segment to (value, first index) and merges it into the row's 64-bit
+// key with one atomicMax (orderable float bits high, ~index low: the larger value wins, then the
+// smaller index -- sampler::max's first maximum).  The last workgroup of the row to arrive
+// (device-scope counter) applies the same sample / EOS / next-token rule as k_greedy_step and
+// clears the key and counter for the next launch.
+__device__ __forceinline__ unsigned long long argmax_key(float v, int i) {
+    unsigned u = __float_as_uint(v);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // total order of non-NaN floats
+    return ((unsigned long long)u << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+}
+
+__global__ __launch_bounds__(256) void k_greedy_step_wide(const float * __restrict__ logits, int B, int NH, int V, int step, int bos,
+                                                          int eos, int32_t * eos_seen, int32_t * hist, int32_t * next,
+                                                          unsigned long long * keys, unsigned * counts) {
+    __shared__ unsigned long long s_k[4];
+    const int row = blockIdx.y, nseg = gridDim.x;
+    const int64_t seg = ((int64_t)V + nseg - 1) / nseg;
+    const int64_t i0 = (int64_t)blockIdx.x * seg, i1 = min((int64_t)V, i0 + seg);
+    const float * l = logits + (int64_t)row * V;
+    unsigned long long best = 0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
+        const unsigned long long k = argmax_key(l[i], (int)i);
+        best = k > best ? k : best;
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(best, off);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) s_k[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int w = 1; w < 4; ++w) best = s_k[w] > best ? s_k[w] : best;
+    atomicMax(keys + row, best);
+    __threadfence();
+    if (atomicAdd(counts + row, 1u) != (unsigned)nseg - 1) return;
+    const unsigned long long k = atomicExch(keys + row, 0ull);
+    atomicExch(counts + row, 0u);
+    const int tok = k ? (int)(0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull)) : 0;
+    const int b = row / NH, h = row % NH;
+    hist[row] = tok;
+    const int seen = eos_seen[row] | (tok == eos);
+    eos_seen[row] = seen;
+    next[h * B + b] = step + 1 > h ? (seen ? eos : tok) : bos;
+}
+
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                         int32_t * hist, int32_t * next) {
+    if (V >= 16384 && B * NH <= kArgmaxRows) {
+        const unsigned nseg = (unsigned)((V + 4095) / 4096 < 64 ? (V + 4095) / 4096 : 64);
+        hipLaunchKernelGGL(k_greedy_step_wide, dim3(nseg, (unsigned)(B * NH)), dim3(256), 0, be->stream, logits, B, NH, V, step, bos, eos,
+                           eos_seen, hist, next, be->argmax_keys, be->argmax_counts);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(k_greedy_step, dim3((unsigned)((B * NH + 3) / 4)), dim3(256), 0, be->stream, logits, B, NH, V, step, bos, eos, eos_seen,
                        hist, next);
     TTS_HIP_CHECK(hipGetLastError());

@@ -561,7 +561,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     // tile t0 + k * tstride; consecutive tiles go to different workgroups, so a small matrix still
     // spreads over every CU
     const int64_t t0 = (int64_t)wave * gridDim.x + blockIdx.x, tstride = (int64_t)gridDim.x * nw;
-    const int64_t nmine = t0 < T ? ((T - 1 - t0) / tstride + 1) * nch : 0;
+    const int64_t nmine = (t0 < T && !(j.dbg & 1)) ? ((T - 1 - t0) / tstride + 1) * nch : 0;
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
         while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
@@ -584,9 +584,15 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
             const uint8_t * bp = wt + (int64_t)min(c * CH + u, nb - 1) * 576;
-            hd[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
-            qa[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-            qb[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+            if (j.dbg & 4) {  // phase study: plain (cached) loads
+                hd[bs][u] = *(const u32x4 *)(bp + ri * 16);
+                qa[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16);
+                qb[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16);
+            } else {
+                hd[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
+                qa[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+                qb[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+            }
         }
         TTS_PIN_LOADS();
     };
@@ -672,7 +678,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
     if (nmine > 0) load(I0{}, 0);
-    q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs);
+    if (!(j.dbg & 2)) q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs);
     __syncthreads();
     for (int64_t i = 0; i < nmine; i += 2) {
         load(I1{}, min(i + 1, nmine - 1));
@@ -1108,6 +1114,7 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
     const int64_t cmax = q4k_mf_max_cols(job.K);
     for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {
         GemvJob j = job;
+        j.dbg = be->gemv_dbg;
         j.M = job.M - m0 < cmax ? job.M - m0 : cmax;
         if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
         j.x = job.x + m0 * job.xcs;

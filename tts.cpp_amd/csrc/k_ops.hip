@@ -22,6 +22,33 @@ __global__ void k_cpy(TD dst, TD src, int64_t n) {
     }
 }
 
+// One source copied into up to 4 destination views of the same shape (the planner's MCPY item:
+// Orpheus' repeat-interleaved KV store); each element is read once.
+struct CpyMulti {
+    TD dst[4];
+    int nd;
+};
+__global__ void k_cpy_multi(CpyMulti m, TD src, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t a0, a1, a2, a3, b0, b1, b2, b3;
+        unravel(k, src.ne, a0, a1, a2, a3);
+        const float v = td_load(src, a0, a1, a2, a3);
+        unravel(k, m.dst[0].ne, b0, b1, b2, b3);
+        for (int i = 0; i < m.nd; ++i) td_store(m.dst[i], b0, b1, b2, b3, v);
+    }
+}
+
+void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_tensor * const * dsts, int nd) {
+    CpyMulti m{};
+    m.nd = nd;
+    for (int i = 0; i < nd; ++i) m.dst[i] = make_td(dsts[i]);
+    const int64_t n = src->ne[0] * src->ne[1] * src->ne[2] * src->ne[3];
+    if (n == 0) return;
+    const int64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_cpy_multi, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, be->stream, m, make_td(src), n);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 // ---- binary with broadcast of src1 (ggml_can_repeat) ----
 template <int OP>
 __global__ void k_binary(TD dst, TD a, TD b, int64_t n) {

@@ -21,12 +21,12 @@ OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "
        "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
-FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048}
+FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048, "MCPY": 4096}
 FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 
 TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
@@ -384,6 +384,12 @@ class Orpheus:
     def weight_bytes(self):
         return self.L.tts_orpheus_weight_bytes(self.ptr)
 
+    def plan_stats(self, mask=None):
+        """Fusion coverage of the last step graph (no device needed)."""
+        n = ctypes.c_int32()
+        p = self.L.tts_orpheus_graph(self.ptr, ctypes.byref(n))
+        return plan_stats(p, n.value, FUSE_ALL if mask is None else mask)
+
     def close(self):
         if self.ptr:
             self.L.tts_orpheus_free(self.ptr)
@@ -632,7 +638,7 @@ class KokoroGenerator:
             self.ptr = None
 
 
-PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain"]
+PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy"]
 
 
 def plan_stats(nodes_ptr, n_nodes, mask):
