@@ -9,6 +9,11 @@ per prompt.  After the K timed steps every prompt's K codec frames are decoded t
 decoder inside the same timed region.  value = audio-seconds produced by all ranks / wall seconds
 (RTF^-1) of AR + DAC; the AR-only and DAC-only rates are reported beside it.
 
+Beside the headline line's fields, two more legs of BASELINE.json's configs run on the same GPU:
+"kokoro" (configs[1], the Kokoro-82M iSTFTNet vocoder path) and "orpheus" (configs[4]'s per-GPU
+shard, Orpheus-3B Q4_K decode), each with its own rate; the orpheus leg carries the dequant-GEMV
+roofline at the sizes where the matrix-core GEMV streams (every Orpheus matrix is >= 4 MiB).
+
 Multi-GPU: one process per GPU (torchrun); prompts shard with no data-path collective; RCCL
 (backend "nccl") carries only the barrier / max-over-ranks timing reduction and the final token
 gather (the codec-token stream every rank produced, gathered to rank 0).
@@ -194,6 +199,46 @@ def run_replicas(fn, n):
         raise errs[0]
 
 
+ORPHEUS_TOK_PER_AUDIO_S = 82.03  # 820 Orpheus tokens = 10.0 s of audio
+
+
+def orpheus_leg(be, args, rank):
+    """BASELINE configs[4] per-GPU shard: Orpheus-3B Q4_K (synthetic weights, every matrix incl. the
+    156 940-row head in Q4_K), `orpheus_batch` prompts in lockstep, greedy decode with device
+    sampling; plus the dequant-GEMV roofline over profiled steps (the tile-layout matrix-core kernel
+    carries every matrix >= 4 MiB)."""
+    B, steps, n_prompt = args.orpheus_batch, args.orpheus_steps, 32
+    cfg = ttship.orpheus_config(batch=B, max_ctx=n_prompt + steps + 64, arena_bytes=1 << 30)
+    o = ttship.Orpheus(be.iface(), cfg)
+    try:
+        prompt = (np.arange(B * n_prompt, dtype=np.int32).reshape(B, n_prompt) * 7919 + 128000 + rank) % cfg.vocab_size
+        first = o.prefill(prompt).argmax(axis=1).astype(np.int32)
+        toks = o.generate(first, 4)
+        be.sync()
+        t0 = time.perf_counter()
+        toks = o.generate(toks[:, -1], steps)
+        be.sync()
+        dt = time.perf_counter() - t0
+        be.set_option(ttship.OPT["PROFILE_GEMV"], 1)
+        be.gemv_stats(-1, reset=True)
+        o.generate(toks[:, -1], 8)
+        ms, launches, nbytes = be.gemv_stats(ttship.Q4_K, reset=True)
+        be.set_option(ttship.OPT["PROFILE_GEMV"], 0)
+        avg_us = 1000.0 * ms / max(launches, 1)
+        gbs = nbytes / max(launches, 1) / (avg_us * 1e-6) / 1e9 if launches else 0.0
+        return {"workload": f"Orpheus-3B Q4_K greedy decode (BASELINE configs[4] per-GPU shard), {B} prompts, "
+                            f"prompt {n_prompt} + {steps} timed steps, synthetic weights",
+                "tokens_per_s": round(B * steps / dt, 1), "audio_sec_per_s": round(B * steps / dt / ORPHEUS_TOK_PER_AUDIO_S, 3),
+                "ms_per_step": round(1000 * dt / steps, 3), "graph_nodes": o.last_graph_nodes(),
+                "weight_bytes": o.weight_bytes(),
+                "roofline": {"bound": "hbm", "kernel": "k_gemv_q4K_mf (tile layout, >= 4 MiB) + k_gemv_q4_K",
+                             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                             "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(nbytes / max(launches, 1), 1),
+                             "launches_sampled": launches}}
+    finally:
+        o.close()
+
+
 def kokoro_inputs(cfg, T, rank):
     """Synthetic generator inputs: decoder features, a voiced F0 contour with unvoiced gaps, a
     style vector and the uniform noise draws (seeded per rank)."""
@@ -226,6 +271,8 @@ def main():
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
     ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
+    ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
+    ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
@@ -316,6 +363,15 @@ def main():
                 "calls_per_gpu": args.kokoro_calls, "graph_nodes": kok.last_graph_nodes(),
                 "dtype": "f32 activations, f16 conv operands (ggml im2col), f64 conv accumulate",
                 "pcm_std": round(float(np.std(kpcm)), 4)}
+    ores = None
+    if args.orpheus_steps > 0:
+        barrier_sync(dist, be)
+        ores = orpheus_leg(be, args, rank)
+        # whole-job rate: every rank decoded its own shard; the slowest rank's step time sets it
+        t = max_over_ranks(dist, local, ores["ms_per_step"])
+        ores["ms_per_step"] = t
+        ores["tokens_per_s"] = round(world * args.orpheus_batch * 1000.0 / t, 1)
+        ores["audio_sec_per_s"] = round(ores["tokens_per_s"] / ORPHEUS_TOK_PER_AUDIO_S, 3)
     dt = max_over_ranks(dist, local, t2 - t0)
     dt_ar = max_over_ranks(dist, local, t1 - t0)
     dt_dac = max_over_ranks(dist, local, t2 - t1)
@@ -355,6 +411,7 @@ def main():
             "codec_tokens_per_s": round(total_prompts * args.steps * HEADS / dt_ar, 1),
             "host_us_per_step": host,
             "kokoro": kres,
+            "orpheus": ores,
             "roofline": roof,
             "cpu_baseline": cpu,
         }
