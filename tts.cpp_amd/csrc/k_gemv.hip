@@ -16,6 +16,11 @@
 
 #include <type_traits>
 
+#ifndef TTS_GEMV_EARLY16
+#define TTS_GEMV_EARLY16 1  // long rows (K > 1024) also issue their first weight loads before a quantize-only prologue
+                            // (the LN prologue holds a whole column in registers: those would spill)
+#endif
+
 namespace tts {
 
 __device__ __forceinline__ float dev_fp16_to_fp32(uint16_t h) {
@@ -481,16 +486,16 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
         }
         TTS_PIN_LOADS();
     };
-    // short rows: the first row's weights are in flight during the prologue; long rows (NBMAX 16)
-    // would need more registers than the prologue leaves, so they start after it
+    // the first row's weights are in flight during the prologue (long rows with an LN prologue would
+    // need more registers than it leaves, so they start after it)
     TTS_TS(j, 0);
-    if (NBMAX <= 4 && g < G) load_row(g, 0);
+    if ((NBMAX <= 4 || (TTS_GEMV_EARLY16 && PRO == PRO_QUANT)) && g < G) load_row(g, 0);
     TTS_TS(j, 1);
     q4k_prologue<PRO, NBMAX>(j, nb, xq_s, xd_s, xs_s);
     TTS_TS(j, 2);
     __syncthreads();
     TTS_TS(j, 3);
-    if (NBMAX > 4 && g < G) load_row(g, 0);
+    if (NBMAX > 4 && !(TTS_GEMV_EARLY16 && PRO == PRO_QUANT) && g < G) load_row(g, 0);
 
     for (; g < G; g += gstride) {
         float sums = 0.f, sumf = 0.f;
@@ -1120,9 +1125,13 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
         j.x = job.x + m0 * job.xcs;
         for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
         if (job.res) j.res = job.res + m0 * job.rcs;
-        // the LN prologue holds one column's K / 256 chunks in registers: 16 (K <= 4096) or 32
-        if (j.pro == PRO_LN && j.K <= 4 * 1024) launch_q4k_mf_pro<PRO_LN, 16>(be, j);
-        else if (j.pro == PRO_LN) launch_q4k_mf_pro<PRO_LN, 32>(be, j);
+        // the LN prologue holds one column's K / 256 chunks in registers (K <= 4096, as the planner's
+        // LN fusion requires)
+        if (j.pro == PRO_LN && j.K > 4 * 1024) {
+            fprintf(stderr, "tts_hip: LN-fused Q4_K GEMV with K = %lld > 4096\n", (long long)j.K);
+            abort();
+        }
+        if (j.pro == PRO_LN) launch_q4k_mf_pro<PRO_LN, 16>(be, j);
         else launch_q4k_mf_pro<PRO_QUANT, 16>(be, j);
     }
 }
