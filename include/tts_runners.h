@@ -114,6 +114,47 @@ int32_t tts_orpheus_last_graph_nodes(const tts_orpheus * p);
 uint64_t tts_orpheus_weight_bytes(const tts_orpheus * p);
 tts_tensor * const * tts_orpheus_graph(const tts_orpheus * p, int32_t * n_nodes);
 
+/* Dia-1.6B config (defaults = dia_model, src/models/dia/model.h:62-85; Q8_0 weights for config 4,
+ * F32 heads).  Classifier-free guidance runs a (conditioned, unconditioned) pair as the graph batch. */
+typedef struct tts_dia_config {
+    int32_t n_output_heads;             /* 9 */
+    int32_t n_encoder_layers;           /* 12 */
+    int32_t n_decoder_layers;           /* 18 */
+    int32_t encoder_hidden_size;        /* 1024 */
+    int32_t decoder_hidden_size;        /* 2048 */
+    int32_t encoder_attn_heads;         /* 16 */
+    int32_t decoder_attn_heads;         /* 16 */
+    int32_t decoder_query_heads;        /* 4 (GQA: 4 K/V heads, repeat-interleaved into the cache) */
+    int32_t head_size;                  /* 128 */
+    int32_t encoder_ffn_size;           /* 4096 */
+    int32_t decoder_ffn_size;           /* 8192 */
+    int32_t output_vocab_size;          /* 1028 */
+    int32_t encoder_vocab_size;         /* 256 (byte tokens) */
+    int32_t max_generation_size;        /* 3072 */
+    int32_t max_encoder_context_length; /* 1024 */
+    int32_t weight_type;                /* TTS_TYPE_Q8_0 */
+    int32_t head_type;                  /* TTS_TYPE_F32 */
+    float cfg_scale;                    /* 3.0 */
+    uint64_t seed;                      /* synthetic weight seed base (0x5EED) */
+    uint64_t arena_bytes;               /* compute arena (0 = default 2 GiB: the encoder step's 1024 x 1024 scores) */
+} tts_dia_config;
+
+typedef struct tts_dia tts_dia;
+
+void tts_dia_default_config(tts_dia_config * cfg);
+tts_dia * tts_dia_create(const tts_backend_iface * be, const tts_dia_config * cfg);
+void tts_dia_free(tts_dia * p);
+/* Encoder step + first decoder step (dia_runner::decode with encoder_step): text [2][max_encoder_context_length]
+ * (conditioned row, unconditioned row), n_text real tokens, audio [n_output_heads]; logits [n_output_heads][vocab]
+ * after cfg_scale. */
+int tts_dia_prefill(tts_dia * p, const int32_t * text, int32_t n_text, const int32_t * audio, float * logits);
+/* One decoder step: audio [n_output_heads] -> logits [n_output_heads][vocab]. */
+int tts_dia_decode(tts_dia * p, const int32_t * audio, float * logits);
+int32_t tts_dia_position(const tts_dia * p);
+int32_t tts_dia_last_graph_nodes(const tts_dia * p);
+uint64_t tts_dia_weight_bytes(const tts_dia * p);
+tts_tensor * const * tts_dia_graph(const tts_dia * p, int32_t * n_nodes);
+
 /* DAC decoder (codec tokens -> PCM): dac_runner::run / build_dac_graph,
  * /root/reference/src/decoder/dac_model.cpp:139-212.  Defaults = DAC 44.1 kHz as used by
  * Parler-TTS mini v1 (9 codebooks x 1024 x 8, latent 1024, decoder 1536, rates 8,8,4,2: 512

@@ -1048,7 +1048,13 @@ struct Planner {
         int skip_k = -1, skip_q = -1, skip_v = -1;
         // V = cont_{3,4}d(transpose(view of a [dims, positions] cache)) (Orpheus model.cpp:265-272): read the
         // transposed cache in place, V'(p, d, h, b) = T(p, d + hd*h, b); the per-step transpose copy disappears
-        if (V->op == TTS_OP_CONT && uses[V] == 1 && V->src[0] && V->src[0]->data) {
+        // folds only read tensors whose storage outlives the graph (caches, weights, inputs): an arena
+        // tensor's memory may be handed to another node once its CONT consumer is skipped
+        auto leaf_backed = [](const tts_tensor * t) {
+            while (t->view_src) t = t->view_src;
+            return t->op == TTS_OP_NONE;
+        };
+        if (V->op == TTS_OP_CONT && uses[V] == 1 && V->src[0] && V->src[0]->data && leaf_backed(V->src[0])) {
             const tts_tensor * T = V->src[0];
             if (T->ne[3] == 1 && V->ne[0] == T->ne[0] && V->ne[1] * V->ne[2] == T->ne[1] && V->ne[3] == T->ne[2] &&
                 T->type == TTS_TYPE_F32 && V->type == TTS_TYPE_F32) {
@@ -1069,6 +1075,23 @@ struct Planner {
             K = Ka->src[0];
             skip_k = index[Ka];
         }
+        // a same-shape CONT of a (permuted) cache view (Dia model.cpp:548,592: cont(cont(permute(view))))
+        // is read in place too, so the attention never reads an arena copy its output may overlap
+        int skip_k2 = -1, skip_v2 = -1;
+        auto same_shape = [](const tts_tensor * a, const tts_tensor * b) {
+            for (int d = 0; d < 4; ++d)
+                if (a->ne[d] != b->ne[d]) return false;
+            return true;
+        };
+        if (K->op == TTS_OP_CONT && uses[K] == 1 && K->src[0] && K->src[0]->data && same_shape(K, K->src[0]) && leaf_backed(K->src[0]) &&
+            index.count(K)) {
+            skip_k2 = index[K];
+            K = K->src[0];
+        }
+        if (V->op == TTS_OP_CONT && uses[V] == 1 && V->src[0] && V->src[0]->data && same_shape(V, V->src[0]) && leaf_backed(V->src[0])) {
+            skip_v2 = index[V];
+            V = V->src[0];
+        }
         const tts_tensor * Q = Qa;
         if (Qa->op == TTS_OP_CONT && uses[Qa] == 1) {
             Q = Qa->src[0];
@@ -1088,6 +1111,25 @@ struct Planner {
         const tts_tensor * Qbase = Q->view_src ? Q->view_src : Q;
         if (overlap(O, K) || overlap(O, V) || (mask && overlap(O, mask))) return;
         if (overlap(O, Qbase) && O->data != Qbase->data) return;
+        // a folded operand is read where its skipped CONT would have copied it from: no node that
+        // still runs between that CONT and the attention (it launches at O) may write over it
+        // (the arena can hand the source's memory on once its CONT consumer has "run")
+        {
+            const int io = index[O];
+            const int mine[] = {i, index[KQ], index[KQV], index[PERM], skip_k, skip_q, skip_v, skip_k2, skip_v2};
+            // span starts at the earliest skipped CONT that read the operand (the inner one of a chain)
+            const std::pair<const tts_tensor *, int> folded[] = {
+                {K, skip_k2 >= 0 ? skip_k2 : skip_k}, {Q, skip_q}, {V, skip_v >= 0 ? skip_v : skip_v2}};
+            for (const auto & f : folded) {
+                if (f.second < 0) continue;
+                for (int j = f.second + 1; j < io; ++j) {
+                    if (act[j] < 0 || is_view(nodes[j]->op)) continue;
+                    bool own = false;
+                    for (int m : mine) own |= m == j;
+                    if (!own && overlap(nodes[j], f.first)) return;
+                }
+            }
+        }
         Item it;
         it.kind = Item::ATTN;
         it.q = Q;
@@ -1102,6 +1144,8 @@ struct Planner {
         if (skip_k >= 0) act[skip_k] = -1;
         if (skip_q >= 0) act[skip_q] = -1;
         if (skip_v >= 0) act[skip_v] = -1;
+        if (skip_k2 >= 0) act[skip_k2] = -1;
+        if (skip_v2 >= 0) act[skip_v2] = -1;
         act[index[O]] = add_item(std::move(it));
     }
 };

@@ -122,6 +122,15 @@ class OrpheusConfig(ctypes.Structure):
     ]
 
 
+class DiaConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "n_output_heads", "n_encoder_layers", "n_decoder_layers", "encoder_hidden_size", "decoder_hidden_size",
+        "encoder_attn_heads", "decoder_attn_heads", "decoder_query_heads", "head_size", "encoder_ffn_size",
+        "decoder_ffn_size", "output_vocab_size", "encoder_vocab_size", "max_generation_size",
+        "max_encoder_context_length", "weight_type", "head_type")] + [
+        ("cfg_scale", ctypes.c_float), ("seed", ctypes.c_uint64), ("arena_bytes", ctypes.c_uint64)]
+
+
 class DacConfig(ctypes.Structure):
     _fields_ = [
         ("n_codebooks", ctypes.c_int32),
@@ -210,6 +219,15 @@ def lib():
         "tts_hip_weight_get": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_repack_q4_K": (None, [vp, vp, i64, ctypes.c_int]),
         "tts_repack_q4_K_tiled": (None, [vp, vp, i64, i64, ctypes.c_int]),
+        "tts_dia_default_config": (None, [ctypes.POINTER(DiaConfig)]),
+        "tts_dia_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(DiaConfig)]),
+        "tts_dia_free": (None, [vp]),
+        "tts_dia_prefill": (ctypes.c_int, [vp, vp, i32, vp, vp]),
+        "tts_dia_decode": (ctypes.c_int, [vp, vp, vp]),
+        "tts_dia_position": (i32, [vp]),
+        "tts_dia_last_graph_nodes": (i32, [vp]),
+        "tts_dia_weight_bytes": (u64, [vp]),
+        "tts_dia_graph": (vp, [vp, ctypes.POINTER(i32)]),
         "tts_orpheus_default_config": (None, [ctypes.POINTER(OrpheusConfig)]),
         "tts_orpheus_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(OrpheusConfig)]),
         "tts_orpheus_free": (None, [vp]),
@@ -326,6 +344,66 @@ class HipBackend:
     def close(self):
         if self.ptr:
             self.L.tts_hip_backend_free(self.ptr)
+            self.ptr = None
+
+
+def dia_config(**kw):
+    cfg = DiaConfig()
+    lib().tts_dia_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Dia:
+    """Dia-1.6B runner (encoder step + CFG decoder steps) over a backend vtable."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_dia_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_dia_create failed")
+
+    def prefill(self, text_ids, audio):
+        """text_ids: byte tokens of the conditioned prompt (the unconditioned row is all padding 0)."""
+        import numpy as np
+        c = self.cfg
+        T = c.max_encoder_context_length
+        t = np.zeros((2, T), dtype=np.int32)
+        t[0, :len(text_ids)] = text_ids
+        a = np.ascontiguousarray(audio, dtype=np.int32)
+        out = np.empty((c.n_output_heads, c.output_vocab_size), dtype=np.float32)
+        st = self.L.tts_dia_prefill(self.ptr, t.ctypes.data, len(text_ids), a.ctypes.data, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"prefill failed {st}")
+        return out
+
+    def decode(self, audio):
+        import numpy as np
+        c = self.cfg
+        a = np.ascontiguousarray(audio, dtype=np.int32)
+        out = np.empty((c.n_output_heads, c.output_vocab_size), dtype=np.float32)
+        st = self.L.tts_dia_decode(self.ptr, a.ctypes.data, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"decode failed {st}")
+        return out
+
+    def position(self):
+        return self.L.tts_dia_position(self.ptr)
+
+    def weight_bytes(self):
+        return self.L.tts_dia_weight_bytes(self.ptr)
+
+    def plan_stats(self, mask=None):
+        n = ctypes.c_int32()
+        p = self.L.tts_dia_graph(self.ptr, ctypes.byref(n))
+        return plan_stats(p, n.value, FUSE_ALL if mask is None else mask)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_dia_free(self.ptr)
             self.ptr = None
 
 
