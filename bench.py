@@ -9,9 +9,9 @@ per prompt.  After the K timed steps every prompt's K codec frames are decoded t
 decoder inside the same timed region.  value = audio-seconds produced by all ranks / wall seconds
 (RTF^-1) of AR + DAC; the AR-only and DAC-only rates are reported beside it.
 
-Beside the headline line's fields, two more legs of BASELINE.json's configs run on the same GPU:
-"kokoro" (configs[1], the Kokoro-82M iSTFTNet vocoder path) and "orpheus" (configs[4]'s per-GPU
-shard, Orpheus-3B Q4_K decode), each with its own rate; the orpheus leg carries the dequant-GEMV
+Beside the headline line's fields, three more legs of BASELINE.json's configs run on the same GPU:
+"kokoro" (configs[1], the Kokoro-82M iSTFTNet vocoder path), "dia" (configs[3], Dia-1.6B Q8_0 CFG
+decode) and "orpheus" (configs[4]'s per-GPU shard, Orpheus-3B Q4_K decode), each with its own rate; the orpheus leg carries the dequant-GEMV
 roofline at the sizes where the matrix-core GEMV streams (every Orpheus matrix is >= 4 MiB).
 
 Multi-GPU: one process per GPU (torchrun); prompts shard with no data-path collective; RCCL
@@ -239,6 +239,30 @@ def orpheus_leg(be, args, rank):
         o.close()
 
 
+def dia_leg(be, args):
+    """BASELINE configs[3]: Dia-1.6B Q8_0 (synthetic weights), encoder step over a Harvard-sentence
+    prompt, then timed CFG decoder steps (conditioned + unconditioned in one graph, greedy heads fed
+    back).  One step = one 9-codebook DAC frame = 512 samples at 44.1 kHz."""
+    d = ttship.Dia(be.iface(), ttship.dia_config(max_generation_size=args.dia_steps + 16))
+    try:
+        text = np.frombuffer(("\x01 " + HARVARD[0] + " " + HARVARD[1]).encode(), dtype=np.uint8).astype(np.int32)
+        t0 = time.perf_counter()
+        audio = d.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1).astype(np.int32)
+        t_enc = time.perf_counter() - t0
+        for _ in range(3):
+            audio = d.decode(audio).argmax(axis=1).astype(np.int32)
+        t0 = time.perf_counter()
+        for _ in range(args.dia_steps):
+            audio = d.decode(audio).argmax(axis=1).astype(np.int32)
+        dt = time.perf_counter() - t0
+        return {"workload": "Dia-1.6B Q8_0 CFG decode (BASELINE configs[3]), 1 prompt, synthetic weights",
+                "ms_per_step": round(1000 * dt / args.dia_steps, 3),
+                "audio_sec_per_s": round(args.dia_steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3),
+                "encoder_step_ms": round(1000 * t_enc, 1), "weight_bytes": d.weight_bytes()}
+    finally:
+        d.close()
+
+
 def kokoro_inputs(cfg, T, rank):
     """Synthetic generator inputs: decoder features, a voiced F0 contour with unvoiced gaps, a
     style vector and the uniform noise draws (seeded per rank)."""
@@ -268,11 +292,13 @@ def main():
                     "backend/stream with batch/replicas prompts (the server's worker model)")
     ap.add_argument("--kv-prefetch", type=int, default=None, help="TTS_HIP_OPT_KV_PREFETCH: min KV length (0 = off)")
     ap.add_argument("--kv-prefetch-blocks", type=int, default=None)
+    ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
     ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
+    ap.add_argument("--dia-steps", type=int, default=32, help="timed Dia-1.6B decoder steps per GPU (0 = skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
@@ -290,6 +316,8 @@ def main():
         if args.no_fusion:
             rb.set_option(0, 0)
         rb.set_option(2, args.graphs)
+        if args.conv_acc is not None:
+            rb.set_option(ttship.OPT["CONV_F32ACC"], args.conv_acc)
         if args.attn_split is not None:
             rb.set_option(ttship.OPT["ATTN_SPLIT"], args.attn_split)
         if args.kv_prefetch is not None:
@@ -372,6 +400,13 @@ def main():
         ores["ms_per_step"] = t
         ores["tokens_per_s"] = round(world * args.orpheus_batch * 1000.0 / t, 1)
         ores["audio_sec_per_s"] = round(ores["tokens_per_s"] / ORPHEUS_TOK_PER_AUDIO_S, 3)
+    dres = None
+    if args.dia_steps > 0:
+        barrier_sync(dist, be)
+        dres = dia_leg(be, args)
+        t = max_over_ranks(dist, local, dres["ms_per_step"])
+        dres["ms_per_step"] = t
+        dres["audio_sec_per_s"] = round(world * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
     dt = max_over_ranks(dist, local, t2 - t0)
     dt_ar = max_over_ranks(dist, local, t1 - t0)
     dt_dac = max_over_ranks(dist, local, t2 - t1)
@@ -412,6 +447,7 @@ def main():
             "host_us_per_step": host,
             "kokoro": kres,
             "orpheus": ores,
+            "dia": dres,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

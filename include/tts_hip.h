@@ -213,7 +213,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_FUSION = 0,      /* TTS_FUSE_* bitmask of enabled patterns (default: all bits, 0 = off) */
     TTS_HIP_OPT_PROFILE_GEMV = 1, /* 1 = time quantized GEMV launches with HIP events */
     TTS_HIP_OPT_GRAPHS = 2,       /* 1 = replay each graph_compute as a HIP graph (capture + exec update) */
-    TTS_HIP_OPT_CONV_F32ACC = 3,  /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity) */
+    TTS_HIP_OPT_CONV_F32ACC = 3,  /* 1 = conv GEMMs accumulate in f32 on f16 MFMA (default 0: f64, PCM parity);
+                                     2 = fused conv_1d on f16 MFMA per 32-term batch, batches summed in f64 */
     TTS_HIP_OPT_CONVT_LDS = 4,    /* 1 (default) = conv_transpose_1d on the LDS-staged f64 MFMA kernel, 0 = per-wave kernel */
     TTS_HIP_OPT_ATTN_SPLIT = 5,   /* decode attention over P >= value keys runs as two position/dim-split kernels
                                      (scores, then softmax + P.V); 0 = always the one-workgroup-per-head kernel */

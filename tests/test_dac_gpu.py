@@ -9,6 +9,7 @@ import ttship
 CFGS = {
     "tiny": dict(latent_dim=64, decoder_dim=64, rates=[2, 2, 2, 2], n_layers=4, max_frames=16),
     "dac44k_narrow": dict(latent_dim=256, decoder_dim=384, rates=[8, 8, 4, 2], n_layers=4, max_frames=8),
+    "dac44k": dict(max_frames=4),
 }
 
 
@@ -21,14 +22,22 @@ def decode(iface, cfg, codes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,T", [("tiny", 6), ("dac44k_narrow", 4)])
-def test_dac_pcm_matches_oracle(hip, name, T):
+@pytest.mark.parametrize("acc", [0, 2])  # TTS_HIP_OPT_CONV_F32ACC: f64 MFMA (default) / f16 MFMA per 32 terms + f64
+@pytest.mark.parametrize("name,T", [("tiny", 6), ("dac44k_narrow", 4), ("dac44k", 3)])
+def test_dac_pcm_matches_oracle(hip, name, T, acc):
     cfg = ttship.dac_config(**CFGS[name])
     codes = np.random.default_rng(11).integers(0, cfg.codebook_size, size=(T, cfg.n_codebooks))
-    gpu = decode(hip.iface(), cfg, codes)
+    hip.set_option(ttship.OPT["CONV_F32ACC"], acc)
+    try:
+        gpu = decode(hip.iface(), cfg, codes)
+    finally:
+        hip.set_option(ttship.OPT["CONV_F32ACC"], 0)
     ref = decode(py_oracle.iface(8), cfg, codes)
-    assert gpu.shape == ref.shape == (T * int(np.prod(CFGS[name]["rates"])),)
+    assert gpu.shape == ref.shape == (T * int(np.prod(list(cfg.rates)[:cfg.n_layers])),)
     assert np.all(np.isfinite(gpu))
     err = float(np.max(np.abs(gpu.astype(np.float64) - ref)))
-    assert err <= 1e-4, f"max |pcm_gpu - pcm_oracle| = {err:.3e}"
+    print(f"dac {name} acc {acc} max err {err:.3e}")
+    # the north_star bar holds for the default (f64) accumulation; mode 2 is a speed option whose
+    # per-32-term f32 rounding flips downstream f16 re-roundings (measured 1.4e-3 on DAC-44k)
+    assert err <= (1e-4 if acc == 0 else 5e-3), f"max |pcm_gpu - pcm_oracle| = {err:.3e}"
     assert float(np.std(ref)) > 0.05  # not a degenerate (saturated / silent) decoder

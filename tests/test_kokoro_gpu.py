@@ -25,16 +25,22 @@ def run(iface, cfg, args):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("acc", [0, 2])  # TTS_HIP_OPT_CONV_F32ACC (see test_dac_gpu.py)
 @pytest.mark.parametrize("name,T,seed", [("tiny", 4, 0), ("tiny", 7, 1), ("narrow", 9, 2), ("kokoro82m", 4, 3)])
-def test_kokoro_generator_pcm_matches_oracle(hip, name, T, seed):
+def test_kokoro_generator_pcm_matches_oracle(hip, name, T, seed, acc):
     cfg = ttship.kokoro_gen_config(**CFGS[name])
     args = inputs(cfg, T, seed)
-    gpu = run(hip.iface(), cfg, args)
+    hip.set_option(ttship.OPT["CONV_F32ACC"], acc)
+    try:
+        gpu = run(hip.iface(), cfg, args)
+    finally:
+        hip.set_option(ttship.OPT["CONV_F32ACC"], 0)
     ref = run(py_oracle.iface(8), cfg, args)
     assert gpu.shape == ref.shape == (300 * T,)
     assert np.all(np.isfinite(gpu))
     err = float(np.max(np.abs(gpu.astype(np.float64) - ref)))
-    assert err <= 1e-4, f"max |pcm_gpu - pcm_oracle| = {err:.3e}"
+    print(f"kokoro {name} acc {acc} max err {err:.3e}")
+    assert err <= (1e-4 if acc == 0 else 1e-3), f"max |pcm_gpu - pcm_oracle| = {err:.3e}"  # mode 2: see test_dac_gpu.py
     assert float(np.std(ref)) > 1e-2
 
 

@@ -375,7 +375,10 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_CONVT_LDS: be->convt_lds = value != 0; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
-        case TTS_HIP_OPT_CONV_F32ACC: be->conv_f32acc = value != 0; return 0;
+        case TTS_HIP_OPT_CONV_F32ACC:
+            be->conv_f32acc = value == 1;
+            be->conv_acc_mode = value == 2 ? 2 : 0;
+            return 0;
         case TTS_HIP_OPT_ATTN_SPLIT: be->attn_split_minp = value; return 0;
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;

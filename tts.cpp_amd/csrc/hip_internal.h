@@ -275,6 +275,7 @@ struct tts_hip_backend {
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
     bool conv_f32acc = false;  // conv GEMM on f16 MFMA with f32 accumulation (faster, misses the PCM bar)
+    int conv_acc_mode = 0;     // fused conv_1d: 0 = f64 MFMA, 2 = f16 MFMA per 32-term batch + f64 accumulation
     hipGraphExec_t gexec = nullptr;
     hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;

@@ -243,7 +243,12 @@ bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node) {
 // + 63*s + (K-1)*d, icc channels) and the kernel slice (64 channels x icc*K taps) are staged in
 // LDS as f16-rounded floats; a per-r offset table maps r to its x-window slot (r >= R points at
 // a zero slot) so the MFMA loop does no division.
-template <bool W16, bool BIAS, bool RES>
+// H32: the f16 matrix cores instead (v_mfma_f32_16x16x32_f16, 32x the f64 MFMA's K per cycle): each
+// 32-wide reduction batch is one MFMA into a zeroed f32 accumulator -- its products are exact and
+// only the 32-term sum rounds -- and the batch result is added to the f64 accumulator, so the
+// rounding stays per 32 terms instead of compounding over the whole K (TTS_HIP_OPT_CONV_F32ACC 2).
+typedef _Float16 h16x8_t __attribute__((ext_vector_type(8)));
+template <bool W16, bool BIAS, bool RES, bool H32 = false>
 __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
     extern __shared__ float sm[];
     __shared__ int xoff[CONV1D_MAX_R];  // r -> x-window slot (ic*xw + k*d), zero slot past R
@@ -332,6 +337,31 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
         // batches of 8 reduction quads: every operand of the batch is read from LDS first (the
         // offset-table reads, then the dependent operand reads, all independent of each other),
         // then 32 MFMAs issue back to back
+        if (H32) {
+            for (int r0 = 0; r0 < Rp; r0 += 32) {
+                // lane (c16, kq) holds A[row c16][r0 + 8kq + j] and B[r0 + 8kq + j][col c16], j = 0..7
+                int xo[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xo[u] = xoff[r0 + 8 * kq + u];
+                h16x8_t A[2], B[2];
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const bool z = xo[u] == zslot;
+                        A[t][u] = (_Float16)ws[(wr0 + 16 * t + c16) * rs + r0 + 8 * kq + u];  // f16-rounded: exact
+                        B[t][u] = (_Float16)xs[z ? zslot : xo[u] + (wc0 + 16 * t + c16) * s];
+                    }
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int tj = 0; tj < 2; ++tj) {
+                        const f32x4 pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(A[ti], B[tj], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc[ti][tj][e] += (double)pr[e];
+                    }
+            }
+        } else
         for (int r0 = 0; r0 < Rp; r0 += 32) {
             int xo[8];
 #pragma unroll
@@ -363,7 +393,8 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
     for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            const int oc = min(oc0 + wr0 + 16 * ti + kq + 4 * e, (int)a.OC - 1);
+            // accumulator row of register e: f64 MFMA (lane >> 4) + 4e, f32 MFMA 4 (lane >> 4) + e
+            const int oc = min(oc0 + wr0 + 16 * ti + (H32 ? 4 * kq + e : kq + 4 * e), (int)a.OC - 1);
             bv[ti][e] = BIAS ? a.bias[(int64_t)oc * a.bcs] : 0.f;
 #pragma unroll
             for (int tj = 0; tj < 2; ++tj) {
@@ -379,7 +410,7 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
         for (int ti = 0; ti < 2; ++ti)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const int oc = oc0 + wr0 + 16 * ti + kq + 4 * e;
+                const int oc = oc0 + wr0 + 16 * ti + (H32 ? 4 * kq + e : kq + 4 * e);
                 if (oc >= a.OC) continue;
                 float v = (float)acc[ti][tj][e];
                 if (BIAS) v = v + bv[ti][e];
@@ -411,7 +442,17 @@ void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a) {
     }
     const dim3 grid((unsigned)((a.OL + 63) / 64), (unsigned)((a.OC + 63) / 64));
     const int sel = (a.w16 ? 4 : 0) | (a.bias ? 2 : 0) | (a.res ? 1 : 0);
-    switch (sel) {
+    if (be->conv_acc_mode == 2) switch (sel) {
+        case 0: hipLaunchKernelGGL((k_conv1d_f64<false, false, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 1: hipLaunchKernelGGL((k_conv1d_f64<false, false, true, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 2: hipLaunchKernelGGL((k_conv1d_f64<false, true, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 3: hipLaunchKernelGGL((k_conv1d_f64<false, true, true, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 4: hipLaunchKernelGGL((k_conv1d_f64<true, false, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 5: hipLaunchKernelGGL((k_conv1d_f64<true, false, true, true>), grid, dim3(256), lds, be->stream, a); break;
+        case 6: hipLaunchKernelGGL((k_conv1d_f64<true, true, false, true>), grid, dim3(256), lds, be->stream, a); break;
+        default: hipLaunchKernelGGL((k_conv1d_f64<true, true, true, true>), grid, dim3(256), lds, be->stream, a); break;
+    }
+    else switch (sel) {
         case 0: hipLaunchKernelGGL((k_conv1d_f64<false, false, false>), grid, dim3(256), lds, be->stream, a); break;
         case 1: hipLaunchKernelGGL((k_conv1d_f64<false, false, true>), grid, dim3(256), lds, be->stream, a); break;
         case 2: hipLaunchKernelGGL((k_conv1d_f64<false, true, false>), grid, dim3(256), lds, be->stream, a); break;
