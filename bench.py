@@ -249,11 +249,11 @@ def dia_leg(be, args):
         t0 = time.perf_counter()
         audio = d.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1).astype(np.int32)
         t_enc = time.perf_counter() - t0
-        for _ in range(3):
-            audio = d.decode(audio).argmax(axis=1).astype(np.int32)
+        audio = d.generate(audio, 3)[-1]  # warm (plans, code objects)
+        be.sync()
         t0 = time.perf_counter()
-        for _ in range(args.dia_steps):
-            audio = d.decode(audio).argmax(axis=1).astype(np.int32)
+        d.generate(audio, args.dia_steps)  # device-resident greedy loop
+        be.sync()
         dt = time.perf_counter() - t0
         return {"workload": "Dia-1.6B Q8_0 CFG decode (BASELINE configs[3]), 1 prompt, synthetic weights",
                 "ms_per_step": round(1000 * dt / args.dia_steps, 3),

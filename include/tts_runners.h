@@ -150,6 +150,10 @@ void tts_dia_free(tts_dia * p);
 int tts_dia_prefill(tts_dia * p, const int32_t * text, int32_t n_text, const int32_t * audio, float * logits);
 /* One decoder step: audio [n_output_heads] -> logits [n_output_heads][vocab]. */
 int tts_dia_decode(tts_dia * p, const int32_t * audio, float * logits);
+/* Greedy decode loop: feeds first_audio [n_output_heads], then each step's per-head argmax of the CFG
+ * logits (both CFG rows); writes tokens [n_steps][n_output_heads].  Device-resident when the backend
+ * offers plans + greedy_step. */
+int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_t n_steps, int32_t * tokens_out);
 int32_t tts_dia_position(const tts_dia * p);
 int32_t tts_dia_last_graph_nodes(const tts_dia * p);
 uint64_t tts_dia_weight_bytes(const tts_dia * p);

@@ -31,3 +31,20 @@ def test_dia_tiny_deterministic_and_finite():
     assert np.isfinite(a).all() and a.shape == (5, 9, 1028)
     # per decoder layer: self-attention over the transposed V cache and cross-attention fused
     assert st["attn"] == 2 * TINY["n_decoder_layers"], st
+
+
+def test_dia_generate_matches_decode_loop():
+    text = np.frombuffer(b"\x01 hi.", dtype=np.uint8).astype(np.int32)
+    a = ttship.Dia(py_oracle.iface(4), ttship.dia_config(**TINY))
+    b = ttship.Dia(py_oracle.iface(4), ttship.dia_config(**TINY))
+    try:
+        first = a.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1).astype(np.int32)
+        b.prefill(text, np.full(9, 1026, dtype=np.int32))
+        toks = a.generate(first, 5)
+        audio = first
+        for s in range(5):
+            audio = b.decode(audio).argmax(axis=1).astype(np.int32)
+            assert np.array_equal(audio, toks[s])
+    finally:
+        a.close()
+        b.close()

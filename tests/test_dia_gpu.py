@@ -42,3 +42,20 @@ def test_dia_tiny(hip):
 @pytest.mark.gpu
 def test_dia_wide_two_layers(hip):
     run_pair(hip, WIDE, 3)
+
+
+@pytest.mark.gpu
+def test_dia_generate_device_loop(hip):
+    """The device-resident greedy loop (plans + greedy_step) gives the oracle's host-loop tokens."""
+    g = ttship.Dia(hip.iface(), ttship.dia_config(**TINY))
+    c = ttship.Dia(py_oracle.iface(16), ttship.dia_config(**TINY))
+    try:
+        text = np.frombuffer(b"\x01 It's easy to tell the depth.", dtype=np.uint8).astype(np.int32)[:32]
+        first = c.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1).astype(np.int32)
+        assert np.array_equal(g.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1), first)
+        tg, tc = g.generate(first, 12), c.generate(first, 12)
+        assert np.array_equal(tg, tc), f"{tg}\n{tc}"
+        assert g.position() == c.position() == 13
+    finally:
+        g.close()
+        c.close()

@@ -365,7 +365,7 @@ static tts_tensor * build_graph(tts_dia * p, bool encoder_step) {
     return logits;
 }
 
-static int run_step(tts_dia * p, bool encoder_step, const int32_t * text, int32_t n_text, const int32_t * audio, float * logits) {
+static int prepare(tts_dia * p, bool encoder_step) {
     const auto & cf = p->cfg;
     if (p->position + 1 > cf.max_generation_size) return TTS_STATUS_BAD_ARG;
     p->res = build_graph(p, encoder_step);
@@ -374,8 +374,14 @@ static int run_step(tts_dia * p, bool encoder_step, const int32_t * text, int32_
         return TTS_STATUS_ALLOC_FAILED;
     }
     p->last_nodes = (int32_t)p->gctx.nodes.size();
+    return 0;
+}
+
+static int run_step(tts_dia * p, bool encoder_step, const int32_t * text, int32_t n_text, const int32_t * audio, float * logits) {
+    const auto & cf = p->cfg;
+    int st = prepare(p, encoder_step);
+    if (st != 0) return st;
     auto & be = p->be;
-    int st = 0;
     if (encoder_step) {
         // set_inputs (model.cpp:722-737): text ids for (cond, uncond), positions, padded-block mask
         const int64_t T = cf.max_encoder_context_length;
@@ -415,6 +421,77 @@ extern "C" int tts_dia_prefill(tts_dia * p, const int32_t * text, int32_t n_text
 extern "C" int tts_dia_decode(tts_dia * p, const int32_t * audio, float * logits) {
     if (p->prompt_size == 0) return TTS_STATUS_FAILED;
     return run_step(p, false, nullptr, 0, audio, logits);
+}
+
+// generate loop with greedy heads (sampler::max per head, fed back as the next step's tokens for
+// both CFG rows): on a backend with graph plans and greedy_step, step s+1 is recorded while the
+// device runs step s and the samples never leave the device until the end.  tokens_out [steps][heads].
+extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_t n_steps, int32_t * tokens_out) {
+    const auto & cf = p->cfg;
+    auto & be = p->be;
+    const int NH = cf.n_output_heads;
+    if (p->prompt_size == 0 || n_steps <= 0) return n_steps <= 0 ? 0 : TTS_STATUS_FAILED;
+    if (!(be.greedy_step && be.set_async && be.copy && be.prepare && be.launch)) {
+        std::vector<float> lg((size_t)NH * cf.output_vocab_size);
+        std::vector<int32_t> a(first_audio, first_audio + NH);
+        for (int s = 0; s < n_steps; ++s) {
+            const int st = run_step(p, false, nullptr, 0, a.data(), lg.data());
+            if (st != 0) return st;
+            for (int h = 0; h < NH; ++h) {
+                const float * l = lg.data() + (size_t)h * cf.output_vocab_size;
+                int best = 0;
+                for (int i = 1; i < cf.output_vocab_size; ++i)
+                    if (l[i] > l[best]) best = i;
+                a[h] = tokens_out[(size_t)s * NH + h] = best;
+            }
+        }
+        return 0;
+    }
+    const size_t rowi = (size_t)NH * sizeof(int32_t);
+    int32_t * d_seen = (int32_t *)be.alloc(be.ctx, rowi);
+    int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
+    int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
+    int st = (d_seen && d_next && d_hist) ? 0 : TTS_STATUS_ALLOC_FAILED;
+    if (st == 0) st = be.memset(be.ctx, d_seen, 0, rowi);
+    std::vector<int32_t> a2((size_t)NH * 2);
+    for (int h = 0; h < NH; ++h) a2[h] = a2[NH + h] = first_audio[h];
+    auto launch = [&](int slot, bool host_tokens) {
+        int r = host_tokens ? be.set_async(be.ctx, p->in_audio->data, a2.data(), a2.size() * sizeof(int32_t)) : 0;
+        const int32_t pp = p->position;
+        if (r == 0) r = be.set_async(be.ctx, p->in_pos->data, &pp, sizeof(int32_t));
+        if (r == 0) r = be.launch(be.ctx, slot);
+        if (r == 0) p->position += 1;
+        return r;
+    };
+    void * out = nullptr;
+    if (st == 0) st = prepare(p, false);
+    if (st == 0) st = be.prepare(be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size(), 0);
+    if (st == 0) {
+        out = p->res->data;
+        st = launch(0, true);
+    }
+    for (int s = 0; st == 0 && s < n_steps; ++s) {
+        const int slot = (s + 1) & 1;
+        void * next_out = nullptr;
+        if (s + 1 < n_steps) {  // record step s+1 while the device runs step s
+            st = prepare(p, false);
+            if (st == 0) st = be.prepare(be.ctx, p->gctx.nodes.data(), (int)p->gctx.nodes.size(), slot);
+            next_out = p->res->data;
+        }
+        // step = NH: past every head's delay, so next = the sample itself (eos -1 never matches)
+        if (st == 0) st = be.greedy_step(be.ctx, (const float *)out, 1, NH, cf.output_vocab_size, NH, 0, -1, d_seen, d_hist + (size_t)s * NH, d_next);
+        if (st == 0 && s + 1 < n_steps) {
+            st = be.copy(be.ctx, p->in_audio->data, d_next, rowi);
+            if (st == 0) st = be.copy(be.ctx, (int32_t *)p->in_audio->data + NH, d_next, rowi);
+            if (st == 0) st = launch(slot, false);
+            out = next_out;
+        }
+    }
+    if (st == 0) st = be.get(be.ctx, tokens_out, d_hist, rowi * (size_t)n_steps);
+    if (d_seen) be.free(be.ctx, d_seen);
+    if (d_next) be.free(be.ctx, d_next);
+    if (d_hist) be.free(be.ctx, d_hist);
+    return st;
 }
 
 extern "C" int32_t tts_dia_position(const tts_dia * p) { return p->position; }

@@ -224,6 +224,7 @@ def lib():
         "tts_dia_free": (None, [vp]),
         "tts_dia_prefill": (ctypes.c_int, [vp, vp, i32, vp, vp]),
         "tts_dia_decode": (ctypes.c_int, [vp, vp, vp]),
+        "tts_dia_generate": (ctypes.c_int, [vp, vp, i32, vp]),
         "tts_dia_position": (i32, [vp]),
         "tts_dia_last_graph_nodes": (i32, [vp]),
         "tts_dia_weight_bytes": (u64, [vp]),
@@ -388,6 +389,15 @@ class Dia:
         st = self.L.tts_dia_decode(self.ptr, a.ctypes.data, out.ctypes.data)
         if st != 0:
             raise RuntimeError(f"decode failed {st}")
+        return out
+
+    def generate(self, first_audio, n_steps):
+        import numpy as np
+        a = np.ascontiguousarray(first_audio, dtype=np.int32)
+        out = np.empty((n_steps, self.cfg.n_output_heads), dtype=np.int32)
+        st = self.L.tts_dia_generate(self.ptr, a.ctypes.data, n_steps, out.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"generate failed {st}")
         return out
 
     def position(self):
