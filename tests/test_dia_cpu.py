@@ -31,6 +31,7 @@ def test_dia_tiny_deterministic_and_finite():
     assert np.isfinite(a).all() and a.shape == (5, 9, 1028)
     # per decoder layer: self-attention over the transposed V cache and cross-attention fused
     assert st["attn"] == 2 * TINY["n_decoder_layers"], st
+    assert st["rint"] == 2 * TINY["n_decoder_layers"], st  # K and V repeat_interleave chains: one pass each
 
 
 def test_dia_generate_matches_decode_loop():

@@ -103,7 +103,7 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT } kind;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -138,6 +138,8 @@ struct Item {
     // ADAIN: per-channel norm + affine (+ snake)
     AdainArgs adain{};
     // MCPY: src (x) copied into every view in `terms`
+    // RINT: dst = repeat_interleave of x along dim 1 by `rint`
+    int rint = 1;
 };
 
 struct Planner {
@@ -184,6 +186,9 @@ struct Planner {
             }
         }
         if (mask & TTS_FUSE_LSTM) try_lstm();
+        if (mask & TTS_FUSE_MCPY)  // roots first: a concat chain is claimed whole by its last CONCAT
+            for (int i = n - 1; i >= 0; --i)
+                if (act[i] == 0 && nodes[i]->op == TTS_OP_CONCAT) try_rint(i);
         if (mask & TTS_FUSE_EMBED)  // roots first: a chain is claimed whole by its last ADD
             for (int i = n - 1; i >= 0; --i)
                 if (act[i] == 0 && nodes[i]->op == TTS_OP_ADD) try_embed(i);
@@ -961,6 +966,64 @@ struct Planner {
         members.push_back(index[r]);
         return true;
     }
+    // repeat_interleave_dim1 (Dia model.cpp:421-434): CONCAT(dim 1) over REPEAT(CONT(VIEW(a, slice i
+    // of dim 1))) for i = 0..n-1 -> one pass, dst(i0, i1, i2, i3) = a(i0, i1 / r, i2, i3)
+    void try_rint(int i) {
+        const tts_tensor * R = nodes[i];
+        if (R->type != TTS_TYPE_F32 || R->op_params[0] != 1 || !contiguous(R)) return;
+        std::vector<const tts_tensor *> leaves;
+        std::vector<int> members{i};
+        const tts_tensor * t = R;
+        while (t->op == TTS_OP_CONCAT && t->op_params[0] == 1) {
+            leaves.push_back(t->src[1]);
+            t = t->src[0];
+            if (t->op == TTS_OP_CONCAT) {
+                if (uses[t] != 1 || !index.count(t)) return;
+                members.push_back(index[t]);
+            }
+        }
+        leaves.push_back(t);
+        std::reverse(leaves.begin(), leaves.end());
+        const tts_tensor * a = nullptr;
+        int64_t r = 0;
+        for (size_t k = 0; k < leaves.size(); ++k) {
+            const tts_tensor * rp = leaves[k];
+            if (rp->op != TTS_OP_REPEAT || uses[rp] != 1 || !index.count(rp)) return;
+            const tts_tensor * c = rp->src[0];
+            if (!c || c->op != TTS_OP_CONT || uses[c] != 1 || !index.count(c)) return;
+            const tts_tensor * v = c->src[0];
+            if (!v || v->op != TTS_OP_VIEW || !v->view_src || v->ne[1] != 1) return;
+            const tts_tensor * base = v->view_src;
+            if (k == 0) {
+                a = base;
+                r = rp->ne[1];
+                if (a->type != TTS_TYPE_F32 || (int64_t)leaves.size() != a->ne[1]) return;
+            }
+            if (base != a || rp->ne[1] != r || (const char *)v->data != (const char *)a->data + k * a->nb[1]) return;
+            for (int d = 0; d < 4; ++d)
+                if (d != 1 && (v->ne[d] != a->ne[d] || v->nb[d] != a->nb[d] || rp->ne[d] != a->ne[d])) return;
+            members.push_back(index[rp]);
+            members.push_back(index[c]);
+        }
+        if (!a || R->ne[1] != a->ne[1] * r || overlap(R, a)) return;
+        for (int m : members)
+            if (act[m] != 0) return;
+        // a is read at R's position: nothing that still runs after a's first (skipped) reader may
+        // have been given a's arena memory
+        const int first = *std::min_element(members.begin(), members.end());
+        for (int j = first + 1; j < i; ++j) {
+            if (is_view(nodes[j]->op) || std::find(members.begin(), members.end(), j) != members.end()) continue;
+            if (overlap(nodes[j], a)) return;
+        }
+        Item it;
+        it.kind = Item::RINT;
+        it.x = a;
+        it.dst = R;
+        it.rint = (int)r;
+        for (int m : members) act[m] = -1;
+        act[i] = add_item(std::move(it));
+    }
+
     void try_embed(int i) {
         const tts_tensor * R = nodes[i];
         if (!contiguous(R)) return;
@@ -1361,6 +1424,9 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             return 0;
         case Item::MCPY:
             launch_cpy_multi(be, it.x, it.terms.data(), (int)it.terms.size());
+            return 0;
+        case Item::RINT:
+            launch_repeat_interleave1(be, it.dst, it.x, it.rint);
             return 0;
         case Item::LSTM:
             if (it.lkind & 1) {

@@ -49,6 +49,24 @@ void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_te
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+// dst(i0, i1, i2, i3) = a(i0, i1 / r, i2, i3): the planner's RINT item (Dia's repeat_interleave_dim1
+// chain of view / cont / repeat / concat nodes, model.cpp:421-434) in one pass; pure copies.
+__global__ void k_repeat_interleave1(TD dst, TD a, int r, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i0, i1, i2, i3;
+        unravel(k, dst.ne, i0, i1, i2, i3);
+        td_store(dst, i0, i1, i2, i3, td_load(a, i0, i1 / r, i2, i3));
+    }
+}
+
+void launch_repeat_interleave1(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * a, int r) {
+    const int64_t n = dst->ne[0] * dst->ne[1] * dst->ne[2] * dst->ne[3];
+    if (n == 0) return;
+    const int64_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_repeat_interleave1, dim3((unsigned)(g < 4096 ? g : 4096)), dim3(256), 0, be->stream, make_td(dst), make_td(a), r, n);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 // ---- binary with broadcast of src1 (ggml_can_repeat) ----
 template <int OP>
 __global__ void k_binary(TD dst, TD a, TD b, int64_t n) {

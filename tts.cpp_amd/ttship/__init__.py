@@ -726,7 +726,7 @@ class KokoroGenerator:
             self.ptr = None
 
 
-PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy"]
+PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy", "rint"]
 
 
 def plan_stats(nodes_ptr, n_nodes, mask):
