@@ -10,7 +10,7 @@ timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_o
 timeout -k 10 600 python3 bench.py > gpurun_out/bench_full.log 2>&1 || { tail -5 gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/bench_full.log; exit 1; }
 tail -1 gpurun_out/pytest_gpu.log; tail -1 gpurun_out/smoke.log
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --orpheus-steps 16 > $R/gpurun_out/prof.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --orpheus-steps 16 --dia-steps 16 > $R/gpurun_out/prof.log 2>&1 || exit 1
 cd $R
 bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1
 rc=$?
