@@ -10,7 +10,8 @@ is doubled; WRITE_SIZE is taken as reported.
 Only the decode-step dispatches the bench's own roofline samples are kept: the last N launches of
 the kernel, N = roofline.launches_sampled of the bench line in FETCH_DIR/../pmc_fetch.log.
 
-usage: pmc_gemv.py FETCH_DIR WRITE_DIR OUT_JSON [kernel-substring]
+usage: pmc_gemv.py FETCH_DIR WRITE_DIR OUT_JSON [kernel-substring [last-N [command]]]
+(an explicit last-N replaces the bench line's launches_sampled, e.g. for the Orpheus leg)
 """
 import csv
 import glob
@@ -46,7 +47,10 @@ def sampled_launches(log):
 def main():
     fdir, wdir, out = sys.argv[1:4]
     pat = sys.argv[4] if len(sys.argv) > 4 else "k_gemv_q4_K"
-    last = sampled_launches(fdir.rstrip("/") + ".log")
+    last = int(sys.argv[5]) if len(sys.argv) > 5 else sampled_launches(fdir.rstrip("/") + ".log")
+    cmd = sys.argv[6] if len(sys.argv) > 6 else (
+        "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --stats -- python3 bench.py --steps 10 "
+        "--warmup 2 --no-cpu-baseline --no-dac --graphs 0 --ctx 16 (decode dispatches only)")
     f, nf, fs = per_kernel(fdir, "FETCH_SIZE", pat, last)
     w, nw, ws = per_kernel(wdir, "WRITE_SIZE", pat, last)
     if not nf or not nw:
@@ -59,7 +63,7 @@ def main():
            "per_shape_hbm_bytes": {k: round(2048.0 * sum(v) / len(v) + 1024.0 * sum(ws.get(k, [0])) / max(len(ws.get(k, [])), 1), 1)
                                    for k, v in fs.items()},
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane streaming reads); WRITE_SIZE KiB x1024",
-           "command": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-dac --graphs 0 --ctx 16 (decode dispatches only)"}
+           "launches_kept": last, "command": cmd}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
