@@ -293,6 +293,7 @@ def main():
     ap.add_argument("--kv-prefetch", type=int, default=None, help="TTS_HIP_OPT_KV_PREFETCH: min KV length (0 = off)")
     ap.add_argument("--kv-prefetch-blocks", type=int, default=None)
     ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
+    ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
     ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
@@ -322,6 +323,8 @@ def main():
             rb.set_option(ttship.OPT["ATTN_SPLIT"], args.attn_split)
         if args.kv_prefetch is not None:
             rb.set_option(ttship.OPT["KV_PREFETCH"], args.kv_prefetch)
+        if args.gemv_unique is not None:
+            rb.set_option(ttship.OPT["GEMV_UNIQUE"], args.gemv_unique)
         if args.kv_prefetch_blocks is not None:
             rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
         rr = ttship.Parler(rb.iface(), cfg)

@@ -226,6 +226,9 @@ enum tts_hip_option {
                                      MFMAs, bit-identical).  Default 4 MiB; 0 = never */
     TTS_HIP_OPT_GEMV_DEBUG = 10, /* matrix-core GEMV phase study: 1 = skip the row phase, 2 = skip the prologue
                                      (results invalid; micro-benchmarks only) */
+    TTS_HIP_OPT_GEMV_UNIQUE = 11, /* 1 (default) = lane-layout Q4_K GEMVs run the unique-load kernel (an octet per
+                                     (row, block), every weight byte loaded once, all columns per lane, ggml's chain
+                                     finished from LDS: bit-identical); 0 = the octet-per-(row, column) kernel */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

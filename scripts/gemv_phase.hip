@@ -33,6 +33,7 @@ int main() {
         {"oproj_quant_m1", 1024, 1024, 1, PRO_QUANT, 1}, {"fc2_quant_m1", 4096, 1024, 1, PRO_QUANT, 1},
     };
     tts_hip_backend be;
+    be.gemv_unique = getenv("GEMV_UNIQUE") ? atoi(getenv("GEMV_UNIQUE")) : 1;
     TTS_HIP_CHECK(hipStreamCreate(&be.stream));
     std::mt19937 rng(1);
     const size_t wbytes = 3ull * 4096 * 4096 / 256 * 144;
@@ -60,6 +61,12 @@ int main() {
     TTS_HIP_CHECK(hipMemcpy(lnw, hx.data(), 4096 * 4, hipMemcpyHostToDevice));
     TTS_HIP_CHECK(hipMemcpy(lnb, hx.data() + 4096, 4096 * 4, hipMemcpyHostToDevice));
     TTS_HIP_CHECK(hipMalloc(&ts, nts * 8));
+    // cold-cache reps: a 512 MiB write between launches evicts the weights from L2 and the
+    // Infinity Cache, as a decode step's other traffic does in the real graph
+    const bool cold = getenv("GEMV_PHASE_COLD") != nullptr;
+    void * flush = nullptr;
+    const size_t flush_bytes = (size_t)512 << 20;
+    if (cold) TTS_HIP_CHECK(hipMalloc(&flush, flush_bytes));
     hipEvent_t e0, e1;
     TTS_HIP_CHECK(hipEventCreate(&e0));
     TTS_HIP_CHECK(hipEventCreate(&e1));
@@ -86,9 +93,10 @@ int main() {
         }
         for (int w = 0; w < 5; ++w) launch_gemv_job(&be, j);
         TTS_HIP_CHECK(hipStreamSynchronize(be.stream));
-        std::vector<double> ev, span, p01, p12, p23, p3e, t0spread, endspread;
+        std::vector<double> ev, span, p01, p12, p23, p3e, t0spread, endspread, p36, p64, p45, p34, p45b;
         for (int r = 0; r < 20; ++r) {
             TTS_HIP_CHECK(hipMemsetAsync(ts, 0, nts * 8, be.stream));
+            if (cold) TTS_HIP_CHECK(hipMemsetAsync(flush, r, flush_bytes, be.stream));
             GemvJob jt = j;
             jt.ts = ts;
             TTS_HIP_CHECK(hipEventRecord(e0, be.stream));
@@ -101,7 +109,7 @@ int main() {
             std::vector<unsigned long long> h(nts);
             TTS_HIP_CHECK(hipMemcpy(h.data(), ts, nts * 8, hipMemcpyDeviceToHost));
             unsigned long long tmin = ~0ull, tmax = 0, t0max = 0, t5min = ~0ull;
-            std::vector<double> a, b, c, d;
+            std::vector<double> a, b, c, d, e6, e4, e5, f34, f45;
             for (size_t w = 0; w + 8 <= nts; w += 8) {
                 if (!h[w]) continue;
                 tmin = std::min(tmin, h[w]);
@@ -112,16 +120,27 @@ int main() {
                 b.push_back((h[w + 2] - h[w + 1]) / 100.0);
                 c.push_back((h[w + 3] - h[w + 2]) / 100.0);
                 d.push_back((h[w + 5] - h[w + 3]) / 100.0);
+                if (h[w + 4]) {
+                    f34.push_back(((long long)h[w + 4] - (long long)h[w + 3]) / 100.0);
+                    f45.push_back(((long long)h[w + 5] - (long long)h[w + 4]) / 100.0);
+                }
+                if (h[w + 6] && h[w + 4]) {
+                    e6.push_back((h[w + 6] - h[w + 3]) / 100.0);
+                    e4.push_back(((long long)h[w + 4] - (long long)h[w + 6]) / 100.0);
+                    e5.push_back((h[w + 5] - h[w + 4]) / 100.0);
+                }
             }
             span.push_back((tmax - tmin) / 100.0);
             t0spread.push_back((t0max - tmin) / 100.0);
             endspread.push_back((tmax - t5min) / 100.0);
             p01.push_back(med(a)), p12.push_back(med(b)), p23.push_back(med(c)), p3e.push_back(med(d));
+            p36.push_back(med(e6)), p64.push_back(med(e4)), p45.push_back(med(e5));
+            p34.push_back(med(f34)), p45b.push_back(med(f45));
         }
-        printf("{\"shape\":\"%s\",\"K\":%lld,\"N\":%lld,\"M\":%lld,\"nmat\":%d,\"event_us\":%.2f,\"span_us\":%.2f,"
-               "\"start_spread_us\":%.2f,\"end_spread_us\":%.2f,\"issue_us\":%.2f,\"prologue_us\":%.2f,\"barrier_us\":%.2f,\"rows_us\":%.2f}\n",
-               s.name, (long long)s.K, (long long)s.N, (long long)s.M, s.nmat, med(ev), med(span), med(t0spread), med(endspread), med(p01),
-               med(p12), med(p23), med(p3e));
+        printf("{\"cold\":%d,\"shape\":\"%s\",\"K\":%lld,\"N\":%lld,\"M\":%lld,\"nmat\":%d,\"event_us\":%.2f,\"span_us\":%.2f,"
+               "\"start_spread_us\":%.2f,\"end_spread_us\":%.2f,\"issue_us\":%.2f,\"prologue_us\":%.2f,\"barrier_us\":%.2f,\"rows_us\":%.2f,\"wait_w_us\":%.2f,\"compute_us\":%.2f,\"store_exit_us\":%.2f,\"t34_us\":%.2f,\"t45_us\":%.2f}\n",
+               (int)cold, s.name, (long long)s.K, (long long)s.N, (long long)s.M, s.nmat, med(ev), med(span), med(t0spread), med(endspread), med(p01),
+               med(p12), med(p23), med(p3e), med(p36), med(p64), med(p45), med(p34), med(p45b));
     }
     return 0;
 }

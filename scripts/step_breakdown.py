@@ -1,5 +1,11 @@
-"""Per-decode-step kernel breakdown from a rocprofv3 kernel trace of bench.py (AR only).
-Usage: step_breakdown.py trace.csv [first_step] [n_steps]"""
+"""Per-decode-step kernel breakdown from a rocprofv3 kernel trace of bench.py.
+Usage: step_breakdown.py trace.csv [first_step] [n_steps] [marker_grid]
+
+Steps are delimited by the device greedy-sampling launches (k_greedy_step*).  The bench runs the
+Parler leg first, then Orpheus / Dia; `marker_grid` (Grid_Size_X of the Parler leg's sampling
+kernel, e.g. 4608 for 8 prompts x 9 heads x 64 lanes) keeps only that leg's markers.  The step
+window is the last n_steps markers before the final `first_step` ones (the profiled roofline pass
+at the end of the leg is skipped)."""
 import collections
 import csv
 import sys
@@ -9,8 +15,12 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     first = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 30
-    g = [i for i, r in enumerate(rows) if "k_greedy_step" in r["Kernel_Name"]]
-    a, b = g[-(first + n)], g[-first]  # the last steps (skip the profiled roofline pass at the end)
+    grid = sys.argv[4] if len(sys.argv) > 4 else None
+    g = [i for i, r in enumerate(rows) if "k_greedy_step" in r["Kernel_Name"] and (grid is None or r["Grid_Size_X"] == grid)]
+    if len(g) < first + n:
+        print(f"only {len(g)} step markers")
+        n = len(g) - first - 1
+    a, b = g[-(first + n)], g[-first]
     seg = rows[a + 1:b + 1]
     span = int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])
     tot = collections.defaultdict(lambda: [0, 0])

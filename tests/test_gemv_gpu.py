@@ -143,3 +143,27 @@ def test_q4_K_mfma_extreme_blocks(hip):
     ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
     got = run_gpu_tiled(hip, w, x, N)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+
+
+KS_SHAPES = [(4096, 1024), (2048, 1024), (3072, 1024), (2560, 3072), (4096, 40), (8192, 100)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ks", [0, 1])
+@pytest.mark.parametrize("K,N", KS_SHAPES)
+@pytest.mark.parametrize("M", [1, 3, 5, 8])
+def test_q4_K_unique(hip, ks, K, N, M):
+    """Lane-layout Q4_K GEMV on the unique-load kernel (TTS_HIP_OPT_GEMV_UNIQUE = 1: an octet per
+    (row, block), ggml's chain finished in block order from LDS) and on the octet-per-(row, column)
+    kernel (0): both bit-identical to ggml's sequential order.  nb = 10 and 12 leave octets idle."""
+    lib = ttship.lib()
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_UNIQUE"], ks) == 0
+    try:
+        rng = np.random.default_rng(K * 3 + N + 11 * M + ks)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_UNIQUE"], 1)

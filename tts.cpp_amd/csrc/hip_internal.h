@@ -231,11 +231,16 @@ struct tts_hip_backend {
     float * attn_buf = nullptr;
     size_t attn_floats = 0;
     int attn_split_minp = 128;
-    // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     unsigned long long * argmax_keys = nullptr;  // k_greedy_step_wide: per-row keys / arrival counts (self-clearing)
     unsigned * argmax_counts = nullptr;
+    // weight_set: Q4_K matrices >= this size use the tile layout + matrix-core GEMV (0 = never)
     int64_t q4k_tile_bytes = 4 << 20;
-    int gemv_dbg = 0;  // tiled GEMVs with <= this many 16-row tiles: residue-split kernel  // weight_set: Q4_K matrices >= this size use the tile layout + MFMA GEMV (0 = never)
+    // TTS_HIP_OPT_GEMV_DEBUG phase-study bitmask of the matrix-core GEMV: 1 = skip the row phase,
+    // 2 = skip the prologue, 4 = plain (cached) weight loads (results invalid; micro-benchmarks only)
+    int gemv_dbg = 0;
+    // Q4_K GEMVs in the lane layout run the unique-load kernel (k_gemv_q4_K_u) where the shape fits
+    int gemv_unique = 1;
+    // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;
     hipStream_t pf_stream = nullptr;

@@ -14,6 +14,7 @@
 #include "hip_internal.h"
 #include <hip/hip_ext.h>
 
+#include <atomic>
 #include <type_traits>
 
 #ifndef TTS_GEMV_EARLY16
@@ -252,9 +253,16 @@ __device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
 // with affine (ggml_compute_forward_norm_f32 / rms_norm_f32: f64 sums, mean and variance rounded
 // to f32, scale = 1/sqrtf(var + eps), then MUL(w) and ADD(b) each rounded).
 // MF: write the MFMA kernel's f16 operand layout (q8k_row_block_mf into mf_b16 / mf_sb) instead.
-template <int PRO, int NCH, bool MF = false>
+// `mid` runs once per wave right after that wave's first activation loads are issued and before any
+// of them is used: callers issue their weight loads there.  Vector loads complete in issue order,
+// so activation loads queued behind a row of HBM weight loads would make the prologue wait for the
+// weights; issued first, they return from L2 / MALL while the weights are still in flight.
+struct NoMid {
+    __device__ void operator()() const {}
+};
+template <int PRO, int NCH, bool MF = false, typename Mid = NoMid>
 __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s,
-                                             _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr) {
+                                             _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr, Mid mid = Mid{}) {
     auto put = [&](const float (&v)[16], int lane, int slot) {
         if constexpr (MF) q8k_row_block_mf(v, lane, mf_b16 + (int64_t)slot * QK_K, mf_sb + slot * 16, xd_s + slot);
         else q8k_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
@@ -267,7 +275,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         // pass p quantizes blocks 4p..4p+3 (block qb = column m, chunk b at x + qb*256)
         constexpr int QP = NCH <= 4 ? 2 : 4;  // passes whose loads a wave keeps in flight
         const int nq = M * nb, npass = (nq + 3) / 4;
-        auto batch = [&](int p0) {
+        auto batch = [&](int p0, bool first) {
             float v[QP][16];
 #pragma unroll
             for (int u = 0; u < QP; ++u) {
@@ -276,6 +284,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 #pragma unroll
                 for (int k = 0; k < 4; ++k) ld4(src + 4 * k, *(float (*)[4]) & v[u][4 * k]);
             }
+            TTS_PIN_LOADS();
+            if (first) mid();
             TTS_PIN_LOADS();
 #pragma unroll
             for (int u = 0; u < QP; ++u) {
@@ -286,8 +296,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         };
         // the first batch is peeled out of the loop: a loop header makes the compiler wait for every
         // outstanding load, including the weight loads issued before the prologue
-        batch(wave);
-        for (int p0 = wave + nw * QP; p0 < npass; p0 += nw * QP) batch(p0);
+        batch(wave, true);
+        for (int p0 = wave + nw * QP; p0 < npass; p0 += nw * QP) batch(p0, false);
     } else {
         // one column per wave; pass p holds chunks 4p + r (K <= 4096: NP <= 4, host-checked).  For
         // K <= 1024 the affine parameters are loaded with x, so the prologue pays one L2 round trip.
@@ -308,7 +318,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
                 }
             }
         }
-        auto column = [&](int m) {
+        auto column = [&](int m, bool first) {
             const float * xr = j.x + m * j.xcs;
             float v[NP][16];
 #pragma unroll
@@ -317,6 +327,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 #pragma unroll
                 for (int k = 0; k < 4; ++k) ld4(xr + off + 4 * k, *(float (*)[4]) & v[p][4 * k]);
             }
+            TTS_PIN_LOADS();
+            if (first) mid();
             TTS_PIN_LOADS();
             float mean = 0.f;
             if (!j.rms) {
@@ -374,8 +386,9 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
                 put(v[p], lane, slot);
             }
         };
-        if (wave < M) column(wave);  // peeled, as above
-        for (int m = wave + nw; m < M; m += nw) column(m);
+        if (wave < M) column(wave, true);  // peeled, as above
+        else mid();
+        for (int m = wave + nw; m < M; m += nw) column(m, false);
     }
 }
 
@@ -383,8 +396,22 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 // 6-bit scales, sumi from the mins and the per-32 Q8_K sums, then ggml's f32 combine
 // sums[l] += d*yd*aux32[l], sumf -= dmin*yd*sumi (vec_dot_q4_K_q8_K generic order).  `xb` is the
 // Q8_K block index in LDS; an invalid (padding) block leaves the accumulators unchanged.
+// The block's two terms of that chain, p = (d*yd)*aux32[l] and q = (dmin*yd)*sumi, each rounded as
+// ggml rounds them; q4k_block folds them in (sums += p, sumf -= q), the K-split kernel hands them to
+// the wave that owns the chain.
+__device__ __forceinline__ void q4k_block_pq(const u32x4 & h, const u32x4 & qw, const int8_t * xq_s, const int16_t * xs_s,
+                                             const float * xd_s, int xb, int l, float & p, float & q);
 __device__ __forceinline__ void q4k_block(const u32x4 & h, const u32x4 & qw, const int8_t * xq_s, const int16_t * xs_s,
                                           const float * xd_s, int xb, int l, bool valid, float & sums, float & sumf) {
+    float p, q;
+    q4k_block_pq(h, qw, xq_s, xs_s, xd_s, xb, l, p, q);
+    const float ns = __fadd_rn(sums, p);
+    const float nf = __fsub_rn(sumf, q);
+    sums = valid ? ns : sums;
+    sumf = valid ? nf : sumf;
+}
+__device__ __forceinline__ void q4k_block_pq(const u32x4 & h, const u32x4 & qw, const int8_t * xq_s, const int16_t * xs_s,
+                                             const float * xd_s, int xb, int l, float & p, float & q) {
     const uint32_t A = h.y, B = h.z, C = h.w;
     // 6-bit scales / mins of the eight 32-element sub-blocks, four per word (get_scale_min_k4)
     const uint32_t sc_lo = A & 0x3F3F3F3Fu, mn_lo = B & 0x3F3F3F3Fu;
@@ -415,10 +442,8 @@ __device__ __forceinline__ void q4k_block(const u32x4 & h, const u32x4 & qw, con
     const float yd = xd_s[xb];
     const float dw = dev_fp16_to_fp32((uint16_t)(h.x & 0xFFFF));
     const float dmw = dev_fp16_to_fp32((uint16_t)(h.x >> 16));
-    const float ns = __fadd_rn(sums, __fmul_rn(__fmul_rn(dw, yd), (float)aux));
-    const float nf = __fsub_rn(sumf, __fmul_rn(__fmul_rn(dmw, yd), (float)sumi));
-    sums = valid ? ns : sums;
-    sumf = valid ? nf : sumf;
+    p = __fmul_rn(__fmul_rn(dw, yd), (float)aux);
+    q = __fmul_rn(__fmul_rn(dmw, yd), (float)sumi);
 }
 
 // sumf += sums[0..7] in order; lane l = 0 of the octet reads lane l = k by row_shl:k
@@ -489,13 +514,19 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
     // the first row's weights are in flight during the prologue (long rows with an LN prologue would
     // need more registers than it leaves, so they start after it)
     TTS_TS(j, 0);
-    if ((NBMAX <= 4 || (TTS_GEMV_EARLY16 && PRO == PRO_QUANT)) && g < G) load_row(g, 0);
-    TTS_TS(j, 1);
-    q4k_prologue<PRO, NBMAX>(j, nb, xq_s, xd_s, xs_s);
+    auto mid = [&]() {
+        if ((NBMAX <= 4 || (TTS_GEMV_EARLY16 && PRO == PRO_QUANT)) && g < G) load_row(g, 0);
+        TTS_TS(j, 1);
+    };
+    q4k_prologue<PRO, NBMAX>(j, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid);
     TTS_TS(j, 2);
     __syncthreads();
     TTS_TS(j, 3);
     if (NBMAX > 4 && !(TTS_GEMV_EARLY16 && PRO == PRO_QUANT) && g < G) load_row(g, 0);
+#ifdef TTS_PHASE_TS
+    __builtin_amdgcn_s_waitcnt(0);  // phase study only: when the first row's weights have landed
+    TTS_TS(j, 6);
+#endif
 
     for (; g < G; g += gstride) {
         float sums = 0.f, sumf = 0.f;
@@ -515,6 +546,182 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
         TTS_TS(j, 4);
         if (l == 0 && m < j.M && row < j.N && mat < j.nmat) gemv_store<MC>(j, mat, row, m, tot);
         if (g + gstride < G) load_row(g + gstride, 0);
+    }
+    TTS_TS(j, 5);
+}
+
+// ------------------------------------------------------------------------------------------
+// The same GEMV with one weight read per lane ("unique-load" kernel, the decode default for the
+// lane layout).  In k_gemv_q4_K every column's lane octet loads the row's bytes again (8x at
+// M = 8), so at Parler shapes the CU's load pipe, not HBM, sets the pace.  Here octet o of the
+// workgroup owns one (row, block) pair -- lane l loads the 16 nibble bytes of residue l and the
+// block header -- decodes scales and nibbles once and loops over the M columns: aux32[l] from
+// eight sdot4 against the Q8_K block in LDS, sumi from the per-32 sums, and ggml's two per-block
+// terms p = (d*yd)*aux32[l] and q = (dmin*yd)*sumi, rounded exactly as the sequential code rounds
+// them.  The terms go to LDS; lane (row, column, l) then runs ggml's chain over the blocks in
+// ascending order (sums[l] += p, sumf -= q, then sumf += sums[0..7]) -- the same additions in the
+// same order, so the result is bit-identical.  512 threads = 64 octets; R rows x nb blocks <= 64.
+struct Q4KLaneBlock {
+    uint32_t nib[8];  // sdot4 operands: nibbles of dword c, low (even) / high (odd) half
+    int sc[8];        // the matching 6-bit scales
+    int mn01, mn23, mn45, mn67;  // mins as int16 pairs (v_dot2 against the per-32 sums)
+    float dw, dmw;
+};
+
+__device__ __forceinline__ void q4k_lane_decode(const u32x4 & h, const u32x4 & qw, Q4KLaneBlock & o) {
+    const uint32_t A = h.y, B = h.z, C = h.w;
+    const uint32_t sc_lo = A & 0x3F3F3F3Fu, mn_lo = B & 0x3F3F3F3Fu;
+    const uint32_t sc_hi = (C & 0x0F0F0F0Fu) | ((A >> 2) & 0x30303030u);
+    const uint32_t mn_hi = ((C >> 4) & 0x0F0F0F0Fu) | ((B >> 2) & 0x30303030u);
+    const uint32_t w[4] = {qw.x, qw.y, qw.z, qw.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        o.nib[2 * c] = w[c] & 0x0F0F0F0Fu;
+        o.nib[2 * c + 1] = (w[c] >> 4) & 0x0F0F0F0Fu;
+        const uint32_t sw = c < 2 ? sc_lo : sc_hi;
+        o.sc[2 * c] = (int)((sw >> (16 * (c & 1))) & 0xFF);
+        o.sc[2 * c + 1] = (int)((sw >> (16 * (c & 1) + 8)) & 0xFF);
+    }
+    o.mn01 = (int)((mn_lo & 0xFF) | ((mn_lo & 0xFF00) << 8));
+    o.mn23 = (int)(((mn_lo >> 16) & 0xFF) | ((mn_lo >> 8) & 0xFF0000));
+    o.mn45 = (int)((mn_hi & 0xFF) | ((mn_hi & 0xFF00) << 8));
+    o.mn67 = (int)(((mn_hi >> 16) & 0xFF) | ((mn_hi >> 8) & 0xFF0000));
+    o.dw = dev_fp16_to_fp32((uint16_t)(h.x & 0xFFFF));
+    o.dmw = dev_fp16_to_fp32((uint16_t)(h.x >> 16));
+}
+
+// p and q of a decoded block against Q8_K slot xb (same arithmetic as q4k_block_pq)
+__device__ __forceinline__ void q4k_lane_pq(const Q4KLaneBlock & o, const int8_t * xq_s, const int16_t * xs_s, const float * xd_s,
+                                            int xb, int l, float & p, float & q) {
+    const int4 xl = *(const int4 *)(xq_s + xb * QK_K + l * 32);
+    const int4 xh = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
+    const int4 bs = *(const int4 *)(xs_s + xb * 8);
+    const int xv[8] = {xl.x, xh.x, xl.y, xh.y, xl.z, xh.z, xl.w, xh.w};
+    int aux = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) aux += __mul24(o.sc[i], __builtin_amdgcn_sdot4((int)o.nib[i], xv[i], 0, false));
+    int sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn01), __builtin_bit_cast(short2_t, bs.x), 0, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn23), __builtin_bit_cast(short2_t, bs.y), sumi, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn45), __builtin_bit_cast(short2_t, bs.z), sumi, false);
+    sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn67), __builtin_bit_cast(short2_t, bs.w), sumi, false);
+    const float yd = xd_s[xb];
+    p = __fmul_rn(__fmul_rn(o.dw, yd), (float)aux);
+    q = __fmul_rn(__fmul_rn(o.dmw, yd), (float)sumi);
+}
+
+template <int MC, int PRO, int NCH>
+__global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK_K);
+    const int M = (int)j.M;
+    int8_t * xq_s = (int8_t *)smem;
+    const int nslot = MC * nb + 1;  // + the prologue's trash slot
+    float * xd_s = (float *)(smem + al16((size_t)nslot * QK_K));
+    int16_t * xs_s = (int16_t *)((char *)xd_s + al16(sizeof(float) * nslot));
+    float * cp = (float *)((char *)xs_s + al16((size_t)16 * nslot));  // [R][MC][nb][8] p terms
+    float * cq = cp + (size_t)R * MC * nb * 8;                          // [R][MC][nb]    q terms
+
+    // octet = (row r, block b, column group cg): NCG groups of CPL columns share a (row, block) when
+    // the workgroup has more octets than (row, block) pairs
+    const int l = threadIdx.x & 7, oct = threadIdx.x >> 3;
+    const int units = R * nb;
+    const int cg = oct / units, u = oct - cg * units;
+    const int r = u / nb, b = u - r * nb;
+    const int CPL = (M + NCG - 1) / NCG;
+    const int m0 = cg * CPL;
+    const int64_t NR = (int64_t)j.nmat * j.N;
+    const int64_t row0 = (int64_t)blockIdx.x * R;
+    const bool own = cg < NCG && m0 < M && row0 + r < NR;  // this octet has (row, block, columns) work
+    auto mat_of = [&](int64_t flat) {
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        return mt;
+    };
+    u32x4 hdr, qw;
+    TTS_TS(j, 0);
+    auto mid = [&]() {
+        int64_t flat = row0 + r;
+        flat = flat < NR ? flat : NR - 1;  // clamped: every lane loads, unused results are dropped
+        const int mat = mat_of(flat);
+        const uint8_t * bp = j.W[mat] + (flat - (int64_t)mat * j.N) * j.w_row_bytes + (int64_t)b * 144;
+        if (cg < NCG) {
+            hdr = __builtin_nontemporal_load((const u32x4 *)bp);
+            qw = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
+        }
+        TTS_PIN_LOADS();
+        TTS_TS(j, 1);
+    };
+    q4k_prologue<PRO, NCH>(j, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid);
+    TTS_TS(j, 2);
+    __syncthreads();
+    TTS_TS(j, 3);
+    if (own) {
+        Q4KLaneBlock o;
+        q4k_lane_decode(hdr, qw, o);
+        constexpr int CM = MC;  // columns per lane, compile-time bound (CPL <= MC)
+        int4 xl[CM], xh[CM], bs[CM];
+        float yd[CM];
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {  // every operand read from LDS first
+            const int xb = min(m0 + c, M - 1) * nb + b;
+            xl[c] = *(const int4 *)(xq_s + xb * QK_K + l * 32);
+            xh[c] = *(const int4 *)(xq_s + xb * QK_K + l * 32 + 16);
+            bs[c] = *(const int4 *)(xs_s + xb * 8);
+            yd[c] = xd_s[xb];
+        }
+#pragma unroll
+        for (int c = 0; c < CM; ++c) {
+            if (c >= CPL || m0 + c >= M) break;
+            const int xv[8] = {xl[c].x, xh[c].x, xl[c].y, xh[c].y, xl[c].z, xh[c].z, xl[c].w, xh[c].w};
+            int aux = 0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) aux += __mul24(o.sc[i], __builtin_amdgcn_sdot4((int)o.nib[i], xv[i], 0, false));
+            int sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn01), __builtin_bit_cast(short2_t, bs[c].x), 0, false);
+            sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn23), __builtin_bit_cast(short2_t, bs[c].y), sumi, false);
+            sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn45), __builtin_bit_cast(short2_t, bs[c].z), sumi, false);
+            sumi = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, o.mn67), __builtin_bit_cast(short2_t, bs[c].w), sumi, false);
+            const float p = __fmul_rn(__fmul_rn(o.dw, yd[c]), (float)aux);
+            const float q = __fmul_rn(__fmul_rn(o.dmw, yd[c]), (float)sumi);
+            const int64_t e = ((int64_t)r * MC + m0 + c) * nb + b;
+            cp[e * 8 + l] = p;
+            if (l == 0) cq[e] = q;
+        }
+    }
+    __syncthreads();
+    TTS_TS(j, 4);
+    // chain lanes: t = ((r * M + m) * 8 + l); whole octets per (row, column)
+    const int nchain = R * M * 8;
+    for (int t = threadIdx.x; t - l < nchain; t += 512) {
+        const int rm = t >> 3;
+        const int rr = rm / M, m = rm - rr * M;
+        const bool ok = t < nchain && row0 + rr < NR;
+        float sums = 0.f, sumf = 0.f;
+        if (ok) {
+            const float * pp = cp + ((int64_t)rr * MC + m) * nb * 8 + l;
+            const float * qq = cq + ((int64_t)rr * MC + m) * nb;
+            constexpr int CB = 16;  // terms fetched per batch (independent LDS reads), then chained in order
+            for (int b0 = 0; b0 < nb; b0 += CB) {
+                float pv[CB], qv[CB];
+#pragma unroll
+                for (int i = 0; i < CB; ++i) {
+                    const int bb = min(b0 + i, nb - 1);
+                    pv[i] = pp[bb * 8];
+                    qv[i] = qq[bb];
+                }
+#pragma unroll
+                for (int i = 0; i < CB; ++i) {
+                    if (b0 + i >= nb) break;
+                    sums = __fadd_rn(sums, pv[i]);
+                    sumf = __fsub_rn(sumf, qv[i]);
+                }
+            }
+        }
+        const float tot = q4k_octet_total(sumf, sums);
+        if (ok && l == 0) {
+            const int64_t flat = row0 + rr;
+            const int mat = mat_of(flat);
+            gemv_store<8>(j, mat, flat - (int64_t)mat * j.N, m, tot);
+        }
     }
     TTS_TS(j, 5);
 }
@@ -682,8 +889,11 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    if (nmine > 0) load(I0{}, 0);
-    if (!(j.dbg & 2)) q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs);
+    auto mid = [&]() {
+        if (nmine > 0) load(I0{}, 0);
+    };
+    if (!(j.dbg & 2)) q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
+    else mid();
     __syncthreads();
     for (int64_t i = 0; i < nmine; i += 2) {
         load(I1{}, min(i + 1, nmine - 1));
@@ -722,12 +932,6 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
     const int64_t row = (int64_t)h * HD + wave * 8 + s;
     const uint8_t * wr = j.W[0] + row * j.w_row_bytes;
     u32x4 hdr[4], q[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int64_t bo = (int64_t)min(u, nb - 1) * 144;
-        hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
-        q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
-    }
     // attention operands for the last wave (position p = lane)
     const int P = a.P;
     const int p = min(lane, P - 1);
@@ -737,15 +941,23 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
     const int bk = b / (a.B / (int)a.k.ne[3]), bv = b / (a.B / (int)a.v.ne[3]);  // K/V shared across prompts or not
     const char * kbase = a.k.data + (int64_t)h * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
     const char * vbase = a.v.data + (int64_t)h * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
-    if (wave == NW - 1) {
+    // weight rows and attention operands are requested behind the prologue's activation loads
+    auto mid = [&]() {
 #pragma unroll
-        for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+        for (int u = 0; u < 4; ++u) {
+            const int64_t bo = (int64_t)min(u, nb - 1) * 144;
+            hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
+            q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
+        }
+        if (wave == NW - 1) {
 #pragma unroll
-        for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
-        if (a.mask) mk = a.mask[p];
-    }
-    TTS_PIN_LOADS();
-    q4k_prologue<PRO, 4>(jb, nb, xq_s, xd_s, xs_s);
+            for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+#pragma unroll
+            for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
+            if (a.mask) mk = a.mask[p];
+        }
+    };
+    q4k_prologue<PRO, 4>(jb, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid);
     __syncthreads();
     float sums = 0.f, sumf = 0.f;
 #pragma unroll
@@ -1026,14 +1238,19 @@ static double gemv_bytes(const GemvJob & j) {
            4.0 * (double)j.K * (double)j.M;
 }
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): replica backends call
+// the launchers from several host threads, so the per-device flags are atomic
+static void set_lds_attr_once(std::atomic<uint32_t> & done, int device, const void * fn) {
+    const uint32_t bit = 1u << (device & 31);
+    if (done.load(std::memory_order_acquire) & bit) return;
+    TTS_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    done.fetch_or(bit, std::memory_order_acq_rel);
+}
+
 template <int MC, int PRO, int NBMAX>
 static void launch_q4k(tts_hip_backend * be, const GemvJob & j, unsigned gx, int nw, size_t lds) {
-    static bool attr_set = false;
-    if (lds > 64 * 1024 && !attr_set) {
-        TTS_HIP_CHECK(hipFuncSetAttribute((const void *)k_gemv_q4_K<MC, PRO, NBMAX>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                          160 * 1024));
-        attr_set = true;
-    }
+    static std::atomic<uint32_t> attr_done{0};
+    if (lds > 64 * 1024) set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4_K<MC, PRO, NBMAX>);
     if (be->profile_gemv) {
         // Profiled: the start/stop events ride in the dispatch packet itself (hipExtLaunchKernel), so
         // they carry the kernel's own begin/end timestamps -- the ones the rocprofv3 kernel trace
@@ -1047,9 +1264,59 @@ static void launch_q4k(tts_hip_backend * be, const GemvJob & j, unsigned gx, int
     hipLaunchKernelGGL((k_gemv_q4_K<MC, PRO, NBMAX>), dim3(gx), dim3(64 * nw), lds, be->stream, j);
 }
 
+// Unique-load geometry (k_gemv_q4_K_u): R rows per 512-thread workgroup with R * nb <= 64 octets,
+// as few rows per workgroup as spreads the matrix over every CU.  False when the shape does not fit.
+static bool q4k_u_geometry(const GemvJob & j, int MC, int & R, int & NCG, int64_t & gx, size_t & lds) {
+    const int64_t nb = j.K / QK_K;
+    if (nb < 1 || nb > 64) return false;
+    const int64_t NR = (int64_t)j.nmat * j.N;
+    const int64_t rmax = 64 / nb;
+    int64_t r = (NR + 255) / 256;
+    r = r > rmax ? rmax : r < 1 ? 1 : r;
+    R = (int)r;
+    gx = (NR + r - 1) / r;
+    // spare octets split the columns: NCG groups of ceil(M / NCG) columns per (row, block)
+    int64_t ncg = 64 / (r * nb);
+    NCG = (int)(ncg < 1 ? 1 : ncg > j.M ? j.M : ncg);
+    lds = q4k_lds(MC, j.K) + (size_t)R * MC * nb * 9 * 4;
+    return lds <= 160 * 1024;
+}
+
+template <int MC, int PRO, int NCH>
+static void launch_q4k_u(tts_hip_backend * be, const GemvJob & j, unsigned gx, int R, int NCG, size_t lds) {
+    static std::atomic<uint32_t> attr_done{0};
+    if (lds > 64 * 1024) set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4_K_u<MC, PRO, NCH>);
+    if (be->profile_gemv) {
+        hipEvent_t e0, e1;
+        profile_pair(be, e0, e1);
+        hipExtLaunchKernelGGL((k_gemv_q4_K_u<MC, PRO, NCH>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j, R, NCG);
+        profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
+        return;
+    }
+    hipLaunchKernelGGL((k_gemv_q4_K_u<MC, PRO, NCH>), dim3(gx), dim3(512), lds, be->stream, j, R, NCG);
+}
+
 template <int MC>
 static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
     constexpr int S = 8 / MC;
+    // unique loads pay off once a row holds >= 8 blocks (Parler fc2: 14.0 -> 11.1 us in the decode
+    // graph at M = 8); at K = 1024 the octet-per-column kernel is faster (6.1 vs 7.7 us)
+    if (be->gemv_unique && j.K >= 8 * QK_K) {
+        int R, NCG;
+        int64_t gx;
+        size_t lds;
+        if (q4k_u_geometry(j, MC, R, NCG, gx, lds)) {
+            const bool wide = j.K > 4 * QK_K;  // LN prologue: NP = NCH / 4 chunk passes per lane
+            if (j.pro == PRO_LN) {
+                if (wide) launch_q4k_u<MC, PRO_LN, 16>(be, j, (unsigned)gx, R, NCG, lds);
+                else launch_q4k_u<MC, PRO_LN, 4>(be, j, (unsigned)gx, R, NCG, lds);
+            } else {
+                if (wide) launch_q4k_u<MC, PRO_QUANT, 16>(be, j, (unsigned)gx, R, NCG, lds);
+                else launch_q4k_u<MC, PRO_QUANT, 4>(be, j, (unsigned)gx, R, NCG, lds);
+            }
+            return;
+        }
+    }
     if (j.nmat > 1 && j.N % S) {  // a wave's S rows must not straddle two matrices: one launch each
         for (int i = 0; i < j.nmat; ++i) {
             GemvJob one = j;
@@ -1094,15 +1361,14 @@ static int64_t q4k_mf_max_cols(int64_t K) {
 }
 static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
     (void)be;
-    return j.wtype == TTS_TYPE_Q4_K && j.tiled;
+    // at least one column's Q8_K operands must fit LDS (K <= ~76k); wider rows would make
+    // launch_q4k_mf's column loop step by 0
+    return j.wtype == TTS_TYPE_Q4_K && j.tiled && q4k_mf_max_cols(j.K) >= 1;
 }
 template <int PRO, int NCH>
 static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
-    static bool attr_set = false;
-    if (!attr_set) {
-        TTS_HIP_CHECK(hipFuncSetAttribute((const void *)k_gemv_q4K_mf<PRO, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr_set = true;
-    }
+    static std::atomic<uint32_t> attr_done{0};
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH>);
     const int64_t T = (j.nmat * j.N + 15) / 16;
     const unsigned gx = (unsigned)(T < 256 ? T : 256);
     const size_t lds = q4k_mf_lds(j.M, j.K);
