@@ -186,6 +186,44 @@ int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, float * pcm);
 int64_t tts_dac_hop(const tts_dac * d);
 int32_t tts_dac_last_graph_nodes(const tts_dac * d);
 
+/* SNAC decoder (Orpheus' vocoder: three codebook streams -> 24 kHz PCM): snac_runner::run /
+ * build_snac_graph, /root/reference/src/decoder/snac_model.cpp:86-208, with the shared codec layers
+ * of general_neural_audio_codec.cpp:133-172 (noise branch, depthwise residual units).  Defaults =
+ * SNAC 24 kHz as used by Orpheus-3B (3 heads x 4096 x 8, vq strides 4,2,1, latent 768, decoder
+ * 1024, rates 8,8,4,2: 512 samples per finest-head frame). */
+typedef struct tts_snac_config {
+    int32_t n_heads;       /* 3 (snac.audio_token_channels) */
+    int32_t codebook_size; /* 4096 */
+    int32_t codebook_dim;  /* 8 */
+    int32_t latent_dim;    /* 768 (snac_model::embd) */
+    int32_t decoder_dim;   /* 1024; halves per layer */
+    int32_t n_layers;      /* 4 */
+    int32_t rates[8];      /* 8, 8, 4, 2 (snac_layer_stride_i) */
+    int32_t repeats[4];    /* 4, 2, 1 (repeat_interleave of head i, snac_model.h:17) */
+    int32_t max_frames;    /* finest-head frames per decode call (arena sizing) */
+    int32_t debug_no_reuse; /* 1 = every graph tensor keeps its own arena memory (node taps in tests) */
+    uint64_t seed;         /* synthetic weight seed base */
+    uint64_t arena_bytes;  /* compute arena (0 = sized from max_frames) */
+} tts_snac_config;
+
+typedef struct tts_snac tts_snac;
+void tts_snac_default_config(tts_snac_config * cfg);
+tts_snac * tts_snac_create(const tts_backend_iface * be, const tts_snac_config * cfg);
+void tts_snac_free(tts_snac * d);
+/* codes: the heads back to back (head i: T / repeats[i] int32 ids, the inp_tokens layout of
+ * snac_runner::set_inputs, snac_model.cpp:161-176); noise: [noise_per_frame * T] f32 (layer l's
+ * T * prod(rates[0..l]) normal draws in order, random_normal_gen's role); pcm: [T * hop] f32. */
+int tts_snac_decode(tts_snac * d, const int32_t * codes, int32_t T, const float * noise, float * pcm);
+int64_t tts_snac_hop(const tts_snac * d);
+int64_t tts_snac_noise_per_frame(const tts_snac * d);
+int32_t tts_snac_last_graph_nodes(const tts_snac * d);
+/* Weight introspection for tests: count, then name / ne[4] / f32 values of weight i (bytes). */
+int32_t tts_snac_n_weights(const tts_snac * d);
+uint64_t tts_snac_weight(tts_snac * d, int32_t i, char * name, uint64_t name_cap, int64_t * ne, float * dst, uint64_t cap);
+/* Debug: bytes of the named node of the last graph ("embd", "in_conv", "up", "convt.<l>",
+ * "noise.<l>", "ru.<l>.<r>", "pcm"), copied to dst when cap suffices; 0 if absent. */
+uint64_t tts_snac_get_node(tts_snac * d, const char * name, void * dst, uint64_t cap);
+
 /* Kokoro-82M iSTFTNet generator (decoder features + F0 + style -> 24 kHz PCM): build_generator,
  * build_sin_gen, build_noise_block and build_kokoro_generator_res_block,
  * /root/reference/src/models/kokoro/model.cpp:136-244, fed as kokoro_runner::set_inputs feeds it

@@ -324,6 +324,19 @@ tts_tensor * conv_1d(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0
     return reshape_3d(c, r, col->ne[1], a->ne[2], col->ne[2]);
 }
 
+// ggml_conv_1d_dw (depthwise, SNAC's input conv and grouped residual units,
+// /root/reference/src/decoder/snac_model.cpp:141, general_neural_audio_codec.cpp:140): kernel
+// a [K, 1, C] and input b [L, C] viewed as [K, 1, C, 1] / [L, 1, C, 1], im2col (F16) treats the
+// channels as the batch -> [K, OL, C], one mul_mat per channel against its own K taps ->
+// [OL, 1, C], reshaped to [L, C] (upstream reshapes with b's length: same-padding convs only).
+tts_tensor * conv_1d_dw(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0) {
+    tts_tensor * na = reshape_4d(c, a, a->ne[0], 1, a->ne[1], a->ne[2]);
+    tts_tensor * nb = reshape_4d(c, b, b->ne[0], 1, b->ne[1], b->ne[2]);
+    tts_tensor * col = im2col(c, na, nb, s0, p0, d0, TTS_TYPE_F16);
+    tts_tensor * r = mul_mat(c, col, a);
+    return reshape_3d(c, r, b->ne[0], b->ne[1], 1);
+}
+
 // Fork op ggml_conv_transpose_1d(a, b, s0, p0, d0, output_padding, groups) with PyTorch
 // ConvTranspose1d semantics: a = kernel [K, OC/g, IC], b = input [L, IC] ->
 // [(L-1)*s0 - 2*p0 + d0*(K-1) + op + 1, OC]; op_params {s0, p0, d0, op, g}.

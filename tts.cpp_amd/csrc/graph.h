@@ -88,6 +88,7 @@ tts_tensor * mul_mat(context & c, tts_tensor * a, tts_tensor * b);
 tts_tensor * soft_max_ext(context & c, tts_tensor * a, tts_tensor * mask, float scale, float max_bias);
 tts_tensor * im2col(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0, int dst_type);
 tts_tensor * conv_1d(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0);
+tts_tensor * conv_1d_dw(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0);
 tts_tensor * conv_transpose_1d(context & c, tts_tensor * a, tts_tensor * b, int s0, int p0, int d0, int op, int g);
 tts_tensor * get_rows(context & c, tts_tensor * a, tts_tensor * idx);
 tts_tensor * concat(context & c, tts_tensor * a, tts_tensor * b, int dim);

@@ -147,6 +147,23 @@ class DacConfig(ctypes.Structure):
     ]
 
 
+class SnacConfig(ctypes.Structure):
+    _fields_ = [
+        ("n_heads", ctypes.c_int32),
+        ("codebook_size", ctypes.c_int32),
+        ("codebook_dim", ctypes.c_int32),
+        ("latent_dim", ctypes.c_int32),
+        ("decoder_dim", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("rates", ctypes.c_int32 * 8),
+        ("repeats", ctypes.c_int32 * 4),
+        ("max_frames", ctypes.c_int32),
+        ("debug_no_reuse", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+    ]
+
+
 class KokoroGenConfig(ctypes.Structure):
     _fields_ = [
         ("in_channels", ctypes.c_int32),
@@ -261,6 +278,16 @@ def lib():
         "tts_dac_decode": (ctypes.c_int, [vp, vp, i32, vp]),
         "tts_dac_hop": (i64, [vp]),
         "tts_dac_last_graph_nodes": (i32, [vp]),
+        "tts_snac_default_config": (None, [ctypes.POINTER(SnacConfig)]),
+        "tts_snac_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(SnacConfig)]),
+        "tts_snac_free": (None, [vp]),
+        "tts_snac_decode": (ctypes.c_int, [vp, vp, i32, vp, vp]),
+        "tts_snac_hop": (i64, [vp]),
+        "tts_snac_noise_per_frame": (i64, [vp]),
+        "tts_snac_last_graph_nodes": (i32, [vp]),
+        "tts_snac_n_weights": (i32, [vp]),
+        "tts_snac_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
+        "tts_snac_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
         "tts_kokoro_gen_default_config": (None, [ctypes.POINTER(KokoroGenConfig)]),
         "tts_kokoro_gen_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(KokoroGenConfig)]),
         "tts_kokoro_gen_free": (None, [vp]),
@@ -621,6 +648,84 @@ class Dac:
     def close(self):
         if self.ptr:
             self.L.tts_dac_free(self.ptr)
+            self.ptr = None
+
+
+def snac_config(**kw):
+    cfg = SnacConfig()
+    lib().tts_snac_default_config(ctypes.byref(cfg))
+    for k, v in kw.items():
+        if k in ("rates", "repeats"):
+            for i, r in enumerate(v):
+                getattr(cfg, k)[i] = r
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+class Snac:
+    """SNAC decoder runner (Orpheus' three codebook streams -> 24 kHz PCM) over a backend vtable."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_snac_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_snac_create failed")
+
+    @property
+    def hop(self):
+        return self.L.tts_snac_hop(self.ptr)
+
+    @property
+    def noise_per_frame(self):
+        return self.L.tts_snac_noise_per_frame(self.ptr)
+
+    def decode(self, heads, noise):
+        """heads: list of n_heads int arrays (head i: T / repeats[i] codes); noise: (noise_per_frame * T,)
+        float32 normal draws -> (T * hop,) float32 PCM."""
+        import numpy as np
+        T = len(heads[-1])
+        c = np.ascontiguousarray(np.concatenate([np.asarray(h, dtype=np.int32) for h in heads]))
+        z = np.ascontiguousarray(noise, dtype=np.float32)
+        if z.size != self.noise_per_frame * T:
+            raise ValueError(f"noise needs {self.noise_per_frame * T} values")
+        pcm = np.empty(T * self.hop, dtype=np.float32)
+        st = self.L.tts_snac_decode(self.ptr, c.ctypes.data, T, z.ctypes.data, pcm.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"tts_snac_decode failed {st}")
+        return pcm
+
+    def last_graph_nodes(self):
+        return self.L.tts_snac_last_graph_nodes(self.ptr)
+
+    def node(self, name, cap=1 << 26):
+        """Named node of the last decode as a flat float32 array (ggml order), or None."""
+        import numpy as np
+        buf = np.empty(cap // 4, dtype=np.float32)
+        n = self.L.tts_snac_get_node(self.ptr, name.encode(), buf.ctypes.data, cap)
+        return buf[: n // 4].copy() if n else None
+
+    def weights(self):
+        """{name: float32 array shaped like torch (reversed ggml ne, leading 1s dropped)}."""
+        import numpy as np
+        out = {}
+        for i in range(self.L.tts_snac_n_weights(self.ptr)):
+            name = ctypes.create_string_buffer(128)
+            ne = (ctypes.c_int64 * 4)()
+            n = self.L.tts_snac_weight(self.ptr, i, name, 128, ne, None, 0)
+            a = np.empty(n // 4, dtype=np.float32)
+            self.L.tts_snac_weight(self.ptr, i, name, 128, ne, a.ctypes.data, n)
+            shape = [int(v) for v in reversed(list(ne))]
+            while len(shape) > 1 and shape[0] == 1:
+                shape.pop(0)
+            out[name.value.decode()] = a.reshape(shape)
+        return out
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_snac_free(self.ptr)
             self.ptr = None
 
 
