@@ -4,6 +4,7 @@ Shapes: the Parler-mini decode matrices, Orpheus-3B / Dia sizes, at M = 1 and 8 
 Prints one JSON line per shape with avg us per launch and algorithmic GB/s.
 """
 import json
+import os
 import pathlib
 import sys
 
@@ -34,6 +35,12 @@ def main():
     hip = ttship.HipBackend(0)
     dbg = int(sys.argv[6]) if len(sys.argv) > 6 else 0  # TTS_HIP_OPT_GEMV_DEBUG phase study
     hip.set_option(ttship.OPT["GEMV_DEBUG"], dbg)
+    # cold: cycle through enough weight copies (>= 512 MiB) that every launch streams from HBM, as in a
+    # decode step (the Infinity Cache holds 256 MiB); kernel selection from the environment
+    cold = int(sys.argv[7]) if len(sys.argv) > 7 else 0
+    for opt in ("GEMV_UNIQUE",):
+        if os.environ.get(opt) is not None:
+            hip.set_option(ttship.OPT[opt], int(os.environ[opt]))
     L = ttship.lib()
     rng = np.random.default_rng(0)
     for name, wt, K, N in SHAPES:
@@ -55,29 +62,33 @@ def main():
             flags = 32
             if N % 4:
                 continue
-        dw = hip.alloc(w.nbytes)
-        hip.set(dw, w)
+        ncopy = max(1, min(64, -(-(512 << 20) // w.nbytes))) if cold else 1
+        dws = [hip.alloc(w.nbytes) for _ in range(ncopy)]
+        for d in dws:
+            hip.set(d, w)
         for M in mlist:
             x = rng.standard_normal((M, K)).astype(np.float32)
             dx = hip.alloc(x.nbytes)
             dy = hip.alloc(4 * M * N)
             hip.set(dx, x)
-            for _ in range(3):
-                L.tts_hip_gemv_ex(hip.ptr, wt, dw, dx, dy, K, N, M, flags)
+            for c in range(3):
+                L.tts_hip_gemv_ex(hip.ptr, wt, dws[c % ncopy], dx, dy, K, N, M, flags)
             hip.sync()
             hip.set_option(1, 1)
             hip.gemv_stats(-1, reset=True)
-            for _ in range(reps):
-                L.tts_hip_gemv_ex(hip.ptr, wt, dw, dx, dy, K, N, M, flags)
+            for c in range(reps):
+                L.tts_hip_gemv_ex(hip.ptr, wt, dws[c % ncopy], dx, dy, K, N, M, flags)
             ms, n, nbytes = hip.gemv_stats(wt, reset=True)
             hip.set_option(1, 0)
             us = 1000.0 * ms / n
             print(json.dumps({"shape": name, "type": ttship.lib().tts_type_name(wt).decode(), "K": K, "N": N, "M": M,
-                              "weight_MB": round(wbytes / 1e6, 3), "tiled": bool(tiled and wt == ttship.Q4_K), "dbg": dbg, "avg_us": round(us, 2),
+                              "weight_MB": round(wbytes / 1e6, 3), "tiled": bool(tiled and wt == ttship.Q4_K), "dbg": dbg, "cold": cold,
+                              "avg_us": round(us, 2),
                               "GBps": round(nbytes / n / (us * 1e-6) / 1e9, 1)}), flush=True)
             hip.free(dx)
             hip.free(dy)
-        hip.free(dw)
+        for d in dws:
+            hip.free(d)
     hip.close()
 
 

@@ -113,7 +113,7 @@ def run_gpu_tiled(hip, w, x, N):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,N", MF_SHAPES)
+@pytest.mark.parametrize("K,N", MF_SHAPES + [(8192, 3072), (3072, 16388)])
 @pytest.mark.parametrize("M", [1, 2, 5, 8, 16, 19])
 def test_q4_K_mfma(hip, K, N, M):
     """Matrix-core Q4_K path (k_gemv_q4K_mf on the tile layout): the integer block dots run as f16
