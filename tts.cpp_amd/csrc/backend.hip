@@ -59,6 +59,8 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     TTS_HIP_CHECK(hipMalloc((void **)&be->attn_buf, kAttnFloats * sizeof(float)));
     be->attn_floats = kAttnFloats;
     TTS_HIP_CHECK(hipMalloc((void **)&be->vec_scratch, kVecScratchFloats * sizeof(float)));
+    be->conv_part_doubles = (size_t)8 << 20;  // 64 MiB of f64 partial sums
+    TTS_HIP_CHECK(hipMalloc((void **)&be->conv_part, be->conv_part_doubles * sizeof(double)));
     be->lstm_floats = kLstmFloats;
     TTS_HIP_CHECK(hipMalloc((void **)&be->argmax_keys, kArgmaxRows * sizeof(unsigned long long)));
     TTS_HIP_CHECK(hipMalloc((void **)&be->argmax_counts, kArgmaxRows * sizeof(unsigned)));
@@ -94,6 +96,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->lstm_buf);
     hipFree(be->attn_buf);
     hipFree(be->vec_scratch);
+    hipFree(be->conv_part);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);
     if (be->gexec) hipGraphExecDestroy(be->gexec);
@@ -373,6 +376,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
     switch (option) {
         case TTS_HIP_OPT_FUSION: be->fusion = value; return 0;
         case TTS_HIP_OPT_CONVT_LDS: be->convt_lds = value != 0; return 0;
+        case TTS_HIP_OPT_CONV_SPLIT: be->conv_split = value != 0; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
         case TTS_HIP_OPT_CONV_F32ACC:

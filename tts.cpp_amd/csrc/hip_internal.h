@@ -266,6 +266,11 @@ struct tts_hip_backend {
     int64_t graph_epoch = 0;
     uint16_t * gelu_table = nullptr;  // 65536 fp16 entries (GGML_GELU_FP16 table)
     bool convt_lds = true;  // conv_transpose_1d on the LDS-staged f64 MFMA kernel (A/B knob)
+    // f64 partial sums of input-channel-split codec convolutions (short sequences: the output
+    // tiles alone would leave most CUs idle), summed in split order by a second pass
+    double * conv_part = nullptr;
+    size_t conv_part_doubles = 0;
+    int conv_split = 1;  // TTS_HIP_OPT_CONV_SPLIT: 1 = split short convolutions, 0 = never
     int fusion = 0x1FFF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
@@ -347,6 +352,8 @@ struct Conv1dArgs {
     int icc = 0, xw = 0, rs = 0;    // set by the launcher
     float * copy_dst = nullptr;     // non-null: y is a staging buffer, copied here (contiguous) after the kernel
     uint32_t x_bytes = 0, w_bytes = 0;  // buffer-descriptor ranges (reads past them return 0)
+    double * part = nullptr;        // split launch: f64 partial sums [gridDim.z][OC][OL], no epilogue
+    int ic_per_split = 0;           // input channels per split (a multiple of icc)
 };
 constexpr int CONV1D_XN = 16, CONV1D_WN = 16;  // staged elements per thread (x window, kernel slice)
 inline int conv1d_icc(int64_t IC, int K, int xw) {  // input channels per LDS chunk

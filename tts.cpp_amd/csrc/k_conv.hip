@@ -140,7 +140,11 @@ typedef double f64x4_t __attribute__((ext_vector_type(4)));
 
 template <bool BF16>
 __global__ __launch_bounds__(256) void k_gemm_f16_f64acc(const __half * __restrict__ A, int64_t lda, const void * __restrict__ B, int64_t ldb,
-                                                         float * __restrict__ D, int64_t ldd, int64_t M, int64_t N, int64_t K) {
+                                                         float * __restrict__ D, int64_t ldd, int64_t M, int64_t N, int64_t K,
+                                                         double * __restrict__ part = nullptr, int64_t kps = 0) {
+    // split launch (part != null): workgroup z reduces k in [z*kps, (z+1)*kps) into part[z][j][i]
+    const int64_t kb = part ? (int64_t)blockIdx.z * kps : 0;
+    const int64_t ke = part ? min(K, kb + kps) : K;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t i0 = (int64_t)blockIdx.x * 64 + (wave & 1) * 32;
     const int64_t j0 = (int64_t)blockIdx.y * 64 + (wave >> 1) * 32;
@@ -155,7 +159,7 @@ __global__ __launch_bounds__(256) void k_gemm_f16_f64acc(const __half * __restri
     half8_t a[2], b[2], an[2], bn[2];
     auto load = [&](int64_t k0, half8_t (&fa)[2], half8_t (&fb)[2]) {
         const int64_t k = k0 + 8 * kq;
-        const bool kin = k < K;
+        const bool kin = k < ke;
         const int64_t kc = kin ? k : 0;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
@@ -166,9 +170,9 @@ __global__ __launch_bounds__(256) void k_gemm_f16_f64acc(const __half * __restri
             fb[t] = kin ? vb : z;
         }
     };
-    load(0, a, b);
-    for (int64_t k0 = 0; k0 < K; k0 += 32) {
-        if (k0 + 32 < K) load(k0 + 32, an, bn);
+    load(kb, a, b);
+    for (int64_t k0 = kb; k0 < ke; k0 += 32) {
+        if (k0 + 32 < ke) load(k0 + 32, an, bn);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             double ad[2], bd[2];
@@ -191,10 +195,48 @@ __global__ __launch_bounds__(256) void k_gemm_f16_f64acc(const __half * __restri
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int64_t i = i0 + 16 * ti + kq + 4 * e;
-                if (i < M) D[j * ldd + i] = (float)acc[ti][tj][e];
+                if (i >= M) continue;
+                if (part) part[((int64_t)blockIdx.z * N + j) * M + i] = acc[ti][tj][e];
+                else D[j * ldd + i] = (float)acc[ti][tj][e];
             }
         }
     }
+}
+
+// Second pass of a split reduction: y[i + j*ldy] = f32(sum over z, in order, of part[z][j][i]),
+// then + bias[j * bcs] and + res[i + j * rcs] (each rounded, as the ADD nodes they replace).
+__global__ __launch_bounds__(256) void k_split_reduce(const double * __restrict__ part, int nz, int64_t M, int64_t N, float * __restrict__ y,
+                                                      int64_t ldy, const float * __restrict__ bias, int64_t bcs, const float * __restrict__ res,
+                                                      int64_t rcs) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= M * N) return;
+    const int64_t j = e / M, i = e - j * M;
+    double s = 0.0;
+    for (int z = 0; z < nz; ++z) s += part[((int64_t)z * N + j) * M + i];
+    float v = (float)s;
+    if (bias) v = v + bias[j * bcs];
+    if (res) v = res[i + j * rcs] + v;
+    y[i + j * ldy] = v;
+}
+
+// Splits for a reduction of length K over an output grid of `tiles` workgroups: enough extra
+// workgroups to fill the chip (~2 per CU) while each split keeps >= `minlen` of the reduction and
+// the partials fit the scratch.  Returns 1 (no split) for grids that already fill the chip.
+static int split_count(const tts_hip_backend * be, int64_t tiles, int64_t K, int64_t minlen, int64_t outs) {
+    if (!be->conv_split || tiles >= 256) return 1;
+    int64_t z = (512 + tiles - 1) / tiles;
+    const int64_t zk = K / minlen;
+    if (z > zk) z = zk;
+    const int64_t zm = outs > 0 ? (int64_t)(be->conv_part_doubles / (size_t)outs) : 1;
+    if (z > zm) z = zm;
+    return z < 2 ? 1 : (int)z;
+}
+
+static void launch_split_reduce(tts_hip_backend * be, int nz, int64_t M, int64_t N, float * y, int64_t ldy, const float * bias, int64_t bcs,
+                                const float * res, int64_t rcs) {
+    const int64_t n = M * N;
+    hipLaunchKernelGGL(k_split_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, be->stream, (const double *)be->conv_part, nz, M, N, y, ldy,
+                       bias, bcs, res, rcs);
 }
 
 // MUL_MAT with an F16 src0 and many src1 columns (the conv_1d GEMM).  Returns false when the
@@ -209,15 +251,22 @@ bool launch_gemm_f16(tts_hip_backend * be, const tts_tensor * node) {
     const size_t bes = tts_type_size(b->type);
     if (K % 8 || a->nb[0] != 2 || b->nb[0] != bes || node->nb[0] != 4) return false;
     if (a->nb[1] % 16 || b->nb[1] % 16 || ((uintptr_t)a->data % 16) || ((uintptr_t)b->data % 16)) return false;
-    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64));
+    dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64));
     if (!be->conv_f32acc) {
+        // short sequences: split K over extra workgroups (f64 partials, summed in split order)
+        const int nz = split_count(be, (int64_t)grid.x * grid.y, K, 256, M * N);
+        const int64_t kps = nz > 1 ? (((K + nz - 1) / nz + 31) & ~(int64_t)31) : K;
+        const int nzr = nz > 1 ? (int)((K + kps - 1) / kps) : 1;
+        double * part = nzr > 1 ? be->conv_part : nullptr;
+        grid.z = (unsigned)nzr;
         if (b->type == TTS_TYPE_F16)
             hipLaunchKernelGGL(k_gemm_f16_f64acc<true>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
-                               (int64_t)(b->nb[1] / 2), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+                               (int64_t)(b->nb[1] / 2), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K, part, kps);
         else
             hipLaunchKernelGGL(k_gemm_f16_f64acc<false>, grid, dim3(256), 0, be->stream, (const __half *)a->data, (int64_t)(a->nb[1] / 2), b->data,
-                               (int64_t)(b->nb[1] / 4), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K);
+                               (int64_t)(b->nb[1] / 4), (float *)node->data, (int64_t)(node->nb[1] / 4), M, N, K, part, kps);
         TTS_HIP_CHECK(hipGetLastError());
+        if (part) launch_split_reduce(be, nzr, M, N, (float *)node->data, (int64_t)(node->nb[1] / 4), nullptr, 0, nullptr, 0);
         return true;
     }
     if (b->type == TTS_TYPE_F16)
@@ -319,8 +368,11 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
             else wv[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(wr, off, 0, 0));
         }
     };
-    fetch(0);
-    for (int ic0 = 0; ic0 < a.IC; ic0 += icc) {
+    // split launch: this workgroup's input channels [ic_lo, ic_hi), whole chunks
+    const int ic_lo = a.part ? (int)blockIdx.z * a.ic_per_split : 0;
+    const int ic_hi = a.part ? (int)min((int64_t)(ic_lo + a.ic_per_split), a.IC) : (int)a.IC;
+    fetch(ic_lo);
+    for (int ic0 = ic_lo; ic0 < ic_hi; ic0 += icc) {
         // f16 rounding (im2col's dst type / MUL_MAT's vec_dot_type) on the way into LDS
 #pragma unroll
         for (int u = 0; u < CONV1D_XN; ++u)
@@ -333,7 +385,7 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
                 ws[oc * rs + (e - oc * Rp)] = W16 ? wv[u] : __half2float(__float2half_rn(wv[u]));
             }
         __syncthreads();
-        if (ic0 + icc < a.IC) fetch(ic0 + icc);
+        if (ic0 + icc < ic_hi) fetch(ic0 + icc);
         // batches of 8 reduction quads: every operand of the batch is read from LDS first (the
         // offset-table reads, then the dependent operand reads, all independent of each other),
         // then 32 MFMAs issue back to back
@@ -386,6 +438,21 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
                         acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)af[u][ti], (double)bf[u][tj], acc[ti][tj], 0, 0, 0);
         }
         __syncthreads();
+    }
+    if (a.part) {  // partial sums of this split, no epilogue (k_split_reduce adds bias and residual)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int64_t ol = ol0 + wc0 + 16 * tj + c16;
+            if (ol >= a.OL) continue;
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int oc = oc0 + wr0 + 16 * ti + (H32 ? 4 * kq + e : kq + 4 * e);
+                    if (oc < a.OC) a.part[((int64_t)blockIdx.z * a.OC + oc) * a.OL + ol] = acc[ti][tj][e];
+                }
+        }
+        return;
     }
     // epilogue: bias and residual operands fetched for all 32 outputs first (clamped, branchless)
     float bv[2][4], rv[2][2][4];
@@ -440,7 +507,18 @@ void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a) {
         fprintf(stderr, "tts_hip: conv1d_fused shape unsupported\n");
         abort();
     }
-    const dim3 grid((unsigned)((a.OL + 63) / 64), (unsigned)((a.OC + 63) / 64));
+    dim3 grid((unsigned)((a.OL + 63) / 64), (unsigned)((a.OC + 63) / 64));
+    // short sequences: split the input channels over extra workgroups (whole chunks per split)
+    Conv1dArgs e = a;  // the epilogue's operands, applied by the split reduction
+    const int64_t nchunk = (a.IC + a.icc - 1) / a.icc;
+    const int nz = be->conv_acc_mode == 2 ? 1 : split_count(be, (int64_t)grid.x * grid.y, nchunk, 2, a.OL * a.OC);
+    if (nz > 1) {
+        a.ic_per_split = (int)(((nchunk + nz - 1) / nz) * a.icc);
+        grid.z = (unsigned)((a.IC + a.ic_per_split - 1) / a.ic_per_split);
+        a.part = be->conv_part;
+        a.bias = nullptr;
+        a.res = nullptr;
+    }
     const int sel = (a.w16 ? 4 : 0) | (a.bias ? 2 : 0) | (a.res ? 1 : 0);
     if (be->conv_acc_mode == 2) switch (sel) {
         case 0: hipLaunchKernelGGL((k_conv1d_f64<false, false, false, true>), grid, dim3(256), lds, be->stream, a); break;
@@ -463,6 +541,7 @@ void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a) {
         default: hipLaunchKernelGGL((k_conv1d_f64<true, true, true>), grid, dim3(256), lds, be->stream, a); break;
     }
     TTS_HIP_CHECK(hipGetLastError());
+    if (a.part) launch_split_reduce(be, (int)grid.z, a.OL, a.OC, e.y, e.ycs, e.bias, e.bcs, e.res, e.rcs);
     if (a.copy_dst)  // the output aliased the input: the kernel wrote a staging buffer
         TTS_HIP_CHECK(hipMemcpyAsync(a.copy_dst, a.y, (size_t)a.OL * (size_t)a.OC * 4, hipMemcpyDeviceToDevice, be->stream));
 }
@@ -551,7 +630,7 @@ __global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w,
 // products.  f32 x f32 products are exact in f64; only the f64 summation order differs from the
 // oracle (tests: rel 1e-5 per layer, PCM 1e-4 end to end).
 template <int S>
-__global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p) {
+__global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, double * __restrict__ part = nullptr, int icps = 0) {
     constexpr int JM = 2, K = 2 * S;  // DAC / SNAC / Kokoro upsamplers: kernel = 2 * stride
     constexpr int QT = 64, OCT = 32, ICC = 16, XW = QT + JM - 1;
     constexpr int NX = ICC * XW, NW4 = ICC * K * OCT / 4;
@@ -605,11 +684,14 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p) 
             o[0] = wr[u].x, o[OCT] = wr[u].y, o[2 * OCT] = wr[u].z, o[3 * OCT] = wr[u].w;
         }
     };
-    fetch(0);
-    for (int ic0 = 0; ic0 < IC; ic0 += ICC) {
+    // split launch: input channels [ic_lo, ic_hi) (whole chunks), f64 partials to part[z][oc][o]
+    const int ic_lo = part ? (int)blockIdx.z * icps : 0;
+    const int ic_hi = part ? min(IC, ic_lo + icps) : IC;
+    fetch(ic_lo);
+    for (int ic0 = ic_lo; ic0 < ic_hi; ic0 += ICC) {
         stage();
         __syncthreads();
-        if (ic0 + ICC < IC) fetch(ic0 + ICC);
+        if (ic0 + ICC < ic_hi) fetch(ic0 + ICC);
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const int icl = 4 * kk + kq;
@@ -644,7 +726,9 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p) 
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const int oc = oc0 + h * 16 + kq + 4 * e;
-                if (oc < OC) *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc[r][h][e];
+                if (oc >= OC) continue;
+                if (part) part[((int64_t)blockIdx.z * OC + oc) * OL + o] = acc[r][h][e];
+                else *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc[r][h][e];
             }
     }
 }
@@ -656,16 +740,24 @@ void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
     // the LDS kernel reads whole 4-tap float4 rows of the weight: contiguous taps (nb0 = 4), 16-B rows
     const bool wvec = w->nb[0] == 4 && w->nb[1] % 16 == 0 && w->nb[2] % 16 == 0 && ((uintptr_t)w->data % 16) == 0;
     if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16 && (s == 2 || s == 4 || s == 6 || s == 8 || s == 10) && w->ne[0] == 2 * s && wvec &&
-        be->convt_lds) {
+        be->convt_lds && node->nb[0] == 4) {
         const int64_t nq = (node->ne[0] + p) / s + 1;
-        const dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((w->ne[1] + 31) / 32));
+        dim3 grid((unsigned)((nq + 63) / 64), (unsigned)((w->ne[1] + 31) / 32));
         const TD Y = make_td(node), X = make_td(x), W = make_td(w);
-        if (s == 2) hipLaunchKernelGGL((k_convt_f64_lds<2>), grid, dim3(256), 0, be->stream, Y, X, W, p);
-        else if (s == 4) hipLaunchKernelGGL((k_convt_f64_lds<4>), grid, dim3(256), 0, be->stream, Y, X, W, p);
-        else if (s == 6) hipLaunchKernelGGL((k_convt_f64_lds<6>), grid, dim3(256), 0, be->stream, Y, X, W, p);
-        else if (s == 8) hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p);
-        else hipLaunchKernelGGL((k_convt_f64_lds<10>), grid, dim3(256), 0, be->stream, Y, X, W, p);
+        // short sequences: split the input channels (chunks of 16) over extra workgroups
+        const int64_t IC = x->ne[1], OL = node->ne[0], OC = node->ne[1];
+        const int64_t nchunk = (IC + 15) / 16;
+        const int nz = split_count(be, (int64_t)grid.x * grid.y, nchunk, 2, OL * OC);
+        const int icps = nz > 1 ? (int)(((nchunk + nz - 1) / nz) * 16) : 0;
+        double * part = nz > 1 ? be->conv_part : nullptr;
+        grid.z = nz > 1 ? (unsigned)((IC + icps - 1) / icps) : 1u;
+        if (s == 2) hipLaunchKernelGGL((k_convt_f64_lds<2>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
+        else if (s == 4) hipLaunchKernelGGL((k_convt_f64_lds<4>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
+        else if (s == 6) hipLaunchKernelGGL((k_convt_f64_lds<6>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
+        else if (s == 8) hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
+        else hipLaunchKernelGGL((k_convt_f64_lds<10>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
         TTS_HIP_CHECK(hipGetLastError());
+        if (part) launch_split_reduce(be, (int)grid.z, OL, OC, (float *)node->data, (int64_t)(node->nb[1] / 4), nullptr, 0, nullptr, 0);
         return;
     }
     if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16) {
