@@ -43,7 +43,7 @@ extern "C" {
 #define TTS_MAX_DIMS 4
 #define TTS_MAX_SRC 4
 #define TTS_MAX_OP_PARAMS 16
-#define TTS_MAX_NAME 48
+#define TTS_MAX_NAME 64 /* GGML_MAX_NAME */
 
 /* ggml_type numbering (ggml.h of the fork's early-2025 base). */
 enum tts_type {
@@ -105,7 +105,17 @@ enum tts_op {
     TTS_OP_ROUND,  /* fork op */
     TTS_OP_STFT,   /* fork op */
     TTS_OP_ISTFT,  /* fork op */
+    TTS_OP_MAP_CUSTOM3, /* ggml_map_custom3 with a CPU callback in the reference; op_params[0] names
+                           which one (tts_custom_op) and the backend runs its device restatement */
     TTS_OP_COUNT
+};
+
+/* The reference's ggml_map_custom* callbacks a graph may carry (op_params[0] of MAP_CUSTOM3). */
+enum tts_custom_op {
+    TTS_CUSTOM_NONE = 0,
+    /* uv_noise_compute (src/util.cpp:140-170): a = shape [L, H, 2], b = upscaled F0 [L],
+     * c = [threshold, noise_std, sin_amp, sin_amp/3, rand[H][L]] (f32) -> plane 0 uv, plane 1 noise */
+    TTS_CUSTOM_UV_NOISE = 1
 };
 
 enum tts_unary_op {

@@ -278,6 +278,65 @@ uint64_t tts_kokoro_gen_node(tts_kokoro_gen * k, int32_t i, int32_t * op, int32_
 /* The last graph's node list (valid until the next run), e.g. for tts_hip_plan_stats. */
 tts_tensor * const * tts_kokoro_gen_graph(const tts_kokoro_gen * k, int32_t * n_nodes);
 
+/* Kokoro-82M end to end (phoneme tokens -> 24 kHz PCM): kokoro_duration_runner's graph
+ * (ALBERT x n_recurrence, prosody DurationEncoder, duration LSTM + projection -> per-token
+ * lengths; src/models/kokoro/model.cpp:938-1047) and kokoro_runner's graph (duration-mask
+ * expansion, shared LSTM, F0 / N AdaIN residual stacks, text encoder, decoder blocks, then the
+ * generator above; model.cpp:1141-1242), with the host steps between them as kokoro_runner::run /
+ * set_inputs do them (model.cpp:1253-1325): read the lengths back, build the [total, n] duration
+ * mask, upload.  Defaults = Kokoro-82M (ALBERT 178 x 128 -> 768, 12 heads, ffn 2048, one shared
+ * layer x 12; d_model 512; decoder 1024; style 2 x 128).  Synthetic weights. */
+typedef struct tts_kokoro_config {
+    tts_kokoro_gen_config gen; /* generator (gen.in_channels = last decoder block width, gen.style_dim = style half) */
+    int32_t n_vocab;           /* 178 phoneme ids */
+    int32_t embd;              /* 128 ALBERT embedding width */
+    int32_t hidden;            /* 768 ALBERT hidden */
+    int32_t n_heads;           /* 12 */
+    int32_t ffn;               /* 2048 */
+    int32_t n_layers;          /* 1 (ALBERT's shared layer group) */
+    int32_t n_recurrence;      /* 12 */
+    int32_t max_context;       /* 512 positions */
+    int32_t d_model;           /* 512: duration_hidden_size, text encoder channels */
+    int32_t n_dur_layers;      /* 3 DurationEncoder LSTM + AdaLayerNorm layers */
+    int32_t max_dur;           /* 50: duration_proj width (and the clamp bound) */
+    int32_t te_kernel;         /* 5 */
+    int32_t te_depth;          /* 3 */
+    int32_t dec_dim;           /* 1024 */
+    int32_t asr_res_dim;       /* 64 */
+    int32_t n_decode;          /* 4 decoder blocks (the last upsamples x2) */
+    int32_t n_voice_rows;      /* 510 rows per voice pack */
+    int32_t max_tokens;        /* per call (arena sizing), <= max_context */
+    int32_t max_total;         /* duration frames per call (arena sizing); PCM = 600 per frame */
+    float dur_bias;            /* synthetic duration_proj bias (-2.6: ~4 frames per token) */
+    float f0_mean;             /* synthetic F0 projection bias (Hz) */
+    int32_t debug_no_reuse;
+    uint64_t seed;
+    uint64_t arena_bytes;      /* 0 = sized from max_tokens / max_total */
+} tts_kokoro_config;
+
+typedef struct tts_kokoro tts_kokoro;
+void tts_kokoro_default_config(tts_kokoro_config * cfg);
+tts_kokoro * tts_kokoro_create(const tts_backend_iface * be, const tts_kokoro_config * cfg);
+void tts_kokoro_free(tts_kokoro * k);
+/* The duration graph alone (kokoro_duration_runner::run): tokens [n] (3 <= n <= max_tokens) ->
+ * hidden [n][d_model + style half] and lengths [n] (rounded, clamped to [1, max_dur]). */
+int tts_kokoro_durations(tts_kokoro * k, const int32_t * tokens, int32_t n, float * hidden, float * lengths);
+/* The main graph from given durations (kokoro_runner's graph + set_inputs): hidden / lengths as
+ * tts_kokoro_durations returns them; rand = [harmonic_num + 1][600 * total] draws or NULL;
+ * pcm gets 600 * total samples (total = sum of lengths). */
+int tts_kokoro_decode(tts_kokoro * k, const int32_t * tokens, int32_t n, const float * hidden, const float * lengths,
+                      const float * rand, float * pcm, uint64_t pcm_cap);
+/* Both (kokoro_runner::run); *n_samples = 600 * total. */
+int tts_kokoro_run(tts_kokoro * k, const int32_t * tokens, int32_t n, const float * rand, float * pcm, uint64_t pcm_cap,
+                   int64_t * n_samples);
+int32_t tts_kokoro_last_graph_nodes(const tts_kokoro * k, int32_t which); /* 0 = duration, 1 = main */
+int32_t tts_kokoro_n_weights(const tts_kokoro * k);
+/* Weight i (front half first, then the generator's): name, ne[4], f32 values; returns bytes. */
+uint64_t tts_kokoro_weight(tts_kokoro * k, int32_t i, char * name, uint64_t name_cap, int64_t * ne, float * dst, uint64_t cap);
+/* Debug: bytes of the named node of the last duration (which = 0) or main (1) graph. */
+uint64_t tts_kokoro_get_node(tts_kokoro * k, int32_t which, const char * name, void * dst, uint64_t cap);
+tts_tensor * const * tts_kokoro_graph(const tts_kokoro * k, int32_t which, int32_t * n_nodes);
+
 #ifdef __cplusplus
 }
 #endif

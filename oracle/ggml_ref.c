@@ -1008,6 +1008,33 @@ static void op_istft(tts_tensor * dst, int ith, int nth) {
     free(tc);
 }
 
+/* MAP_CUSTOM3 / uv_noise_compute (src/util.cpp:140-170): per upsampled sample r (threads split
+ * r as the reference's ith/nth do), voiced = f0_up[r] > threshold; over harmonics h,
+ * uv[h][r] = voiced ? sin_amp : 0, noise[h][r] = (voiced ? noise_std : sin_amp/3) * rand[h][r]. */
+static int op_map_custom3(tts_tensor * dst, int ith, int nth) {
+    if (dst->op_params[0] != TTS_CUSTOM_UV_NOISE) return TTS_STATUS_UNSUPPORTED;
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    const float * cd = (const float *)dst->src[2]->data;
+    const float thr = cd[0], noise_std = cd[1], sin_amp = cd[2], amp_div = cd[3];
+    const float * rnd = cd + 4;
+    const float * tgt = (const float *)b->data;
+    float * uv = (float *)dst->data;
+    float * noise = (float *)((char *)dst->data + dst->nb[2]);
+    const int64_t L = dst->ne[0];
+    const int64_t rpt = (b->ne[0] + nth - 1) / nth;
+    const int64_t r0 = ith * rpt, r1 = (ith + 1) * rpt < b->ne[0] ? (ith + 1) * rpt : b->ne[0];
+    for (int64_t r = r0; r < r1; ++r) {
+        const int voiced = tgt[r] > thr;
+        for (int64_t h = 0; h < a->ne[1]; ++h) {
+            const int64_t i = h * L + r;
+            uv[i] = voiced ? sin_amp : 0.0f;
+            noise[i] = (voiced ? noise_std : amp_div) * rnd[i];
+        }
+    }
+    return 0;
+}
+
 static int is_view_op(int op) {
     return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
 }
@@ -1036,6 +1063,7 @@ static int compute_node_mt(tts_tensor * node, int ith, int nth) {
         case TTS_OP_UPSCALE: op_upscale(node, ith, nth); return 0;
         case TTS_OP_STFT: op_stft(node, ith, nth); return 0;
         case TTS_OP_ISTFT: op_istft(node, ith, nth); return 0;
+        case TTS_OP_MAP_CUSTOM3: return op_map_custom3(node, ith, nth);
         default: return TTS_STATUS_UNSUPPORTED;
     }
 }

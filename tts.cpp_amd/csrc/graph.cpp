@@ -413,6 +413,15 @@ tts_tensor * istft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, 
     return t;
 }
 
+// ggml_map_custom3(a, b, c, fn): dst has a's shape; fn is one of tts_custom_op (the reference's
+// CPU callback, restated on the device by the backend)
+tts_tensor * map_custom3(context & c, tts_tensor * a, tts_tensor * b, tts_tensor * cc, int fn) {
+    tts_tensor * t = new_op(c, TTS_OP_MAP_CUSTOM3, TTS_TYPE_F32, a->ne, a, b);
+    t->src[2] = cc;
+    t->op_params[0] = fn;
+    return t;
+}
+
 tts_tensor * sum_rows(context & c, tts_tensor * a) {
     int64_t ne[4] = {1, a->ne[1], a->ne[2], a->ne[3]};
     return new_op(c, TTS_OP_SUM_ROWS, TTS_TYPE_F32, ne, a);

@@ -1550,6 +1550,11 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     Planner pl;
     pl.mask = mask;
     pl.vec_cap = 1u << 18;
+    // the LSTM scratch is only addressed, never touched, while planning: a stand-in base with the
+    // backend's capacity lets the stats see the fusions a device run makes
+    static float lstm_stand_in alignas(256);
+    pl.lstm_buf = &lstm_stand_in;
+    pl.lstm_cap = (size_t)4 << 20;
     if (mask) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
     for (int k = 0; k < 16; ++k) counts[k] = 0;

@@ -193,6 +193,19 @@ __global__ __launch_bounds__(ISTFT_TILE) void k_istft(TD dst, TD a, TD win, int 
 
 // ------------------------------------------------------------------------------------------
 
+// ---- MAP_CUSTOM3 / uv_noise_compute (src/util.cpp:140-170) -------------------------------------
+// One thread per (sample r, harmonic h): the reference's CPU callback as a device elementwise pass
+// over the upsampled F0 it reads, so the sine source needs no mid-graph round trip to the host.
+__global__ __launch_bounds__(256) void k_uv_noise(float * __restrict__ uv, float * __restrict__ noise, const float * __restrict__ f0up,
+                                                  const float * __restrict__ cdata, int64_t L, int64_t n) {
+    const float thr = cdata[0], noise_std = cdata[1], sin_amp = cdata[2], amp_div = cdata[3];
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const bool voiced = f0up[i % L] > thr;
+        uv[i] = voiced ? sin_amp : 0.0f;
+        noise[i] = (voiced ? noise_std : amp_div) * cdata[4 + i];
+    }
+}
+
 static size_t istft_lds(int N, int H, int K) { return (size_t)16 * N + (size_t)16 * istft_tile_frames(N, H) * K; }
 
 bool audio_op_supported(const tts_tensor * n) {
@@ -206,6 +219,14 @@ bool audio_op_supported(const tts_tensor * n) {
         case TTS_OP_STFT: {
             const int N = n->op_params[0], H = n->op_params[1];
             return N >= 1 && H >= 1 && 16 * (size_t)N <= 64 * 1024 && a->ne[0] > N / 2 && n->src[1] && n->src[1]->type == TTS_TYPE_F32;
+        }
+        case TTS_OP_MAP_CUSTOM3: {
+            // contiguous [L, H, 2] destination, F0 of length L, data = 4 + L*H floats
+            const tts_tensor *b = n->src[1], *c = n->src[2];
+            return n->op_params[0] == TTS_CUSTOM_UV_NOISE && b && c && b->type == TTS_TYPE_F32 && c->type == TTS_TYPE_F32 &&
+                   n->ne[2] == 2 && n->ne[3] == 1 && b->ne[0] == n->ne[0] && b->nb[0] == 4 && n->nb[0] == 4 &&
+                   n->nb[1] == 4 * (size_t)n->ne[0] && n->nb[2] == n->nb[1] * (size_t)n->ne[1] &&
+                   c->ne[0] * c->ne[1] * c->ne[2] * c->ne[3] >= 4 + n->ne[0] * n->ne[1];
         }
         case TTS_OP_ISTFT: {
             const int N = n->op_params[0], H = n->op_params[1];
@@ -250,6 +271,14 @@ int launch_audio_op(tts_hip_backend * be, const tts_tensor * n) {
             const unsigned tiles = (unsigned)((n->ne[0] + ISTFT_TILE - 1) / ISTFT_TILE);
             hipLaunchKernelGGL(k_istft, dim3(tiles, (unsigned)n->ne[1]), dim3(ISTFT_TILE), lds, be->stream, d, a,
                                make_td(n->src[1]), N, H, n->op_params[2]);
+        } break;
+        case TTS_OP_MAP_CUSTOM3: {
+            const int64_t L = n->ne[0], cnt = L * n->ne[1];
+            int64_t g = (cnt + 255) / 256;
+            if (g > 8192) g = 8192;
+            float * uv = (float *)n->data;
+            hipLaunchKernelGGL(k_uv_noise, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, be->stream, uv, (float *)((char *)n->data + n->nb[2]),
+                               (const float *)n->src[1]->data, (const float *)n->src[2]->data, L, cnt);
         } break;
         default: return TTS_STATUS_UNSUPPORTED;
     }

@@ -2,9 +2,10 @@
 // node list of build_generator (/root/reference/src/models/kokoro/model.cpp:195-244) with
 // build_sin_gen (:172-193), build_noise_block (:167-171), build_kokoro_generator_res_block
 // (:136-165), snake_1d / reciprocal (util.cpp:86-101) and the util.cpp stft / istft wrappers
-// (:111-130).  Two pieces the reference runs on the CPU stay on the host here as they do there:
-// the uv / noise custom map (uv_noise_compute, util.cpp:140-170) and the window-envelope
-// normaliser (compute_window_squared_sum, util.cpp:203-217); both are uploaded as inputs.
+// (:111-130).  The reference's uv / noise custom map (uv_noise_compute, util.cpp:140-170, a CPU
+// ggml_map_custom3) is the same MAP_CUSTOM3 node here, run by the backend on the device over the
+// upscaled F0 it reads; its uniform draws and the window-envelope normaliser
+// (compute_window_squared_sum, util.cpp:203-217) are host inputs, as in kokoro_runner::set_inputs.
 // Weights are deterministic synthetic tensors in Kokoro-82M shapes (no checkpoints offline).
 #include <cmath>
 #include <cstring>
@@ -13,6 +14,7 @@
 #include <vector>
 
 #include "graph.h"
+#include "kokoro_gen.h"
 #include "synth.h"
 #include "tts_hip.h"
 #include "tts_runners.h"
@@ -62,8 +64,8 @@ struct tts_kokoro_gen {
     char * arena = nullptr;
     size_t arena_size = 0;
     tg::context gctx;
-    tts_tensor *in_x = nullptr, *in_f0 = nullptr, *in_style = nullptr, *in_uv = nullptr, *in_noise = nullptr, *in_wss = nullptr;
-    std::vector<float> h_uv, h_noise, h_wss, h_rand, h_window;
+    tts_tensor *in_x = nullptr, *in_f0 = nullptr, *in_style = nullptr, *in_uvdata = nullptr, *in_wss = nullptr;
+    std::vector<float> h_uvdata, h_wss, h_window;
 };
 
 extern "C" void tts_kokoro_gen_default_config(tts_kokoro_gen_config * c) {
@@ -220,7 +222,7 @@ extern "C" tts_kokoro_gen * tts_kokoro_gen_create(const tts_backend_iface * be, 
     // the 11-tap im2col in f16; the sine source adds a few [300, 9] tensors
     const int64_t U = kUpsample;
     const size_t per_frame = (size_t)(U / c.hop) * (size_t)ch * 4 * 14 + (size_t)(U / c.hop) * 11 * (size_t)ch * 2 * 2 +
-                             (size_t)U * (size_t)(c.harmonic_num + 1) * 4 * 8 + (size_t)(U / c.hop / c.up_rates[c.n_ups - 1]) * (size_t)c.in_channels * 4 * 16;
+                             (size_t)U * (size_t)(c.harmonic_num + 1) * 4 * 16 + (size_t)(U / c.hop / c.up_rates[c.n_ups - 1]) * (size_t)c.in_channels * 4 * 16;
     k->arena_size = c.arena_bytes ? c.arena_bytes : (size_t)c.max_frames * per_frame + ((size_t)64 << 20);
     k->arena = (char *)k->be.alloc(k->be.ctx, k->arena_size);
     if (!k->arena) {
@@ -267,27 +269,29 @@ static tts_tensor * res_block(tts_kokoro_gen * k, tg::context & c, const kk_res 
     return inpl;
 }
 
-static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
+// build_sin_gen + build_generator (model.cpp:172-244) into `c`: x [C, T] features (channel
+// fastest), f0 [T] (or [T, 1]) Hz, style [style_dim].  Registers the uv_noise data and envelope
+// inputs on k (filled by kokoro_gen_set_inputs) and returns the PCM node [300 T].
+tts_tensor * tts::kokoro_gen_build(tts_kokoro_gen * k, tg::context & c, tts_tensor * x, tts_tensor * f0, tts_tensor * style, int64_t T) {
     const auto & cf = k->cfg;
-    tg::context & c = k->gctx;
-    c.reset();
     const int64_t H = cf.harmonic_num + 1, L = T * kUpsample;
-    k->in_x = tg::new_tensor_2d(c, TTS_TYPE_F32, cf.in_channels, T);
-    k->in_f0 = tg::new_tensor_1d(c, TTS_TYPE_F32, T);
-    k->in_style = tg::new_tensor_1d(c, TTS_TYPE_F32, cf.style_dim);
-    k->in_uv = tg::new_tensor_2d(c, TTS_TYPE_F32, L, H);
-    k->in_noise = tg::new_tensor_2d(c, TTS_TYPE_F32, L, H);
+    k->in_uvdata = tg::new_tensor_1d(c, TTS_TYPE_F32, 4 + L * H);
     k->in_wss = tg::new_tensor_1d(c, TTS_TYPE_F32, L);
-    for (tts_tensor * t : {k->in_x, k->in_f0, k->in_style, k->in_uv, k->in_noise, k->in_wss}) tg::set_input(t);
-    tts_tensor * style = k->in_style;
+    tg::set_input(k->in_uvdata);
+    tg::set_input(k->in_wss);
 
-    // build_sin_gen (model.cpp:172-193): harmonic phases, x300 linear interpolation, sin; the
-    // custom uv/noise map's two planes arrive as inputs
-    tts_tensor * f0 = k->in_f0;
+    // build_sin_gen (model.cpp:172-193): harmonic phases, x300 linear interpolation, sin, and the
+    // uv / noise planes from the custom map over the nearest-x300 F0
     tts_tensor * cur = tg::mul(c, tg::repeat(c, f0, tg::new_tensor_2d(c, TTS_TYPE_F32, T, H)), k->harm_norm);
     cur = tg::mul(c, tg::cumsum(c, tg::mod(c, cur, 1.0f)), k->samp_scalar);
     cur = tg::upscale_linear(c, cur, kUpsample);
-    tts_tensor * sing = tg::cont(c, tg::transpose(c, tg::add(c, tg::mul(c, tg::sin(c, cur), k->in_uv), k->in_noise)));
+    tts_tensor * upscaled = tg::upscale_ext(c, f0, f0->ne[0] * kUpsample, f0->ne[1], f0->ne[2], f0->ne[3]);
+    tts_tensor * fake = tg::new_tensor_3d(c, TTS_TYPE_F32, L, H, 2);
+    tts_tensor * uv_noise = tg::map_custom3(c, fake, upscaled, k->in_uvdata, TTS_CUSTOM_UV_NOISE);
+    tg::set_name(uv_noise, "uv_noise");
+    tts_tensor * noise = tg::cont(c, tg::view_2d(c, uv_noise, uv_noise->ne[0], uv_noise->ne[1], uv_noise->nb[1], uv_noise->nb[2]));
+    tts_tensor * uv = tg::cont(c, tg::view_2d(c, uv_noise, uv_noise->ne[0], uv_noise->ne[1], uv_noise->nb[1], 0));
+    tts_tensor * sing = tg::cont(c, tg::transpose(c, tg::add(c, tg::mul(c, tg::sin(c, cur), uv), noise)));
 
     // build_generator (model.cpp:195-244)
     tts_tensor * har = tg::tanh(c, tg::add(c, tg::mul_mat(c, k->m_w, sing), k->m_b));
@@ -300,7 +304,7 @@ static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
     tg::set_name(sing, "sine_source");
     tg::set_name(combined, "har_spec");
 
-    cur = k->in_x;
+    cur = x;
     for (int i = 0; i < cf.n_ups; ++i) {
         const kk_up & u = k->ups[i];
         cur = tg::leaky_relu(c, cur, 0.1f);
@@ -339,35 +343,38 @@ static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
     cur = tg::istft(c, tg::cont(c, tg::transpose(c, cur)), k->window, cf.n_fft, cf.hop, true);
     cur = tg::div(c, cur, k->in_wss);
     tg::set_name(cur, "after_res_gen");
+    return cur;
+}
+
+static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
+    const auto & cf = k->cfg;
+    tg::context & c = k->gctx;
+    c.reset();
+    k->in_x = tg::new_tensor_2d(c, TTS_TYPE_F32, cf.in_channels, T);
+    k->in_f0 = tg::new_tensor_1d(c, TTS_TYPE_F32, T);
+    k->in_style = tg::new_tensor_1d(c, TTS_TYPE_F32, cf.style_dim);
+    for (tts_tensor * t : {k->in_x, k->in_f0, k->in_style}) tg::set_input(t);
+    tts_tensor * cur = kokoro_gen_build(k, c, k->in_x, k->in_f0, k->in_style, T);
     tg::set_output(cur);
     tg::build_forward_expand(c, cur);
     return cur;
 }
 
-// uv_noise_compute (util.cpp:140-170) over the nearest-upscaled F0 (ggml upscale: i / (ne_dst /
-// ne_src) in f32), and compute_window_squared_sum (util.cpp:203-217)
-static void host_inputs(tts_kokoro_gen * k, const float * f0, int64_t T, const float * rand) {
+// kokoro_runner::set_inputs (model.cpp:1253-1256): the uv_noise custom map's data block -- its
+// four constants, then random_uniform_gen's [H][300 T] draws -- and compute_window_squared_sum
+// (util.cpp:203-217); uploads both to the inputs kokoro_gen_build registered.
+int tts::kokoro_gen_set_inputs(tts_kokoro_gen * k, int64_t T, const float * rand) {
     const auto & cf = k->cfg;
     const int64_t H = cf.harmonic_num + 1, L = T * kUpsample;
-    k->h_rand.resize((size_t)(L * H));
+    k->h_uvdata.resize((size_t)(4 + L * H));
+    float * d = k->h_uvdata.data();
+    d[0] = cf.voice_threshold, d[1] = cf.noise_std, d[2] = cf.sin_amp, d[3] = cf.sin_amp / 3.0f;
     if (rand) {
-        memcpy(k->h_rand.data(), rand, sizeof(float) * (size_t)(L * H));
+        memcpy(d + 4, rand, sizeof(float) * (size_t)(L * H));
     } else {
         std::minstd_rand0 e((uint32_t)(cf.seed ^ 0x5A5A));
         std::uniform_real_distribution<float> dis(0.0f, 1.0f);
-        for (auto & v : k->h_rand) v = dis(e);
-    }
-    k->h_uv.resize((size_t)(L * H));
-    k->h_noise.resize((size_t)(L * H));
-    const float sf = (float)L / (float)T;
-    const float amp_div = cf.sin_amp / 3.0f;
-    for (int64_t r = 0; r < L; ++r) {
-        const bool voiced = f0[(int64_t)((float)r / sf)] > cf.voice_threshold;
-        for (int64_t h = 0; h < H; ++h) {
-            const int64_t i = h * L + r;
-            k->h_uv[i] = voiced ? cf.sin_amp : 0.0f;
-            k->h_noise[i] = (voiced ? cf.noise_std : amp_div) * k->h_rand[i];
-        }
+        for (int64_t i = 0; i < L * H; ++i) d[4 + i] = dis(e);
     }
     const int64_t n_frames = L / cf.hop, cutoff = n_frames * cf.hop, half = cf.n_fft / 2;
     k->h_wss.assign((size_t)L, 0.0f);
@@ -377,6 +384,9 @@ static void host_inputs(tts_kokoro_gen * k, const float * f0, int64_t T, const f
             if (idx < 0 || idx >= cutoff) continue;
             k->h_wss[idx] += powf(k->h_window[j], 2);
         }
+    int st = k->be.set(k->be.ctx, k->in_uvdata->data, k->h_uvdata.data(), sizeof(float) * k->h_uvdata.size());
+    if (st == 0) st = k->be.set(k->be.ctx, k->in_wss->data, k->h_wss.data(), sizeof(float) * k->h_wss.size());
+    return st;
 }
 
 extern "C" int tts_kokoro_gen_run(tts_kokoro_gen * k, const float * x, const float * f0, const float * style, const float * rand,
@@ -387,14 +397,11 @@ extern "C" int tts_kokoro_gen_run(tts_kokoro_gen * k, const float * x, const flo
         fprintf(stderr, "kokoro: compute arena too small (%zu needed)\n", k->gctx.arena_used);
         return TTS_STATUS_ALLOC_FAILED;
     }
-    host_inputs(k, f0, T, rand);
     const auto & cf = k->cfg;
-    int st = k->be.set(k->be.ctx, k->in_x->data, x, sizeof(float) * (size_t)T * cf.in_channels);
+    int st = kokoro_gen_set_inputs(k, T, rand);
+    if (st == 0) st = k->be.set(k->be.ctx, k->in_x->data, x, sizeof(float) * (size_t)T * cf.in_channels);
     if (st == 0) st = k->be.set(k->be.ctx, k->in_f0->data, f0, sizeof(float) * (size_t)T);
     if (st == 0) st = k->be.set(k->be.ctx, k->in_style->data, style, sizeof(float) * (size_t)cf.style_dim);
-    if (st == 0) st = k->be.set(k->be.ctx, k->in_uv->data, k->h_uv.data(), sizeof(float) * k->h_uv.size());
-    if (st == 0) st = k->be.set(k->be.ctx, k->in_noise->data, k->h_noise.data(), sizeof(float) * k->h_noise.size());
-    if (st == 0) st = k->be.set(k->be.ctx, k->in_wss->data, k->h_wss.data(), sizeof(float) * k->h_wss.size());
     if (st == 0) st = k->be.compute(k->be.ctx, k->gctx.nodes.data(), (int)k->gctx.nodes.size());
     if (st == 0 && pcm) st = k->be.get(k->be.ctx, pcm, out->data, sizeof(float) * (size_t)tg::nelements(out));
     return st;

@@ -18,7 +18,7 @@ F32, F16, Q4_0, Q8_0, Q4_K, Q8_K, I32 = 0, 1, 2, 8, 12, 15, 26
 OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "SUM_ROWS", "REPEAT",
        "CONCAT", "NORM", "RMS_NORM", "MUL_MAT", "SCALE", "CPY", "CONT", "RESHAPE", "VIEW", "PERMUTE",
        "TRANSPOSE", "GET_ROWS", "SOFT_MAX", "ROPE", "CLAMP", "CONV_TRANSPOSE_1D", "IM2COL", "UPSCALE",
-       "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT"]
+       "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT", "MAP_CUSTOM3"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
 FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048, "MCPY": 4096}
@@ -49,7 +49,7 @@ TtsTensor._fields_ = [
     ("data", ctypes.c_void_p),
     ("flags", ctypes.c_int32),
     ("pad_", ctypes.c_int32),
-    ("name", ctypes.c_char * 48),
+    ("name", ctypes.c_char * 64),
 ]
 
 
@@ -189,6 +189,36 @@ class KokoroGenConfig(ctypes.Structure):
     ]
 
 
+class KokoroConfig(ctypes.Structure):
+    _fields_ = [
+        ("gen", KokoroGenConfig),
+        ("n_vocab", ctypes.c_int32),
+        ("embd", ctypes.c_int32),
+        ("hidden", ctypes.c_int32),
+        ("n_heads", ctypes.c_int32),
+        ("ffn", ctypes.c_int32),
+        ("n_layers", ctypes.c_int32),
+        ("n_recurrence", ctypes.c_int32),
+        ("max_context", ctypes.c_int32),
+        ("d_model", ctypes.c_int32),
+        ("n_dur_layers", ctypes.c_int32),
+        ("max_dur", ctypes.c_int32),
+        ("te_kernel", ctypes.c_int32),
+        ("te_depth", ctypes.c_int32),
+        ("dec_dim", ctypes.c_int32),
+        ("asr_res_dim", ctypes.c_int32),
+        ("n_decode", ctypes.c_int32),
+        ("n_voice_rows", ctypes.c_int32),
+        ("max_tokens", ctypes.c_int32),
+        ("max_total", ctypes.c_int32),
+        ("dur_bias", ctypes.c_float),
+        ("f0_mean", ctypes.c_float),
+        ("debug_no_reuse", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+    ]
+
+
 _lib = None
 
 
@@ -288,6 +318,17 @@ def lib():
         "tts_snac_n_weights": (i32, [vp]),
         "tts_snac_get_node": (u64, [vp, ctypes.c_char_p, vp, u64]),
         "tts_snac_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
+        "tts_kokoro_default_config": (None, [ctypes.POINTER(KokoroConfig)]),
+        "tts_kokoro_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(KokoroConfig)]),
+        "tts_kokoro_free": (None, [vp]),
+        "tts_kokoro_durations": (ctypes.c_int, [vp, vp, i32, vp, vp]),
+        "tts_kokoro_decode": (ctypes.c_int, [vp, vp, i32, vp, vp, vp, vp, u64]),
+        "tts_kokoro_run": (ctypes.c_int, [vp, vp, i32, vp, vp, u64, ctypes.POINTER(ctypes.c_int64)]),
+        "tts_kokoro_last_graph_nodes": (i32, [vp, i32]),
+        "tts_kokoro_n_weights": (i32, [vp]),
+        "tts_kokoro_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
+        "tts_kokoro_get_node": (u64, [vp, i32, ctypes.c_char_p, vp, u64]),
+        "tts_kokoro_graph": (vp, [vp, i32, ctypes.POINTER(i32)]),
         "tts_kokoro_gen_default_config": (None, [ctypes.POINTER(KokoroGenConfig)]),
         "tts_kokoro_gen_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(KokoroGenConfig)]),
         "tts_kokoro_gen_free": (None, [vp]),
@@ -740,6 +781,120 @@ def kokoro_gen_config(**kw):
         else:
             setattr(cfg, k, v)
     return cfg
+
+
+def kokoro_config(gen=None, **kw):
+    """tts_kokoro_config with Kokoro-82M defaults; gen = dict of generator fields."""
+    cfg = KokoroConfig()
+    lib().tts_kokoro_default_config(ctypes.byref(cfg))
+    for k, v in (gen or {}).items():
+        if isinstance(v, (list, tuple)):
+            arr = getattr(cfg.gen, k)
+            for i, r in enumerate(v):
+                arr[i] = r
+        else:
+            setattr(cfg.gen, k, v)
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+class Kokoro:
+    """Kokoro-82M end to end (phoneme ids -> durations -> 24 kHz PCM) over a backend vtable."""
+
+    def __init__(self, iface, cfg):
+        self.L = lib()
+        self.cfg = cfg
+        self._iface = iface
+        self.ptr = self.L.tts_kokoro_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if not self.ptr:
+            raise RuntimeError("tts_kokoro_create failed")
+
+    def durations(self, tokens):
+        """tokens (n,) int -> (hidden (n, d_model + style), lengths (n,))."""
+        import numpy as np
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        n = t.shape[0]
+        hidden = np.empty((n, self.cfg.d_model + self.cfg.gen.style_dim), dtype=np.float32)
+        lens = np.empty(n, dtype=np.float32)
+        st = self.L.tts_kokoro_durations(self.ptr, t.ctypes.data, n, hidden.ctypes.data, lens.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"tts_kokoro_durations failed {st}")
+        return hidden, lens
+
+    def decode(self, tokens, hidden, lengths, rand=None):
+        """-> (600 * sum(lengths),) float32 PCM; rand (harmonic_num + 1, 600 * total) or None."""
+        import numpy as np
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        hidden = np.ascontiguousarray(hidden, dtype=np.float32)
+        lengths = np.ascontiguousarray(lengths, dtype=np.float32)
+        total = int(sum(int(v) for v in lengths))
+        pcm = np.empty(600 * total, dtype=np.float32)
+        rp = None
+        if rand is not None:
+            rand = np.ascontiguousarray(rand, dtype=np.float32)
+            assert rand.shape == (self.cfg.gen.harmonic_num + 1, 600 * total)
+            rp = rand.ctypes.data
+        st = self.L.tts_kokoro_decode(self.ptr, t.ctypes.data, t.shape[0], hidden.ctypes.data, lengths.ctypes.data, rp,
+                                      pcm.ctypes.data, pcm.nbytes)
+        if st != 0:
+            raise RuntimeError(f"tts_kokoro_decode failed {st}")
+        return pcm
+
+    def run(self, tokens, rand=None, max_samples=None):
+        """Both graphs (kokoro_runner::run) -> PCM."""
+        import numpy as np
+        t = np.ascontiguousarray(tokens, dtype=np.int32)
+        cap = max_samples or 600 * self.cfg.max_total
+        pcm = np.empty(cap, dtype=np.float32)
+        ns = ctypes.c_int64()
+        rp = None
+        if rand is not None:
+            rand = np.ascontiguousarray(rand, dtype=np.float32)
+            rp = rand.ctypes.data
+        st = self.L.tts_kokoro_run(self.ptr, t.ctypes.data, t.shape[0], rp, pcm.ctypes.data, pcm.nbytes, ctypes.byref(ns))
+        if st != 0:
+            raise RuntimeError(f"tts_kokoro_run failed {st}")
+        return pcm[: ns.value]
+
+    def weights(self):
+        """{name: float32 array shaped like torch (reversed ggml ne, leading 1s dropped)}."""
+        import numpy as np
+        out = {}
+        for i in range(self.L.tts_kokoro_n_weights(self.ptr)):
+            name = ctypes.create_string_buffer(128)
+            ne = (ctypes.c_int64 * 4)()
+            n = self.L.tts_kokoro_weight(self.ptr, i, name, 128, ne, None, 0)
+            a = np.empty(n // 4, dtype=np.float32)
+            self.L.tts_kokoro_weight(self.ptr, i, name, 128, ne, a.ctypes.data, n)
+            shape = [int(v) for v in reversed(list(ne))]
+            while len(shape) > 1 and shape[0] == 1:
+                shape.pop(0)
+            out[name.value.decode()] = a.reshape(shape)
+        return out
+
+    def node(self, name, which=1):
+        """float32 values of a named node of the last duration (0) / main (1) graph, or None."""
+        import numpy as np
+        n = self.L.tts_kokoro_get_node(self.ptr, which, name.encode(), None, 0)
+        if not n:
+            return None
+        a = np.empty(n // 4, dtype=np.float32)
+        self.L.tts_kokoro_get_node(self.ptr, which, name.encode(), a.ctypes.data, n)
+        return a
+
+    def plan_stats(self, which=1, mask=None):
+        n = ctypes.c_int32()
+        p = self.L.tts_kokoro_graph(self.ptr, which, ctypes.byref(n))
+        return plan_stats(p, n.value, FUSE_ALL if mask is None else mask)
+
+    def last_graph_nodes(self, which=1):
+        return self.L.tts_kokoro_last_graph_nodes(self.ptr, which)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_kokoro_free(self.ptr)
+            self.ptr = None
 
 
 class KokoroGenerator:
