@@ -893,14 +893,32 @@ struct Planner {
         // not alias x.  ggml-alloc often hands a conv's output the memory of its input (freed
         // after IM2COL); then the kernel writes the im2col buffer instead -- dead in the fused
         // form, allocated while x was alive -- and a D2D copy moves the result into place.
-        if (overlap(out, kern) || (bias && overlap(out, bias))) return plan_reject("conv", 10);
+        // The fused item runs at the last absorbed node but reads x (and writes the staging
+        // buffer) then: a node scheduled in between (e.g. a shortcut branch ahead of the residual
+        // ADD, kokoro/model.cpp:122-133) may own that memory by then.  Without the residual the
+        // span usually closes; otherwise the chain is left unfused.
         float * stage = nullptr;
-        if (overlap(out, x)) {
-            const size_t need = (size_t)OL * (size_t)OC * 4;
-            if (tbytes(col) < need || overlap(col, x) || overlap(col, out) || (res && overlap(col, res)) || overlap(col, kern) ||
-                (bias && overlap(col, bias)))
-                return plan_reject("conv", 11);
-            stage = (float *)col->data;
+        for (;;) {
+            if (overlap(out, kern) || (bias && overlap(out, bias))) return plan_reject("conv", 10);
+            stage = nullptr;
+            bool ok = true;
+            if (overlap(out, x)) {
+                const size_t need = (size_t)OL * (size_t)OC * 4;
+                if (tbytes(col) < need || overlap(col, x) || overlap(col, out) || (res && overlap(col, res)) || overlap(col, kern) ||
+                    (bias && overlap(col, bias)))
+                    ok = false;
+                else
+                    stage = (float *)col->data;
+            }
+            for (int j = i + 1; ok && j < absorbed.back(); ++j) {
+                if (std::find(absorbed.begin(), absorbed.end(), j) != absorbed.end() || is_view(nodes[j]->op)) continue;
+                if (overlap(nodes[j], x) || (stage && overlap(nodes[j], col))) ok = false;
+            }
+            if (ok) break;
+            if (!res) return plan_reject("conv", 11);
+            res = nullptr;  // retry with the chain ending at the bias ADD
+            absorbed.pop_back();
+            out = bias ? nb : mm;
         }
         a.x = make_td(x);
         a.w = kern->data;
