@@ -10,7 +10,7 @@ decoder inside the same timed region.  value = audio-seconds produced by all ran
 (RTF^-1) of AR + DAC; the AR-only and DAC-only rates are reported beside it.
 
 Beside the headline line's fields, three more legs of BASELINE.json's configs run on the same GPU:
-"kokoro" (configs[1], the Kokoro-82M iSTFTNet vocoder path), "dia" (configs[3], Dia-1.6B Q8_0 CFG
+"kokoro" (configs[1], Kokoro-82M end to end: durations, decoder, iSTFTNet vocoder), "dia" (configs[3], Dia-1.6B Q8_0 CFG
 decode) and "orpheus" (configs[4]'s per-GPU shard, Orpheus-3B Q4_K decode), each with its own rate; the orpheus leg carries the dequant-GEMV
 roofline at the sizes where the matrix-core GEMV streams (every Orpheus matrix is >= 4 MiB).
 
@@ -263,16 +263,47 @@ def dia_leg(be, args):
         d.close()
 
 
-def kokoro_inputs(cfg, T, rank):
-    """Synthetic generator inputs: decoder features, a voiced F0 contour with unvoiced gaps, a
-    style vector and the uniform noise draws (seeded per rank)."""
-    rng = np.random.default_rng(1000 + rank)
-    x = (rng.standard_normal((T, cfg.in_channels)) * 0.5).astype(np.float32)
-    f0 = (120.0 + 40.0 * np.sin(np.arange(T) / 9.0)).astype(np.float32)
-    f0[(np.arange(T) // 25) % 4 == 3] = 0.0
-    style = rng.standard_normal(cfg.style_dim).astype(np.float32)
-    rand = rng.random((cfg.harmonic_num + 1, 300 * T), dtype=np.float32)
-    return x, f0, style, rand
+def kokoro_prompt(g, vocab):
+    """Synthetic phoneme ids for global prompt g: a Harvard sentence's bytes mapped into the
+    phoneme vocabulary, wrapped in the boundary id 0 as the phonemizer wraps a prompt."""
+    s = HARVARD[g % len(HARVARD)].encode()
+    ids = [(b * 131 + i * 7 + g) % (vocab - 1) + 1 for i, b in enumerate(s)]
+    return np.asarray([0] + ids + [0], dtype=np.int32)
+
+
+def kokoro_leg(be, args, rank, dist, local, world):
+    """BASELINE configs[1]: Kokoro-82M end to end (kokoro_runner::run: duration graph, host mask
+    step, main graph with the iSTFTNet generator) over `kokoro_prompts` Harvard-sentence prompts per
+    GPU, one after another as the reference's runner serves them; synthetic weights."""
+    kcfg = ttship.kokoro_config(max_tokens=64, max_total=600)
+    kok = ttship.Kokoro(be.iface(), kcfg)
+    try:
+        prompts = [kokoro_prompt(rank * args.kokoro_prompts + i, kcfg.n_vocab) for i in range(args.kokoro_prompts)]
+        kok.run(prompts[0])  # warm (code objects, arena)
+        barrier_sync(dist, be)
+        t0 = time.perf_counter()
+        samples = 0
+        for p in prompts:
+            samples += kok.run(p).shape[0]
+        be.sync()
+        dt = max_over_ranks(dist, local, time.perf_counter() - t0)
+        # per-stage split on the first prompt (durations graph vs main graph incl. generator)
+        t1 = time.perf_counter()
+        hidden, lens = kok.durations(prompts[0])
+        t2 = time.perf_counter()
+        kok.decode(prompts[0], hidden, lens)
+        t3 = time.perf_counter()
+        audio = samples / kcfg.gen.sample_rate
+        return {"workload": f"Kokoro-82M end to end (BASELINE configs[1]): tokens -> durations -> decoder -> iSTFTNet PCM, "
+                            f"{args.kokoro_prompts} prompts per GPU, synthetic weights",
+                "audio_sec_per_s": round(world * audio / dt, 3), "ms_per_prompt": round(1000.0 * dt / len(prompts), 3),
+                "audio_sec_per_gpu": round(audio, 3), "tokens_per_prompt": [int(p.shape[0]) for p in prompts],
+                "first_prompt_ms": {"durations": round(1000 * (t2 - t1), 3), "decode": round(1000 * (t3 - t2), 3),
+                                    "frames": int(lens.sum())},
+                "graph_nodes": [kok.last_graph_nodes(0), kok.last_graph_nodes(1)],
+                "dtype": "f32 activations and weights, f16 conv operands (ggml im2col), f64 conv accumulate"}
+    finally:
+        kok.close()
 
 
 def main():
@@ -295,8 +326,7 @@ def main():
     ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
-    ap.add_argument("--kokoro-frames", type=int, default=800, help="Kokoro generator input frames per call (800 = 10 s)")
-    ap.add_argument("--kokoro-calls", type=int, default=4, help="timed Kokoro generator calls per GPU (0 = skip)")
+    ap.add_argument("--kokoro-prompts", type=int, default=8, help="Kokoro-82M prompts per GPU, end to end (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
     ap.add_argument("--dia-steps", type=int, default=32, help="timed Dia-1.6B decoder steps per GPU (0 = skip)")
@@ -335,13 +365,6 @@ def main():
             rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
         reps.append((rb, rr, rd))
     be, runner, dac = reps[0]
-    kok = None
-    if args.kokoro_calls > 0:
-        kcfg = ttship.kokoro_gen_config(max_frames=args.kokoro_frames)
-        kok = ttship.KokoroGenerator(be.iface(), kcfg)
-        kin = kokoro_inputs(kcfg, args.kokoro_frames, rank)
-        kpcm = np.empty(300 * args.kokoro_frames, dtype=np.float32)
-        kok.run(*kin, out=kpcm)  # warm (code objects, arena)
     # text-prompt pass to reach the measured KV length
     for r, (rb, rr, rd) in enumerate(reps):
         rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * args.batch + r * bl))
@@ -379,21 +402,9 @@ def main():
     # capture (incl. planner), exec update
     host.update({k.replace("_ns", "_us"): round(v, 1) for k, v in cdelta.items()})
     kres = None
-    if kok is not None:
-        # BASELINE configs[1]: the Kokoro-82M iSTFTNet vocoder path, timed on its own
+    if args.kokoro_prompts > 0:
         barrier_sync(dist, be)
-        t3 = time.perf_counter()
-        for _ in range(args.kokoro_calls):
-            kok.run(*kin, out=kpcm)
-        barrier_sync(dist, be)
-        dt_k = max_over_ranks(dist, local, time.perf_counter() - t3)
-        k_audio = world * args.kokoro_calls * args.kokoro_frames * 300 / kcfg.sample_rate
-        kres = {"workload": "Kokoro-82M iSTFTNet generator (BASELINE configs[1] vocoder path), synthetic weights",
-                "audio_sec_per_s": round(k_audio / dt_k, 3), "ms_per_call": round(1000.0 * dt_k / args.kokoro_calls, 3),
-                "frames_per_call": args.kokoro_frames, "audio_sec_per_call": args.kokoro_frames * 300 / kcfg.sample_rate,
-                "calls_per_gpu": args.kokoro_calls, "graph_nodes": kok.last_graph_nodes(),
-                "dtype": "f32 activations, f16 conv operands (ggml im2col), f64 conv accumulate",
-                "pcm_std": round(float(np.std(kpcm)), 4)}
+        kres = kokoro_leg(be, args, rank, dist, local, world)
     ores = None
     if args.orpheus_steps > 0:
         barrier_sync(dist, be)
@@ -455,8 +466,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    if kok is not None:
-        kok.close()
     for rb, rr, rd in reps:
         if rd is not None:
             rd.close()

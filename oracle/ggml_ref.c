@@ -1011,8 +1011,20 @@ static void op_istft(tts_tensor * dst, int ith, int nth) {
 /* MAP_CUSTOM3 / uv_noise_compute (src/util.cpp:140-170): per upsampled sample r (threads split
  * r as the reference's ith/nth do), voiced = f0_up[r] > threshold; over harmonics h,
  * uv[h][r] = voiced ? sin_amp : 0, noise[h][r] = (voiced ? noise_std : sin_amp/3) * rand[h][r]. */
+/* The uniform draw of element i when the graph asks for device-side draws (op_params[1] = 1):
+ * splitmix64 of (seed, i), top 24 bits -> [0, 1).  The HIP kernel computes the same values. */
+static float uv_draw(uint64_t seed, uint64_t i) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
 static int op_map_custom3(tts_tensor * dst, int ith, int nth) {
     if (dst->op_params[0] != TTS_CUSTOM_UV_NOISE) return TTS_STATUS_UNSUPPORTED;
+    const int hashed = dst->op_params[1] == 1;
+    const uint64_t seed = (uint64_t)(uint32_t)dst->op_params[2] | ((uint64_t)(uint32_t)dst->op_params[3] << 32);
     const tts_tensor * a = dst->src[0];
     const tts_tensor * b = dst->src[1];
     const float * cd = (const float *)dst->src[2]->data;
@@ -1029,7 +1041,7 @@ static int op_map_custom3(tts_tensor * dst, int ith, int nth) {
         for (int64_t h = 0; h < a->ne[1]; ++h) {
             const int64_t i = h * L + r;
             uv[i] = voiced ? sin_amp : 0.0f;
-            noise[i] = (voiced ? noise_std : amp_div) * rnd[i];
+            noise[i] = (voiced ? noise_std : amp_div) * (hashed ? uv_draw(seed, (uint64_t)i) : rnd[i]);
         }
     }
     return 0;

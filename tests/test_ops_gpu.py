@@ -112,6 +112,27 @@ def test_mul_mat_f32_batched(hip, K, N, M, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,N,M", [(1090, 1024, 332), (46, 319, 640), (768, 768, 64), (640, 256, 9), (33, 70, 100), (2048, 768, 17)])
+@pytest.mark.parametrize("epi", [None, "GELU", "ADD"])
+def test_mul_mat_f32_gemm(hip, K, N, M, epi):
+    """2-D float MUL_MATs with more than 8 columns run on the tiled GEMM (k_gemm.hip), through the
+    planner's GEMV items (<= 64 columns, with their fused GELU / residual epilogues) or the plain op
+    path; sequential f64 sums, so bit-identical to the oracle."""
+    a = rnd(11, N, K, scale=0.2)
+    b = rnd(12, M, K)
+    r = rnd(13, M, N)
+
+    def build(g):
+        mm = g.node("MUL_MAT", F32, [N, M], [g.leaf(a), g.leaf(b)])
+        if epi == "GELU":
+            return [g.node("UNARY", F32, [N, M], [mm], params=[5])]
+        if epi == "ADD":
+            return [g.node("ADD", F32, [N, M], [mm, g.leaf(r)])]
+        return [mm]
+    assert_bits(run_both(hip, build), f"gemm {epi}")
+
+
+@pytest.mark.gpu
 def test_get_rows_and_concat_and_cpy(hip):
     tab = rnd(9, 40, 96)
     idx = np.array([3, 0, 39, 7, 7], dtype=np.int32)

@@ -512,12 +512,36 @@ struct FreeList {
 };
 }  // namespace
 
+// Per-tensor slots for the allocator: open addressing on the tensor address (a 20k-node graph
+// would otherwise spend most of its allocation time in std::unordered_map node allocations).
+namespace {
+struct TensorSlots {
+    std::vector<tts_tensor *> keys;
+    std::vector<int> last_use;
+    std::vector<int64_t> off;  // -1: not (or no longer) allocated by this pass
+    size_t mask = 0;
+    explicit TensorSlots(size_t n) {
+        size_t cap = 64;
+        while (cap < 2 * n) cap <<= 1;
+        keys.assign(cap, nullptr);
+        last_use.assign(cap, -1);
+        off.assign(cap, -1);
+        mask = cap - 1;
+    }
+    size_t at(tts_tensor * t) {  // insert if absent
+        size_t i = (size_t)(((uint64_t)(uintptr_t)t * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+        while (keys[i] && keys[i] != t) i = (i + 1) & mask;
+        keys[i] = t;
+        return i;
+    }
+};
+}  // namespace
+
 bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) {
     FreeList fl;
     fl.cap = arena_size;
-    std::unordered_map<tts_tensor *, size_t> offs;
-    std::unordered_map<tts_tensor *, int> last_use;
     const int n = (int)c.nodes.size();
+    TensorSlots ts((size_t)n + c.leafs.size() + 16);
     auto needs_alloc = [](tts_tensor * t) { return t && !t->data && !t->view_src; };
     for (int i = 0; i < n; ++i) {
         tts_tensor * t = c.nodes[i];
@@ -525,9 +549,12 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) 
             tts_tensor * x = t->src[s];
             if (!x) continue;
             tts_tensor * b = x->view_src ? x->view_src : x;
-            last_use[b] = i;
+            ts.last_use[ts.at(b)] = i;
         }
-        if (t->view_src) last_use[t->view_src] = std::max(last_use[t->view_src], i);
+        if (t->view_src) {
+            int & lu = ts.last_use[ts.at(t->view_src)];
+            lu = std::max(lu, i);
+        }
     }
     bool ok = true;
     // inputs (leafs without data) live for the whole graph
@@ -535,7 +562,7 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) 
         if (needs_alloc(l)) {
             size_t off;
             ok &= fl.alloc(nbytes(l), off);
-            offs[l] = off;
+            ts.off[ts.at(l)] = (int64_t)off;
             l->data = arena_base + off;
         }
     }
@@ -544,7 +571,7 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) 
         if (needs_alloc(t)) {
             size_t off;
             ok &= fl.alloc(nbytes(t), off);
-            offs[t] = off;
+            ts.off[ts.at(t)] = (int64_t)off;
             t->data = arena_base + off;
         } else if (t->view_src && !t->data) {
             if (!t->view_src->data) {
@@ -558,11 +585,11 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) 
             tts_tensor * x = t->src[s];
             if (!x) continue;
             tts_tensor * b = x->view_src ? x->view_src : x;
-            auto it = offs.find(b);
-            if (it == offs.end()) continue;
-            if (reuse && last_use[b] == i && !(b->flags & (TG_FLAG_OUTPUT | TG_FLAG_INPUT)) && b->op != TTS_OP_NONE) {
-                fl.release(it->second, nbytes(b));
-                offs.erase(it);
+            const size_t k = ts.at(b);
+            if (ts.off[k] < 0) continue;
+            if (reuse && ts.last_use[k] == i && !(b->flags & (TG_FLAG_OUTPUT | TG_FLAG_INPUT)) && b->op != TTS_OP_NONE) {
+                fl.release((size_t)ts.off[k], nbytes(b));
+                ts.off[k] = -1;
             }
         }
     }

@@ -127,12 +127,18 @@ struct Item {
     bool rms = false;
     // EMBED: GET_ROWS terms summed in order into dst
     std::vector<const tts_tensor *> terms;
-    // LSTM: bit 1 = run recurrence step `ls`, bit 2 = write the chain's output `lfinal` from `lhist`
+    // LSTM: bit 1 = run recurrence step `ls` (and `ls2` when lpair: two independent chains in one
+    // launch), bit 2 = write the chain output(s) `lfinal` (`lfinal2`) from `lhist` (`lhist2`), bit 4 =
+    // stash a paired chain's four input projections (lstash_src[g] -> lstash_dst[g], lstash_bytes)
     int lkind = 0;
-    LstmStepArgs ls{};
-    const tts_tensor * lfinal = nullptr;
-    const float * lhist = nullptr;
+    LstmStepArgs ls{}, ls2{};
+    bool lpair = false;
+    const tts_tensor *lfinal = nullptr, *lfinal2 = nullptr;
+    const float *lhist = nullptr, *lhist2 = nullptr;
     int64_t lHd = 0, lT = 0;
+    const void * lstash_src[4] = {};
+    void * lstash_dst[4] = {};
+    size_t lstash_bytes = 0;
     // CONV: implicit-GEMM conv_1d with its bias / residual ADDs
     Conv1dArgs conv{};
     // ADAIN: per-channel norm + affine (+ snake)
@@ -142,12 +148,100 @@ struct Item {
     int rint = 1;
 };
 
+// Open-addressing map keyed by tensor address, for the planner's per-tensor tables (a 20k-node
+// Kokoro graph spends more time in std::unordered_map's node allocations than in the planning).
+// The unordered_map subset the planner uses: operator[] (inserting a default), find() returning an
+// entry pointer with .first / .second or end() == nullptr, count().
+// A tensor's consumer list: almost always one or two nodes, kept inline.
+struct SmallIdx {
+    int inl[3];
+    std::vector<int> more;
+    int n = 0;
+    void push_back(int v) {
+        if (n < 3) inl[n] = v;
+        else more.push_back(v);
+        ++n;
+    }
+    size_t size() const { return (size_t)n; }
+    int operator[](size_t i) const { return i < 3 ? inl[i] : more[i - 3]; }
+    struct iter {
+        const SmallIdx * s;
+        size_t i;
+        int operator*() const { return (*s)[i]; }
+        iter & operator++() {
+            ++i;
+            return *this;
+        }
+        bool operator!=(const iter & o) const { return i != o.i; }
+        bool operator==(const iter & o) const { return i == o.i; }
+        using iterator_category = std::input_iterator_tag;
+        using value_type = int;
+        using difference_type = std::ptrdiff_t;
+        using pointer = const int *;
+        using reference = int;
+    };
+    iter begin() const { return {this, 0}; }
+    iter end() const { return {this, (size_t)n}; }
+};
+
+template <typename V>
+struct PtrMap {
+    struct Entry {
+        const tts_tensor * first;
+        V second;
+    };
+    std::vector<Entry> entries;
+    std::vector<int32_t> slots;  // -1 empty, else index into entries
+    size_t mask_ = 0;
+    void reserve(size_t n) {
+        size_t cap = 64;
+        while (cap < 2 * n) cap <<= 1;
+        slots.assign(cap, -1);
+        mask_ = cap - 1;
+        entries.clear();
+        entries.reserve(n);
+    }
+    size_t slot(const tts_tensor * k) const {
+        uint64_t h = (uint64_t)(uintptr_t)k * 0x9E3779B97F4A7C15ull;
+        size_t i = (size_t)(h >> 32) & mask_;
+        while (slots[i] >= 0 && entries[slots[i]].first != k) i = (i + 1) & mask_;
+        return i;
+    }
+    V & operator[](const tts_tensor * k) {
+        if (slots.empty()) reserve(64);
+        size_t i = slot(k);
+        if (slots[i] < 0) {
+            if (2 * (entries.size() + 1) > slots.size()) {  // grow: rehash every entry
+                std::vector<Entry> old;
+                old.swap(entries);
+                reserve(old.size() * 2 + 1);
+                for (auto & e : old) {
+                    const size_t j = slot(e.first);
+                    slots[j] = (int32_t)entries.size();
+                    entries.push_back(std::move(e));
+                }
+                i = slot(k);
+            }
+            slots[i] = (int32_t)entries.size();
+            entries.push_back(Entry{k, V{}});
+        }
+        return entries[slots[i]].second;
+    }
+    Entry * find(const tts_tensor * k) {
+        if (slots.empty()) return nullptr;
+        const size_t i = slot(k);
+        return slots[i] < 0 ? nullptr : &entries[slots[i]];
+    }
+    Entry * end() { return nullptr; }
+    size_t count(const tts_tensor * k) { return find(k) ? 1 : 0; }
+};
+
 struct Planner {
     tts_tensor * const * nodes;
     int n;
-    std::unordered_map<const tts_tensor *, int> uses;
-    std::unordered_map<const tts_tensor *, int> index;
-    std::unordered_map<const tts_tensor *, std::vector<int>> consumers;
+    PtrMap<int> uses;
+    PtrMap<int> index;
+    PtrMap<SmallIdx> consumers;
     std::vector<int> act;  // -1 skip, 0 run node, k>0 run items[k-1]
     std::vector<Item> items;
     std::deque<tts_tensor> derived;  // strided stand-ins for folded CONT nodes (stable addresses)
@@ -172,6 +266,9 @@ struct Planner {
         nodes = nodes_;
         n = n_;
         act.assign(n, 0);
+        index.reserve((size_t)n);
+        uses.reserve((size_t)n * 2);
+        consumers.reserve((size_t)n * 2);
         for (int i = 0; i < n; ++i) {
             index[nodes[i]] = i;
             for (int s = 0; s < TTS_MAX_SRC; ++s) {
@@ -548,7 +645,7 @@ struct Planner {
 
     void try_lstm() {
         std::vector<LStep> st;
-        std::unordered_map<const tts_tensor *, int> by_h;
+        PtrMap<int> by_h;
         for (int i = 0; i < n; ++i) {
             LStep s;
             if (nodes[i]->op == TTS_OP_MUL && lstm_step(nodes[i], s)) {
@@ -564,26 +661,125 @@ struct Planner {
             st[k].prev = it->second;
             p.next = (int)k;
         }
+        std::vector<ChainPlan> plans;
         for (size_t k0 = 0; k0 < st.size(); ++k0) {
             if (st[k0].prev != -1) continue;
             std::vector<int> seq;
             for (int k = (int)k0; k != -1; k = st[k].next) seq.push_back(k);
-            lstm_chain(st, seq);
+            ChainPlan cp;
+            if (lstm_chain(st, seq, cp)) plans.push_back(std::move(cp));
+        }
+        std::sort(plans.begin(), plans.end(), [](const ChainPlan & x, const ChainPlan & y) { return x.steps[0] < y.steps[0]; });
+        // build_lstm's bidirectional cell runs its forward chain, then its reverse chain: the two are
+        // independent, so one launch can advance both.  The earlier chain (A) is delayed to the
+        // later one's (B) step positions; its input projections are stashed first (their arena
+        // memory may be handed to B's projections once A's own steps have passed) and its output
+        // is written at B's end, which is safe when nothing reads it before then.
+        std::vector<int> partner(plans.size(), -1);
+        for (size_t a = 0; a + 1 < plans.size(); ++a) {
+            if (partner[a] != -1) continue;
+            ChainPlan & A = plans[a];
+            ChainPlan & B = plans[a + 1];
+            if (partner[a + 1] != -1 || A.Hd != B.Hd || A.T != B.T || A.K != B.K || A.wtype != B.wtype || A.fin_idx >= B.steps[0]) continue;
+            bool ok = A.stash_ok && lstm_used + 4 * (size_t)A.Hd * (size_t)A.T <= lstm_cap;
+            auto cs = consumers.find(A.fin);
+            if (cs != consumers.end())
+                for (int j : cs->second) ok = ok && j > B.fin_idx;
+            if (!ok) continue;
+            partner[a] = (int)a + 1;
+            partner[a + 1] = (int)a;
+        }
+        for (size_t k = 0; k < plans.size(); ++k) {
+            ChainPlan & P = plans[k];
+            for (int m : P.members) act[m] = -1;
+            if (partner[k] == -1) {
+                emit_chain(P, nullptr);
+            } else if (partner[k] > (int)k) {
+                ChainPlan & B = plans[partner[k]];
+                for (int m : B.members) act[m] = -1;
+                if (lstm_used + 4 * (size_t)P.Hd * (size_t)P.T + 64 <= lstm_cap) {
+                    emit_chain(B, &P);
+                } else {  // no room left for the stash: two plain chains
+                    emit_chain(P, nullptr);
+                    emit_chain(B, nullptr);
+                }
+                ++k;
+            }
         }
     }
 
-    void lstm_chain(const std::vector<LStep> & st, const std::vector<int> & seq) {
+    struct ChainPlan {
+        std::vector<int> steps;  // node index of each step's h, in chain order
+        std::vector<LstmStepArgs> args;
+        std::vector<int> members;
+        std::vector<int64_t> cols;
+        const tts_tensor * fin = nullptr;
+        int fin_idx = -1;
+        const tts_tensor * pre[4] = {};
+        bool stash_ok = false;
+        float *hist = nullptr, *cbuf = nullptr;
+        int64_t Hd = 0, T = 0, K = 0;
+        int wtype = 0;
+    };
+
+    // One chain's items; with `other`, its steps also advance `other` (stashed projections) and its
+    // output write also writes other's.
+    void emit_chain(ChainPlan & P, ChainPlan * other) {
+        float * stash = nullptr;
+        if (other) {
+            stash = lstm_buf + lstm_used;
+            lstm_used += (4 * (size_t)other->Hd * (size_t)other->T + 63) & ~(size_t)63;
+            Item it;
+            it.kind = Item::LSTM;
+            it.lkind = 4;
+            for (int g = 0; g < 4; ++g) {
+                it.lstash_src[g] = other->pre[g]->data;
+                it.lstash_dst[g] = stash + (size_t)g * other->Hd * other->T;
+            }
+            it.lstash_bytes = sizeof(float) * (size_t)other->Hd * (size_t)other->T;
+            act[other->steps[0]] = add_item(std::move(it));
+            for (size_t s = 0; s < other->args.size(); ++s)
+                for (int g = 0; g < 4; ++g) other->args[s].pre[g] = stash + (size_t)g * other->Hd * other->T + other->cols[s] * other->Hd;
+        }
+        for (int64_t s = 0; s < P.T; ++s) {
+            Item it;
+            it.kind = Item::LSTM;
+            it.lkind = 1;
+            it.ls = P.args[s];
+            if (other) {
+                it.ls2 = other->args[s];
+                it.lpair = true;
+            }
+            if (s == P.T - 1 && P.T == 1) {
+                it.lkind = 3;
+                it.lfinal = P.fin, it.lhist = P.hist, it.lHd = P.Hd, it.lT = P.T;
+                if (other) it.lfinal2 = other->fin, it.lhist2 = other->hist;
+            }
+            act[P.steps[s]] = add_item(std::move(it));
+        }
+        if (P.T > 1) {
+            Item it;
+            it.kind = Item::LSTM;
+            it.lkind = 2;
+            it.lfinal = P.fin, it.lhist = P.hist, it.lHd = P.Hd, it.lT = P.T;
+            if (other) it.lfinal2 = other->fin, it.lhist2 = other->hist;
+            act[P.fin_idx] = add_item(std::move(it));
+        }
+    }
+
+    bool lstm_chain(const std::vector<LStep> & st, const std::vector<int> & seq, ChainPlan & P) {
         const int64_t T = (int64_t)seq.size();
         const LStep & s0 = st[seq[0]];
         const int64_t Hd = s0.h->ne[0];
         int dir = 1;
         if (T > 1) dir = (int)(st[seq[1]].col - s0.col);
-        if (dir != 1 && dir != -1) return;
-        if (s0.col != (dir == 1 ? 0 : T - 1)) return;
+        if (dir != 1 && dir != -1) return false;
+        if (s0.col != (dir == 1 ? 0 : T - 1)) return false;
         for (int64_t s = 1; s < T; ++s)
-            if (st[seq[s]].col != s0.col + dir * s) return;
+            if (st[seq[s]].col != s0.col + dir * s) return false;
         // the concat chain that accumulates the outputs
-        std::unordered_map<const tts_tensor *, int> mem;  // chain members
+        PtrMap<int> mem;  // chain members
+        mem.reserve((size_t)T * 32);
         auto add = [&](const tts_tensor * t) { mem[t] = 1; };
         const tts_tensor * out = s0.h;
         for (int64_t s = 0; s < T; ++s) {
@@ -593,40 +789,53 @@ struct Planner {
             if (s == 0) continue;
             const tts_tensor * C = nullptr;
             auto cs = consumers.find(S.h);
-            if (cs == consumers.end()) return;
+            if (cs == consumers.end()) return false;
             for (int j : cs->second) {
                 const tts_tensor * x = nodes[j];
                 if (x->op != TTS_OP_CONCAT || x->op_params[0] != 1) continue;
                 if ((dir == 1 && x->src[0] == out && x->src[1] == S.h) || (dir == -1 && x->src[0] == S.h && x->src[1] == out)) C = x;
             }
-            if (!C) return;
+            if (!C) return false;
             add(C);
             out = C;
         }
         const tts_tensor * fin = out;
-        if (fin->type != TTS_TYPE_F32 || fin->ne[0] != Hd || fin->ne[1] != T || fin->ne[2] * fin->ne[3] != 1 || fin->nb[0] != 4) return;
+        if (fin->type != TTS_TYPE_F32 || fin->ne[0] != Hd || fin->ne[1] != T || fin->ne[2] * fin->ne[3] != 1 || fin->nb[0] != 4) return false;
         // nothing outside the chain may read an intermediate (the final output excepted)
-        for (const auto & kv : mem) {
+        for (const auto & kv : mem.entries) {
             if (kv.first == fin) continue;
             auto cs = consumers.find(kv.first);
             if (cs == consumers.end()) continue;
             for (int j : cs->second)
-                if (!mem.count(nodes[j])) return;
+                if (!mem.count(nodes[j])) return false;
         }
-        for (const auto & kv : mem)
-            if (act[index[kv.first]] != 0) return;
+        for (const auto & kv : mem.entries)
+            if (act[index[kv.first]] != 0) return false;
         const size_t need = (size_t)Hd * (size_t)(T + 1);
-        if (!lstm_buf || lstm_used + need > lstm_cap) return;
+        if (!lstm_buf || lstm_used + need > lstm_cap) return false;
         float * cbuf = lstm_buf + lstm_used;
         float * hist = cbuf + Hd;
         lstm_used += (need + 63) & ~(size_t)63;
-        for (const auto & kv : mem) act[index[kv.first]] = -1;
+        P.members.reserve(mem.entries.size());
+        for (const auto & kv : mem.entries) P.members.push_back(index[kv.first]);
+        P.fin = fin;
+        P.fin_idx = index[fin];
+        P.hist = hist, P.cbuf = cbuf;
+        P.Hd = Hd, P.T = T;
+        P.K = s0.g[0].mm->src[0]->ne[0];
+        P.wtype = s0.g[0].mm->src[0]->type;
+        // the stash copies each gate's whole [Hd, T] projection: dense f32, four distinct tensors
+        P.stash_ok = true;
+        for (int g = 0; g < 4; ++g) {
+            const tts_tensor * pre = s0.g[g].view->src[0];
+            P.pre[g] = pre;
+            P.stash_ok = P.stash_ok && pre->type == TTS_TYPE_F32 && pre->ne[0] == Hd && pre->ne[1] == T && pre->nb[1] == (size_t)Hd * 4 &&
+                         contiguous(pre);
+            for (int g2 = 0; g2 < g; ++g2) P.stash_ok = P.stash_ok && P.pre[g2] != pre;
+        }
         for (int64_t s = 0; s < T; ++s) {
             const LStep & S = st[seq[s]];
-            Item it;
-            it.kind = Item::LSTM;
-            it.lkind = 1;
-            LstmStepArgs & a = it.ls;
+            LstmStepArgs a;
             for (int g = 0; g < 4; ++g) {
                 a.pre[g] = (const float *)S.g[g].view->data;
                 a.w[g] = S.g[g].mm->src[0]->data;
@@ -640,19 +849,11 @@ struct Planner {
             a.Hd = (int)Hd;
             a.K = (int)S.g[0].mm->src[0]->ne[0];
             a.wtype = S.g[0].mm->src[0]->type;
-            if (s == T - 1 && T == 1) {
-                it.lkind = 3;
-                it.lfinal = fin, it.lhist = hist, it.lHd = Hd, it.lT = T;
-            }
-            act[index[S.h]] = add_item(std::move(it));
+            P.args.push_back(a);
+            P.steps.push_back(index[S.h]);
+            P.cols.push_back(S.col);
         }
-        if (T > 1) {
-            Item it;
-            it.kind = Item::LSTM;
-            it.lkind = 2;
-            it.lfinal = fin, it.lhist = hist, it.lHd = Hd, it.lT = T;
-            act[index[fin]] = add_item(std::move(it));
-        }
+        return true;
     }
 
     // snake_1d (src/util.cpp:98-101): ADD(x, MUL(SQR(SIN(MUL(x, alpha))), recip)) -> one pass.
@@ -1070,7 +1271,7 @@ struct Planner {
         if (!src || src->type != TTS_TYPE_F32 || C->type != TTS_TYPE_F32) return;
         auto it = consumers.find(src);
         if (it == consumers.end() || it->second.size() < 2 || it->second.size() > 4) return;
-        std::vector<int> idx = it->second;
+        std::vector<int> idx(it->second.begin(), it->second.end());
         std::sort(idx.begin(), idx.end());
         if (idx[0] != i) return;
         for (int j : idx) {
@@ -1447,13 +1648,20 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             launch_repeat_interleave1(be, it.dst, it.x, it.rint);
             return 0;
         case Item::LSTM:
+            if (it.lkind & 4)
+                for (int g = 0; g < 4; ++g)
+                    TTS_HIP_CHECK(hipMemcpyAsync(it.lstash_dst[g], it.lstash_src[g], it.lstash_bytes, hipMemcpyDeviceToDevice, be->stream));
             if (it.lkind & 1) {
-                launch_lstm_step(be, it.ls);
-                be->lstm_steps++;
+                launch_lstm_step(be, it.ls, it.lpair ? &it.ls2 : nullptr);
+                be->lstm_steps += it.lpair ? 2 : 1;
             }
             if (it.lkind & 2) {
                 launch_lstm_finish(be, it.lfinal, it.lhist, it.lHd, it.lT);
                 be->lstm_chains++;
+                if (it.lfinal2) {
+                    launch_lstm_finish(be, it.lfinal2, it.lhist2, it.lHd, it.lT);
+                    be->lstm_chains++;
+                }
             }
             return 0;
     }
@@ -1519,7 +1727,12 @@ static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_
 extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
-    if (!capture_worthy(be, nodes, n_nodes)) return graph_compute_launches(be, nodes, n_nodes);
+    // Recording pays off when the same graph comes back (a decode step): the first call of a
+    // shape launches eagerly, so one-shot graphs (a Kokoro prompt's duration / synthesis graphs,
+    // whose sizes follow the prompt) never pay for a capture and an instantiation.
+    const bool repeat = n_nodes == be->last_compute_nodes;
+    be->last_compute_nodes = n_nodes;
+    if (!repeat || !capture_worthy(be, nodes, n_nodes)) return graph_compute_launches(be, nodes, n_nodes);
     // the step's launches replay back to back on the device instead of at the host's launch rate
     const int st = capture_into(be, nodes, n_nodes, be->gexec);
     if (st != 0) return st;

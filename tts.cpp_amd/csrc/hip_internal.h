@@ -284,6 +284,7 @@ struct tts_hip_backend {
     size_t repack_tmp_size = 0;
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
+    int last_compute_nodes = -1;  // node count of the previous tts_hip_graph_compute (repeat detection)
     bool conv_f32acc = false;  // conv GEMM on f16 MFMA with f32 accumulation (faster, misses the PCM bar)
     int conv_acc_mode = 0;     // fused conv_1d: 0 = f64 MFMA, 2 = f16 MFMA per 32-term batch + f64 accumulation
     hipGraphExec_t gexec = nullptr;
@@ -305,6 +306,9 @@ namespace tts {
 // Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
+// F32 weights x many columns (k_gemm.hip): bit-identical to the sequential-f64 float dot
+bool gemm_f32_ok(const GemvJob & j);
+void launch_gemm_f32(tts_hip_backend * be, const GemvJob & j);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);
 void launch_profile_spin(tts_hip_backend * be, double us);
 void launch_im2col(tts_hip_backend * be, const tts_tensor * node);
@@ -322,7 +326,8 @@ struct LstmStepArgs {
     float * c;              // [Hd] out (may alias cprev: per-unit read-then-write)
     int Hd, K, wtype;
 };
-void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a);
+// b: a second, independent chain advanced by the same launch (bidirectional pairs), or null
+void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a, const LstmStepArgs * b = nullptr);
 void launch_repeat_interleave1(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * a, int r);
 void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,

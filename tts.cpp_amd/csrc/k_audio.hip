@@ -196,13 +196,23 @@ __global__ __launch_bounds__(ISTFT_TILE) void k_istft(TD dst, TD a, TD win, int 
 // ---- MAP_CUSTOM3 / uv_noise_compute (src/util.cpp:140-170) -------------------------------------
 // One thread per (sample r, harmonic h): the reference's CPU callback as a device elementwise pass
 // over the upsampled F0 it reads, so the sine source needs no mid-graph round trip to the host.
+// hashed = 1: the draws come from splitmix64(seed, i) (oracle/ggml_ref.c uv_draw) instead of cdata.
+__device__ __forceinline__ float uv_draw(uint64_t seed, uint64_t i) {
+    uint64_t z = seed * 0x9E3779B97F4A7C15ull + i + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
 __global__ __launch_bounds__(256) void k_uv_noise(float * __restrict__ uv, float * __restrict__ noise, const float * __restrict__ f0up,
-                                                  const float * __restrict__ cdata, int64_t L, int64_t n) {
+                                                  const float * __restrict__ cdata, int64_t L, int64_t n, int hashed, uint64_t seed) {
     const float thr = cdata[0], noise_std = cdata[1], sin_amp = cdata[2], amp_div = cdata[3];
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         const bool voiced = f0up[i % L] > thr;
         uv[i] = voiced ? sin_amp : 0.0f;
-        noise[i] = (voiced ? noise_std : amp_div) * cdata[4 + i];
+        const float r = hashed ? uv_draw(seed, (uint64_t)i) : cdata[4 + i];
+        noise[i] = (voiced ? noise_std : amp_div) * r;
     }
 }
 
@@ -226,7 +236,7 @@ bool audio_op_supported(const tts_tensor * n) {
             return n->op_params[0] == TTS_CUSTOM_UV_NOISE && b && c && b->type == TTS_TYPE_F32 && c->type == TTS_TYPE_F32 &&
                    n->ne[2] == 2 && n->ne[3] == 1 && b->ne[0] == n->ne[0] && b->nb[0] == 4 && n->nb[0] == 4 &&
                    n->nb[1] == 4 * (size_t)n->ne[0] && n->nb[2] == n->nb[1] * (size_t)n->ne[1] &&
-                   c->ne[0] * c->ne[1] * c->ne[2] * c->ne[3] >= 4 + n->ne[0] * n->ne[1];
+                   c->ne[0] * c->ne[1] * c->ne[2] * c->ne[3] >= 4 + (n->op_params[1] == 1 ? 0 : n->ne[0] * n->ne[1]);
         }
         case TTS_OP_ISTFT: {
             const int N = n->op_params[0], H = n->op_params[1];
@@ -278,7 +288,8 @@ int launch_audio_op(tts_hip_backend * be, const tts_tensor * n) {
             if (g > 8192) g = 8192;
             float * uv = (float *)n->data;
             hipLaunchKernelGGL(k_uv_noise, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, be->stream, uv, (float *)((char *)n->data + n->nb[2]),
-                               (const float *)n->src[1]->data, (const float *)n->src[2]->data, L, cnt);
+                               (const float *)n->src[1]->data, (const float *)n->src[2]->data, L, cnt, n->op_params[1] == 1 ? 1 : 0,
+                               (uint64_t)(uint32_t)n->op_params[2] | ((uint64_t)(uint32_t)n->op_params[3] << 32));
         } break;
         default: return TTS_STATUS_UNSUPPORTED;
     }

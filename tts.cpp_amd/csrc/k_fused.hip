@@ -60,12 +60,16 @@ void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_te
 // adds of the precomputed input projection column, sigmoid/tanh, the cell update and a concat
 // that re-copies the whole output so far.  Here one launch runs a step: wave w of workgroup b owns
 // hidden unit u = 4b + w and computes its four gate rows together (each lane keeps 4 partial f64
-// sums over its k-slice, as ggml_vec_dot_f32 / _f16 accumulate in double), reduces them, and lane
-// 0 applies the node chain in the reference's order with every intermediate rounded to f32:
+// sums over its k-slice, as ggml_vec_dot_f32 / _f16 accumulate in double), reduces them, and
+// applies the node chain in the reference's order with every intermediate rounded to f32:
 //   g = act(pre[u] + (float(W_g[u] . h) + b_g[u]))      act = sigmoid for I, F, O; tanh for G
 //   c = F*c_prev + I*G,  h = tanh(c) * O
+// Lanes 0-3 evaluate the four gate activations side by side (each an f64 transcendental), so the
+// serial tail is one activation plus tanh(c).  blockIdx.y selects one of two independent chains
+// (a bidirectional cell's forward and reverse runs advance in the same launch).
 // F16 weights take the activation rounded to fp16 first (ggml's vec_dot_type for F16).
-__global__ __launch_bounds__(256) void k_lstm_step(LstmStepArgs a) {
+__global__ __launch_bounds__(256) void k_lstm_step(LstmStepArgs a0, LstmStepArgs a1) {
+    const LstmStepArgs & a = blockIdx.y ? a1 : a0;
     const int lane = threadIdx.x & 63;
     const int u = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (u >= a.Hd) return;
@@ -99,22 +103,22 @@ __global__ __launch_bounds__(256) void k_lstm_step(LstmStepArgs a) {
         }
     }
 #pragma unroll
-    for (int g = 0; g < 4; ++g) acc[g] = wave_sum_f64(acc[g]);
+    for (int g = 0; g < 4; ++g) acc[g] = wave_sum_f64(acc[g]);  // wave-uniform
+    // lane g (< 4) evaluates gate g
+    const int g = lane & 3;
+    const double dg = g == 0 ? acc[0] : g == 1 ? acc[1] : g == 2 ? acc[2] : acc[3];
+    const float t1 = __fadd_rn((float)dg, a.bias[g][u]);
+    const float x = __fadd_rn(a.pre[g][u], t1);
+    const float gate = g == 2 ? cr_tanhf(x) : cr_divf(1.f, __fadd_rn(1.f, cr_expf(-x)));
+    const float gi = __shfl(gate, 0), gf = __shfl(gate, 1), gg = __shfl(gate, 2), go = __shfl(gate, 3);
     if (lane != 0) return;
-    float gv[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        const float t1 = __fadd_rn((float)acc[g], a.bias[g][u]);
-        const float x = __fadd_rn(a.pre[g][u], t1);
-        gv[g] = g == 2 ? cr_tanhf(x) : cr_divf(1.f, __fadd_rn(1.f, cr_expf(-x)));
-    }
-    const float c = __fadd_rn(__fmul_rn(gv[1], a.cprev[u]), __fmul_rn(gv[0], gv[2]));
+    const float c = __fadd_rn(__fmul_rn(gf, a.cprev[u]), __fmul_rn(gi, gg));
     a.c[u] = c;
-    a.h[u] = __fmul_rn(cr_tanhf(c), gv[3]);
+    a.h[u] = __fmul_rn(cr_tanhf(c), go);
 }
 
-void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a) {
-    hipLaunchKernelGGL(k_lstm_step, dim3((unsigned)((a.Hd + 3) / 4)), dim3(256), 0, be->stream, a);
+void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a, const LstmStepArgs * b) {
+    hipLaunchKernelGGL(k_lstm_step, dim3((unsigned)((a.Hd + 3) / 4), b ? 2u : 1u), dim3(256), 0, be->stream, a, b ? *b : a);
     TTS_HIP_CHECK(hipGetLastError());
 }
 

@@ -1,0 +1,160 @@
+// F32 x F32 GEMM with ggml's float dot semantics: y(row, col) = sum_k (double)(w[row][k] * x[col][k])
+// -- every product rounded to f32, the sum carried in f64 and taken in ascending k, rounded to f32
+// once (ggml_vec_dot_f32's generic path, oracle/ggml_ref.c).  Used where a float MUL_MAT has more
+// columns than the GEMV kernels batch (ALBERT's projections over a prompt, Kokoro's LSTM input
+// projections and 1x1 shortcut convs over a duration-expanded sequence, the mask expansions).
+//
+// Tiles of 64 weight rows x 64 columns per 256-thread workgroup; K in slabs of 16 staged through
+// LDS k-major, so a wave's 16 row-lanes read consecutive words.  Each thread owns a 4 x 4 block of
+// outputs (rows tm + 16 i, columns tn + 16 j) and walks its K range in ascending order.  Skinny
+// products (a 768 x 768 projection over 64 tokens is 12 tiles) split K over extra workgroups to fill
+// the chip; their f64 partials are summed in split order by a second pass, so every output is a
+// short chain of in-order f64 sums, equal to the oracle's sequential sum up to f64 rounding: the f32
+// results agree unless an f64 sum lies within f64 rounding of an f32 rounding boundary.  The loop is VALU-bound (f32 multiply, f32->f64 convert, f64 add per MAC);
+// the matrix cores cannot reproduce the per-product f32 rounding.
+#include "hip_internal.h"
+
+namespace tts {
+
+namespace {
+
+constexpr int GT = 64;   // tile rows / columns
+constexpr int GK = 16;   // K slab
+constexpr int GLD = GT + 4;
+
+__device__ __forceinline__ void gemm_store(const GemvJob & j, int mat, int64_t row, int64_t col, double acc) {
+    float v = (float)acc;
+    if (j.epi == EPI_GELU) {
+        if (v <= -10.0f) v = 0.0f;
+        else if (v < 10.0f) v = __half2float(__ushort_as_half(j.gelu[__half_as_ushort(__float2half_rn(v))]));
+    } else if (j.epi == EPI_ADD) {
+        v = __fadd_rn(v, j.res[col * j.rcs + row]);
+    }
+    j.Y[mat][col * j.ycs[mat] + row * j.yrs[mat]] = v;
+}
+
+// ks > 1: blockIdx.z = mat * ks + split, K range [split * kc, (split + 1) * kc), f64 partials to
+// part[((mat * ks + split) * M + col) * N + row]
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_gemm_f32_f64(GemvJob j, int ks, int64_t kc, double * __restrict__ part) {
+    __shared__ float As[GK][GLD];
+    __shared__ float Bs[GK][GLD];
+    const int tid = threadIdx.x;
+    const int mat = blockIdx.z / ks, split = blockIdx.z % ks;
+    const int64_t row0 = (int64_t)blockIdx.x * GT, col0 = (int64_t)blockIdx.y * GT;
+    const int64_t N = j.N, M = j.M;
+    const int64_t kbeg = (int64_t)split * kc, K = kbeg + kc < j.K ? kbeg + kc : j.K;
+    const float * W = (const float *)j.W[mat];
+    const int64_t wrs = j.w_row_bytes / 4;
+    const int tm = tid & 15, tn = tid >> 4;
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    // loader: thread -> (tile row / column lr, k quad kq)
+    const int lr = tid >> 2, kq = (tid & 3) * 4;
+    const int64_t wr = row0 + lr, xc = col0 + lr;
+    const float * wp = W + (wr < N ? wr : N - 1) * wrs;
+    const float * xp = j.x + (xc < M ? xc : M - 1) * j.xcs;
+    for (int64_t k0 = kbeg; k0 < K; k0 += GK) {
+        float wv[4], xv[4];
+        const int64_t k = k0 + kq;
+        if (VEC && k + 3 < K) {
+            const float4 w4 = *(const float4 *)(wp + k), x4 = *(const float4 *)(xp + k);
+            wv[0] = w4.x, wv[1] = w4.y, wv[2] = w4.z, wv[3] = w4.w;
+            xv[0] = x4.x, xv[1] = x4.y, xv[2] = x4.z, xv[3] = x4.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                wv[e] = k + e < K ? wp[k + e] : 0.0f;
+                xv[e] = k + e < K ? xp[k + e] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            As[kq + e][lr] = wv[e];
+            Bs[kq + e][lr] = xv[e];
+        }
+        __syncthreads();
+        const int kn = K - k0 < GK ? (int)(K - k0) : GK;
+        if (kn == GK) {
+#pragma unroll 4
+            for (int kk = 0; kk < GK; ++kk) {
+                float a[4], b[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = As[kk][tm + 16 * i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[i] = Bs[kk][tn + 16 * i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[i][c] += (double)__fmul_rn(a[i], b[c]);
+            }
+        } else {
+            for (int kk = 0; kk < kn; ++kk) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[i][c] += (double)__fmul_rn(As[kk][tm + 16 * i], Bs[kk][tn + 16 * c]);
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int64_t col = col0 + tn + 16 * c;
+        if (col >= M) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t row = row0 + tm + 16 * i;
+            if (row >= N) continue;
+            if (ks == 1) gemm_store(j, mat, row, col, acc[i][c]);
+            else part[((int64_t)blockIdx.z * M + col) * N + row] = acc[i][c];
+        }
+    }
+}
+
+// the splits' partials of each output summed in split order, then the f32 rounding and epilogue
+__global__ __launch_bounds__(256) void k_gemm_reduce(GemvJob j, int ks, const double * __restrict__ part) {
+    const int64_t per = j.M * j.N, n = per * j.nmat;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += (int64_t)gridDim.x * 256) {
+        const int mat = (int)(e / per);
+        const int64_t r = e % per, col = r / j.N, row = r % j.N;
+        double a = 0.0;
+        for (int s = 0; s < ks; ++s) a += part[((int64_t)(mat * ks + s) * j.M + col) * j.N + row];
+        gemm_store(j, mat, row, col, a);
+    }
+}
+
+}  // namespace
+
+bool gemm_f32_ok(const GemvJob & j) {
+    return j.wtype == TTS_TYPE_F32 && j.x && j.K > 0 && j.N > 0 && j.M > 0 && j.nmat >= 1 && (j.N + GT - 1) / GT <= INT32_MAX &&
+           (j.M + GT - 1) / GT <= 65535 && (j.w_row_bytes % 4) == 0 && (j.xcs >= j.K);
+}
+
+void launch_gemm_f32(tts_hip_backend * be, const GemvJob & j) {
+    bool vec = (j.K % 4) == 0 && (j.w_row_bytes % 16) == 0 && (j.xcs % 4) == 0 && ((uintptr_t)j.x % 16) == 0;
+    for (int i = 0; i < j.nmat; ++i) vec = vec && ((uintptr_t)j.W[i] % 16) == 0;
+    const int64_t tiles = ((j.N + GT - 1) / GT) * ((j.M + GT - 1) / GT) * j.nmat;
+    // split K until ~2 workgroups per CU, each split keeping >= 64 of K (whole slabs)
+    int ks = 1;
+    const int64_t want = 2 * 256;
+    while (ks < 64 && tiles * ks * 2 <= want && j.K / (ks * 2) >= 64) ks *= 2;
+    const int64_t kc = ks == 1 ? j.K : ((j.K + ks - 1) / ks + GK - 1) / GK * GK;
+    if (ks > 1 && (size_t)ks * j.M * j.N * j.nmat > be->conv_part_doubles) ks = 1;
+    const dim3 grid((unsigned)((j.N + GT - 1) / GT), (unsigned)((j.M + GT - 1) / GT), (unsigned)(j.nmat * ks));
+    const int64_t kcc = ks == 1 ? j.K : kc;
+    if (vec) hipLaunchKernelGGL(k_gemm_f32_f64<true>, grid, dim3(256), 0, be->stream, j, ks, kcc, be->conv_part);
+    else hipLaunchKernelGGL(k_gemm_f32_f64<false>, grid, dim3(256), 0, be->stream, j, ks, kcc, be->conv_part);
+    if (ks > 1) {
+        const int64_t n = j.M * j.N * j.nmat;
+        int64_t g = (n + 255) / 256;
+        if (g > 4096) g = 4096;
+        hipLaunchKernelGGL(k_gemm_reduce, dim3((unsigned)g), dim3(256), 0, be->stream, j, ks, (const double *)be->conv_part);
+    }
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace tts

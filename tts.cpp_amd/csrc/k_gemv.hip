@@ -1448,6 +1448,14 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
         TTS_HIP_CHECK(hipEventRecord(e0, be->stream));
     }
     const int64_t K = job.K;
+    if (job.wtype == TTS_TYPE_F32 && job.M > 8 && gemm_f32_ok(job)) {
+        launch_gemm_f32(be, job);  // one tiled pass instead of a GEMV launch per 8 columns
+        if (prof) {
+            TTS_HIP_CHECK(hipEventRecord(e1, be->stream));
+            profile_push(be, e0, e1, gemv_bytes(job), job.wtype);
+        }
+        return;
+    }
     if (q4k_mf_eligible(be, job)) {
         launch_q4k_mf(be, job);
         TTS_HIP_CHECK(hipGetLastError());

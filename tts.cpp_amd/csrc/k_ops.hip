@@ -644,6 +644,28 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
             // float path (quantized weights go through the GEMV kernels)
             if (launch_gemm_f16(be, node)) return 0;
             const int64_t nout = nel(node);
+            // plain float GEMM (2-D weights, columns collapsible, dense output) on the tiled kernel
+            if (s0->type == TTS_TYPE_F32 && s1->type == TTS_TYPE_F32 && node->type == TTS_TYPE_F32 && s0->ne[0] > 32 && s0->ne[1] >= 16 &&
+                s0->ne[2] * s0->ne[3] == 1 && s0->nb[0] == 4 && s1->nb[0] == 4 && is_cont(node) && (s0->nb[1] % 4) == 0 &&
+                (s1->nb[1] % 4) == 0 &&
+                (s1->ne[2] * s1->ne[3] == 1 || (s1->nb[2] == s1->nb[1] * (size_t)s1->ne[1] && s1->nb[3] == s1->nb[2] * (size_t)s1->ne[2]))) {
+                GemvJob j;
+                j.wtype = TTS_TYPE_F32;
+                j.K = s0->ne[0];
+                j.N = s0->ne[1];
+                j.M = s1->ne[1] * s1->ne[2] * s1->ne[3];
+                j.w_row_bytes = (int64_t)s0->nb[1];
+                j.W[0] = (const uint8_t *)s0->data;
+                j.x = (const float *)s1->data;
+                j.xcs = (int64_t)(s1->nb[1] / 4);
+                j.Y[0] = (float *)node->data;
+                j.ycs[0] = (int64_t)(node->nb[1] / 4);
+                j.yrs[0] = 1;
+                if (j.M > 8 && gemm_f32_ok(j)) {
+                    launch_gemm_f32(be, j);
+                    return 0;
+                }
+            }
             if (s0->ne[0] <= 32) {
                 hipLaunchKernelGGL(k_mul_mat_smallk, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
                 break;

@@ -65,6 +65,7 @@ struct tts_kokoro_gen {
     size_t arena_size = 0;
     tg::context gctx;
     tts_tensor *in_x = nullptr, *in_f0 = nullptr, *in_style = nullptr, *in_uvdata = nullptr, *in_wss = nullptr;
+    bool device_draws = false;
     std::vector<float> h_uvdata, h_wss, h_window;
 };
 
@@ -272,10 +273,14 @@ static tts_tensor * res_block(tts_kokoro_gen * k, tg::context & c, const kk_res 
 // build_sin_gen + build_generator (model.cpp:172-244) into `c`: x [C, T] features (channel
 // fastest), f0 [T] (or [T, 1]) Hz, style [style_dim].  Registers the uv_noise data and envelope
 // inputs on k (filled by kokoro_gen_set_inputs) and returns the PCM node [300 T].
-tts_tensor * tts::kokoro_gen_build(tts_kokoro_gen * k, tg::context & c, tts_tensor * x, tts_tensor * f0, tts_tensor * style, int64_t T) {
+// device_draws: the custom map draws its uniforms from a counter hash on the device (seeded from
+// cfg.seed) instead of reading [H][L] host draws -- no host RNG loop and no upload per call.
+tts_tensor * tts::kokoro_gen_build(tts_kokoro_gen * k, tg::context & c, tts_tensor * x, tts_tensor * f0, tts_tensor * style, int64_t T,
+                                   bool device_draws) {
     const auto & cf = k->cfg;
     const int64_t H = cf.harmonic_num + 1, L = T * kUpsample;
-    k->in_uvdata = tg::new_tensor_1d(c, TTS_TYPE_F32, 4 + L * H);
+    k->device_draws = device_draws;
+    k->in_uvdata = tg::new_tensor_1d(c, TTS_TYPE_F32, device_draws ? 4 : 4 + L * H);
     k->in_wss = tg::new_tensor_1d(c, TTS_TYPE_F32, L);
     tg::set_input(k->in_uvdata);
     tg::set_input(k->in_wss);
@@ -288,6 +293,12 @@ tts_tensor * tts::kokoro_gen_build(tts_kokoro_gen * k, tg::context & c, tts_tens
     tts_tensor * upscaled = tg::upscale_ext(c, f0, f0->ne[0] * kUpsample, f0->ne[1], f0->ne[2], f0->ne[3]);
     tts_tensor * fake = tg::new_tensor_3d(c, TTS_TYPE_F32, L, H, 2);
     tts_tensor * uv_noise = tg::map_custom3(c, fake, upscaled, k->in_uvdata, TTS_CUSTOM_UV_NOISE);
+    if (device_draws) {
+        const uint64_t seed = cf.seed ^ 0x5A5Aull;
+        uv_noise->op_params[1] = 1;
+        uv_noise->op_params[2] = (int32_t)(uint32_t)seed;
+        uv_noise->op_params[3] = (int32_t)(uint32_t)(seed >> 32);
+    }
     tg::set_name(uv_noise, "uv_noise");
     tts_tensor * noise = tg::cont(c, tg::view_2d(c, uv_noise, uv_noise->ne[0], uv_noise->ne[1], uv_noise->nb[1], uv_noise->nb[2]));
     tts_tensor * uv = tg::cont(c, tg::view_2d(c, uv_noise, uv_noise->ne[0], uv_noise->ne[1], uv_noise->nb[1], 0));
@@ -346,7 +357,7 @@ tts_tensor * tts::kokoro_gen_build(tts_kokoro_gen * k, tg::context & c, tts_tens
     return cur;
 }
 
-static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
+static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T, bool device_draws) {
     const auto & cf = k->cfg;
     tg::context & c = k->gctx;
     c.reset();
@@ -354,28 +365,24 @@ static tts_tensor * build_graph(tts_kokoro_gen * k, int64_t T) {
     k->in_f0 = tg::new_tensor_1d(c, TTS_TYPE_F32, T);
     k->in_style = tg::new_tensor_1d(c, TTS_TYPE_F32, cf.style_dim);
     for (tts_tensor * t : {k->in_x, k->in_f0, k->in_style}) tg::set_input(t);
-    tts_tensor * cur = kokoro_gen_build(k, c, k->in_x, k->in_f0, k->in_style, T);
+    tts_tensor * cur = kokoro_gen_build(k, c, k->in_x, k->in_f0, k->in_style, T, device_draws);
     tg::set_output(cur);
     tg::build_forward_expand(c, cur);
     return cur;
 }
 
 // kokoro_runner::set_inputs (model.cpp:1253-1256): the uv_noise custom map's data block -- its
-// four constants, then random_uniform_gen's [H][300 T] draws -- and compute_window_squared_sum
+// four constants, then random_uniform_gen's [H][300 T] draws (given by the caller, or drawn on the
+// device when the graph was built with device_draws) -- and compute_window_squared_sum
 // (util.cpp:203-217); uploads both to the inputs kokoro_gen_build registered.
 int tts::kokoro_gen_set_inputs(tts_kokoro_gen * k, int64_t T, const float * rand) {
     const auto & cf = k->cfg;
     const int64_t H = cf.harmonic_num + 1, L = T * kUpsample;
-    k->h_uvdata.resize((size_t)(4 + L * H));
+    if (k->device_draws == (rand != nullptr)) return TTS_STATUS_BAD_ARG;  // built for the other mode
+    k->h_uvdata.resize((size_t)(rand ? 4 + L * H : 4));
     float * d = k->h_uvdata.data();
     d[0] = cf.voice_threshold, d[1] = cf.noise_std, d[2] = cf.sin_amp, d[3] = cf.sin_amp / 3.0f;
-    if (rand) {
-        memcpy(d + 4, rand, sizeof(float) * (size_t)(L * H));
-    } else {
-        std::minstd_rand0 e((uint32_t)(cf.seed ^ 0x5A5A));
-        std::uniform_real_distribution<float> dis(0.0f, 1.0f);
-        for (int64_t i = 0; i < L * H; ++i) d[4 + i] = dis(e);
-    }
+    if (rand) memcpy(d + 4, rand, sizeof(float) * (size_t)(L * H));
     const int64_t n_frames = L / cf.hop, cutoff = n_frames * cf.hop, half = cf.n_fft / 2;
     k->h_wss.assign((size_t)L, 0.0f);
     for (int64_t i = 0; i < n_frames + half / cf.hop; ++i)
@@ -392,7 +399,7 @@ int tts::kokoro_gen_set_inputs(tts_kokoro_gen * k, int64_t T, const float * rand
 extern "C" int tts_kokoro_gen_run(tts_kokoro_gen * k, const float * x, const float * f0, const float * style, const float * rand,
                                   int32_t T, float * pcm) {
     if (!k || !x || !f0 || !style || T <= 0 || T > k->cfg.max_frames) return TTS_STATUS_BAD_ARG;
-    tts_tensor * out = build_graph(k, T);
+    tts_tensor * out = build_graph(k, T, rand == nullptr);
     if (!tg::alloc_graph(k->gctx, k->arena, k->arena_size, !k->cfg.debug_no_reuse)) {
         fprintf(stderr, "kokoro: compute arena too small (%zu needed)\n", k->gctx.arena_used);
         return TTS_STATUS_ALLOC_FAILED;

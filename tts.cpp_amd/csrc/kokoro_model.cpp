@@ -19,7 +19,9 @@
 // recurrence into one kernel per step (graph_exec.hip try_lstm).
 // Weights are deterministic synthetic tensors in Kokoro-82M shapes (no checkpoints offline),
 // named as the GGUF converter names them (py-gguf/tts_encoders/kokoro_gguf_encoder.py).
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -343,6 +345,25 @@ extern "C" void tts_kokoro_free(tts_kokoro * k) {
     delete k;
 }
 
+// TTS_KOKORO_TIMING=1: host phase times per call on stderr (build / alloc / inputs / compute / read)
+namespace {
+struct phase_clock {
+    bool on = getenv("TTS_KOKORO_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    char buf[256];
+    int len = 0;
+    void mark(const char * what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        len += snprintf(buf + len, sizeof(buf) - len, " %s %.3f", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+    void done(const char * which) {
+        if (on) fprintf(stderr, "kokoro %s ms:%s\n", which, buf);
+    }
+};
+}  // namespace
+
 // build_albert_norm (model.cpp:24-30): eps 1e-12
 static tts_tensor * albert_norm(tg::context & c, tts_tensor * cur, tts_tensor * w, tts_tensor * b) {
     cur = tg::norm(c, cur, 0.000000000001f);
@@ -504,7 +525,7 @@ static tts_tensor * build_duration_graph(tts_kokoro * k, int64_t n) {
 }
 
 // kokoro_runner::build_kokoro_graph (model.cpp:1141-1242); total = sum of the lengths
-static tts_tensor * build_main_graph(tts_kokoro * k, int64_t n, int64_t total) {
+static tts_tensor * build_main_graph(tts_kokoro * k, int64_t n, int64_t total, bool device_draws) {
     const auto & cf = k->cfg;
     tg::context & c = k->gctx;
     c.reset();
@@ -572,7 +593,7 @@ static tts_tensor * build_main_graph(tts_kokoro * k, int64_t n, int64_t total) {
     cur = tg::cont(c, tg::transpose(c, cur));
     tg::set_name(cur, "decoder_out");
 
-    cur = kokoro_gen_build(k->gen, c, cur, f0_curve, style_half2, f0_curve->ne[0]);
+    cur = kokoro_gen_build(k->gen, c, cur, f0_curve, style_half2, f0_curve->ne[0], device_draws);
     tg::set_output(cur);
     tg::build_forward_expand(c, cur);
     k->m_out = cur;
@@ -583,7 +604,9 @@ extern "C" int tts_kokoro_durations(tts_kokoro * k, const int32_t * tokens, int3
     if (!k || !tokens || n < 3 || n > k->cfg.max_tokens) return TTS_STATUS_BAD_ARG;
     for (int32_t i = 0; i < n; ++i)
         if (tokens[i] < 0 || tokens[i] >= k->cfg.n_vocab) return TTS_STATUS_BAD_ARG;
+    phase_clock pc;
     build_duration_graph(k, n);
+    pc.mark("build");
     if (!tg::alloc_graph(k->dctx, k->arena, k->arena_size, !k->cfg.debug_no_reuse)) {
         fprintf(stderr, "kokoro: compute arena too small (%zu needed)\n", k->dctx.arena_used);
         return TTS_STATUS_ALLOC_FAILED;
@@ -595,9 +618,13 @@ extern "C" int tts_kokoro_durations(tts_kokoro * k, const int32_t * tokens, int3
     int st = k->be.set(k->be.ctx, k->d_tokens->data, tokens, sizeof(int32_t) * (size_t)n);
     if (st == 0) st = k->be.set(k->be.ctx, k->d_pos->data, k->h_pos.data(), sizeof(int32_t) * (size_t)n);
     if (st == 0) st = k->be.set(k->be.ctx, k->d_mask->data, k->h_zero.data(), sizeof(float) * k->h_zero.size());
+    pc.mark("alloc+inputs");
     if (st == 0) st = k->be.compute(k->be.ctx, k->dctx.nodes.data(), (int)k->dctx.nodes.size());
+    pc.mark("compute");
     if (st == 0 && lengths) st = k->be.get(k->be.ctx, lengths, k->d_len->data, sizeof(float) * (size_t)n);
     if (st == 0 && hidden) st = k->be.get(k->be.ctx, hidden, k->d_hidden->data, tg::nbytes(k->d_hidden));
+    pc.mark("read");
+    pc.done("durations");
     return st;
 }
 
@@ -612,7 +639,9 @@ extern "C" int tts_kokoro_decode(tts_kokoro * k, const int32_t * tokens, int32_t
     }
     if (total < 1 || total > k->cfg.max_total) return TTS_STATUS_BAD_ARG;
     if (pcm && pcm_cap < (uint64_t)(600 * total) * sizeof(float)) return TTS_STATUS_BAD_ARG;
-    build_main_graph(k, n, total);
+    phase_clock pc;
+    build_main_graph(k, n, total, rand == nullptr);
+    pc.mark("build");
     if (!tg::alloc_graph(k->gctx, k->arena, k->arena_size, !k->cfg.debug_no_reuse)) {
         fprintf(stderr, "kokoro: compute arena too small (%zu needed)\n", k->gctx.arena_used);
         return TTS_STATUS_ALLOC_FAILED;
@@ -630,8 +659,12 @@ extern "C" int tts_kokoro_decode(tts_kokoro * k, const int32_t * tokens, int32_t
     if (st == 0) st = k->be.set(k->be.ctx, k->m_tokens->data, tokens, sizeof(int32_t) * (size_t)n);
     if (st == 0) st = k->be.set(k->be.ctx, k->m_dpred->data, hidden, tg::nbytes(k->m_dpred));
     if (st == 0) st = k->be.set(k->be.ctx, k->m_dmask->data, k->h_dmask.data(), sizeof(float) * k->h_dmask.size());
+    pc.mark("alloc+inputs");
     if (st == 0) st = k->be.compute(k->be.ctx, k->gctx.nodes.data(), (int)k->gctx.nodes.size());
+    pc.mark("compute");
     if (st == 0 && pcm) st = k->be.get(k->be.ctx, pcm, k->m_out->data, tg::nbytes(k->m_out));
+    pc.mark("read");
+    pc.done("decode");
     return st;
 }
 
