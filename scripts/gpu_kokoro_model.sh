@@ -4,7 +4,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_ops_gpu.py tests/test_kokoro_model_gpu.py tests/test_kokoro_gpu.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/t_kokoro.log 2>&1 || { tail -40 gpurun_out/t_kokoro.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_ops_gpu.py tests/test_lstm_gpu.py tests/test_fusion_gpu.py tests/test_kokoro_model_gpu.py tests/test_kokoro_gpu.py -m gpu -x -v -s --timeout 300 --timeout-method thread > gpurun_out/t_kokoro.log 2>&1 || { tail -40 gpurun_out/t_kokoro.log; exit 1; }
 grep -E "kokoro |passed|failed|FAIL" gpurun_out/t_kokoro.log
 timeout -k 10 200 python -u scripts/bench_kokoro_model.py 16 64 > gpurun_out/b_kokoro_model.log 2>&1 || { tail -30 gpurun_out/b_kokoro_model.log; exit 1; }
 cat gpurun_out/b_kokoro_model.log
