@@ -59,6 +59,8 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     TTS_HIP_CHECK(hipMalloc((void **)&be->attn_buf, kAttnFloats * sizeof(float)));
     be->attn_floats = kAttnFloats;
     TTS_HIP_CHECK(hipMalloc((void **)&be->vec_scratch, kVecScratchFloats * sizeof(float)));
+    be->conv_stage_floats = (size_t)8 << 20;  // 32 MiB: a [T, C] conv output of the largest vocoder level
+    TTS_HIP_CHECK(hipMalloc((void **)&be->conv_stage, be->conv_stage_floats * sizeof(float)));
     be->conv_part_doubles = (size_t)8 << 20;  // 64 MiB of f64 partial sums
     TTS_HIP_CHECK(hipMalloc((void **)&be->conv_part, be->conv_part_doubles * sizeof(double)));
     be->lstm_floats = kLstmFloats;
@@ -96,6 +98,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->lstm_buf);
     hipFree(be->attn_buf);
     hipFree(be->vec_scratch);
+    hipFree(be->conv_stage);
     hipFree(be->conv_part);
     hipFree(be->gelu_table);
     if (be->repack_tmp) hipFree(be->repack_tmp);

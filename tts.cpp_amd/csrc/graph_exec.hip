@@ -248,6 +248,8 @@ struct Planner {
     int mask = 0xFF;
     float * lstm_buf = nullptr;  // backend scratch for fused LSTM chains (hidden history + cell)
     size_t vec_cap = 0;          // floats of the backend's vector scratch (fused AdaIN staging)
+    float * conv_stage = nullptr;  // backend scratch for fused conv outputs that cannot stage in their im2col buffer
+    size_t conv_stage_cap = 0;
     size_t lstm_cap = 0, lstm_used = 0;
 
     const tts_tensor * sole_consumer(const tts_tensor * t) {
@@ -1103,17 +1105,22 @@ struct Planner {
             if (overlap(out, kern) || (bias && overlap(out, bias))) return plan_reject("conv", 10);
             stage = nullptr;
             bool ok = true;
+            bool in_col = false;
             if (overlap(out, x)) {
                 const size_t need = (size_t)OL * (size_t)OC * 4;
-                if (tbytes(col) < need || overlap(col, x) || overlap(col, out) || (res && overlap(col, res)) || overlap(col, kern) ||
-                    (bias && overlap(col, bias)))
-                    ok = false;
-                else
+                if (tbytes(col) >= need && !overlap(col, x) && !overlap(col, out) && !(res && overlap(col, res)) && !overlap(col, kern) &&
+                    !(bias && overlap(col, bias))) {
                     stage = (float *)col->data;
+                    in_col = true;
+                } else if (conv_stage && need <= 4 * conv_stage_cap) {
+                    stage = conv_stage;  // the backend's own staging buffer (never arena memory)
+                } else {
+                    ok = false;
+                }
             }
             for (int j = i + 1; ok && j < absorbed.back(); ++j) {
                 if (std::find(absorbed.begin(), absorbed.end(), j) != absorbed.end() || is_view(nodes[j]->op)) continue;
-                if (overlap(nodes[j], x) || (stage && overlap(nodes[j], col))) ok = false;
+                if (overlap(nodes[j], x) || (in_col && overlap(nodes[j], col))) ok = false;
             }
             if (ok) break;
             if (!res) return plan_reject("conv", 11);
@@ -1786,6 +1793,9 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     static float lstm_stand_in alignas(256);
     pl.lstm_buf = &lstm_stand_in;
     pl.lstm_cap = (size_t)4 << 20;
+    static float conv_stand_in alignas(256);
+    pl.conv_stage = &conv_stand_in;
+    pl.conv_stage_cap = (size_t)8 << 20;
     if (mask) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
     for (int k = 0; k < 16; ++k) counts[k] = 0;
@@ -1808,6 +1818,8 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     pl.lstm_buf = be->lstm_buf;
     pl.lstm_cap = be->lstm_floats;
     pl.vec_cap = be->vec_scratch ? (1u << 18) : 0;
+    pl.conv_stage = be->conv_stage;
+    pl.conv_stage_cap = be->conv_stage_floats;
     if (be->fusion) pl.build(nodes, n_nodes);
     be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
     // long-context attention items in launch order: each one's K/V is prefetched into MALL on the

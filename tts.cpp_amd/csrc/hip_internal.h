@@ -260,6 +260,8 @@ struct tts_hip_backend {
     hipEvent_t plan_ev[2] = {nullptr, nullptr};
     bool plan_ev_pending[2] = {false, false};
     float * lstm_buf = nullptr;  // fused LSTM chains: per chain [Hd] cell state + [Hd, T] hidden history
+    float * conv_stage = nullptr;  // fused conv output staging when it would alias its input and the im2col buffer is too small
+    size_t conv_stage_floats = 0;
     float * vec_scratch = nullptr;  // 256K floats: per-channel vectors a fused item copies away from its output
     size_t lstm_floats = 0;
     tts::ActQuant aq;
