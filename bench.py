@@ -35,7 +35,8 @@ SAMPLES_PER_STEP = 512          # DAC hop: one Parler step = 512 samples
 SAMPLE_RATE = 44100.0
 HEADS = 9
 HBM_PEAK_GBS = 8000.0           # MI355X spec (MI355X_MICROARCH.md chip table)
-PMC_FILE = ROOT / "profiles" / "r01" / "pmc_gemv_q4k.json"  # offline rocprofv3 --pmc result
+# offline rocprofv3 --pmc result (scripts/gpu_pmc.sh): the newest round's
+PMC_FILE = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k.json"), default=ROOT / "profiles" / "r01" / "pmc_gemv_q4k.json")
 
 HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), token ids derived from bytes
     "The birch canoe slid on the smooth planks.",

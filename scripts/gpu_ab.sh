@@ -8,7 +8,7 @@ f=${1:-scripts/ab_args.txt}
 while read -r a; do
   [ -z "$a" ] && continue
   echo "== $a" >> gpurun_out/ab.log
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --kokoro-calls 0 $a >> gpurun_out/ab.log 2>&1 || { echo "FAILED: $a"; exit 1; }
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --kokoro-prompts 0 $a >> gpurun_out/ab.log 2>&1 || { echo "FAILED: $a"; exit 1; }
 done < "$f"
 python3 - <<'PY'
 import json

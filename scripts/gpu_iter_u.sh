@@ -12,6 +12,6 @@ for l in open('gpurun_out/phase_u$u.jsonl'):
     d=json.loads(l); print('u=$u', d['shape'], 'span', d['span_us'], 'issue', d['issue_us'], 'pro', d['prologue_us'], 'bar', d['barrier_us'], 'rows', d['rows_us'])"
 done
 for u in 0 1; do
-  timeout -k 10 200 python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-dac --kokoro-calls 0 --orpheus-steps 0 --dia-steps 0 --gemv-unique $u > gpurun_out/b_u$u.log 2>&1 || exit 1
+  timeout -k 10 200 python3 bench.py --steps 40 --warmup 3 --no-cpu-baseline --no-dac --kokoro-prompts 0 --orpheus-steps 0 --dia-steps 0 --gemv-unique $u > gpurun_out/b_u$u.log 2>&1 || exit 1
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/b_u$u.log').read().strip().splitlines()[-1]); print('u=$u', d['ar_ms_per_step'], d['roofline']['avg_launch_us'], d['roofline']['achieved'])"
 done

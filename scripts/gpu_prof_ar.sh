@@ -5,7 +5,7 @@ R=$GRAFT_REPO_ROOT
 B=${1:-8}; CTX=${2:-448}; shift 2 2>/dev/null
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/arprof -o ar --output-format csv -- python3 $R/bench.py --steps 40 --warmup 2 --no-cpu-baseline --no-dac --kokoro-calls 0 --batch $B --replicas 1 --ctx $CTX "$@" > $R/gpurun_out/ar_prof.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/arprof -o ar --output-format csv -- python3 $R/bench.py --steps 40 --warmup 2 --no-cpu-baseline --no-dac --kokoro-prompts 0 --batch $B --replicas 1 --ctx $CTX "$@" > $R/gpurun_out/ar_prof.log 2>&1
 rc=$?
 cd $R
 tail -1 gpurun_out/ar_prof.log | cut -c1-600

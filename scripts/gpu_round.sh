@@ -12,7 +12,8 @@ tail -1 gpurun_out/pytest_gpu.log; tail -1 gpurun_out/smoke.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 2 --no-cpu-baseline --orpheus-steps 16 --dia-steps 16 > $R/gpurun_out/prof.log 2>&1 || exit 1
 cd $R
-bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1
+bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1 &&
+bash scripts/gpu_pmc_orpheus.sh > gpurun_out/pmc_orpheus.log 2>&1
 rc=$?
 tail -1 gpurun_out/bench_full.log | cut -c1-400
 exit $rc
