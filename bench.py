@@ -272,39 +272,49 @@ def kokoro_prompt(g, vocab):
     return np.asarray([0] + ids + [0], dtype=np.int32)
 
 
-def kokoro_leg(be, args, rank, dist, local, world):
+def kokoro_leg(backends, args, rank, dist, local, world):
     """BASELINE configs[1]: Kokoro-82M end to end (kokoro_runner::run: duration graph, host mask
     step, main graph with the iSTFTNet generator) over `kokoro_prompts` Harvard-sentence prompts per
-    GPU, one after another as the reference's runner serves them; synthetic weights."""
+    GPU, synthetic weights.  Each replica backend (its own HIP stream) owns a runner and serves every
+    R-th prompt from a host thread, as the server's workers each own a runner
+    (examples/server/server.cpp:316-321): one prompt's host-side graph building overlaps another's
+    device work."""
     kcfg = ttship.kokoro_config(max_tokens=64, max_total=600)
-    kok = ttship.Kokoro(be.iface(), kcfg)
+    R = len(backends)
+    koks = [ttship.Kokoro(b.iface(), kcfg) for b in backends]
     try:
         prompts = [kokoro_prompt(rank * args.kokoro_prompts + i, kcfg.n_vocab) for i in range(args.kokoro_prompts)]
-        kok.run(prompts[0])  # warm (code objects, arena)
-        barrier_sync(dist, be)
+        for k in koks:
+            k.run(prompts[0])  # warm (code objects, arena)
+        samples = [0] * R
+
+        def serve(r):
+            for p in prompts[r::R]:
+                samples[r] += koks[r].run(p).shape[0]
+            backends[r].sync()
+
+        barrier_sync(dist, backends[0])
         t0 = time.perf_counter()
-        samples = 0
-        for p in prompts:
-            samples += kok.run(p).shape[0]
-        be.sync()
+        run_replicas(serve, R)
         dt = max_over_ranks(dist, local, time.perf_counter() - t0)
-        # per-stage split on the first prompt (durations graph vs main graph incl. generator)
+        # per-stage split on the first prompt, one runner alone (durations graph vs main graph incl. generator)
         t1 = time.perf_counter()
-        hidden, lens = kok.durations(prompts[0])
+        hidden, lens = koks[0].durations(prompts[0])
         t2 = time.perf_counter()
-        kok.decode(prompts[0], hidden, lens)
+        koks[0].decode(prompts[0], hidden, lens)
         t3 = time.perf_counter()
-        audio = samples / kcfg.gen.sample_rate
+        audio = sum(samples) / kcfg.gen.sample_rate
         return {"workload": f"Kokoro-82M end to end (BASELINE configs[1]): tokens -> durations -> decoder -> iSTFTNet PCM, "
-                            f"{args.kokoro_prompts} prompts per GPU, synthetic weights",
+                            f"{args.kokoro_prompts} prompts per GPU served by {R} replica runners, synthetic weights",
                 "audio_sec_per_s": round(world * audio / dt, 3), "ms_per_prompt": round(1000.0 * dt / len(prompts), 3),
-                "audio_sec_per_gpu": round(audio, 3), "tokens_per_prompt": [int(p.shape[0]) for p in prompts],
+                "audio_sec_per_gpu": round(audio, 3), "tokens_per_prompt": [int(p.shape[0]) for p in prompts], "replicas": R,
                 "first_prompt_ms": {"durations": round(1000 * (t2 - t1), 3), "decode": round(1000 * (t3 - t2), 3),
                                     "frames": int(lens.sum())},
-                "graph_nodes": [kok.last_graph_nodes(0), kok.last_graph_nodes(1)],
+                "graph_nodes": [koks[0].last_graph_nodes(0), koks[0].last_graph_nodes(1)],
                 "dtype": "f32 activations and weights, f16 conv operands (ggml im2col), f64 conv accumulate"}
     finally:
-        kok.close()
+        for k in koks:
+            k.close()
 
 
 def main():
@@ -327,6 +337,9 @@ def main():
     ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
+    ap.add_argument("--dac-workers", type=int, default=8, help="concurrent DAC decoders per GPU (each its own backend / "
+                    "stream; the AR replicas' backends first): short codec sequences fill few CUs, so several "
+                    "prompts decode side by side")
     ap.add_argument("--kokoro-prompts", type=int, default=8, help="Kokoro-82M prompts per GPU, end to end (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
@@ -340,10 +353,7 @@ def main():
     bl = args.batch // R  # prompts per replica
     cfg = ttship.parler_config(batch=bl, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
                                arena_bytes=4 << 30)
-    reps = []
-    for r in range(R):
-        # a replica = one backend (its own HIP stream) + its own runners, as a server worker owns its
-        # runners (examples/server/server.cpp:316-321); replicas run concurrently from host threads
+    def new_backend():
         rb = ttship.HipBackend(local)
         if args.no_fusion:
             rb.set_option(0, 0)
@@ -358,14 +368,30 @@ def main():
             rb.set_option(ttship.OPT["GEMV_UNIQUE"], args.gemv_unique)
         if args.kv_prefetch_blocks is not None:
             rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
+        return rb
+
+    dcfg = ttship.dac_config(max_frames=args.steps)
+
+    def new_dac(rb):
+        rd = ttship.Dac(rb.iface(), dcfg)
+        rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+        return rd
+
+    reps = []
+    for r in range(R):
+        # a replica = one backend (its own HIP stream) + its own runners, as a server worker owns its
+        # runners (examples/server/server.cpp:316-321); replicas run concurrently from host threads
+        rb = new_backend()
         rr = ttship.Parler(rb.iface(), cfg)
-        rd = None
-        if not args.no_dac:
-            dcfg = ttship.dac_config(max_frames=args.steps)
-            rd = ttship.Dac(rb.iface(), dcfg)
-            rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+        rd = None if args.no_dac else new_dac(rb)
         reps.append((rb, rr, rd))
     be, runner, dac = reps[0]
+    # DAC workers: the replicas' decoders plus extra backends of their own
+    W = 0 if args.no_dac else max(1, min(args.dac_workers, args.batch))
+    dac_workers = [(rb, rd) for rb, _, rd in reps[:W]]
+    while len(dac_workers) < W:
+        xb = new_backend()
+        dac_workers.append((xb, new_dac(xb)))
     # text-prompt pass to reach the measured KV length
     for r, (rb, rr, rd) in enumerate(reps):
         rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * args.batch + r * bl))
@@ -382,11 +408,12 @@ def main():
         toks_r[r] = rr.generate(args.steps)
         rb.sync()
 
-    def dac_leg(r):
-        rb, _, rd = reps[r]
-        for b in range(bl):
-            rd.decode(dac_codes(toks_r[r][b], dcfg.codebook_size))
-        rb.sync()
+    def dac_leg(w):
+        # worker w decodes every W-th prompt of the whole per-GPU batch
+        xb, rd = dac_workers[w]
+        for g in range(w, args.batch, W):
+            rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
+        xb.sync()
 
     t0 = time.perf_counter()
     run_replicas(ar_leg, R)
@@ -394,7 +421,7 @@ def main():
     c1 = be.counters()
     cdelta = {k: (c1.get(k, 0) - c0.get(k, 0)) / 1e3 / max(1, args.steps) for k in ("plan_wait_ns", "cap_plan_ns", "cap_launch_ns", "cap_update_ns")}
     if dac is not None:
-        run_replicas(dac_leg, R)
+        run_replicas(dac_leg, W)
     barrier_sync(dist, be)
     t2 = time.perf_counter()
     toks = np.concatenate(toks_r, axis=0)
@@ -405,7 +432,7 @@ def main():
     kres = None
     if args.kokoro_prompts > 0:
         barrier_sync(dist, be)
-        kres = kokoro_leg(be, args, rank, dist, local, world)
+        kres = kokoro_leg([rb for rb, _, _ in reps], args, rank, dist, local, world)
     ores = None
     if args.orpheus_steps > 0:
         barrier_sync(dist, be)
@@ -453,7 +480,8 @@ def main():
             "config": {"workload": f"Parler-TTS-mini-v1 Q4_K, greedy AR decode + DAC-44k (BASELINE configs[2])",
                        "model": "parler-tts-mini-v1", "prompts_per_gpu": args.batch, "global_batch": total_prompts,
                        "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
-                       "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} prompts per GPU", "graph_nodes_per_step": runner.last_graph_nodes(),
+                       "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} prompts per GPU, {W} concurrent DAC decoders",
+                       "graph_nodes_per_step": runner.last_graph_nodes(),
                        "dac_graph_nodes": dac.last_graph_nodes() if dac is not None else None},
             "ar_audio_sec_per_s": round(audio_s / dt_ar, 3),
             "ar_ms_per_step": round(1000.0 * dt_ar / args.steps, 4),
@@ -467,6 +495,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
+    for xb, rd in dac_workers[R:]:
+        rd.close()
+        xb.close()
     for rb, rr, rd in reps:
         if rd is not None:
             rd.close()

@@ -107,6 +107,7 @@ enum tts_op {
     TTS_OP_ISTFT,  /* fork op */
     TTS_OP_MAP_CUSTOM3, /* ggml_map_custom3 with a CPU callback in the reference; op_params[0] names
                            which one (tts_custom_op) and the backend runs its device restatement */
+    TTS_OP_MAP_CUSTOM2, /* ggml_map_custom2, likewise */
     TTS_OP_COUNT
 };
 
@@ -115,7 +116,11 @@ enum tts_custom_op {
     TTS_CUSTOM_NONE = 0,
     /* uv_noise_compute (src/util.cpp:140-170): a = shape [L, H, 2], b = upscaled F0 [L],
      * c = [threshold, noise_std, sin_amp, sin_amp/3, rand[H][L]] (f32) -> plane 0 uv, plane 1 noise */
-    TTS_CUSTOM_UV_NOISE = 1
+    TTS_CUSTOM_UV_NOISE = 1,
+    /* cfg_scale (src/util.cpp:175-200, MAP_CUSTOM2 in build_dia_head_outputs, src/models/dia/model.cpp:370):
+     * a = cond, b = uncond (same shape) -> cond + scale * (cond - uncond); op_params[1] = scale (f32 bits).
+     * The callback's "-INFINITY past max_output" store is overwritten by the next line, so it has no effect. */
+    TTS_CUSTOM_CFG_SCALE = 2
 };
 
 enum tts_unary_op {

@@ -1047,6 +1047,28 @@ static int op_map_custom3(tts_tensor * dst, int ith, int nth) {
     return 0;
 }
 
+/* MAP_CUSTOM2 / cfg_scale (src/util.cpp:175-200): per element out = c + scale * (c - u), each
+ * operation rounded to f32; threads split the rows' element range as the reference's ith/nth do. */
+static int op_map_custom2(tts_tensor * dst, int ith, int nth) {
+    if (dst->op_params[0] != TTS_CUSTOM_CFG_SCALE) return TTS_STATUS_UNSUPPORTED;
+    const tts_tensor * a = dst->src[0];
+    const tts_tensor * b = dst->src[1];
+    float scale;
+    memcpy(&scale, &dst->op_params[1], sizeof(float));
+    const int64_t ne0 = b->ne[0];
+    const int64_t rpt = (ne0 + nth - 1) / nth;
+    const int64_t r0 = ith * rpt, r1 = (ith + 1) * rpt < ne0 ? (ith + 1) * rpt : ne0;
+    for (int64_t bt = 0; bt < b->ne[2]; ++bt)
+        for (int64_t h = 0; h < b->ne[1]; ++h)
+            for (int64_t r = r0; r < r1; ++r) {
+                const float cr = load_elem(a, r, h, bt, 0), ur = load_elem(b, r, h, bt, 0);
+                const float d = cr - ur;
+                const float sd = scale * d;
+                store_elem(dst, r, h, bt, 0, cr + sd);
+            }
+    return 0;
+}
+
 static int is_view_op(int op) {
     return op == TTS_OP_NONE || op == TTS_OP_VIEW || op == TTS_OP_RESHAPE || op == TTS_OP_PERMUTE || op == TTS_OP_TRANSPOSE;
 }
@@ -1076,6 +1098,7 @@ static int compute_node_mt(tts_tensor * node, int ith, int nth) {
         case TTS_OP_STFT: op_stft(node, ith, nth); return 0;
         case TTS_OP_ISTFT: op_istft(node, ith, nth); return 0;
         case TTS_OP_MAP_CUSTOM3: return op_map_custom3(node, ith, nth);
+        case TTS_OP_MAP_CUSTOM2: return op_map_custom2(node, ith, nth);
         default: return TTS_STATUS_UNSUPPORTED;
     }
 }

@@ -133,6 +133,30 @@ def test_mul_mat_f32_gemm(hip, K, N, M, epi):
 
 
 @pytest.mark.gpu
+def test_custom_maps(hip):
+    """The reference's CPU callbacks restated on the device: cfg_scale (MAP_CUSTOM2, Dia) and
+    uv_noise_compute (MAP_CUSTOM3, Kokoro, host draws and device-hashed draws)."""
+    c, u = rnd(21, 3, 2, 1028), rnd(22, 3, 2, 1028)
+    L, H = 900, 9
+    f0 = np.abs(rnd(23, L)) * 20.0  # some below the voicing threshold 10
+    data = np.concatenate([np.array([10.0, 0.003, 0.1, np.float32(0.1) / np.float32(3)], np.float32),
+                           np.random.default_rng(24).random(L * H, dtype=np.float32)])
+
+    def build(g):
+        cfg = g.node("MAP_CUSTOM2", F32, [1028, 2, 3], [g.leaf(c), g.leaf(u)], params=[2], fparams={1: 3.0})
+        uvn = g.node("MAP_CUSTOM3", F32, [L, H, 2], [g.leaf(np.zeros((2, H, L), np.float32)), g.leaf(f0), g.leaf(data)], params=[1])
+        uvh = g.node("MAP_CUSTOM3", F32, [L, H, 2], [g.leaf(np.zeros((2, H, L), np.float32)), g.leaf(f0), g.leaf(data[:4].copy())],
+                     params=[1, 1, 0x1234, 0])
+        return [cfg, uvn, uvh]
+    pairs = run_both(hip, build)
+    assert_bits(pairs, "custom maps")
+    voiced = f0 > 10.0
+    uv = pairs[1][1].reshape(2, H, L)
+    assert np.all(uv[0][:, voiced] == np.float32(0.1)) and np.all(uv[0][:, ~voiced] == 0)
+    assert 0.0 < float(pairs[2][1].reshape(2, H, L)[1].std()) < 0.1  # hashed draws present
+
+
+@pytest.mark.gpu
 def test_get_rows_and_concat_and_cpy(hip):
     tab = rnd(9, 40, 96)
     idx = np.array([3, 0, 39, 7, 7], dtype=np.int32)

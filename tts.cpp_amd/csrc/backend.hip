@@ -350,7 +350,7 @@ int tts_hip_supports_op(const tts_tensor * n) {
             return is_f32(n->src[1]) && n->op_params[6] == 0 && (n->type == TTS_TYPE_F16 || n->type == TTS_TYPE_F32);
         case TTS_OP_CONV_TRANSPOSE_1D:
             return is_f32(n->src[0]) && is_f32(n->src[1]) && n->op_params[4] >= 1;
-        case TTS_OP_CUMSUM: case TTS_OP_UPSCALE: case TTS_OP_STFT: case TTS_OP_ISTFT: case TTS_OP_MAP_CUSTOM3:
+        case TTS_OP_CUMSUM: case TTS_OP_UPSCALE: case TTS_OP_STFT: case TTS_OP_ISTFT: case TTS_OP_MAP_CUSTOM3: case TTS_OP_MAP_CUSTOM2:
             return tts::audio_op_supported(n);
         case TTS_OP_GET_ROWS:
             return n->src[1]->type == TTS_TYPE_I32 &&

@@ -4,8 +4,8 @@
 // K/V store (build_dia_cross_kv_store, :476-514), and the decoder step (build_dia_decoder, :516-637)
 // with the GQA repeat-interleave KV store (build_dia_self_kv_store, :443-474).  Classifier-free
 // guidance runs the conditioned and unconditioned sequences as the graph's batch of 2; the heads'
-// cfg_scale (util.cpp:175-200, a CPU map_custom2 in the reference) is written as the same
-// arithmetic in graph ops: cond + 3 * (cond - uncond), each op rounded to f32.
+// cfg_scale (util.cpp:175-200, a CPU map_custom2 in the reference) is the same MAP_CUSTOM2 node here,
+// run by the backend on the device: cond + 3 * (cond - uncond), each op rounded to f32.
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -358,7 +358,9 @@ static tts_tensor * build_graph(tts_dia * p, bool encoder_step) {
     }
     tts_tensor * cond = tg::cont(c, tg::view_2d(c, out, out->ne[0], out->ne[2], out->nb[2], 0));
     tts_tensor * uncond = tg::cont(c, tg::view_2d(c, out, out->ne[0], out->ne[2], out->nb[2], out->nb[1]));
-    tts_tensor * logits = tg::add(c, cond, tg::scale(c, tg::sub(c, cond, uncond), cf.cfg_scale));
+    // ggml_map_custom2(cond, uncond, cfg_scale) as the reference builds it, run on the device
+    tts_tensor * logits = tg::map_custom2(c, cond, uncond, TTS_CUSTOM_CFG_SCALE);
+    memcpy(&logits->op_params[1], &cf.cfg_scale, sizeof(float));
     tg::set_name(logits, "decoder_output");
     tg::set_output(logits);
     tg::build_forward_expand(c, logits);

@@ -422,6 +422,13 @@ tts_tensor * map_custom3(context & c, tts_tensor * a, tts_tensor * b, tts_tensor
     return t;
 }
 
+// ggml_map_custom2(a, b, fn): dst has a's shape (tts_custom_op fn, restated on the device)
+tts_tensor * map_custom2(context & c, tts_tensor * a, tts_tensor * b, int fn) {
+    tts_tensor * t = new_op(c, TTS_OP_MAP_CUSTOM2, TTS_TYPE_F32, a->ne, a, b);
+    t->op_params[0] = fn;
+    return t;
+}
+
 tts_tensor * sum_rows(context & c, tts_tensor * a) {
     int64_t ne[4] = {1, a->ne[1], a->ne[2], a->ne[3]};
     return new_op(c, TTS_OP_SUM_ROWS, TTS_TYPE_F32, ne, a);

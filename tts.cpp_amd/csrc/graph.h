@@ -100,6 +100,7 @@ tts_tensor * stft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, i
 tts_tensor * istft(context & c, tts_tensor * a, tts_tensor * window, int n_fft, int hop, bool abs_and_angle);
 tts_tensor * repeat(context & c, tts_tensor * a, tts_tensor * shape);
 tts_tensor * map_custom3(context & c, tts_tensor * a, tts_tensor * b, tts_tensor * cc, int fn);
+tts_tensor * map_custom2(context & c, tts_tensor * a, tts_tensor * b, int fn);
 tts_tensor * rope_ext(context & c, tts_tensor * a, tts_tensor * pos, tts_tensor * freq_factors, int n_dims, int mode,
                       int n_ctx_orig, float freq_base, float freq_scale, float ext_factor, float attn_factor,
                       float beta_fast, float beta_slow);

@@ -216,6 +216,16 @@ __global__ __launch_bounds__(256) void k_uv_noise(float * __restrict__ uv, float
     }
 }
 
+// ---- MAP_CUSTOM2 / cfg_scale (src/util.cpp:175-200) -------------------------------------------
+__global__ __launch_bounds__(256) void k_cfg_scale(TD dst, TD a, TD b, float scale, int64_t n) {
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < n; k += (int64_t)gridDim.x * 256) {
+        int64_t i0, i1, i2, i3;
+        unravel(k, dst.ne, i0, i1, i2, i3);
+        const float cr = td_load(a, i0, i1, i2, i3), ur = td_load(b, i0, i1, i2, i3);
+        td_store(dst, i0, i1, i2, i3, __fadd_rn(cr, __fmul_rn(scale, __fsub_rn(cr, ur))));
+    }
+}
+
 static size_t istft_lds(int N, int H, int K) { return (size_t)16 * N + (size_t)16 * istft_tile_frames(N, H) * K; }
 
 bool audio_op_supported(const tts_tensor * n) {
@@ -229,6 +239,11 @@ bool audio_op_supported(const tts_tensor * n) {
         case TTS_OP_STFT: {
             const int N = n->op_params[0], H = n->op_params[1];
             return N >= 1 && H >= 1 && 16 * (size_t)N <= 64 * 1024 && a->ne[0] > N / 2 && n->src[1] && n->src[1]->type == TTS_TYPE_F32;
+        }
+        case TTS_OP_MAP_CUSTOM2: {
+            const tts_tensor * b = n->src[1];
+            return n->op_params[0] == TTS_CUSTOM_CFG_SCALE && b && b->type == TTS_TYPE_F32 && b->ne[0] == a->ne[0] &&
+                   b->ne[1] == a->ne[1] && b->ne[2] == a->ne[2] && b->ne[3] == a->ne[3];
         }
         case TTS_OP_MAP_CUSTOM3: {
             // contiguous [L, H, 2] destination, F0 of length L, data = 4 + L*H floats
@@ -281,6 +296,13 @@ int launch_audio_op(tts_hip_backend * be, const tts_tensor * n) {
             const unsigned tiles = (unsigned)((n->ne[0] + ISTFT_TILE - 1) / ISTFT_TILE);
             hipLaunchKernelGGL(k_istft, dim3(tiles, (unsigned)n->ne[1]), dim3(ISTFT_TILE), lds, be->stream, d, a,
                                make_td(n->src[1]), N, H, n->op_params[2]);
+        } break;
+        case TTS_OP_MAP_CUSTOM2: {
+            float scale;
+            memcpy(&scale, &n->op_params[1], sizeof(float));
+            int64_t g = (ne + 255) / 256;
+            if (g > 8192) g = 8192;
+            hipLaunchKernelGGL(k_cfg_scale, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, be->stream, d, a, make_td(n->src[1]), scale, ne);
         } break;
         case TTS_OP_MAP_CUSTOM3: {
             const int64_t L = n->ne[0], cnt = L * n->ne[1];

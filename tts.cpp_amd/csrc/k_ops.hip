@@ -674,7 +674,7 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
         } break;
         case TTS_OP_IM2COL: launch_im2col(be, node); return 0;
         case TTS_OP_CONV_TRANSPOSE_1D: launch_conv_transpose_1d(be, node); return 0;
-        case TTS_OP_CUMSUM: case TTS_OP_UPSCALE: case TTS_OP_STFT: case TTS_OP_ISTFT: case TTS_OP_MAP_CUSTOM3: return launch_audio_op(be, node);
+        case TTS_OP_CUMSUM: case TTS_OP_UPSCALE: case TTS_OP_STFT: case TTS_OP_ISTFT: case TTS_OP_MAP_CUSTOM3: case TTS_OP_MAP_CUSTOM2: return launch_audio_op(be, node);
         default:
             return TTS_STATUS_UNSUPPORTED;
     }

@@ -18,7 +18,7 @@ F32, F16, Q4_0, Q8_0, Q4_K, Q8_K, I32 = 0, 1, 2, 8, 12, 15, 26
 OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "SUM_ROWS", "REPEAT",
        "CONCAT", "NORM", "RMS_NORM", "MUL_MAT", "SCALE", "CPY", "CONT", "RESHAPE", "VIEW", "PERMUTE",
        "TRANSPOSE", "GET_ROWS", "SOFT_MAX", "ROPE", "CLAMP", "CONV_TRANSPOSE_1D", "IM2COL", "UPSCALE",
-       "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT", "MAP_CUSTOM3"]
+       "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT", "MAP_CUSTOM3", "MAP_CUSTOM2"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
 FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048, "MCPY": 4096}
