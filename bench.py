@@ -121,6 +121,36 @@ def gather_tokens(dist, rank, world, local, toks):
     return np.concatenate([p.cpu().numpy() for p in parts], axis=0).astype(np.int32)
 
 
+def gather_audio(dist, rank, world, local, pcms):
+    """The final audio gather: every prompt's PCM to rank 0 in global prompt order.
+    An all-gather of the per-prompt sample counts, then a gatherv as point-to-point sends of each
+    rank's concatenated samples (RCCL send / recv over xGMI; gloo on CPU).  Returns the list of all
+    prompts' PCM on rank 0, None elsewhere."""
+    if dist is None:
+        return list(pcms)
+    import torch
+    dev = _comm_device(dist, local)
+    lens = torch.tensor([len(p) for p in pcms], dtype=torch.int64, device=dev)
+    all_lens = [torch.empty_like(lens) for _ in range(world)]
+    dist.all_gather(all_lens, lens)
+    flat = torch.from_numpy(np.concatenate(pcms).astype(np.float32)).to(dev)
+    if rank != 0:
+        dist.send(flat, dst=0)
+        return None
+    out = []
+    for r in range(world):
+        n = [int(v) for v in all_lens[r].cpu()]
+        if r == 0:
+            buf = flat
+        else:
+            buf = torch.empty(sum(n), dtype=torch.float32, device=dev)
+            dist.recv(buf, src=r)
+        host = buf.cpu().numpy()
+        offs = np.cumsum([0] + n)
+        out += [host[offs[i]:offs[i + 1]] for i in range(len(n))]
+    return out
+
+
 def cpu_baseline(args, n_threads):
     """Oracle (C restatement of ggml-cpu) running the same Parler step graph and the same DAC graph
     on host cores; end-to-end rate = 1 / (1/AR + 1/DAC) per audio-second."""
@@ -408,11 +438,13 @@ def main():
         toks_r[r] = rr.generate(args.steps)
         rb.sync()
 
+    pcm = [None] * args.batch
+
     def dac_leg(w):
         # worker w decodes every W-th prompt of the whole per-GPU batch
         xb, rd = dac_workers[w]
         for g in range(w, args.batch, W):
-            rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
+            pcm[g] = rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
         xb.sync()
 
     t0 = time.perf_counter()
@@ -453,6 +485,12 @@ def main():
     dt_ar = max_over_ranks(dist, local, t1 - t0)
     dt_dac = max_over_ranks(dist, local, t2 - t1)
     gather_tokens(dist, rank, world, local, toks)
+    # the one data exchange of the sharded job: every prompt's audio to rank 0
+    gathered = None
+    if dac is not None:
+        tg0 = time.perf_counter()
+        gathered = gather_audio(dist, rank, world, local, pcm)
+        t_gather = time.perf_counter() - tg0
 
     total_prompts = args.batch * world
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
@@ -488,6 +526,9 @@ def main():
             "dac_audio_sec_per_s": round(audio_s / dt_dac, 3) if dac is not None else None,
             "codec_tokens_per_s": round(total_prompts * args.steps * HEADS / dt_ar, 1),
             "host_us_per_step": host,
+            "audio_gather": None if gathered is None else {
+                "prompts": len(gathered), "audio_sec": round(sum(len(p) for p in gathered) / SAMPLE_RATE, 3),
+                "ms": round(1000.0 * t_gather, 3), "transport": "RCCL send/recv (gatherv) to rank 0" if world > 1 else "local"},
             "kokoro": kres,
             "orpheus": ores,
             "dia": dres,

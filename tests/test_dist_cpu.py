@@ -1,7 +1,8 @@
 """Multi-rank path of bench.py on CPU: world_size 2 over gloo, each rank stepping its prompt shard
 through the oracle backend (the same C++ Parler runner the GPU uses).  Checks that the shards are the
-matching rows of the whole batch, that the max-over-ranks timing reduction works, and that the one
-data exchange (token gather to rank 0) reproduces a single-process run of the whole batch exactly."""
+matching rows of the whole batch, that the max-over-ranks timing reduction works, that the token
+gather to rank 0 reproduces a single-process run of the whole batch exactly, and that the final audio
+gather (ragged per-prompt PCM, all-gathered lengths + point-to-point gatherv) arrives in prompt order."""
 import os
 import pathlib
 import sys
@@ -42,7 +43,10 @@ def _worker(rank, world, port, q):
         bench.barrier_sync(dist, None)
         dt = bench.max_over_ranks(dist, local, 1.0 + r)
         full = bench.gather_tokens(dist, r, w, local, toks)
-        q.put((r, dt, full))
+        # audio gather: ragged per-prompt PCM lengths, rank-tagged values
+        pcms = [np.full(100 + 37 * i + 11 * r, r * 10 + i, dtype=np.float32) for i in range(PER_RANK)]
+        audio = bench.gather_audio(dist, r, w, local, pcms)
+        q.put((r, dt, full, audio))
     finally:
         dist.destroy_process_group()
 
@@ -62,13 +66,18 @@ def test_two_rank_gloo_gather_matches_single_process():
         p.start()
     got = {}
     for _ in range(world):
-        r, dt, full = q.get(timeout=300)
-        got[r] = (dt, full)
+        r, dt, full, audio = q.get(timeout=300)
+        got[r] = (dt, full, audio)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert all(dt == pytest.approx(2.0) for dt, _ in got.values())   # max over ranks
-    assert got[1][1] is None
+    assert all(dt == pytest.approx(2.0) for dt, _, _ in got.values())   # max over ranks
+    assert got[1][1] is None and got[1][2] is None
+    audio = got[0][2]  # global prompt order, each prompt's own length and values
+    assert len(audio) == world * PER_RANK
+    for g, a in enumerate(audio):
+        r, i = divmod(g, PER_RANK)
+        assert a.shape == (100 + 37 * i + 11 * r,) and np.all(a == r * 10 + i)
     ref = _run(world * PER_RANK, offset=0)
     assert got[0][1].shape == ref.shape
     assert np.array_equal(got[0][1], ref)
