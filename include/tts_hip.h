@@ -207,6 +207,11 @@ int tts_hip_synchronize(tts_hip_backend_t backend);
  * TTS_FLAG_REPACKED on `t`; get returns ggml's native bytes. */
 int tts_hip_weight_set(tts_hip_backend_t backend, tts_tensor * t, const void * src_host);
 int tts_hip_weight_get(tts_hip_backend_t backend, const tts_tensor * t, void * dst_host);
+/* Weight quantization on the device, ggml's quantize_row_q4_K_ref / quantize_row_q8_0_ref
+ * (ggml-quants.c; the reference's examples/quantize path, quantize_impl.cpp:82-292): x [rows][K] f32
+ * -> dst [rows][K / blck] ggml blocks (native layout, both device pointers; K % 256 == 0 for Q4_K,
+ * K % 32 == 0 for Q8_0).  Bytes equal the CPU reference's (f32 operations in source order). */
+int tts_hip_quantize(tts_hip_backend_t backend, int type, const float * x_dev, void * dst_dev, int64_t rows, int64_t K);
 /* Host helper: (inverse = 0) ggml Q4_K blocks -> backend lane layout, (1) the reverse. */
 void tts_repack_q4_K(const void * src, void * dst, int64_t nblocks, int inverse);
 /* The 4-row tile layout of a Q4_K matrix [nrows][nb blocks] (nrows % 4 == 0): per (tile t of rows

@@ -180,6 +180,142 @@ void ref_quantize_row_q8_0(const float * x, ref_block_q8_0 * y, int64_t k) {
     }
 }
 
+/* make_qkx2_quants (ggml-quants.c): weighted min/scale search for one sub-block, nmax = 15,
+ * rmin = -1, rdelta = 0.1, nstep = 20, squared error (use_mad false), every operation rounded to f32
+ * in source order (no contraction). */
+static float ref_make_qkx2_quants(int n, int nmax, const float * x, const float * weights, uint8_t * L, float * the_min,
+                                  uint8_t * Laux, float rmin, float rdelta, int nstep) {
+    float min = x[0];
+    float max = x[0];
+    float sum_w = weights[0];
+    float sum_x = sum_w * x[0];
+    for (int i = 1; i < n; ++i) {
+        if (x[i] < min) min = x[i];
+        if (x[i] > max) max = x[i];
+        const float w = weights[i];
+        sum_w += w;
+        sum_x += w * x[i];
+    }
+    if (min > 0) min = 0;
+    if (max == min) {
+        for (int i = 0; i < n; ++i) L[i] = 0;
+        *the_min = -min;
+        return 0.f;
+    }
+    float iscale = nmax / (max - min);
+    float scale = 1 / iscale;
+    float best_mad = 0;
+    for (int i = 0; i < n; ++i) {
+        const int l = ref_nearest_int(iscale * (x[i] - min));
+        L[i] = (uint8_t)MAX(0, MIN(nmax, l));
+        float diff = scale * L[i] + min - x[i];
+        diff = diff * diff;
+        const float w = weights[i];
+        best_mad += w * diff;
+    }
+    for (int is = 0; is <= nstep; ++is) {
+        iscale = (rmin + rdelta * is + nmax) / (max - min);
+        float sum_l = 0, sum_l2 = 0, sum_xl = 0;
+        for (int i = 0; i < n; ++i) {
+            int l = ref_nearest_int(iscale * (x[i] - min));
+            l = MAX(0, MIN(nmax, l));
+            Laux[i] = (uint8_t)l;
+            const float w = weights[i];
+            sum_l += w * l;
+            sum_l2 += w * l * l;
+            sum_xl += w * l * x[i];
+        }
+        const float D = sum_w * sum_l2 - sum_l * sum_l;
+        if (D > 0) {
+            float this_scale = (sum_w * sum_xl - sum_x * sum_l) / D;
+            float this_min = (sum_l2 * sum_x - sum_l * sum_xl) / D;
+            if (this_min > 0) {
+                this_min = 0;
+                this_scale = sum_xl / sum_l2;
+            }
+            float mad = 0;
+            for (int i = 0; i < n; ++i) {
+                float diff = this_scale * Laux[i] + this_min - x[i];
+                diff = diff * diff;
+                const float w = weights[i];
+                mad += w * diff;
+            }
+            if (mad < best_mad) {
+                for (int i = 0; i < n; ++i) L[i] = Laux[i];
+                best_mad = mad;
+                scale = this_scale;
+                min = this_min;
+            }
+        }
+    }
+    *the_min = -min;
+    return scale;
+}
+
+/* quantize_row_q4_K_ref (ggml-quants.c): per 256-block, make_qkx2_quants per 32 with weights
+ * av_x + |x|, 6-bit scales / mins against the block's max, fp16 d / dmin, then the 4-bit codes
+ * against the rounded scales (a sub-block whose rounded scale is 0 keeps the search's codes). */
+void ref_quantize_row_q4_K(const float * x, ref_block_q4_K * y, int64_t k) {
+    const int64_t nb = k / QK_K;
+    uint8_t L[QK_K];
+    uint8_t Laux[32];
+    float weights[32];
+    float mins[QK_K / 32];
+    float scales[QK_K / 32];
+    for (int64_t i = 0; i < nb; i++) {
+        float max_scale = 0;
+        float max_min = 0;
+        for (int j = 0; j < QK_K / 32; ++j) {
+            float sum_x2 = 0;
+            for (int l = 0; l < 32; ++l) sum_x2 += x[32 * j + l] * x[32 * j + l];
+            const float av_x = sqrtf(sum_x2 / 32);
+            for (int l = 0; l < 32; ++l) weights[l] = av_x + fabsf(x[32 * j + l]);
+            scales[j] = ref_make_qkx2_quants(32, 15, x + 32 * j, weights, L + 32 * j, &mins[j], Laux, -1.f, 0.1f, 20);
+            const float scale = scales[j];
+            if (scale > max_scale) max_scale = scale;
+            const float min = mins[j];
+            if (min > max_min) max_min = min;
+        }
+        const float inv_scale = max_scale > 0 ? 63.f / max_scale : 0.f;
+        const float inv_min = max_min > 0 ? 63.f / max_min : 0.f;
+        memset(y[i].scales, 0, sizeof(y[i].scales));
+        for (int j = 0; j < QK_K / 32; ++j) {
+            uint8_t ls = (uint8_t)ref_nearest_int(inv_scale * scales[j]);
+            uint8_t lm = (uint8_t)ref_nearest_int(inv_min * mins[j]);
+            ls = MIN(63, ls);
+            lm = MIN(63, lm);
+            if (j < 4) {
+                y[i].scales[j] = ls;
+                y[i].scales[j + 4] = lm;
+            } else {
+                y[i].scales[j + 4] = (uint8_t)((ls & 0xF) | ((lm & 0xF) << 4));
+                y[i].scales[j - 4] |= (uint8_t)((ls >> 4) << 6);
+                y[i].scales[j - 0] |= (uint8_t)((lm >> 4) << 6);
+            }
+        }
+        y[i].d = ref_fp32_to_fp16(max_scale / 63.f);
+        y[i].dmin = ref_fp32_to_fp16(max_min / 63.f);
+        uint8_t sc, m;
+        for (int j = 0; j < QK_K / 32; ++j) {
+            ref_get_scale_min_k4(j, y[i].scales, &sc, &m);
+            const float d = ref_fp16_to_fp32(y[i].d) * sc;
+            if (!d) continue;
+            const float dm = ref_fp16_to_fp32(y[i].dmin) * m;
+            for (int ii = 0; ii < 32; ++ii) {
+                int l = ref_nearest_int((x[32 * j + ii] + dm) / d);
+                l = MAX(0, MIN(15, l));
+                L[32 * j + ii] = (uint8_t)l;
+            }
+        }
+        uint8_t * q = y[i].qs;
+        for (int j = 0; j < QK_K; j += 64) {
+            for (int l = 0; l < 32; ++l) q[l] = (uint8_t)(L[j + l] | (L[j + l + 32] << 4));
+            q += 32;
+        }
+        x += QK_K;
+    }
+}
+
 void ref_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy) {
     const ref_block_q4_K * x = (const ref_block_q4_K *)vx;
     const ref_block_q8_K * y = (const ref_block_q8_K *)vy;

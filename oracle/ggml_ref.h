@@ -60,6 +60,7 @@ void ref_dequantize_row_q4_K(const ref_block_q4_K * x, float * y, int64_t k);
 void ref_dequantize_row_q8_0(const ref_block_q8_0 * x, float * y, int64_t k);
 void ref_quantize_row_q8_K(const float * x, ref_block_q8_K * y, int64_t k);
 void ref_quantize_row_q8_0(const float * x, ref_block_q8_0 * y, int64_t k);
+void ref_quantize_row_q4_K(const float * x, ref_block_q4_K * y, int64_t k);
 void ref_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy);
 void ref_vec_dot_q8_0_q8_0(int n, float * s, const void * vx, const void * vy);
 void ref_vec_dot_f16(int n, float * s, const ref_fp16_t * x, const ref_fp16_t * y);

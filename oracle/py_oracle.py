@@ -30,6 +30,7 @@ def lib():
         "ref_dequantize_row_q8_0": (None, [vp, vp, i64]),
         "ref_quantize_row_q8_K": (None, [vp, vp, i64]),
         "ref_quantize_row_q8_0": (None, [vp, vp, i64]),
+        "ref_quantize_row_q4_K": (None, [vp, vp, i64]),
         "ref_vec_dot_q4_K_q8_K": (None, [ctypes.c_int, vp, vp, vp]),
         "ref_vec_dot_q8_0_q8_0": (None, [ctypes.c_int, vp, vp, vp]),
         "ref_gelu_f32": (ctypes.c_float, [ctypes.c_float]),
@@ -81,4 +82,17 @@ def dequant_q8_0(w_bytes, K, N):
     rs = K // 32 * 34
     for n in range(N):
         lib().ref_dequantize_row_q8_0(w[n * rs:].ctypes.data, out[n].ctypes.data, K)
+    return out
+
+
+def quantize(wtype, x):
+    """quantize_row_q4_K_ref / quantize_row_q8_0_ref over the rows of x [N][K] -> ggml bytes."""
+    import numpy as np
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    N, K = x.shape
+    rs = K // 256 * 144 if wtype == ttship.Q4_K else K // 32 * 34
+    out = np.zeros(N * rs, dtype=np.uint8)
+    fn = lib().ref_quantize_row_q4_K if wtype == ttship.Q4_K else lib().ref_quantize_row_q8_0
+    for n in range(N):
+        fn(x[n].ctypes.data, out[n * rs:].ctypes.data, K)
     return out

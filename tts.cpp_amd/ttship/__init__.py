@@ -263,6 +263,7 @@ def lib():
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
         "tts_hip_weight_set": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
+        "tts_hip_quantize": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, i64, i64]),
         "tts_hip_weight_get": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_repack_q4_K": (None, [vp, vp, i64, ctypes.c_int]),
         "tts_repack_q4_K_tiled": (None, [vp, vp, i64, i64, ctypes.c_int]),
@@ -387,6 +388,25 @@ class HipBackend:
         st = self.L.tts_hip_tensor_get(self.ptr, host_arr.ctypes.data, dev, host_arr.nbytes)
         if st != 0:
             raise RuntimeError(f"tensor_get failed {st}")
+
+    def quantize(self, wtype, x):
+        """Device quantization of f32 rows x [N][K] to ggml Q4_K / Q8_0 bytes (host array out)."""
+        import numpy as np
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        N, K = x.shape
+        rs = K // 256 * 144 if wtype == Q4_K else K // 32 * 34
+        dx, dq = self.alloc(x.nbytes), self.alloc(N * rs)
+        try:
+            self.set(dx, x)
+            st = self.L.tts_hip_quantize(self.ptr, wtype, dx, dq, N, K)
+            if st != 0:
+                raise RuntimeError(f"tts_hip_quantize failed {st}")
+            out = np.empty(N * rs, dtype=np.uint8)
+            self.get(out, dq)
+            return out
+        finally:
+            self.free(dx)
+            self.free(dq)
 
     def sync(self):
         if self.L.tts_hip_synchronize(self.ptr) != 0:
