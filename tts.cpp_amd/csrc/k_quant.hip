@@ -58,8 +58,7 @@ __device__ void q4k_search(const float * x, const float * w, uint8_t * L, float 
         the_scale = 0.f;
         return;
     }
-    const float range = __fsub_rn(mx, mn);
-    float iscale = cr_divf(15.f, range);
+    float iscale = cr_divf(15.f, __fsub_rn(mx, mn));
     float scale = cr_divf(1.f, iscale);
     float best_mad = 0;
     for (int i = 0; i < 32; ++i) {
@@ -71,7 +70,8 @@ __device__ void q4k_search(const float * x, const float * w, uint8_t * L, float 
     }
     uint8_t Laux[32];
     for (int is = 0; is <= 20; ++is) {
-        iscale = cr_divf(__fadd_rn(__fadd_rn(-1.f, __fmul_rn(0.1f, (float)is)), 15.f), range);
+        // (max - min) with the current min: an accepted candidate moves min for the later ones
+        iscale = cr_divf(__fadd_rn(__fadd_rn(-1.f, __fmul_rn(0.1f, (float)is)), 15.f), __fsub_rn(mx, mn));
         float sum_l = 0, sum_l2 = 0, sum_xl = 0;
         for (int i = 0; i < 32; ++i) {
             int l = q_nearest_int(__fmul_rn(iscale, __fsub_rn(x[i], mn)));
