@@ -251,6 +251,9 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_UNIQUE = 11, /* 1 (default) = lane-layout Q4_K GEMVs run the unique-load kernel (an octet per
                                      (row, block), every weight byte loaded once, all columns per lane, ggml's chain
                                      finished from LDS: bit-identical); 0 = the octet-per-(row, column) kernel */
+    TTS_HIP_OPT_GEMV_KS = 13,     /* tile-layout Q4_K GEMVs of at most `value` 16-row tiles (M <= 8 columns, K <= 4096)
+                                     run the K-split matrix-core kernel (a workgroup per tile, its blocks over the
+                                     waves, ggml's chain finished from LDS: bit-identical).  Default 256; 0 = never */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

@@ -18,6 +18,7 @@ SHAPES = [  # (name, type, K, N)
     ("parler_qkvo", ttship.Q4_K, 1024, 1024),
     ("parler_fc1", ttship.Q4_K, 1024, 4096),
     ("parler_fc2", ttship.Q4_K, 4096, 1024),
+    ("orpheus_q", ttship.Q4_K, 3072, 3072),
     ("orpheus_up", ttship.Q4_K, 3072, 8192),
     ("orpheus_down", ttship.Q4_K, 8192, 3072),
     ("orpheus_head", ttship.Q4_K, 3072, 156940),
@@ -38,7 +39,7 @@ def main():
     # cold: cycle through enough weight copies (>= 512 MiB) that every launch streams from HBM, as in a
     # decode step (the Infinity Cache holds 256 MiB); kernel selection from the environment
     cold = int(sys.argv[7]) if len(sys.argv) > 7 else 0
-    for opt in ("GEMV_UNIQUE",):
+    for opt in ("GEMV_UNIQUE", "GEMV_KS"):
         if os.environ.get(opt) is not None:
             hip.set_option(ttship.OPT[opt], int(os.environ[opt]))
     L = ttship.lib()

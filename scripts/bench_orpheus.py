@@ -28,6 +28,9 @@ def main():
     be = ttship.HipBackend(0)
     if os.environ.get("TTS_BENCH_GRAPHS") is not None:  # 0: eager launches (rocprofv3 kernel traces)
         be.set_option(ttship.OPT["GRAPHS"], int(os.environ["TTS_BENCH_GRAPHS"]))
+    for env, opt in (("TTS_BENCH_KS", "GEMV_KS"), ("TTS_BENCH_TILE_BYTES", "Q4K_TILE_BYTES")):
+        if os.environ.get(env) is not None:
+            be.set_option(ttship.OPT[opt], int(os.environ[env]))
     t0 = time.perf_counter()
     cfg = ttship.orpheus_config(batch=B, max_ctx=n_prompt + steps + 64, arena_bytes=1 << 30, **kw)
     o = ttship.Orpheus(be.iface(), cfg)

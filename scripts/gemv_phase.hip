@@ -5,6 +5,7 @@
 // Prints one JSON line per shape: event-timed duration, body span and per-phase medians (us).
 #define TTS_PHASE_TS
 #include "../tts.cpp_amd/csrc/k_gemv.hip"
+#include "../tts.cpp_amd/csrc/k_gemm.hip"
 #include "../tts.cpp_amd/csrc/types.cpp"
 
 #include <algorithm>
@@ -34,6 +35,7 @@ int main() {
     };
     tts_hip_backend be;
     be.gemv_unique = getenv("GEMV_UNIQUE") ? atoi(getenv("GEMV_UNIQUE")) : 1;
+    if (getenv("GEMV_KS")) be.gemv_ks_tiles = atoi(getenv("GEMV_KS"));
     TTS_HIP_CHECK(hipStreamCreate(&be.stream));
     std::mt19937 rng(1);
     const size_t wbytes = 3ull * 4096 * 4096 / 256 * 144;
@@ -88,6 +90,7 @@ int main() {
         j.x = x;
         j.xcs = s.K;
         j.pro = s.pro;
+        j.tiled = getenv("GEMV_PHASE_TILED") ? 1 : 0;  // tile layout (random bytes: layout-agnostic timing)
         if (s.pro == PRO_LN) {
             j.lnw = lnw, j.lnb = lnb, j.eps = 1e-5f, j.lnout = lno, j.locs = s.K;
         }
@@ -137,9 +140,30 @@ int main() {
             p36.push_back(med(e6)), p64.push_back(med(e4)), p45.push_back(med(e5));
             p34.push_back(med(f34)), p45b.push_back(med(f45));
         }
-        printf("{\"cold\":%d,\"shape\":\"%s\",\"K\":%lld,\"N\":%lld,\"M\":%lld,\"nmat\":%d,\"event_us\":%.2f,\"span_us\":%.2f,"
+        // in-chain cost: 50 back-to-back launches captured as one HIP graph, replayed (warm caches)
+        double chain_us = 0;
+        {
+            hipGraph_t g;
+            hipGraphExec_t ge;
+            TTS_HIP_CHECK(hipStreamBeginCapture(be.stream, hipStreamCaptureModeRelaxed));
+            for (int i = 0; i < 50; ++i) launch_gemv_job(&be, j);
+            TTS_HIP_CHECK(hipStreamEndCapture(be.stream, &g));
+            TTS_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+            for (int w = 0; w < 3; ++w) TTS_HIP_CHECK(hipGraphLaunch(ge, be.stream));
+            TTS_HIP_CHECK(hipStreamSynchronize(be.stream));
+            TTS_HIP_CHECK(hipEventRecord(e0, be.stream));
+            for (int r = 0; r < 10; ++r) TTS_HIP_CHECK(hipGraphLaunch(ge, be.stream));
+            TTS_HIP_CHECK(hipEventRecord(e1, be.stream));
+            TTS_HIP_CHECK(hipStreamSynchronize(be.stream));
+            float ms;
+            TTS_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            chain_us = 1000.0 * ms / 500.0;
+            TTS_HIP_CHECK(hipGraphExecDestroy(ge));
+            TTS_HIP_CHECK(hipGraphDestroy(g));
+        }
+        printf("{\"chain_us\":%.2f,\"cold\":%d,\"shape\":\"%s\",\"K\":%lld,\"N\":%lld,\"M\":%lld,\"nmat\":%d,\"event_us\":%.2f,\"span_us\":%.2f,"
                "\"start_spread_us\":%.2f,\"end_spread_us\":%.2f,\"issue_us\":%.2f,\"prologue_us\":%.2f,\"barrier_us\":%.2f,\"rows_us\":%.2f,\"wait_w_us\":%.2f,\"compute_us\":%.2f,\"store_exit_us\":%.2f,\"t34_us\":%.2f,\"t45_us\":%.2f}\n",
-               (int)cold, s.name, (long long)s.K, (long long)s.N, (long long)s.M, s.nmat, med(ev), med(span), med(t0spread), med(endspread), med(p01),
+               chain_us, (int)cold, s.name, (long long)s.K, (long long)s.N, (long long)s.M, s.nmat, med(ev), med(span), med(t0spread), med(endspread), med(p01),
                med(p12), med(p23), med(p3e), med(p36), med(p64), med(p45), med(p34), med(p45b));
     }
     return 0;

@@ -112,12 +112,26 @@ def run_gpu_tiled(hip, w, x, N):
         hip.free(dy)
 
 
+KS_DEFAULT = 256  # backend default of TTS_HIP_OPT_GEMV_KS
+
+
+@pytest.fixture(params=[0, KS_DEFAULT, 1 << 20], ids=["mf", "ks", "ks_loop"])
+def ks_tiles(request, hip):
+    """Tile-layout GEMVs on k_gemv_q4K_mf (0), on the K-split kernel k_gemv_q4K_ks where it applies
+    (M <= 8, K <= 4096, N % 16 == 0) with the default tile cap, and on the K-split kernel for every
+    tile count (grids of more than 2048 tiles loop over tiles)."""
+    assert ttship.lib().tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], request.param) == 0
+    yield request.param
+    ttship.lib().tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], KS_DEFAULT)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,N", MF_SHAPES + [(8192, 3072), (3072, 16388)])
+@pytest.mark.parametrize("K,N", MF_SHAPES + [(8192, 3072), (3072, 16388), (3072, 40960), (256, 48)])
 @pytest.mark.parametrize("M", [1, 2, 5, 8, 16, 19])
-def test_q4_K_mfma(hip, K, N, M):
-    """Matrix-core Q4_K path (k_gemv_q4K_mf on the tile layout): the integer block dots run as f16
-    MFMAs whose sums are exact integers, so the result is bit-identical to ggml's order."""
+def test_q4_K_mfma(hip, ks_tiles, K, N, M):
+    """Matrix-core Q4_K paths on the tile layout (k_gemv_q4K_mf; k_gemv_q4K_ks): the integer block
+    dots run as f16 MFMAs whose sums are exact integers, and ggml's f32 chain runs in block order,
+    so the result is bit-identical to ggml's order."""
     rng = np.random.default_rng(K * 5 + N + 3 * M)
     w = helpers.rand_q4_K(rng, N, K)
     x = rng.standard_normal((M, K)).astype(np.float32)
@@ -127,7 +141,7 @@ def test_q4_K_mfma(hip, K, N, M):
 
 
 @pytest.mark.gpu
-def test_q4_K_mfma_extreme_blocks(hip):
+def test_q4_K_mfma_extreme_blocks(hip, ks_tiles):
     """Largest integer sums the MFMA path must keep exact: all scales / mins 63, nibbles 15, and
     activations quantized to +-127 (|aux32| up to 3.84e6, bsum up to 4064)."""
     K, N, M = 1024, 64, 4

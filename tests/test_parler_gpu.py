@@ -58,11 +58,14 @@ def test_full_parler_mini_q4k_tokens(hip):
 
 
 @pytest.mark.gpu
-def test_full_parler_mini_q4k_tokens_mfma(hip):
+@pytest.mark.parametrize("ks", [0, 256])
+def test_full_parler_mini_q4k_tokens_mfma(hip, ks):
     """Full Parler-mini at batch 3 with every Q4_K matrix in the tile layout: all GEMVs (LN /
-    quantize prologues, grouped q/k/v with KV-store epilogues, GELU / residual epilogues) on the
-    matrix-core kernel, cross-attention unfused, embeddings gathered from tiled tables."""
+    quantize prologues, grouped q/k/v with KV-store epilogues, GELU / residual epilogues) on a
+    matrix-core kernel (k_gemv_q4K_mf with GEMV_KS = 0, the K-split k_gemv_q4K_ks otherwise),
+    cross-attention unfused, embeddings gathered from tiled tables."""
     hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], 1)  # every Q4_K matrix (and embedding table) tiled
+    hip.set_option(ttship.OPT["GEMV_KS"], ks)
     try:
         g, c = make_pair(hip, batch=3)
     finally:
@@ -75,6 +78,7 @@ def test_full_parler_mini_q4k_tokens_mfma(hip):
         tc = c.generate(6)
         assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
     finally:
+        hip.set_option(ttship.OPT["GEMV_KS"], 256)
         g.close()
         c.close()
 

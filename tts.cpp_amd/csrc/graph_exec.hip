@@ -1563,7 +1563,7 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         const char * o1 = o0 + tbytes(A.out);
         const char * x0 = (const char *)j.x;
         const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
-        const bool ok = !tmp && j.wtype == TTS_TYPE_Q4_K && j.K <= 1024 && j.N == 64 * A.q->ne[2] && k.nb[0] == 4 &&
+        const bool ok = !tmp && !j.tiled && j.wtype == TTS_TYPE_Q4_K && j.K <= 1024 && j.N == 64 * A.q->ne[2] && k.nb[0] == 4 &&
                         (k.nb[1] % 16) == 0 && (k.nb[2] % 16) == 0 && (k.nb[3] % 16) == 0 && ((uintptr_t)k.data % 16) == 0 &&
                         A.k->ne[1] >= 1 && A.k->ne[1] <= 64 && !(o0 < x1 && x0 < o1) && contiguous(A.out);
         if (ok) {

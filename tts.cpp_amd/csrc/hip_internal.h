@@ -240,6 +240,9 @@ struct tts_hip_backend {
     int gemv_dbg = 0;
     // Q4_K GEMVs in the lane layout run the unique-load kernel (k_gemv_q4_K_u) where the shape fits
     int gemv_unique = 1;
+    // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
+    // matrix-core kernel k_gemv_q4K_ks (0 = never)
+    int64_t gemv_ks_tiles = 256;
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;

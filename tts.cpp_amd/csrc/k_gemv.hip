@@ -904,6 +904,161 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Matrix-core Q4_K GEMV for latency-bound decode matrices (k_gemv_q4K_ks).  Parler's matrices are
+// 0.6-2.4 MB: the row phase of the VALU kernels is ~1.2-2.5 us of dependent integer dots at one wave
+// per SIMD, and k_gemv_q4K_mf streams a tile's blocks through ONE wave.  Here a workgroup owns one
+// 16-row tile and splits its work units (block b, residue half rh) over its waves, so every weight
+// load of the tile is issued at kernel entry (before the prologue) and the integer dots are a few
+// MFMAs per wave:
+//   unit (b, rh): 4 v_mfma_f32_16x16x32_f16 for residues l = 4rh..4rh+3 (+ the mins MFMA when
+//   rh = 0), exactly the integers of k_gemv_q4K_mf; the lane turns them into ggml's two per-block
+//   terms p_l = (d*yd)*aux32[l] and q = (dmin*yd)*sumi, each rounded as the sequential code rounds
+//   them, and writes them to LDS;
+//   chain: lane (row, column, l) runs ggml's chain over the blocks in ascending order
+//   (sums[l] += p_l, sumf -= q, then sumf += sums[0..7] across the octet) -- the same additions in
+//   the same order as vec_dot_q4_K_q8_K, so the output is bit-identical.
+// LDS: the Q8_K B operands of all M <= 8 columns (q4k_prologue, MF layout), then the terms
+// p[nb][16 rows][8 columns][8] and q[nb][16 rows][8 columns].  Large grids loop over tiles.
+template <int PRO, int NCH, int UPW, int NWMAX>
+__global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK_K);
+    const int M = (int)j.M;
+    const int nslot = M * nb + 1;  // + the prologue's trash slot
+    _Float16 * b16 = (_Float16 *)smem;                   // [nslot][256]
+    _Float16 * sbs = b16 + (size_t)nslot * QK_K;         // [nslot][16]
+    float * xd_s = (float *)(sbs + (size_t)nslot * 16);  // [nslot]
+    float * tp = (float *)(smem + al16((size_t)nslot * (2 * QK_K + 32 + 4)));  // [nb][16][8][8]
+    float * tq = tp + (size_t)nb * 1024;                                       // [nb][16][8]
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+    const int r = lane & 15, kg = lane >> 4;
+    const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
+    const int nu = 2 * nb;
+    const int64_t T = (int64_t)j.nmat * j.N / 16;  // launcher: N % 16 == 0, so a tile is in one matrix
+    auto mat_of = [&](int64_t flat) {
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        return mt;
+    };
+
+    u32x4 hd[UPW], qv[UPW];
+    auto load = [&](int64_t t) {
+        const int mat = mat_of(t * 16);
+        const int64_t row = t * 16 - (int64_t)mat * j.N + r;
+        const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
+        const int ri = (int)(row & 3);
+#pragma unroll
+        for (int k = 0; k < UPW; ++k) {  // unconditional (clamped): every load issues before any use
+            const int u = min(wave + k * nw, nu - 1);
+            const uint8_t * bp = wt + (int64_t)(u >> 1) * 576;
+            hd[k] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
+            qv[k] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + (u & 1)) * 4 + ri) * 16));
+        }
+        TTS_PIN_LOADS();
+    };
+
+    // the integer dots of this wave's units -> the terms in LDS
+    auto units = [&]() {
+#pragma unroll
+        for (int k = 0; k < UPW; ++k) {
+            const int u = wave + k * nw;
+            if (u >= nu) break;  // wave-uniform
+            const int b = u >> 1, rh = u & 1;
+            const u32x4 h = hd[k];
+            const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
+            const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+            const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+            const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
+            const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
+            const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
+            const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
+            const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
+            const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8 + rh * 128;
+            f32x4 acc[4];
+#pragma unroll
+            for (int li = 0; li < 4; ++li) {
+                const uint32_t D = qv[k][li];
+                const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+                const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
+                const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
+                const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
+                const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
+                const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+                const f16x8 B = *(const f16x8 *)(bsl + li * 32);
+                acc[li] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+            f32x4 si = {0.f, 0.f, 0.f, 0.f};
+            if (rh == 0) {
+                const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
+                const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
+                const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
+                const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
+                const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
+                const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
+                const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+                const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
+                si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+            const float yd = xd_s[cc * nb + b];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
+                const float dy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+                const int pr = (b * 16 + 4 * kg + q) * 8 + r;  // (block, row, column)
+                if (r < M) {
+                    *(float4 *)(tp + (size_t)pr * 8 + rh * 4) =
+                        make_float4(__fmul_rn(dy, acc[0][q]), __fmul_rn(dy, acc[1][q]), __fmul_rn(dy, acc[2][q]), __fmul_rn(dy, acc[3][q]));
+                    if (rh == 0) tq[pr] = __fmul_rn(__fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd), si[q]);
+                }
+            }
+        }
+    };
+
+    int64_t t = blockIdx.x;
+    TTS_TS(j, 0);
+    auto mid = [&]() {
+        if (t < T) load(t);
+        TTS_TS(j, 1);
+    };
+    q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
+    TTS_TS(j, 2);
+    __syncthreads();
+    TTS_TS(j, 3);
+    for (; t < T; t += gridDim.x) {
+        units();
+        if (t + gridDim.x < T) load(t + gridDim.x);  // the next tile's weights fly during the chain
+        __syncthreads();
+        const int mat = mat_of(t * 16);
+        TTS_TS(j, 4);
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) {  // i = (row * 8 + column) * 8 + l
+            // every term is read before the chain starts (one LDS round trip, not one per block)
+            float p[NCH], q[NCH];
+#pragma unroll
+            for (int b = 0; b < NCH; ++b) {
+                const int bb = min(b, nb - 1);
+                p[b] = tp[(size_t)bb * 1024 + i];
+                q[b] = tq[bb * 128 + (i >> 3)];
+            }
+            float sums = 0.f, sumf = 0.f;
+#pragma unroll
+            for (int b = 0; b < NCH; ++b) {
+                if (b < nb) {
+                    sums = __fadd_rn(sums, p[b]);
+                    sumf = __fsub_rn(sumf, q[b]);
+                }
+            }
+            const float tot = q4k_octet_total(sumf, sums);
+            const int col = (i >> 3) & 7, row = i >> 6;
+            if ((i & 7) == 0 && col < M) gemv_store<8>(j, mat, t * 16 - (int64_t)mat * j.N + row, col, tot);
+        }
+        __syncthreads();
+    }
+    TTS_TS(j, 5);
+}
+
 // Cross-attention query GEMV + attention in one launch (Parler model.cpp:583-594: q = W_q
 // LN(x), then cont(K) -> mul_mat -> soft_max_ext -> mul_mat(V) -> permute -> cont over the n_enc
 // encoder positions).  Workgroup (h, b) owns head h of prompt b: 8 waves x 8 rows = the head's 64
@@ -1402,6 +1557,49 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
     }
 }
 
+// ---- K-split matrix-core path (k_gemv_q4K_ks) ----
+static size_t q4k_ks_lds(int64_t M, int64_t nb) {
+    return (((size_t)(M * nb + 1) * (2 * QK_K + 32 + 4) + 15) & ~(size_t)15) + (size_t)nb * (1024 + 128) * 4;
+}
+static bool q4k_ks_eligible(const tts_hip_backend * be, const GemvJob & j) {
+    if (be->gemv_ks_tiles <= 0 || j.wtype != TTS_TYPE_Q4_K || !j.tiled || j.M < 1 || j.M > 8) return false;
+    const int64_t nb = j.K / QK_K;
+    if (nb < 1 || nb > 16 || j.N % 16) return false;
+    if (j.pro == PRO_LN && j.K > 4 * 1024) return false;  // the LN prologue holds <= 16 chunks per lane
+    if ((int64_t)j.nmat * j.N / 16 > be->gemv_ks_tiles) return false;
+    return q4k_ks_lds(j.M, nb) <= 160 * 1024;
+}
+template <int PRO, int NCH, int UPW, int NWMAX>
+static void launch_q4k_ks_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, int nw, size_t lds) {
+    static std::atomic<uint32_t> attr_done{0};
+    if (lds > 64 * 1024) set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_ks<PRO, NCH, UPW, NWMAX>);
+    if (be->profile_gemv) {
+        hipEvent_t e0, e1;
+        profile_pair(be, e0, e1);
+        hipExtLaunchKernelGGL((k_gemv_q4K_ks<PRO, NCH, UPW, NWMAX>), dim3(gx), dim3(64 * nw), (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
+        return;
+    }
+    hipLaunchKernelGGL((k_gemv_q4K_ks<PRO, NCH, UPW, NWMAX>), dim3(gx), dim3(64 * nw), lds, be->stream, j);
+}
+static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
+    const int64_t nb = j.K / QK_K, T = (int64_t)j.nmat * j.N / 16;
+    // units (block, residue half) per wave: one for nb <= 4 (<= 8 waves); above, two (<= 16 waves)
+    // after a quantize-only prologue, four (<= 8 waves) after an LN prologue, whose K / 256 chunks
+    // per lane need the registers of a 512-thread workgroup
+    const int upw = nb <= 4 ? 1 : j.pro == PRO_LN ? 4 : 2;
+    const int nw = (int)((2 * nb + upw - 1) / upw);
+    const unsigned gx = (unsigned)(T < 2048 ? T : 2048);
+    const size_t lds = q4k_ks_lds(j.M, nb);
+    if (nb <= 4) {
+        if (j.pro == PRO_LN) launch_q4k_ks_t<PRO_LN, 4, 1, 8>(be, j, gx, nw, lds);
+        else launch_q4k_ks_t<PRO_QUANT, 4, 1, 8>(be, j, gx, nw, lds);
+    } else {
+        if (j.pro == PRO_LN) launch_q4k_ks_t<PRO_LN, 16, 4, 8>(be, j, gx, nw, lds);
+        else launch_q4k_ks_t<PRO_QUANT, 16, 2, 16>(be, j, gx, nw, lds);
+    }
+}
+
 template <int MC>
 static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
     const unsigned nmat = (unsigned)j.nmat;
@@ -1454,6 +1652,11 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
             TTS_HIP_CHECK(hipEventRecord(e1, be->stream));
             profile_push(be, e0, e1, gemv_bytes(job), job.wtype);
         }
+        return;
+    }
+    if (q4k_ks_eligible(be, job)) {
+        launch_q4k_ks(be, job);
+        TTS_HIP_CHECK(hipGetLastError());
         return;
     }
     if (q4k_mf_eligible(be, job)) {
