@@ -28,11 +28,20 @@ static double med(std::vector<double> v) {
 }
 
 int main() {
-    const Shape shapes[] = {
+    const Shape parler[] = {
         {"oproj_quant_m8", 1024, 1024, 8, PRO_QUANT, 1}, {"qkv_ln_m8", 1024, 1024, 8, PRO_LN, 3},
         {"fc1_ln_m8", 1024, 4096, 8, PRO_LN, 1},         {"fc2_quant_m8", 4096, 1024, 8, PRO_QUANT, 1},
         {"oproj_quant_m1", 1024, 1024, 1, PRO_QUANT, 1}, {"fc2_quant_m1", 4096, 1024, 1, PRO_QUANT, 1},
     };
+    // GEMV_PHASE_ORPHEUS: Orpheus-3B decode matrices (hidden 3072, ffn 8192) at M = 8
+    const Shape orpheus[] = {
+        {"orph_q_ln_m8", 3072, 3072, 8, PRO_LN, 1},        {"orph_o_quant_m8", 3072, 3072, 8, PRO_QUANT, 1},
+        {"orph_gateup_ln_m8", 3072, 8192, 8, PRO_LN, 2},   {"orph_down_quant_m8", 8192, 3072, 8, PRO_QUANT, 1},
+        {"orph_qkv_ln_m8", 3072, 5120, 8, PRO_LN, 1},
+    };
+    const bool orph = getenv("GEMV_PHASE_ORPHEUS") != nullptr;
+    const std::vector<Shape> shapes = orph ? std::vector<Shape>(std::begin(orpheus), std::end(orpheus))
+                                           : std::vector<Shape>(std::begin(parler), std::end(parler));
     tts_hip_backend be;
     be.gemv_unique = getenv("GEMV_UNIQUE") ? atoi(getenv("GEMV_UNIQUE")) : 1;
     if (getenv("GEMV_KS")) be.gemv_ks_tiles = atoi(getenv("GEMV_KS"));
@@ -51,12 +60,12 @@ int main() {
     const size_t nts = 1 << 20;
     TTS_HIP_CHECK(hipMalloc(&W, wbytes));
     TTS_HIP_CHECK(hipMemcpy(W, hw.data(), wbytes, hipMemcpyHostToDevice));
-    std::vector<float> hx(8 * 4096);
+    std::vector<float> hx(8 * 8192);
     std::normal_distribution<float> nd(0.f, 1.f);
     for (auto & v : hx) v = nd(rng);
     TTS_HIP_CHECK(hipMalloc(&x, hx.size() * 4));
     TTS_HIP_CHECK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
-    TTS_HIP_CHECK(hipMalloc(&y, 3 * 8 * 4096 * 4));
+    TTS_HIP_CHECK(hipMalloc(&y, 4 * 8 * 8192 * 4));
     TTS_HIP_CHECK(hipMalloc(&lnw, 4096 * 4));
     TTS_HIP_CHECK(hipMalloc(&lnb, 4096 * 4));
     TTS_HIP_CHECK(hipMalloc(&lno, 8 * 4096 * 4));
@@ -83,7 +92,7 @@ int main() {
         j.w_row_bytes = s.K / 256 * 144;
         for (int i = 0; i < s.nmat; ++i) {
             j.W[i] = W + (size_t)i * s.N * j.w_row_bytes;
-            j.Y[i] = y + (size_t)i * 8 * s.N;
+            j.Y[i] = y + (size_t)i * 8 * s.N;  // y holds 4 x 8 x 8192
             j.ycs[i] = s.N;
             j.yrs[i] = 1;
         }

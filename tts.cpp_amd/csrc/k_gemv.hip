@@ -763,6 +763,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     _Float16 * sbs = b16 + (size_t)nslot * QK_K;           // [nslot][16]  bsum lo / hi
     float * xd_s = (float *)(sbs + (size_t)nslot * 16);    // [nslot]      Q8_K d
 
+    TTS_TS(j, 0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int r = lane & 15, kg = lane >> 4;
     const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
@@ -891,10 +892,13 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     using I1 = std::integral_constant<int, 1>;
     auto mid = [&]() {
         if (nmine > 0) load(I0{}, 0);
+        TTS_TS(j, 1);
     };
     if (!(j.dbg & 2)) q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
     else mid();
+    TTS_TS(j, 2);
     __syncthreads();
+    TTS_TS(j, 3);
     for (int64_t i = 0; i < nmine; i += 2) {
         load(I1{}, min(i + 1, nmine - 1));
         compute(I0{}, i);
@@ -902,6 +906,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         load(I0{}, min(i + 2, nmine - 1));
         compute(I1{}, i + 1);
     }
+    TTS_TS(j, 5);
 }
 
 // ------------------------------------------------------------------------------------------
