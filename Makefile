@@ -41,3 +41,14 @@ clean:
 	rm -rf build $(OUT) oracle/_build
 
 .PHONY: all clean
+
+# Cache-policy variants of the backend for the MALL-residency study (scripts/gpu_cachepol.sh):
+# lib/<variant>/libtts_hip.so, selected with TTS_HIP_LIB_VARIANT=<variant>.
+VARIANT_DEFS_wplain := -DTTS_W_PLAIN
+VARIANT_DEFS_kvnt := -DTTS_KV_NT
+VARIANT_DEFS_wplain_kvnt := -DTTS_W_PLAIN -DTTS_KV_NT
+variant-%:
+	@mkdir -p build/obj_$* $(OUT)/$*
+	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(VARIANT_DEFS_$*) -c $$f -o build/obj_$*/$$(basename $$f).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(OUT)/$*/libtts_hip.so build/obj_$*/*.hip.o $(CPP_OBJS) -lpthread
+.PHONY: variant-%

@@ -254,6 +254,9 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_KS = 13,     /* tile-layout Q4_K GEMVs of at most `value` 16-row tiles (M <= 8 columns, K <= 4096)
                                      run the K-split matrix-core kernel (a workgroup per tile, its blocks over the
                                      waves, ggml's chain finished from LDS: bit-identical).  Default 256; 0 = never */
+    TTS_HIP_OPT_ATTN_FUSED = 14,  /* decode attention over P >= value keys (hd 64 / 128, 16-B K and V rows) runs as
+                                     ONE 1024-thread launch per attention (k_attn_fused; default 0 = off: the split pair,
+                                     TTS_HIP_OPT_ATTN_SPLIT; tests and studies use 128) */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

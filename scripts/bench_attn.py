@@ -39,7 +39,8 @@ def run(hip, P, hd, H, Hk, B, reps, split):
     for t in g.tensors:
         if getattr(t, "_root", None) is not None:
             t.data = dev[id(t._root)] + t._root_offs
-    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
+    hip.set_option(ttship.OPT["ATTN_FUSED"], ttship.ATTN_FUSED_ON if split == "fused" else 0)
+    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split == "split" else 0)
     ptrs = g.node_ptrs()
     L = ttship.lib()
     for _ in range(3):
@@ -53,6 +54,7 @@ def run(hip, P, hd, H, Hk, B, reps, split):
     for d in dev.values():
         hip.free(d)
     hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT)
+    hip.set_option(ttship.OPT["ATTN_FUSED"], 0)
     kv = 2 * B * Hk * P * hd * 4 if Hk == H else 2 * B * H * P * hd * 4  # bytes the kernel streams
     return {"hd": hd, "H": H, "Hk": Hk, "B": B, "P": P, "split": split, "us_per_call": round(dt * 1e6, 2),
             "kv_MB": round(kv / 1e6, 2), "GBps_wall": round(kv / dt / 1e9, 1)}
@@ -63,7 +65,7 @@ def main():
     hip = ttship.HipBackend(0)
     for (hd, H, Hk, B) in [(64, 16, 16, 8), (128, 24, 8, 1)]:
         for P in (448, 900, 1309, 2048):
-            for split in (False, True):
+            for split in ("rows", "split", "fused"):
                 print(json.dumps(run(hip, P, hd, H, Hk, B, reps, split)), flush=True)
     hip.close()
 

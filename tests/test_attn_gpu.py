@@ -3,10 +3,13 @@
 mul_mat(kq, V view) -> permute(2, 0, 1, 3) -> cont, with K / V read from cache layouts.
 
 Kernel choice depends on the context length (k_attn.hip): P <= 64 -> k_attn_small (sequential
-sums, bit-exact); P >= TTS_HIP_OPT_ATTN_SPLIT (default 128) -> k_attn_scores + k_attn_pv (split over
+sums, bit-exact); P >= TTS_HIP_OPT_ATTN_FUSED (default off) -> k_attn_fused (one 1024-thread launch);
+otherwise P >= TTS_HIP_OPT_ATTN_SPLIT (default 128) -> k_attn_scores + k_attn_pv (split over
 positions, then over output dims); otherwise k_attn_decode_rows with V prefetched (P <= 512) or
-streamed; hd 128 (Dia / Orpheus head size).  `split` runs every case both ways.  The row kernel reassociates
-the f64 sums (quad / row DPP reductions), so it is held to <= 1 ulp with almost all elements exact.
+streamed; hd 128 (Dia / Orpheus head size).  `mode` runs every case through each kernel.  The row
+kernels reassociate the f64 sums (quad / row DPP reductions), so they are held to <= 1 ulp with almost
+all elements exact; the fused kernel runs the row kernel's sums in its order, so it is bit-identical
+to it.
 """
 import numpy as np
 import pytest
@@ -42,9 +45,9 @@ def build(g, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx):
                                          (37, 128, 16, 16, 2), (430, 128, 8, 8, 1), (1, 64, 4, 4, 1),
                                          (1309, 64, 16, 16, 8), (2100, 128, 24, 24, 1), (128, 64, 16, 16, 3),
                                          (257, 128, 16, 16, 2), (4096, 64, 16, 16, 2)])
-@pytest.mark.parametrize("split", [True, False])
-def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, split):
-    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
+@pytest.mark.parametrize("mode", ["fused", "split", "rows"])
+def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, mode):
+    set_mode(hip, mode)
     rng = np.random.default_rng(P * 7 + hd)
     max_ctx = P + 40
     q = rng.standard_normal((B, H, hd)).astype(np.float32)
@@ -58,9 +61,37 @@ def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, split):
     o2 = build(g2, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx)
     g1.run_hip(hip)
     g2.run_oracle(n_threads=8)
-    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT)
+    set_mode(hip, "default")
     gpu, ref = g1.node_array(o1), g2.node_array(o2)
     if P <= 64:
         assert np.array_equal(gpu, ref)
     else:
         assert ao.ulp_diff(gpu, ref) <= 1 and np.mean(gpu != ref) <= 1e-3
+
+
+def set_mode(hip, mode):
+    hip.set_option(ttship.OPT["ATTN_FUSED"], ttship.ATTN_FUSED_ON if mode == "fused" else 0)
+    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if mode in ("split", "default") else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,hd,B", [(129, 64, 2), (880, 64, 8), (1309, 64, 4), (3000, 64, 1), (700, 128, 2), (2100, 128, 1)])
+def test_fused_attention_bit_identical_to_row_kernel(hip, P, hd, B):
+    """k_attn_fused runs k_attn_decode_rows' f64 sums in the same order: identical bits."""
+    H = 16
+    rng = np.random.default_rng(P + hd)
+    max_ctx = P + 8
+    q = rng.standard_normal((B, H, hd)).astype(np.float32)
+    kc = rng.standard_normal((B, max_ctx, H * hd)).astype(np.float32)
+    vc = rng.standard_normal((B, H * hd, max_ctx)).astype(np.float32)
+    mask = np.zeros(P, np.float32)
+    mask[P // 2] = -np.inf
+    outs = []
+    for mode in ("fused", "rows"):
+        set_mode(hip, mode)
+        g = nd.Graph()
+        o = build(g, q, kc, vc, mask, P, hd, H, H, B, max_ctx)
+        g.run_hip(hip)
+        outs.append(g.node_array(o))
+    set_mode(hip, "default")
+    assert np.array_equal(outs[0], outs[1])

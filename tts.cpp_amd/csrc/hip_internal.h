@@ -55,6 +55,25 @@ __device__ __forceinline__ float cr_divf(float a, float b) { return (float)__ddi
 // full memory round trip per load.  Emits no instruction.
 #define TTS_PIN_LOADS() asm volatile("" ::: "memory")
 
+// Cache policy of the two big decode streams (build-time, for the MALL-residency study):
+// TTS_WLOAD = quantized weight rows (default non-temporal), TTS_KVLOAD = K/V cache rows of decode
+// attention (default plain).
+#ifdef TTS_W_PLAIN
+#define TTS_WLOAD(p) (*(p))
+#else
+#define TTS_WLOAD(p) __builtin_nontemporal_load(p)
+#endif
+__device__ __forceinline__ float4 kv_ld4(const float4 * p) {
+#ifdef TTS_KV_NT
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v v = __builtin_nontemporal_load((const f4v *)p);
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+#define TTS_KVLOAD(p) kv_ld4(p)
+
 // ---- wave64 cross-lane helpers on DPP + readlane (no LDS crossbar, no lgkmcnt waits) ----
 // DPP controls (gfx9): quad_perm [1,0,3,2] = lane^1, [2,3,0,1] = lane^2, row_half_mirror (i <-> 7-i
 // in each 8), row_mirror (i <-> 15-i in each 16), row_shl:n (lane i reads lane i+n in its row).
@@ -231,6 +250,7 @@ struct tts_hip_backend {
     float * attn_buf = nullptr;
     size_t attn_floats = 0;
     int attn_split_minp = 128;
+    int attn_fused_minp = 0;  // the one-launch 1024-thread decode attention from this many keys (0 = off: measured no faster in the Parler step)
     unsigned long long * argmax_keys = nullptr;  // k_greedy_step_wide: per-row keys / arrival counts (self-clearing)
     unsigned * argmax_counts = nullptr;
     // weight_set: Q4_K matrices >= this size use the tile layout + matrix-core GEMV (0 = never)

@@ -232,7 +232,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
         for (int u = 0; u < KS; ++u) {
             const int i = min(i0 + 128 * u + pos0, P - 1);
 #pragma unroll
-            for (int c = 0; c < F; ++c) kv[u][c] = *(const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + c));
+            for (int c = 0; c < F; ++c) kv[u][c] = TTS_KVLOAD((const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + c)));
         }
     };
     load_k(0);
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
             const char * vrow = vbase + (int64_t)(ps * 32 + wave * 4 + r) * vnb1;
 #pragma unroll
             for (int u = 0; u < ATTN_UV; ++u) {
-                if (VVEC) vv4[VVEC ? ps * ATTN_UV + u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(64 * u + 4 * t, ilast));
+                if (VVEC) vv4[VVEC ? ps * ATTN_UV + u : 0] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(64 * u + 4 * t, ilast)));
                 else vv1[VVEC ? 0 : ps * ATTN_UV + u] = *(const float *)(vrow + (int64_t)min(16 * u + t, P - 1) * vnb0);
             }
         }
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
             } else {
 #pragma unroll
                 for (int u = 0; u < ATTN_UV; ++u) {
-                    if (VVEC) w4[VVEC ? u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast));
+                    if (VVEC) w4[VVEC ? u : 0] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast)));
                     else w1[VVEC ? 0 : u] = *(const float *)(vrow + (int64_t)min(k0 + 16 * u + t, P - 1) * vnb0);
                 }
                 TTS_PIN_LOADS();
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float 
     for (int u = 0; u < KS; ++u) {
         const int i = min(i0 + 128 * u, P - 1);
 #pragma unroll
-        for (int f = 0; f < F; ++f) kv[u][f] = *(const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + f));
+        for (int f = 0; f < F; ++f) kv[u][f] = TTS_KVLOAD((const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + f)));
     }
     float qv[F][4];
 #pragma unroll
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float 
     auto load_v = [&](int k0) {
 #pragma unroll
         for (int u = 0; u < UV; ++u) {
-            if (VVEC) w4[VVEC ? u : 0] = *(const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast));
+            if (VVEC) w4[VVEC ? u : 0] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast)));
             else w1[VVEC ? 0 : u] = *(const float *)(vrow + (int64_t)min(k0 + 16 * u + t, P - 1) * vnb0);
         }
     };
@@ -543,6 +543,180 @@ __global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float 
 }
 
 // ------------------------------------------------------------------------------------------
+// Fused decode attention for long contexts: ONE launch per attention, one 1024-thread workgroup per
+// (head, query, sequence).  The split pair above pays two launch ramps and an L2 round trip of the
+// scores; here every byte of K and V is requested as early as registers allow:
+//   A: 256 quads x KS positions per group, two groups in flight (the second requested before the
+//      first is summed); kq[i] = f64 sum of f32 products over the quad's dims, finished by DPP;
+//   V: the first UVC 16-B chunks of every lane's V row slice are requested as soon as A has finished
+//      with its registers -- the softmax runs while they are in flight;
+//   B: soft_max_ext over the P scores in LDS (the k_attn_decode_rows arithmetic);
+//   C: 16 lanes per output dim, 64 dims per pass (DPR passes), lane t holds positions 4t + 64u in
+//      ascending u, f64 accumulation and the DPP row reduction of k_attn_decode_rows: the same sums
+//      in the same order, so the output is bit-identical to that kernel.
+constexpr int FUSED_THREADS = 1024;
+template <int DPR, int UVC>
+__global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
+    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    __shared__ float s_wf[FUSED_THREADS / 64];
+    __shared__ double s_wd[FUSED_THREADS / 64];
+    constexpr int NW = FUSED_THREADS / 64;
+    constexpr int F = 4 * DPR;   // float4 per lane per key position
+    constexpr int KS = 3 - DPR;  // positions per quad per group (2 for hd 64, 1 for hd 128)
+    constexpr int GP = 256 * KS; // positions per group
+    const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane >> 4, t = lane & 15, qd = lane & 3;
+    const int P = a.P;
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const int64_t knb1 = a.k.nb[1], vnb1 = a.v.nb[1];
+    const int pos0 = wave * 16 + (lane >> 2);
+
+    float4 kv[2][KS][F];
+    auto load_k = [&](auto BS, int i0) {
+        constexpr int bs = decltype(BS)::value;
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            const int i = min(i0 + 256 * u + pos0, P - 1);
+#pragma unroll
+            for (int c = 0; c < F; ++c) kv[bs][u][c] = TTS_KVLOAD((const float4 *)(kbase + (int64_t)i * knb1 + 16 * (F * qd + c)));
+        }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    load_k(I0{}, 0);
+    float qv[F][4];
+#pragma unroll
+    for (int c = 0; c < F; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) qv[c][e] = ((const float *)qbase)[16 * DPR * qd + 4 * c + e];
+    load_k(I1{}, min(GP, ((P - 1) / GP) * GP));
+    TTS_PIN_LOADS();
+
+    auto score = [&](auto BS, int i0) {
+        constexpr int bs = decltype(BS)::value;
+#pragma unroll
+        for (int u = 0; u < KS; ++u) {
+            double s = 0.0;
+#pragma unroll
+            for (int c = 0; c < F; ++c) {
+                s += (double)__fmul_rn(kv[bs][u][c].x, qv[c][0]);
+                s += (double)__fmul_rn(kv[bs][u][c].y, qv[c][1]);
+                s += (double)__fmul_rn(kv[bs][u][c].z, qv[c][2]);
+                s += (double)__fmul_rn(kv[bs][u][c].w, qv[c][3]);
+            }
+            s += dpp_f64<DPP_XOR1>(s);
+            s += dpp_f64<DPP_XOR2>(s);
+            const int i = i0 + 256 * u + pos0;
+            if (qd == 0 && i < P) s_p[i] = (float)s;
+        }
+    };
+    // ---- A: groups g = 0, 1, 2, ...: group g + 1 is in flight while group g is summed ----
+    for (int i0 = 0; i0 < P; i0 += 2 * GP) {
+        score(I0{}, i0);
+        if (i0 + 2 * GP < P) {
+            load_k(I0{}, i0 + 2 * GP);
+            TTS_PIN_LOADS();
+        }
+        if (i0 + GP >= P) break;
+        score(I1{}, i0 + GP);
+        if (i0 + 3 * GP < P) {
+            load_k(I1{}, i0 + 3 * GP);
+            TTS_PIN_LOADS();
+        }
+    }
+
+    // ---- V: the first UVC chunks of pass 0 are requested before the softmax ----
+    const int ilast = ((P - 1) >> 2) << 2;
+    float4 w4[UVC];
+    auto load_v = [&](int ps, int k0) {
+        const char * vrow = vbase + (int64_t)min(ps * 64 + wave * 4 + r, a.hd - 1) * vnb1;
+#pragma unroll
+        for (int u = 0; u < UVC; ++u) w4[u] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast)));
+    };
+    load_v(0, 0);
+    TTS_PIN_LOADS();
+    __syncthreads();
+
+    // ---- B: soft_max_ext ----
+    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    float mx = -INFINITY;
+    for (int i = tid; i < P; i += FUSED_THREADS) {
+        float w = __fmul_rn(s_p[i], a.scale);
+        if (mrow) w = __fadd_rn(w, __fmul_rn(1.0f, mrow[i]));
+        s_p[i] = w;
+        mx = fmaxf(mx, w);
+    }
+    mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+    mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+    mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+    if (lane == 0) s_wf[wave] = mx;
+    __syncthreads();
+    mx = s_wf[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, s_wf[w]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += FUSED_THREADS) {
+        const float e = cr_expf(__fsub_rn(s_p[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_f64(sum);
+    if (lane == 0) s_wd[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += s_wd[w];
+    const float inv = (float)(1.0 / sum);
+    const int P64 = (P + 63) & ~63;
+    for (int i = tid; i < P64; i += FUSED_THREADS) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    __syncthreads();
+
+    // ---- C: out[d] = sum_i (f32)(p[i] * V[d,i]) in f64 ----
+    float * orow = a.out + (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    float * orow2 = a.out2 ? a.out2 + (((int64_t)b * a.n + tq) * a.H + h) * a.hd : nullptr;
+    constexpr int kstep = 64 * UVC;
+#pragma unroll
+    for (int ps = 0; ps < DPR; ++ps) {
+        const int d = ps * 64 + wave * 4 + r;
+        double acc = 0.0;
+        for (int k0 = 0; k0 < P; k0 += kstep) {
+            if (ps > 0 || k0 > 0) {
+                load_v(ps, k0);
+                TTS_PIN_LOADS();
+            }
+#pragma unroll
+            for (int u = 0; u < UVC; ++u) {
+                const int i = k0 + 64 * u + 4 * t;
+                const float4 pp = *(const float4 *)(s_p + min(i, P64 - 4));
+                const float4 vq = w4[u];
+                acc += i + 0 < P ? (double)__fmul_rn(pp.x, vq.x) : 0.0;
+                acc += i + 1 < P ? (double)__fmul_rn(pp.y, vq.y) : 0.0;
+                acc += i + 2 < P ? (double)__fmul_rn(pp.z, vq.z) : 0.0;
+                acc += i + 3 < P ? (double)__fmul_rn(pp.w, vq.w) : 0.0;
+            }
+        }
+        acc += dpp_f64<DPP_XOR1>(acc);
+        acc += dpp_f64<DPP_XOR2>(acc);
+        acc += dpp_f64<DPP_HALF_MIRROR>(acc);
+        acc += dpp_f64<DPP_MIRROR>(acc);
+        if (t == 0 && d < a.hd) {
+            orow[d] = (float)acc;
+            if (orow2) orow2[d] = (float)acc;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Short contexts (P <= 64: Parler's cross-attention over the T5 prompt encoding, n_enc = 3; the
 // first decode steps): one wave per (head, query, sequence), lane = key position, every sum in the
 // oracle's sequential order -- the q.K dot over d, the soft_max denominator over positions (lane 0
@@ -564,7 +738,7 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
     const int p = min(lane, P - 1);
     float4 kr[F];
 #pragma unroll
-    for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+    for (int c = 0; c < F; ++c) kr[c] = TTS_KVLOAD((const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c));
     float qv[HD];
 #pragma unroll
     for (int d = 0; d < HD; ++d) qv[d] = *(const float *)(qbase + (int64_t)d * a.q.nb[0]);
@@ -691,6 +865,15 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
         const dim3 grid((unsigned)H, (unsigned)n, (unsigned)B);
         if (hd == 64) hipLaunchKernelGGL(k_attn_small<64>, grid, dim3(64), 0, be->stream, a);
         else hipLaunchKernelGGL(k_attn_small<128>, grid, dim3(64), 0, be->stream, a);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    const bool vvec_all = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
+                          (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
+    if (krows && vvec_all && be->attn_fused_minp > 0 && P >= be->attn_fused_minp && P <= ATTN_MAXP) {
+        const dim3 grid((unsigned)H, (unsigned)n, (unsigned)B);
+        if (hd == 64) hipLaunchKernelGGL((k_attn_fused<1, 8>), grid, dim3(FUSED_THREADS), 0, be->stream, a);
+        else hipLaunchKernelGGL((k_attn_fused<2, 8>), grid, dim3(FUSED_THREADS), 0, be->stream, a);
         TTS_HIP_CHECK(hipGetLastError());
         return;
     }

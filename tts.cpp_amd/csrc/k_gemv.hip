@@ -506,8 +506,8 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
 #pragma unroll
         for (int u = 0; u < NBMAX; ++u) {  // unconditional (clamped) so all loads issue before use
             const int64_t bo = (int64_t)min(b0 + u, nb - 1) * 144;
-            hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
-            q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
+            hdr[u] = TTS_WLOAD((const u32x4 *)(wr + bo));
+            q[u] = TTS_WLOAD((const u32x4 *)(wr + bo + 16 + l * 16));
         }
         TTS_PIN_LOADS();
     };
@@ -645,8 +645,8 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) 
         const int mat = mat_of(flat);
         const uint8_t * bp = j.W[mat] + (flat - (int64_t)mat * j.N) * j.w_row_bytes + (int64_t)b * 144;
         if (cg < NCG) {
-            hdr = __builtin_nontemporal_load((const u32x4 *)bp);
-            qw = __builtin_nontemporal_load((const u32x4 *)(bp + 16 + l * 16));
+            hdr = TTS_WLOAD((const u32x4 *)bp);
+            qw = TTS_WLOAD((const u32x4 *)(bp + 16 + l * 16));
         }
         TTS_PIN_LOADS();
         TTS_TS(j, 1);
@@ -802,9 +802,9 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
                 qa[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16);
                 qb[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16);
             } else {
-                hd[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
-                qa[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-                qb[bs][u] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+                hd[bs][u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+                qa[bs][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+                qb[bs][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
             }
         }
         TTS_PIN_LOADS();
@@ -959,8 +959,8 @@ __global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
         for (int k = 0; k < UPW; ++k) {  // unconditional (clamped): every load issues before any use
             const int u = min(wave + k * nw, nu - 1);
             const uint8_t * bp = wt + (int64_t)(u >> 1) * 576;
-            hd[k] = __builtin_nontemporal_load((const u32x4 *)(bp + ri * 16));
-            qv[k] = __builtin_nontemporal_load((const u32x4 *)(bp + 64 + ((kg * 2 + (u & 1)) * 4 + ri) * 16));
+            hd[k] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+            qv[k] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + (u & 1)) * 4 + ri) * 16));
         }
         TTS_PIN_LOADS();
     };
@@ -1106,8 +1106,8 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int64_t bo = (int64_t)min(u, nb - 1) * 144;
-            hdr[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo));
-            q[u] = __builtin_nontemporal_load((const u32x4 *)(wr + bo + 16 + l * 16));
+            hdr[u] = TTS_WLOAD((const u32x4 *)(wr + bo));
+            q[u] = TTS_WLOAD((const u32x4 *)(wr + bo + 16 + l * 16));
         }
         if (wave == NW - 1) {
 #pragma unroll
@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(256) void k_gemv_float(GemvJob j) {
         const float * w = (const float *)(j.W[mat] + row * j.w_row_bytes);
         const float * x = j.x;
         for (int64_t k = lane * 4; k < K; k += 256) {
-            const f32x4 wv = __builtin_nontemporal_load((const f32x4 *)(w + k));
+            const f32x4 wv = TTS_WLOAD((const f32x4 *)(w + k));
 #pragma unroll
             for (int m = 0; m < MC; ++m) {
                 if (m >= M) break;

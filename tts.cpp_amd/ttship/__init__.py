@@ -26,8 +26,9 @@ FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
+ATTN_FUSED_ON = 128  # P >= 128 keys -> one 1024-thread launch (k_attn_fused; backend default 0 = off)
 
 TYPE_SIZE = {F32: 4, F16: 2, Q4_K: 144, Q8_0: 34, I32: 4}
 BLCK_SIZE = {F32: 1, F16: 1, Q4_K: 256, Q8_0: 32, I32: 1}
@@ -231,9 +232,13 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise RuntimeError(f"{LIB_PATH} missing: run `make -j8` (or __graft_entry__.build())")
-    L = ctypes.CDLL(str(LIB_PATH))
+    path = LIB_PATH
+    variant = os.environ.get("TTS_HIP_LIB_VARIANT")  # build-variant studies (scripts/): lib/<variant>/libtts_hip.so
+    if variant:
+        path = PKG_ROOT / "lib" / variant / "libtts_hip.so"
+    if not path.exists():
+        raise RuntimeError(f"{path} missing: run `make -j8` (or __graft_entry__.build())")
+    L = ctypes.CDLL(str(path))
     vp, i32, i64, u64, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_size_t
     sig = {
         "tts_type_size": (sz, [ctypes.c_int]),
