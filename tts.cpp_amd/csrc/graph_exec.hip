@@ -474,12 +474,51 @@ struct Planner {
         return false;
     }
 
+    // SwiGLU MLP (Orpheus model.cpp:296-300): MUL(UNARY SILU(MUL_MAT(gate, x)), MUL_MAT(up, x)) with
+    // tile-layout Q4_K gate / up: one matrix-core GEMV launch over both matrices whose epilogue
+    // writes silu(gate) * up to the MUL's output; gate, silu(gate) and up are never stored.  Every
+    // node between the gate product and the MUL must belong to the pattern (or be a view), so the
+    // MUL's output can be written at the gate product's position.
+    bool try_swiglu(int i) {
+        const tts_tensor * G = nodes[i];
+        const tts_tensor * a0 = G->src[0];
+        const tts_tensor * x = G->src[1];
+        if (a0->type != TTS_TYPE_Q4_K || !(a0->flags & TTS_FLAG_TILED) || a0->ne[1] % 16) return false;
+        const tts_tensor * S = sole_consumer(G);
+        if (!S || S->op != TTS_OP_UNARY || S->op_params[0] != TTS_UNARY_SILU || S->src[0] != G) return false;
+        const tts_tensor * E = sole_consumer(S);
+        if (!E || E->op != TTS_OP_MUL || E->src[0] != S) return false;
+        const tts_tensor * U = E->src[1];
+        if (!U || U->op != TTS_OP_MUL_MAT || U->src[1] != x || uses[U] != 1 || !is_gemv(U)) return false;
+        const tts_tensor * a = U->src[0];
+        if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->ne[1] != a0->ne[1] || a->nb[1] != a0->nb[1] ||
+            ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED)))
+            return false;
+        if (E->type != TTS_TYPE_F32 || !contiguous(E) || !contiguous(G) || !contiguous(S) || !contiguous(U)) return false;
+        for (int d = 0; d < 4; ++d)
+            if (E->ne[d] != G->ne[d] || U->ne[d] != G->ne[d] || S->ne[d] != G->ne[d]) return false;
+        const int iS = index[S], iU = index[U], iE = index[E];
+        if (iS <= i || iU <= i || iE <= iS || iE <= iU || act[iS] || act[iU] || act[iE]) return false;
+        for (int k = i + 1; k < iE; ++k)
+            if (k != iS && k != iU && !(is_view(nodes[k]->op) && act[k] == 0)) return false;
+        Item it;
+        it.kind = Item::GEMV;
+        it.epi = EPI_SWIGLU;
+        it.mms = {G, U};
+        const GemvTarget t{(float *)E->data, (int64_t)(E->nb[1] / 4), 1};
+        it.tgt = {t, t};
+        act[iS] = act[iU] = act[iE] = -1;
+        act[i] = add_item(std::move(it));
+        return true;
+    }
+
     void try_gemv(int i) {
         const tts_tensor * mm0 = nodes[i];
         if (!is_gemv(mm0)) return;
         const tts_tensor * a0 = mm0->src[0];
         const tts_tensor * x = mm0->src[1];
         const int64_t M = x->ne[1] * x->ne[2] * x->ne[3];
+        if ((mask & TTS_FUSE_EPI) && try_swiglu(i)) return;
         Item it;
         it.kind = Item::GEMV;
         std::vector<int> skips;

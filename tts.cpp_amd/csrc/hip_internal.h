@@ -49,6 +49,8 @@ __device__ __forceinline__ float cr_tanhf(float x) { return (float)tanh((double)
 // result rounded to f32 is the correctly rounded f32 value (53 >= 2*24 + 2).
 __device__ __forceinline__ float cr_sqrtf(float x) { return (float)__dsqrt_rn((double)x); }
 __device__ __forceinline__ float cr_divf(float a, float b) { return (float)__ddiv_rn((double)a, (double)b); }
+// ggml's silu (ggml_vec_silu_f32 / ggml_silu_f32: x / (1 + exp(-x))), correctly rounded pieces
+__device__ __forceinline__ float dev_silu(float x) { return cr_divf(x, __fadd_rn(1.0f, cr_expf(-x))); }
 
 // Compiler memory barrier placed after a batch of independent loads: keeps the compiler from
 // sinking a load into the (guarded) block that uses it, which would serialize the batch into one
@@ -176,7 +178,9 @@ struct ActQuant {
 // One GEMV launch: up to GEMV_MAX_MATS weight matrices of identical type/shape sharing one
 // activation (q/k/v; the 9 codebook heads), y(row n, column m) = Y[i][m*ycs + n*yrs], with an
 // optional fused epilogue (GELU table, or + residual(row n, column m) = res[m*rcs + n]).
-enum { EPI_NONE = 0, EPI_GELU = 1, EPI_ADD = 2 };
+// EPI_SWIGLU (matrix-core Q4_K kernel only, nmat == 2: gate, up): Y[0] = silu(gate) * up, the
+// UNARY SILU and MUL of the SwiGLU MLP (Orpheus model.cpp:296-300); gate / up are never stored.
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_ADD = 2, EPI_SWIGLU = 3 };
 constexpr int GEMV_MAX_MATS = 16;
 struct GemvJob {
     int wtype = 0;

@@ -769,12 +769,24 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
     constexpr int CH = 4;
     const int nch = (nb + CH - 1) / CH;
-    const int64_t NR = (int64_t)j.nmat * j.N;
+    // EPI_SWIGLU: a wave runs tile t of gate, then tile t of up (units = tile pairs), and keeps the
+    // gate results in registers until the up tile is done
+    // When every pair fits one wave slot of the first half of the workgroups' waves (xpair), wave w
+    // of the first half runs gate tile t and wave w + nw/2 up tile t instead, and the gate results
+    // cross over through LDS after one barrier.
+    const bool swiglu = j.epi == EPI_SWIGLU;
+    const int64_t NR = swiglu ? j.N : (int64_t)j.nmat * j.N;
     const int64_t T = (NR + 15) / 16;
+    const int half = nw >> 1;
+    const bool xpair = swiglu && T <= (int64_t)gridDim.x * half;
+    const int per = swiglu && !xpair ? 2 : 1;
+    const int xmat = xpair && wave >= half ? 1 : 0;  // xpair: this wave's matrix (0 gate, 1 up)
     // tile t0 + k * tstride; consecutive tiles go to different workgroups, so a small matrix still
     // spreads over every CU
-    const int64_t t0 = (int64_t)wave * gridDim.x + blockIdx.x, tstride = (int64_t)gridDim.x * nw;
-    const int64_t nmine = (t0 < T && !(j.dbg & 1)) ? ((T - 1 - t0) / tstride + 1) * nch : 0;
+    const int64_t t0 = (int64_t)(wave - xmat * half) * gridDim.x + blockIdx.x;
+    const int64_t tstride = xpair ? T : (int64_t)gridDim.x * nw;
+    const int64_t nmine = (t0 < T && !(j.dbg & 1)) ? ((T - 1 - t0) / tstride + 1) * nch * per : 0;
+    float * xg = (float *)(smem + al16((size_t)nslot * (2 * QK_K + 32 + 4)));  // xpair: [half][64 lanes][4]
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
         while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
@@ -786,12 +798,13 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     u32x4 hd[2][CH], qa[2][CH], qb[2][CH];
     auto load = [&](auto BS, int64_t i) {
         constexpr int bs = decltype(BS)::value;
-        const int64_t t = t0 + (i / nch) * tstride;
+        const int64_t ti = i / nch;
+        const int64_t t = t0 + (ti / per) * tstride;
         const int c = (int)(i % nch);
         int64_t flat = t * 16 + r;
         flat = flat < NR ? flat : NR - 1;
-        const int mat = mat_of(flat);
-        const int64_t row = flat - (int64_t)mat * j.N;
+        const int mat = xpair ? xmat : swiglu ? (int)(ti & 1) : mat_of(flat);
+        const int64_t row = swiglu ? flat : flat - (int64_t)mat * j.N;
         const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
         const int ri = (int)(row & 3);
 #pragma unroll
@@ -810,10 +823,11 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         TTS_PIN_LOADS();
     };
 
-    float sums[8][4], sumf[4];
+    float sums[8][4], sumf[4], gate[4];
     auto compute = [&](auto BS, int64_t i) {
         constexpr int bs = decltype(BS)::value;
-        const int64_t t = t0 + (i / nch) * tstride;
+        const int64_t ti = i / nch;
+        const int64_t t = t0 + (ti / per) * tstride;
         const int c = (int)(i % nch);
         if (c == 0) {
 #pragma unroll
@@ -880,7 +894,12 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 #pragma unroll
                 for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[l][q]);
                 const int64_t flat = t * 16 + 4 * kg + q;
-                if (r < M && flat < NR) {
+                if (xpair) {
+                    gate[q] = tot;  // gate or up row: crossed over after the loop
+                } else if (swiglu) {
+                    if ((ti & 1) == 0) gate[q] = tot;  // gate row; the up row follows in this wave
+                    else if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gate[q]), tot);
+                } else if (r < M && flat < NR) {
                     const int mat = mat_of(flat);
                     gemv_store<8>(j, mat, flat - (int64_t)mat * j.N, r, tot);
                 }
@@ -905,6 +924,20 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         if (i + 1 >= nmine) break;
         load(I0{}, min(i + 2, nmine - 1));
         compute(I1{}, i + 1);
+    }
+    if (xpair) {  // one tile per wave at most: out = silu(gate) * up
+        if (nmine > 0 && xmat == 0)
+            *(float4 *)(xg + ((size_t)wave * 64 + lane) * 4) = make_float4(gate[0], gate[1], gate[2], gate[3]);
+        __syncthreads();
+        if (nmine > 0 && xmat == 1) {
+            const float4 g4 = *(const float4 *)(xg + ((size_t)(wave - half) * 64 + lane) * 4);
+            const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t flat = t0 * 16 + 4 * kg + q;
+                if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), gate[q]);
+            }
+        }
     }
     TTS_TS(j, 5);
 }
@@ -1514,9 +1547,10 @@ static size_t q80_lds(int MC, int64_t K, int RW) {
 }
 
 // ---- MFMA path (k_gemv_q4K_mf) ----
-static size_t q4k_mf_lds(int64_t M, int64_t K) { return (size_t)(M * (K / QK_K) + 1) * (2 * QK_K + 32 + 4); }
+// + the SwiGLU cross-over buffer (4 waves x 64 lanes x 4 floats)
+static size_t q4k_mf_lds(int64_t M, int64_t K) { return ((size_t)(M * (K / QK_K) + 1) * (2 * QK_K + 32 + 4) + 15) / 16 * 16 + 4096; }
 static int64_t q4k_mf_max_cols(int64_t K) {
-    const int64_t c = ((int64_t)(160 * 1024) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
+    const int64_t c = ((int64_t)(160 * 1024 - 4096 - 16) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
     return c >= 16 ? 16 : c >= 8 ? 8 : c;
 }
 static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
@@ -1567,7 +1601,7 @@ static size_t q4k_ks_lds(int64_t M, int64_t nb) {
     return (((size_t)(M * nb + 1) * (2 * QK_K + 32 + 4) + 15) & ~(size_t)15) + (size_t)nb * (1024 + 128) * 4;
 }
 static bool q4k_ks_eligible(const tts_hip_backend * be, const GemvJob & j) {
-    if (be->gemv_ks_tiles <= 0 || j.wtype != TTS_TYPE_Q4_K || !j.tiled || j.M < 1 || j.M > 8) return false;
+    if (be->gemv_ks_tiles <= 0 || j.wtype != TTS_TYPE_Q4_K || !j.tiled || j.M < 1 || j.M > 8 || j.epi == EPI_SWIGLU) return false;
     const int64_t nb = j.K / QK_K;
     if (nb < 1 || nb > 16 || j.N % 16) return false;
     if (j.pro == PRO_LN && j.K > 4 * 1024) return false;  // the LN prologue holds <= 16 chunks per lane
@@ -1668,6 +1702,10 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
         launch_q4k_mf(be, job);
         TTS_HIP_CHECK(hipGetLastError());
         return;
+    }
+    if (job.epi == EPI_SWIGLU) {  // the planner forms these for tile-layout Q4_K pairs only
+        fprintf(stderr, "tts_hip: SwiGLU GEMV epilogue needs the matrix-core Q4_K kernel\n");
+        abort();
     }
     const int64_t cmax = job.wtype == TTS_TYPE_Q4_K ? q4k_max_cols(K) : 8;
     for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {

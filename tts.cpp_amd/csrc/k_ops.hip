@@ -159,7 +159,7 @@ __device__ __forceinline__ float unary_apply(const UnaryParams & P, float x) {
             const uint16_t h = __half_as_ushort(__float2half_rn(x));
             return __half2float(__ushort_as_half(P.gelu_table[h]));
         }
-        case TTS_UNARY_SILU: return cr_divf(x, __fadd_rn(1.0f, cr_expf(-x)));
+        case TTS_UNARY_SILU: return dev_silu(x);
         case TTS_UNARY_EXP: return cr_expf(x);
     }
     return x;
