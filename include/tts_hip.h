@@ -266,8 +266,10 @@ enum tts_fuse_bits {
     TTS_FUSE_CONV = 512,  /* conv_1d's IM2COL -> MUL_MAT (+ bias ADD, + residual ADD) -> one implicit-GEMM kernel */
     TTS_FUSE_ADAIN = 1024, /* Kokoro AdaIN1d (norm, transposes, affine) + snake_1d -> one pass per channel row */
     TTS_FUSE_XATTN = 2048, /* short-context attention (P <= 64) folded into the Q4_K GEMV producing its query */
-    TTS_FUSE_MCPY = 4096   /* CPYs of one source into several views (Orpheus' repeat-interleaved KV store) -> one pass;
+    TTS_FUSE_MCPY = 4096,  /* CPYs of one source into several views (Orpheus' repeat-interleaved KV store) -> one pass;
                               Dia's repeat_interleave_dim1 view/cont/repeat/concat chain -> one pass */
+    TTS_FUSE_CONTREAD = 8192 /* CONT of a contiguous tensor whose only reader is the next node (Orpheus' cont before
+                                rope): that node reads the source and the copy is never made */
 };
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for

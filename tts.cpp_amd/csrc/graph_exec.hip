@@ -103,7 +103,9 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT, NODE } kind;
+    // NODE: a node run with a rewritten source (TTS_FUSE_CONTREAD)
+    tts_tensor node{};
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -310,6 +312,7 @@ struct Planner {
                 default: break;
             }
         }
+        if (mask & TTS_FUSE_CONTREAD) skip_cont_reads();
         if (mask & TTS_FUSE_LN) fuse_ln_into_gemv();
         link_attn_shadow();
         if (mask & TTS_FUSE_XATTN) fuse_xattn();
@@ -369,6 +372,36 @@ struct Planner {
             if (!clear) continue;
             G.xattn = (int)ai;
             A.fused = true;
+        }
+    }
+
+    // CONT C of a contiguous tensor of the same type (through views) whose only reader is the next
+    // node R (an elementwise op or rope, still launched on its own): R reads C's source instead, and
+    // the copy is skipped.  R's output must not overlap that source (the copy would have separated
+    // them) unless it coincides with it exactly.
+    void skip_cont_reads() {
+        for (int i = 0; i < n; ++i) {
+            const tts_tensor * C = nodes[i];
+            if (act[i] != 0 || C->op != TTS_OP_CONT || !C->src[0]) continue;
+            const tts_tensor * s = C->src[0];
+            if (s->type != C->type || !contiguous(s) || !contiguous(C) || uses[C] != 1) continue;
+            const int r = next_real(i);
+            if (r < 0 || act[r] != 0) continue;
+            const tts_tensor * R = nodes[r];
+            if (R->src[0] != C || (R->op != TTS_OP_ROPE && R->op != TTS_OP_UNARY)) continue;
+            bool other = false;
+            for (int si = 1; si < TTS_MAX_SRC; ++si) other |= R->src[si] == C;
+            // in place is fine when R's output coincides exactly with the source (rope and unary ops read
+            // every element they write before writing it, in the same thread)
+            bool same = R->data == s->data && R->type == s->type;
+            for (int d = 0; d < 4 && same; ++d) same = R->ne[d] == s->ne[d] && R->nb[d] == s->nb[d];
+            if (other || (overlap(R, s) && !same)) continue;
+            Item it;
+            it.kind = Item::NODE;
+            it.node = *R;
+            it.node.src[0] = const_cast<tts_tensor *>(s);
+            act[i] = -1;
+            act[r] = add_item(std::move(it));
         }
     }
 
@@ -1693,6 +1726,8 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
         case Item::RINT:
             launch_repeat_interleave1(be, it.dst, it.x, it.rint);
             return 0;
+        case Item::NODE:
+            return run_node(be, &it.node);
         case Item::LSTM:
             if (it.lkind & 4)
                 for (int g = 0; g < 4; ++g)
@@ -1837,7 +1872,7 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     pl.conv_stage_cap = (size_t)8 << 20;
     if (mask) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
-    for (int k = 0; k < 16; ++k) counts[k] = 0;
+    for (int k = 0; k < 16; ++k) counts[k] = 0;  // (NODE items count under counts[10])
     for (const Item & it : pl.items) {
         counts[(int)it.kind]++;
         if (it.xattn >= 0) counts[14]++;

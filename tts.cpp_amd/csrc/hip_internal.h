@@ -300,7 +300,7 @@ struct tts_hip_backend {
     double * conv_part = nullptr;
     size_t conv_part_doubles = 0;
     int conv_split = 1;  // TTS_HIP_OPT_CONV_SPLIT: 1 = split short convolutions, 0 = never
-    int fusion = 0x1FFF;  // bitmask of TTS_FUSE_* patterns (all on)
+    int fusion = 0x3FFF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};
     int64_t gemv_launches[TTS_TYPE_COUNT] = {0};

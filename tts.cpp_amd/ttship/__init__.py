@@ -21,7 +21,7 @@ OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "
        "PAD", "LEAKY_RELU", "UNARY", "CUMSUM", "MOD", "ROUND", "STFT", "ISTFT", "MAP_CUSTOM3", "MAP_CUSTOM2"]
 OP = {n: i for i, n in enumerate(OPS)}
 # TTS_FUSE_* bits (include/tts_hip.h); FUSE_ALL is the backend default
-FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048, "MCPY": 4096}
+FUSE = {"LN": 1, "GROUP": 2, "KV": 4, "EPI": 8, "HEADS": 16, "ATTN": 32, "LSTM": 64, "SNAKE": 128, "EMBED": 256, "CONV": 512, "ADAIN": 1024, "XATTN": 2048, "MCPY": 4096, "CONTREAD": 8192}
 FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
