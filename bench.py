@@ -366,6 +366,7 @@ def main():
     ap.add_argument("--kv-prefetch-blocks", type=int, default=None)
     ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
     ap.add_argument("--tile-bytes", type=int, default=None, help="TTS_HIP_OPT_Q4K_TILE_BYTES: Q4_K matrices of >= value bytes use the 4-row tile layout (matrix-core GEMVs)")
+    ap.add_argument("--attn-pv16", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV16: split P.V requests the whole V slice (P <= 1024) before the softmax (0 = two batches)")
     ap.add_argument("--attn-fused", type=int, default=None, help="TTS_HIP_OPT_ATTN_FUSED: decode attention over >= value keys as one 1024-thread launch (0 = off)")
     ap.add_argument("--gemv-ks", type=int, default=None, help="TTS_HIP_OPT_GEMV_KS: max 16-row tiles of a tile-layout GEMV on the K-split matrix-core kernel (0 = never)")
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
@@ -405,6 +406,8 @@ def main():
             rb.set_option(ttship.OPT["GEMV_KS"], args.gemv_ks)
         if args.attn_fused is not None:
             rb.set_option(ttship.OPT["ATTN_FUSED"], args.attn_fused)
+        if args.attn_pv16 is not None:
+            rb.set_option(ttship.OPT["ATTN_PV16"], args.attn_pv16)
         if args.kv_prefetch_blocks is not None:
             rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
         return rb

@@ -257,6 +257,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_ATTN_FUSED = 14,  /* decode attention over P >= value keys (hd 64 / 128, 16-B K and V rows) runs as
                                      ONE 1024-thread launch per attention (k_attn_fused; default 0 = off: the split pair,
                                      TTS_HIP_OPT_ATTN_SPLIT; tests and studies use 128) */
+    TTS_HIP_OPT_ATTN_PV16 = 15,   /* 1: the split P.V kernel requests a lane's whole V slice (16 x 16 B) before the
+                                     softmax when P <= 1024; 0 (default): two 8-chunk batches (measured equal) */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

@@ -30,9 +30,17 @@ def per_kernel(d, counter, pat, last):
                 rows.append(r)
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     rows = rows[-last:]
+    # key each launch by its position within the decode step (the period of the launch sequence), so
+    # different matrices with one template / grid (Orpheus q / o / down) stay apart
+    sig = [(r["Kernel_Name"], r["Grid_Size"]) for r in rows]
+    period = len(sig)
+    for p in range(1, len(sig) // 2 + 1):
+        if all(sig[i] == sig[i - p] for i in range(p, len(sig))):
+            period = p
+            break
     shapes = {}
-    for r in rows:
-        k = f'{r["Kernel_Name"].split("<")[-1].split(">")[0]} grid {r["Grid_Size"]}'
+    for i, r in enumerate(rows):
+        k = f'step pos {i % period:03d}: {r["Kernel_Name"].split("<")[-1].split(">")[0]} grid {r["Grid_Size"]}'
         shapes.setdefault(k, []).append(float(r["Counter_Value"]))
     return sum(float(r["Counter_Value"]) for r in rows), len(rows), shapes
 
@@ -62,7 +70,9 @@ def main():
            "write_bytes_per_launch": write, "hbm_bytes_per_launch": round(fetch + write, 1),
            "per_shape_hbm_bytes": {k: round(2048.0 * sum(v) / len(v) + 1024.0 * sum(ws.get(k, [0])) / max(len(ws.get(k, [])), 1), 1)
                                    for k, v in fs.items()},
-           "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane streaming reads); WRITE_SIZE KiB x1024",
+           "largest_launch_fetch_bytes_raw": max(1024.0 * sum(v) / len(v) for v in fs.values()),
+           "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count of 16B/lane streaming reads); WRITE_SIZE KiB x1024; "
+                         "check it on a launch of known weight bytes (largest_launch_fetch_bytes_raw: the Orpheus head, 271 MB)",
            "launches_kept": last, "command": cmd}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))

@@ -388,6 +388,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
             return 0;
         case TTS_HIP_OPT_ATTN_SPLIT: be->attn_split_minp = value; return 0;
         case TTS_HIP_OPT_ATTN_FUSED: be->attn_fused_minp = value; return 0;
+        case TTS_HIP_OPT_ATTN_PV16: be->attn_pv_uv16 = value != 0; return 0;
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;

@@ -892,7 +892,9 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
                               (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
             const dim3 g2((unsigned)(hd / 16), (unsigned)H, (unsigned)(n * B));
-            if (vvec) hipLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
+            if (vvec && P <= 1024 && be->attn_pv_uv16) hipLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            else if (vvec) hipLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
             else hipLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
             TTS_HIP_CHECK(hipGetLastError());
             return;
