@@ -106,6 +106,8 @@ struct Item {
     enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT, NODE } kind;
     // NODE: a node run with a rewritten source (TTS_FUSE_CONTREAD)
     tts_tensor node{};
+    // MCPY: the ROPE node producing the copies' source, applied on the way (x = the rope's source)
+    const tts_tensor * rope = nullptr;
     // GEMV
     std::vector<const tts_tensor *> mms;
     std::vector<GemvTarget> tgt;
@@ -1381,6 +1383,34 @@ struct Planner {
         Item m;
         m.kind = Item::MCPY;
         m.x = src;
+        // the source is a ROPE read only by these copies, with nothing but views since it ran (Orpheus'
+        // rope(K) -> repeat copies into the cache, model.cpp:194-228): rotate straight into every copy,
+        // and read a contiguous CONT's source the same way (the copy before the rope is never made)
+        const auto only_views = [&](int a, int b) {
+            for (int k = a + 1; k < b; ++k)
+                if (!is_view(nodes[k]->op) || act[k] != 0) return false;
+            return true;
+        };
+        if (src->op == TTS_OP_ROPE && act[index[src]] == 0 && uses[src] == (int)idx.size() && only_views(index[src], i)) {
+            const tts_tensor * rs = src->src[0];
+            bool ok = true;
+            for (int d = 0; d < 4; ++d) ok &= rs->ne[d] == src->ne[d] && C->ne[d] == src->ne[d];
+            for (int j : idx) ok &= !overlap(nodes[j], rs);
+            if (ok) {
+                m.rope = src;
+                act[index[src]] = -1;
+                if (rs->op == TTS_OP_CONT && act[index[rs]] == 0 && uses[rs] == 1 && rs->src[0] && rs->src[0]->type == rs->type &&
+                    contiguous(rs) && contiguous(rs->src[0]) && only_views(index[rs], index[src])) {
+                    bool ok2 = true;
+                    for (int j : idx) ok2 &= !overlap(nodes[j], rs->src[0]);
+                    if (ok2) {
+                        act[index[rs]] = -1;
+                        rs = rs->src[0];
+                    }
+                }
+                m.x = rs;
+            }
+        }
         for (int j : idx) {
             m.terms.push_back(nodes[j]);
             act[j] = -1;
@@ -1721,7 +1751,8 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             launch_adain_snake(be, it.adain);
             return 0;
         case Item::MCPY:
-            launch_cpy_multi(be, it.x, it.terms.data(), (int)it.terms.size());
+            if (it.rope) launch_rope_multi(be, it.rope, it.x, it.terms.data(), (int)it.terms.size());
+            else launch_cpy_multi(be, it.x, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::RINT:
             launch_repeat_interleave1(be, it.dst, it.x, it.rint);

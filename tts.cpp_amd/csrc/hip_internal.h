@@ -360,6 +360,7 @@ struct LstmStepArgs {
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a, const LstmStepArgs * b = nullptr);
 void launch_repeat_interleave1(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * a, int r);
 void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
+void launch_rope_multi(tts_hip_backend * be, const tts_tensor * rope, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                         int32_t * hist, int32_t * next);
 constexpr int EMBED_MAX_TERMS = 16;

@@ -823,7 +823,12 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         TTS_PIN_LOADS();
     };
 
-    float sums[8][4], sumf[4], gate[4];
+    // ggml's f32 chain per (row q, column): sums[l] += (d*yd)*aux32[l], sumf -= (dmin*yd)*sumi, kept
+    // as pairs of rows (q = 0,1 / 2,3) so the products and sums issue as packed f32 ops (each element
+    // still one rounded multiply and one rounded add)
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v sums[8][2], sumf[2];
+    float gate[4];
     auto compute = [&](auto BS, int64_t i) {
         constexpr int bs = decltype(BS)::value;
         const int64_t ti = i / nch;
@@ -831,10 +836,10 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         const int c = (int)(i % nch);
         if (c == 0) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                sumf[q] = 0.f;
+            for (int h = 0; h < 2; ++h) {
+                sumf[h] = f2v{0.f, 0.f};
 #pragma unroll
-                for (int l = 0; l < 8; ++l) sums[l][q] = 0.f;
+                for (int l = 0; l < 8; ++l) sums[l][h] = f2v{0.f, 0.f};
             }
         }
 #pragma unroll
@@ -877,22 +882,27 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
             const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
             const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             const float yd = xd_s[cc * nb + b];
+            float dyq[4], dmyq[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
-                const float dy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
-                const float dmy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+                dyq[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+                dmyq[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+            }
 #pragma unroll
-                for (int l = 0; l < 8; ++l) sums[l][q] = __fadd_rn(sums[l][q], __fmul_rn(dy, acc[l][q]));
-                sumf[q] = __fsub_rn(sumf[q], __fmul_rn(dmy, si[q]));
+            for (int hq = 0; hq < 2; ++hq) {
+                const f2v dy = {dyq[2 * hq], dyq[2 * hq + 1]}, dmy = {dmyq[2 * hq], dmyq[2 * hq + 1]};
+#pragma unroll
+                for (int l = 0; l < 8; ++l) sums[l][hq] = sums[l][hq] + dy * f2v{acc[l][2 * hq], acc[l][2 * hq + 1]};
+                sumf[hq] = sumf[hq] - dmy * f2v{si[2 * hq], si[2 * hq + 1]};
             }
         }
         if (c == nch - 1) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                float tot = sumf[q];
+                float tot = sumf[q >> 1][q & 1];
 #pragma unroll
-                for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[l][q]);
+                for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[l][q >> 1][q & 1]);
                 const int64_t flat = t * 16 + 4 * kg + q;
                 if (xpair) {
                     gate[q] = tot;  // gate or up row: crossed over after the loop

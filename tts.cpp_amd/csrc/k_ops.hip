@@ -419,8 +419,13 @@ __global__ __launch_bounds__(256) void k_sum_rows(TD dst, TD a) {
 }
 
 // ---- ROPE (NORM / NEOX, optional freq factors; theta by repeated multiply as ggml_rope_cache_init) ----
-__global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int n_dims, int neox, float theta_scale,
+// dst: one or more destinations of the source's shape (the planner's rope + repeat-copy item writes
+// every repeat copy of the rotated K directly)
+__global__ void k_rope(CpyMulti m, TD a, const int32_t * pos, const float * ff, int n_dims, int neox, float theta_scale,
                        float freq_scale, float attn_factor) {
+    auto td_store_all = [&](int64_t j0, int64_t i1, int64_t i2, int64_t i3, float v) {
+        for (int d = 0; d < m.nd; ++d) td_store(m.dst[d], j0, i1, i2, i3, v);
+    };
     const int64_t i1 = blockIdx.x, i2 = blockIdx.y, i3 = blockIdx.z;
     const int64_t p = pos[i2];
     for (int64_t i0 = 2 * threadIdx.x; i0 < a.ne[0]; i0 += 2 * blockDim.x) {
@@ -439,11 +444,13 @@ __global__ void k_rope(TD dst, TD a, const int32_t * pos, const float * ff, int 
                 j1 = i0 + 1;
             }
             const float x0 = td_load(a, j0, i1, i2, i3), x1 = td_load(a, j1, i1, i2, i3);
-            td_store(dst, j0, i1, i2, i3, __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s)));
-            td_store(dst, j1, i1, i2, i3, __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c)));
+            td_store_all(j0, i1, i2, i3, __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s)));
+            td_store_all(j1, i1, i2, i3, __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c)));
         } else {
-            td_store(dst, i0, i1, i2, i3, td_load(a, i0, i1, i2, i3));
-            if (i0 + 1 < a.ne[0]) td_store(dst, i0 + 1, i1, i2, i3, td_load(a, i0 + 1, i1, i2, i3));
+            const float x0 = td_load(a, i0, i1, i2, i3);
+            const float x1 = i0 + 1 < a.ne[0] ? td_load(a, i0 + 1, i1, i2, i3) : 0.f;
+            td_store_all(i0, i1, i2, i3, x0);
+            if (i0 + 1 < a.ne[0]) td_store_all(i0 + 1, i1, i2, i3, x1);
         }
     }
 }
@@ -519,6 +526,23 @@ static inline unsigned grid_for(int64_t n, int bs = 256) {
     if (g > 65536) g = 65536;
     if (g < 1) g = 1;
     return (unsigned)g;
+}
+
+// ROPE node `rope` over `src` (its source, or the tensor a skipped copy would have produced it from),
+// written to every tensor in dsts (each of the source's shape)
+void launch_rope_multi(tts_hip_backend * be, const tts_tensor * rope, const tts_tensor * src, const tts_tensor * const * dsts, int nd) {
+    CpyMulti m{};
+    m.nd = nd;
+    for (int i = 0; i < nd; ++i) m.dst[i] = make_td(dsts[i]);
+    const int n_dims = rope->op_params[1];
+    const int mode = rope->op_params[2];
+    const float freq_base = op_f(rope, 5), freq_scale = op_f(rope, 6), attn_factor = op_f(rope, 8);
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    const tts_tensor * ff = rope->src[2];
+    dim3 grid((unsigned)src->ne[1], (unsigned)src->ne[2], (unsigned)src->ne[3]);
+    hipLaunchKernelGGL(k_rope, grid, dim3(64), 0, be->stream, m, make_td(src), (const int32_t *)rope->src[1]->data,
+                       ff ? (const float *)ff->data : nullptr, n_dims, (mode & 2) ? 1 : 0, theta_scale, freq_scale, attn_factor);
+    TTS_HIP_CHECK(hipGetLastError());
 }
 
 int launch_op(tts_hip_backend * be, const tts_tensor * node) {
@@ -629,16 +653,7 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
             const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
             hipLaunchKernelGGL(k_sum_rows, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0));
         } break;
-        case TTS_OP_ROPE: {
-            const int n_dims = node->op_params[1];
-            const int mode = node->op_params[2];
-            const float freq_base = op_f(node, 5), freq_scale = op_f(node, 6), attn_factor = op_f(node, 8);
-            const float theta_scale = powf(freq_base, -2.0f / n_dims);
-            const tts_tensor * ff = node->src[2];
-            dim3 grid((unsigned)s0->ne[1], (unsigned)s0->ne[2], (unsigned)s0->ne[3]);
-            hipLaunchKernelGGL(k_rope, grid, dim3(64), 0, st, d, make_td(s0), (const int32_t *)s1->data,
-                               ff ? (const float *)ff->data : nullptr, n_dims, (mode & 2) ? 1 : 0, theta_scale, freq_scale, attn_factor);
-        } break;
+        case TTS_OP_ROPE: launch_rope_multi(be, node, s0, &node, 1); break;
         case TTS_OP_MUL_MAT: {
             // F16 src0 with many columns (conv_1d's GEMM) on the matrix cores; otherwise the generic
             // float path (quantized weights go through the GEMV kernels)
