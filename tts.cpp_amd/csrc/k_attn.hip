@@ -742,16 +742,21 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
     float qv[HD];
 #pragma unroll
     for (int d = 0; d < HD; ++d) qv[d] = *(const float *)(qbase + (int64_t)d * a.q.nb[0]);
-    constexpr int VB = 8;  // V positions per batch, per output dim
-    float vv[HD / 64][VB];
-    auto load_v = [&](int i0) {
+    // V positions per batch, per output dim; two batches in flight (the next one is requested before
+    // the current one is summed; loads are clamped, never guarded, so the wait counts stay exact)
+    constexpr int VB = 16;
+    float vv[2][HD / 64][VB];
+    auto load_v = [&](auto BS, int i0) {
+        constexpr int bs = decltype(BS)::value;
 #pragma unroll
         for (int j = 0; j < HD / 64; ++j)
 #pragma unroll
             for (int u = 0; u < VB; ++u)
-                vv[j][u] = *(const float *)(vbase + (int64_t)(lane + 64 * j) * a.v.nb[1] + (int64_t)min(i0 + u, P - 1) * a.v.nb[0]);
+                vv[bs][j][u] = *(const float *)(vbase + (int64_t)(lane + 64 * j) * a.v.nb[1] + (int64_t)min(i0 + u, P - 1) * a.v.nb[0]);
     };
-    load_v(0);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    load_v(I0{}, 0);
     TTS_PIN_LOADS();
     double acc = 0.0;
 #pragma unroll
@@ -778,18 +783,24 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
     double o[HD / 64];
 #pragma unroll
     for (int j = 0; j < HD / 64; ++j) o[j] = 0.0;
-    for (int i0 = 0; i0 < P; i0 += VB) {
-        if (i0 > 0) {
-            load_v(i0);
-            TTS_PIN_LOADS();
-        }
+    auto consume = [&](auto BS, int i0) {
+        constexpr int bs = decltype(BS)::value;
 #pragma unroll
         for (int u = 0; u < VB; ++u) {
             if (i0 + u >= P) break;
             const float pi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), i0 + u));
 #pragma unroll
-            for (int j = 0; j < HD / 64; ++j) o[j] += (double)__fmul_rn(pi, vv[j][u]);
+            for (int j = 0; j < HD / 64; ++j) o[j] += (double)__fmul_rn(pi, vv[bs][j][u]);
         }
+    };
+    for (int i0 = 0; i0 < P; i0 += 2 * VB) {
+        load_v(I1{}, i0 + VB);
+        TTS_PIN_LOADS();
+        consume(I0{}, i0);
+        if (i0 + VB >= P) break;
+        load_v(I0{}, i0 + 2 * VB);
+        TTS_PIN_LOADS();
+        consume(I1{}, i0 + VB);
     }
     const int64_t orow = (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
 #pragma unroll
