@@ -150,6 +150,8 @@ enum tts_status {
 #define TTS_FLAG_OUTPUT 4
 #define TTS_FLAG_PERSIST 8
 #define TTS_FLAG_REPACKED 16 /* set by the HIP backend: the tensor is stored in its Q4_K lane layout */
+#define TTS_FLAG_TILED_COPY 64 /* set by the HIP backend: a lane-layout Q4_K matrix that also has a tile-layout copy
+                                  (medium matrices, TTS_HIP_OPT_Q4K_DUAL_BYTES), read by GEMVs of >= 8 columns */
 #define TTS_FLAG_TILED 32    /* set by the HIP backend: Q4_K stored in its 4-row tile layout (tts_repack_q4_K_tiled),
                                 read by the matrix-core GEMV (large matrices, tts_hip_weight_set) */
 
@@ -257,6 +259,10 @@ enum tts_hip_option {
     TTS_HIP_OPT_ATTN_FUSED = 14,  /* decode attention over P >= value keys (hd 64 / 128, 16-B K and V rows) runs as
                                      ONE 1024-thread launch per attention (k_attn_fused; default 0 = off: the split pair,
                                      TTS_HIP_OPT_ATTN_SPLIT; tests and studies use 128) */
+    TTS_HIP_OPT_Q4K_DUAL_BYTES = 16, /* tts_hip_weight_set keeps a tile-layout copy of lane-layout Q4_K matrices of >= value
+                                        bytes (default 1 MiB; 0 = never); a GEMV of >= 8 columns over >= 2048 rows of such
+                                        matrices runs on the matrix-core kernels, and matrices of different row counts
+                                        sharing the activation (Orpheus q / k / v) then run as one launch */
     TTS_HIP_OPT_ATTN_PV16 = 15,   /* 1: the split P.V kernel requests a lane's whole V slice (16 x 16 B) before the
                                      softmax when P <= 1024; 0 (default): two 8-chunk batches (measured equal) */
 };

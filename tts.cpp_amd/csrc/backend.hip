@@ -298,6 +298,23 @@ int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
         tts_repack_q4_K(src, tmp.data(), (int64_t)(n / 144), 0);
         int st = tts_hip_tensor_set(be, t->data, tmp.data(), n);
         if (st == 0) t->flags |= TTS_FLAG_REPACKED;
+        auto old = be->tiled_copy.find(t->data);
+        if (old != be->tiled_copy.end()) {  // a re-upload replaces the copy
+            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+            TTS_HIP_CHECK(hipFree(old->second));
+            be->tiled_copy.erase(old);
+            t->flags &= ~TTS_FLAG_TILED_COPY;
+        }
+        if (st == 0 && be->q4k_dual_bytes > 0 && (int64_t)n >= be->q4k_dual_bytes && t->ne[1] % 16 == 0 && t->ne[2] == 1 &&
+            t->ne[3] == 1) {
+            // medium matrix: also a tile-layout copy for the matrix-core kernels at >= 8 columns
+            tts_repack_q4_K_tiled(src, tmp.data(), t->ne[1], t->ne[0] / 256, 0);
+            uint8_t * cp = nullptr;
+            if (hipMalloc((void **)&cp, n) != hipSuccess) return TTS_STATUS_ALLOC_FAILED;
+            if (hipMemcpy(cp, tmp.data(), n, hipMemcpyHostToDevice) != hipSuccess) return TTS_STATUS_FAILED;
+            be->tiled_copy[t->data] = cp;
+            t->flags |= TTS_FLAG_TILED_COPY;
+        }
         return st;
     }
     return tts_hip_tensor_set(be, t->data, src, n);
@@ -391,6 +408,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_ATTN_PV16: be->attn_pv_uv16 = value != 0; return 0;
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
+        case TTS_HIP_OPT_Q4K_DUAL_BYTES: be->q4k_dual_bytes = value; return 0;
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;

@@ -563,8 +563,13 @@ struct Planner {
             const tts_tensor * mm = nodes[j];
             if (mm->op != TTS_OP_MUL_MAT || mm->src[1] != x || !is_gemv(mm)) break;
             const tts_tensor * a = mm->src[0];
-            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->ne[1] != a0->ne[1] || a->nb[1] != a0->nb[1]) break;
-            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED))) break;
+            // another row count: only Q4_K matrices the tile-layout kernels can read (stored tiled, or
+            // with a tile-layout copy), each a multiple of 16 rows; run_gemv_item splits the launch
+            // when it ends up on a lane-layout kernel
+            const bool tl = a->type == TTS_TYPE_Q4_K && (a->flags & (TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) &&
+                            (a0->flags & (TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) && a->ne[1] % 16 == 0 && a0->ne[1] % 16 == 0;
+            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->nb[1] != a0->nb[1] || (a->ne[1] != a0->ne[1] && !tl)) break;
+            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED)) && !tl) break;
             GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
             GemvTarget kt;
             std::vector<int> ks;
@@ -1564,7 +1569,15 @@ static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, in
     return 0;
 }
 
-static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a) {
+static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a, bool tiled_copy = false) {
+    if (tiled_copy) {
+        auto c = be->tiled_copy.find(a->data);
+        if (c == be->tiled_copy.end()) {
+            fprintf(stderr, "tts_hip: missing tile-layout copy of %s\n", a->name);
+            abort();
+        }
+        return c->second;
+    }
     if (a->type != TTS_TYPE_Q4_K || (a->flags & TTS_FLAG_REPACKED)) return a->data;
     // Q4_K matrix written with plain tensor_set (native ggml layout): repack into a temp
     const size_t bytes = (size_t)a->nb[1] * (size_t)a->ne[1];
@@ -1692,19 +1705,41 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             return 0;
         }
     }
+    // lane-layout matrices with tile-layout copies: GEMVs of >= 8 columns over >= 2048 rows read the
+    // copies on the matrix-core kernels (enough 16-row tiles to fill the chip)
+    // (a group holding a matrix stored tiled runs there whatever M is: that matrix has no other layout)
+    bool all_tl = j.wtype == TTS_TYPE_Q4_K && !tmp, any_tiled = false;
+    int64_t rows = 0;
+    for (const tts_tensor * mm : it.mms) {
+        const int f = mm->src[0]->flags;
+        all_tl &= (f & (TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) != 0;
+        any_tiled |= (f & TTS_FLAG_TILED) != 0;
+        rows += mm->src[0]->ne[1];
+    }
+    const bool use_copy = all_tl && (any_tiled || (j.M >= 8 && rows >= 2048));
+    if (use_copy) j.tiled = 1;
     size_t k = 0;
     while (k < it.mms.size()) {
         GemvJob jj = j;
         jj.nmat = 0;
+        jj.hetero = 0;
+        jj.roff[0] = 0;
         while (k < it.mms.size() && jj.nmat < GEMV_MAX_MATS) {
-            jj.W[jj.nmat] = (const uint8_t *)weight_ptr(be, it.mms[k]->src[0]);
+            const tts_tensor * a = it.mms[k]->src[0];
+            // matrices of another row count share a launch only on the tile-layout kernels
+            if (jj.nmat > 0 && a->ne[1] != jj.N && !jj.tiled) break;
+            if (a->ne[1] != jj.N) jj.hetero = 1;
+            jj.W[jj.nmat] = (const uint8_t *)weight_ptr(be, a, use_copy && !(a->flags & TTS_FLAG_TILED));
             jj.Y[jj.nmat] = it.tgt[k].y;
             jj.ycs[jj.nmat] = it.tgt[k].ycs;
             jj.yrs[jj.nmat] = it.tgt[k].yrs;
+            if (jj.nmat == 0) jj.N = a->ne[1];
+            jj.roff[jj.nmat + 1] = jj.roff[jj.nmat] + a->ne[1];
             jj.nmat++;
             k++;
             if (tmp) break;
         }
+        if (jj.hetero) jj.N = 0;  // every row count comes from roff
         launch_gemv_job(be, jj);
     }
     if (xattn) return run_attn_item(be, *xattn);  // unfused fallback: the attention right after its query

@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <deque>
+#include <unordered_map>
 #include <vector>
 
 #include "common.h"
@@ -200,6 +201,10 @@ struct GemvJob {
     // (NORM/RMS_NORM -> MUL -> ADD, parler_build_layer_norm), written to lnout by workgroup 0.
     int pro = 0;
     int tiled = 0;  // W in the 4-row tile layout (TTS_FLAG_TILED): k_gemv_q4K_mf
+    // matrices of different row counts (tile-layout kernels only): matrix m holds flat rows
+    // roff[m] .. roff[m + 1] - 1 (each a multiple of 16); otherwise N rows each
+    int hetero = 0;
+    int64_t roff[GEMV_MAX_MATS + 1] = {};
     int dbg = 0;    // phase study (TTS_HIP_OPT_GEMV_DEBUG): 1 = skip the row phase, 2 = skip the prologue
     const float * lnw = nullptr;
     const float * lnb = nullptr;
@@ -209,6 +214,8 @@ struct GemvJob {
     int64_t locs = 0;
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
 };
+__host__ __device__ inline int64_t job_roff(const GemvJob & j, int m) { return j.hetero ? j.roff[m] : (int64_t)m * j.N; }
+__host__ __device__ inline int64_t job_rows(const GemvJob & j) { return job_roff(j, j.nmat); }
 // In-kernel phase timestamps (s_memrealtime, 100 MHz) per wave, compiled in only by the
 // micro-benchmark build (-DTTS_PHASE_TS): ts[(wg * waves + wave) * 8 + k].
 #ifdef TTS_PHASE_TS
@@ -268,6 +275,10 @@ struct tts_hip_backend {
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;
+    // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
+    // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)
+    int64_t q4k_dual_bytes = 1 << 20;
+    std::unordered_map<const void *, uint8_t *> tiled_copy;
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;

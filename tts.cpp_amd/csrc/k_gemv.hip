@@ -775,7 +775,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     // of the first half runs gate tile t and wave w + nw/2 up tile t instead, and the gate results
     // cross over through LDS after one barrier.
     const bool swiglu = j.epi == EPI_SWIGLU;
-    const int64_t NR = swiglu ? j.N : (int64_t)j.nmat * j.N;
+    const int64_t NR = swiglu ? j.N : job_rows(j);
     const int64_t T = (NR + 15) / 16;
     const int half = nw >> 1;
     const bool xpair = swiglu && T <= (int64_t)gridDim.x * half;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     float * xg = (float *)(smem + al16((size_t)nslot * (2 * QK_K + 32 + 4)));  // xpair: [half][64 lanes][4]
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
-        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
         return mt;
     };
 
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         int64_t flat = t * 16 + r;
         flat = flat < NR ? flat : NR - 1;
         const int mat = xpair ? xmat : swiglu ? (int)(ti & 1) : mat_of(flat);
-        const int64_t row = swiglu ? flat : flat - (int64_t)mat * j.N;
+        const int64_t row = swiglu ? flat : flat - job_roff(j, mat);
         const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
         const int ri = (int)(row & 3);
 #pragma unroll
@@ -911,7 +911,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
                     else if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gate[q]), tot);
                 } else if (r < M && flat < NR) {
                     const int mat = mat_of(flat);
-                    gemv_store<8>(j, mat, flat - (int64_t)mat * j.N, r, tot);
+                    gemv_store<8>(j, mat, flat - job_roff(j, mat), r, tot);
                 }
             }
         }
@@ -985,17 +985,17 @@ __global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
     const int r = lane & 15, kg = lane >> 4;
     const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
     const int nu = 2 * nb;
-    const int64_t T = (int64_t)j.nmat * j.N / 16;  // launcher: N % 16 == 0, so a tile is in one matrix
+    const int64_t T = job_rows(j) / 16;  // launcher: every matrix a multiple of 16 rows, so a tile is in one matrix
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
-        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
+        while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
         return mt;
     };
 
     u32x4 hd[UPW], qv[UPW];
     auto load = [&](int64_t t) {
         const int mat = mat_of(t * 16);
-        const int64_t row = t * 16 - (int64_t)mat * j.N + r;
+        const int64_t row = t * 16 - job_roff(j, mat) + r;
         const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
         const int ri = (int)(row & 3);
 #pragma unroll
@@ -1100,7 +1100,7 @@ __global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
             }
             const float tot = q4k_octet_total(sumf, sums);
             const int col = (i >> 3) & 7, row = i >> 6;
-            if ((i & 7) == 0 && col < M) gemv_store<8>(j, mat, t * 16 - (int64_t)mat * j.N + row, col, tot);
+            if ((i & 7) == 0 && col < M) gemv_store<8>(j, mat, t * 16 - job_roff(j, mat) + row, col, tot);
         }
         __syncthreads();
     }
@@ -1437,8 +1437,8 @@ static void profile_push(tts_hip_backend * be, hipEvent_t e0, hipEvent_t e1, dou
 
 // algorithmic bytes of one launch: every weight byte once + the activation read + the outputs written
 static double gemv_bytes(const GemvJob & j) {
-    return (double)j.nmat * ((double)tts_row_size(j.wtype, j.K) * (double)j.N + 4.0 * (double)j.N * (double)j.M) +
-           4.0 * (double)j.K * (double)j.M;
+    const double rows = (double)job_rows(j);
+    return rows * ((double)tts_row_size(j.wtype, j.K) + 4.0 * (double)j.M) + 4.0 * (double)j.K * (double)j.M;
 }
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): replica backends call
@@ -1573,7 +1573,7 @@ template <int PRO, int NCH>
 static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
     static std::atomic<uint32_t> attr_done{0};
     set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH>);
-    const int64_t T = (j.nmat * j.N + 15) / 16;
+    const int64_t T = (job_rows(j) + 15) / 16;
     const unsigned gx = (unsigned)(T < 256 ? T : 256);
     const size_t lds = q4k_mf_lds(j.M, j.K);
     if (be->profile_gemv) {
@@ -1613,9 +1613,11 @@ static size_t q4k_ks_lds(int64_t M, int64_t nb) {
 static bool q4k_ks_eligible(const tts_hip_backend * be, const GemvJob & j) {
     if (be->gemv_ks_tiles <= 0 || j.wtype != TTS_TYPE_Q4_K || !j.tiled || j.M < 1 || j.M > 8 || j.epi == EPI_SWIGLU) return false;
     const int64_t nb = j.K / QK_K;
-    if (nb < 1 || nb > 16 || j.N % 16) return false;
+    if (nb < 1 || nb > 16) return false;
+    for (int m = 0; m <= j.nmat; ++m)
+        if (job_roff(j, m) % 16) return false;
     if (j.pro == PRO_LN && j.K > 4 * 1024) return false;  // the LN prologue holds <= 16 chunks per lane
-    if ((int64_t)j.nmat * j.N / 16 > be->gemv_ks_tiles) return false;
+    if (job_rows(j) / 16 > be->gemv_ks_tiles) return false;
     return q4k_ks_lds(j.M, nb) <= 160 * 1024;
 }
 template <int PRO, int NCH, int UPW, int NWMAX>
@@ -1632,7 +1634,7 @@ static void launch_q4k_ks_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
     hipLaunchKernelGGL((k_gemv_q4K_ks<PRO, NCH, UPW, NWMAX>), dim3(gx), dim3(64 * nw), lds, be->stream, j);
 }
 static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
-    const int64_t nb = j.K / QK_K, T = (int64_t)j.nmat * j.N / 16;
+    const int64_t nb = j.K / QK_K, T = job_rows(j) / 16;
     // units (block, residue half) per wave: one for nb <= 4 (<= 8 waves); above, two (<= 16 waves)
     // after a quantize-only prologue, four (<= 8 waves) after an LN prologue, whose K / 256 chunks
     // per lane need the registers of a 512-thread workgroup
