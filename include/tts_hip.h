@@ -263,6 +263,8 @@ enum tts_hip_option {
                                         bytes (default 1 MiB; 0 = never); a GEMV of >= 8 columns over >= 2048 rows of such
                                         matrices runs on the matrix-core kernels, and matrices of different row counts
                                         sharing the activation (Orpheus q / k / v) then run as one launch */
+    TTS_HIP_OPT_GEMV_RSPLIT = 17, /* 1 (default): matrix-core Q4_K GEMVs with few 16-row tiles split each tile's residues over
+                                     2 or 4 waves (chains joined in ggml's order: bit-identical); 0 = one wave per tile */
     TTS_HIP_OPT_ATTN_PV16 = 15,   /* 1: the split P.V kernel requests a lane's whole V slice (16 x 16 B) before the
                                      softmax when P <= 1024; 0 (default): two 8-chunk batches (measured equal) */
 };

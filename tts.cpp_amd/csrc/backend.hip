@@ -409,6 +409,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_KV_PREFETCH: be->kv_prefetch_minp = value; return 0;
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
         case TTS_HIP_OPT_Q4K_DUAL_BYTES: be->q4k_dual_bytes = value; return 0;
+        case TTS_HIP_OPT_GEMV_RSPLIT: be->gemv_mf_rsplit = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;

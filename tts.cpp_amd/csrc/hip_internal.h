@@ -275,6 +275,7 @@ struct tts_hip_backend {
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;
+    int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)
     int64_t q4k_dual_bytes = 1 << 20;

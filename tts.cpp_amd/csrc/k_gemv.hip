@@ -753,7 +753,14 @@ __device__ __forceinline__ f16x2 byte2_f16_biased(uint32_t w, uint32_t sel) {
     return __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(0u, w, sel) | 0x64006400u);
 }
 
-template <int PRO, int NCH>
+// RS > 1 (residue split; the launcher guarantees one tile per wave slot and no SwiGLU epilogue): the
+// RS waves w = part * (nw / RS) + slot of a workgroup share tile `slot`, wave `part` running the
+// MFMAs and f32 chains of residues l = part * 8 / RS .. + 8 / RS - 1 (the last part also the mins
+// chain).  ggml's chains are per residue (sums[l]) plus sumf, joined only at the end
+// (sumf + sums[0] + ... + sums[7]), so after one barrier the last part adds the others' sums from LDS
+// in residue order: the same additions as the one-wave kernel.  Few-tile matrices (Orpheus down:
+// 192 tiles of 32 blocks) then keep all four SIMDs of a CU busy instead of one.
+template <int PRO, int NCH, int RS = 1>
 __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
@@ -778,13 +785,17 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     const int64_t NR = swiglu ? j.N : job_rows(j);
     const int64_t T = (NR + 15) / 16;
     const int half = nw >> 1;
-    const bool xpair = swiglu && T <= (int64_t)gridDim.x * half;
+    const bool xpair = RS == 1 && swiglu && T <= (int64_t)gridDim.x * half;
     const int per = swiglu && !xpair ? 2 : 1;
     const int xmat = xpair && wave >= half ? 1 : 0;  // xpair: this wave's matrix (0 gate, 1 up)
+    constexpr int LPW = 8 / RS;                      // residues per wave
+    const int nws = nw / RS;                         // tile slots per workgroup
+    const int part = RS > 1 ? wave / nws : 0;
+    const int slot = RS > 1 ? wave - part * nws : wave;
     // tile t0 + k * tstride; consecutive tiles go to different workgroups, so a small matrix still
     // spreads over every CU
-    const int64_t t0 = (int64_t)(wave - xmat * half) * gridDim.x + blockIdx.x;
-    const int64_t tstride = xpair ? T : (int64_t)gridDim.x * nw;
+    const int64_t t0 = (int64_t)(slot - xmat * half) * gridDim.x + blockIdx.x;
+    const int64_t tstride = (xpair || RS > 1) ? T : (int64_t)gridDim.x * nw;
     const int64_t nmine = (t0 < T && !(j.dbg & 1)) ? ((T - 1 - t0) / tstride + 1) * nch * per : 0;
     float * xg = (float *)(smem + al16((size_t)nslot * (2 * QK_K + 32 + 4)));  // xpair: [half][64 lanes][4]
     auto mat_of = [&](int64_t flat) {
@@ -795,7 +806,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 
     // tile layout (tts_repack_q4_K_tiled): lane (r, kg) reads its row's header and the two 16-B
     // pieces of chunk c = kg (residues 0..3, 4..7); a quarter wave covers four 64-B runs
-    u32x4 hd[2][CH], qa[2][CH], qb[2][CH];
+    u32x4 hd[2][CH], qa[2][CH], qb[2][RS == 1 ? CH : 1];  // RS > 1: qa holds this wave's 16-B piece
     auto load = [&](auto BS, int64_t i) {
         constexpr int bs = decltype(BS)::value;
         const int64_t ti = i / nch;
@@ -810,14 +821,17 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
             const uint8_t * bp = wt + (int64_t)min(c * CH + u, nb - 1) * 576;
-            if (j.dbg & 4) {  // phase study: plain (cached) loads
+            if (RS > 1) {  // the piece holding residues part * LPW ..: 0..3 (half 0) or 4..7 (half 1)
+                hd[bs][u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+                qa[bs][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + (part * LPW >= 4 ? 1 : 0)) * 4 + ri) * 16));
+            } else if (j.dbg & 4) {  // phase study: plain (cached) loads
                 hd[bs][u] = *(const u32x4 *)(bp + ri * 16);
                 qa[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16);
-                qb[bs][u] = *(const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16);
+                qb[bs][RS == 1 ? u : 0] = *(const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16);
             } else {
                 hd[bs][u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
                 qa[bs][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-                qb[bs][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+                qb[bs][RS == 1 ? u : 0] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
             }
         }
         TTS_PIN_LOADS();
@@ -827,7 +841,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     // as pairs of rows (q = 0,1 / 2,3) so the products and sums issue as packed f32 ops (each element
     // still one rounded multiply and one rounded add)
     typedef float f2v __attribute__((ext_vector_type(2)));
-    f2v sums[8][2], sumf[2];
+    f2v sums[LPW][2], sumf[2];
     float gate[4];
     auto compute = [&](auto BS, int64_t i) {
         constexpr int bs = decltype(BS)::value;
@@ -839,7 +853,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
             for (int h = 0; h < 2; ++h) {
                 sumf[h] = f2v{0.f, 0.f};
 #pragma unroll
-                for (int l = 0; l < 8; ++l) sums[l][h] = f2v{0.f, 0.f};
+                for (int l = 0; l < LPW; ++l) sums[l][h] = f2v{0.f, 0.f};
             }
         }
 #pragma unroll
@@ -857,10 +871,14 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
             const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
             const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
             const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8;
-            f32x4 acc[8];
+            f32x4 acc[LPW];
 #pragma unroll
-            for (int l = 0; l < 8; ++l) {
-                const uint32_t D = l < 4 ? qa[bs][u][l] : qb[bs][u][l - 4];
+            for (int ll = 0; ll < LPW; ++ll) {
+                const int l = part * LPW + ll;
+                uint32_t D;
+                if (RS == 1) D = ll < 4 ? qa[bs][u][ll & 3] : qb[bs][RS == 1 ? u : 0][ll & 3];
+                else if (RS == 2) D = qa[bs][u][ll];
+                else D = (part & 1) ? qa[bs][u][2 + ll] : qa[bs][u][ll];
                 const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
                 // fma(1024 + n, s, -1024 s) = s * n exactly (single rounding of an exact value)
                 const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
@@ -869,8 +887,9 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
                 const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
                 const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
                 const f16x8 B = *(const f16x8 *)(bsl + l * 32);
-                acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                acc[ll] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             }
+            const bool mins = RS == 1 || part == RS - 1;  // wave-uniform
             // sumi: lane group 0 holds the 8 mins, group 1 the mins times 64, groups 2, 3 zero
             const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
             const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
@@ -880,7 +899,8 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
             const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
             const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
             const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
-            const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            f32x4 si = {0.f, 0.f, 0.f, 0.f};
+            if (mins) si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             const float yd = xd_s[cc * nb + b];
             float dyq[4], dmyq[4];
 #pragma unroll
@@ -893,16 +913,16 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
             for (int hq = 0; hq < 2; ++hq) {
                 const f2v dy = {dyq[2 * hq], dyq[2 * hq + 1]}, dmy = {dmyq[2 * hq], dmyq[2 * hq + 1]};
 #pragma unroll
-                for (int l = 0; l < 8; ++l) sums[l][hq] = sums[l][hq] + dy * f2v{acc[l][2 * hq], acc[l][2 * hq + 1]};
-                sumf[hq] = sumf[hq] - dmy * f2v{si[2 * hq], si[2 * hq + 1]};
+                for (int l = 0; l < LPW; ++l) sums[l][hq] = sums[l][hq] + dy * f2v{acc[l][2 * hq], acc[l][2 * hq + 1]};
+                if (mins) sumf[hq] = sumf[hq] - dmy * f2v{si[2 * hq], si[2 * hq + 1]};
             }
         }
-        if (c == nch - 1) {
+        if (RS == 1 && c == nch - 1) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float tot = sumf[q >> 1][q & 1];
 #pragma unroll
-                for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[l][q >> 1][q & 1]);
+                for (int l = 0; l < LPW; ++l) tot = __fadd_rn(tot, sums[l][q >> 1][q & 1]);
                 const int64_t flat = t * 16 + 4 * kg + q;
                 if (xpair) {
                     gate[q] = tot;  // gate or up row: crossed over after the loop
@@ -934,6 +954,34 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         if (i + 1 >= nmine) break;
         load(I0{}, min(i + 2, nmine - 1));
         compute(I1{}, i + 1);
+    }
+    if (RS > 1) {  // one tile per wave at most: join the parts' chains in residue order
+        float * xs = xg;  // [RS - 1 parts][nws slots][64 lanes][LPW * 4]
+        if (nmine > 0 && part < RS - 1) {
+            float * o = xs + (((size_t)part * nws + slot) * 64 + lane) * LPW * 4;
+#pragma unroll
+            for (int l = 0; l < LPW; ++l)
+                *(float4 *)(o + 4 * l) = make_float4(sums[l][0][0], sums[l][0][1], sums[l][1][0], sums[l][1][1]);
+        }
+        __syncthreads();
+        if (nmine > 0 && part == RS - 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float tot = sumf[q >> 1][q & 1];
+                for (int p = 0; p < RS - 1; ++p) {
+                    const float * o = xs + (((size_t)p * nws + slot) * 64 + lane) * LPW * 4;
+#pragma unroll
+                    for (int l = 0; l < LPW; ++l) tot = __fadd_rn(tot, o[4 * l + q]);
+                }
+#pragma unroll
+                for (int l = 0; l < LPW; ++l) tot = __fadd_rn(tot, sums[l][q >> 1][q & 1]);
+                const int64_t flat = t0 * 16 + 4 * kg + q;
+                if (r < M && flat < NR) {
+                    const int mat = mat_of(flat);
+                    gemv_store<8>(j, mat, flat - job_roff(j, mat), r, tot);
+                }
+            }
+        }
     }
     if (xpair) {  // one tile per wave at most: out = silu(gate) * up
         if (nmine > 0 && xmat == 0)
@@ -1557,10 +1605,11 @@ static size_t q80_lds(int MC, int64_t K, int RW) {
 }
 
 // ---- MFMA path (k_gemv_q4K_mf) ----
-// + the SwiGLU cross-over buffer (4 waves x 64 lanes x 4 floats)
-static size_t q4k_mf_lds(int64_t M, int64_t K) { return ((size_t)(M * (K / QK_K) + 1) * (2 * QK_K + 32 + 4) + 15) / 16 * 16 + 4096; }
+// + the cross-over buffer: SwiGLU gate results (4 waves x 64 lanes x 4 floats) or the residue-split
+// partial chains ((RS - 1) / RS x 8 waves x 64 lanes x 8 / RS x 4 floats <= 16 KiB)
+static size_t q4k_mf_lds(int64_t M, int64_t K) { return ((size_t)(M * (K / QK_K) + 1) * (2 * QK_K + 32 + 4) + 15) / 16 * 16 + 16384; }
 static int64_t q4k_mf_max_cols(int64_t K) {
-    const int64_t c = ((int64_t)(160 * 1024 - 4096 - 16) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
+    const int64_t c = ((int64_t)(160 * 1024 - 16384 - 16) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
     return c >= 16 ? 16 : c >= 8 ? 8 : c;
 }
 static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
@@ -1569,21 +1618,29 @@ static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
     // launch_q4k_mf's column loop step by 0
     return j.wtype == TTS_TYPE_Q4_K && j.tiled && q4k_mf_max_cols(j.K) >= 1;
 }
-template <int PRO, int NCH>
-static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
+template <int PRO, int NCH, int RS>
+static void launch_q4k_mf_rs(tts_hip_backend * be, const GemvJob & j, unsigned gx) {
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH>);
-    const int64_t T = (job_rows(j) + 15) / 16;
-    const unsigned gx = (unsigned)(T < 256 ? T : 256);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH, RS>);
     const size_t lds = q4k_mf_lds(j.M, j.K);
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH>), dim3(gx), dim3(512), lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS>), dim3(gx), dim3(512), lds, be->stream, j);
+}
+template <int PRO, int NCH>
+static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
+    const int64_t T = (job_rows(j) + 15) / 16;
+    const unsigned gx = (unsigned)(T < 256 ? T : 256);
+    // residue split when every tile fits one slot of RS waves (8 waves per workgroup)
+    const int rs = j.epi == EPI_SWIGLU || !be->gemv_mf_rsplit ? 1 : T <= (int64_t)gx * 2 ? 4 : T <= (int64_t)gx * 4 ? 2 : 1;
+    if (rs == 4) launch_q4k_mf_rs<PRO, NCH, 4>(be, j, gx);
+    else if (rs == 2) launch_q4k_mf_rs<PRO, NCH, 2>(be, j, gx);
+    else launch_q4k_mf_rs<PRO, NCH, 1>(be, j, gx);
 }
 static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
     const int64_t cmax = q4k_mf_max_cols(job.K);
