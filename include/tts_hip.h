@@ -260,8 +260,8 @@ enum tts_hip_option {
                                      ONE 1024-thread launch per attention (k_attn_fused; default 0 = off: the split pair,
                                      TTS_HIP_OPT_ATTN_SPLIT; tests and studies use 128) */
     TTS_HIP_OPT_Q4K_DUAL_BYTES = 16, /* tts_hip_weight_set keeps a tile-layout copy of lane-layout Q4_K matrices of >= value
-                                        bytes (default 1 MiB; 0 = never); a GEMV of >= 8 columns over >= 2048 rows of such
-                                        matrices runs on the matrix-core kernels, and matrices of different row counts
+                                        bytes (default 1 MiB; 0 = never); a GEMV of >= 8 columns over >= 2048 rows (K >= 2048)
+                                        of such matrices runs on the matrix-core kernels, and matrices of different row counts
                                         sharing the activation (Orpheus q / k / v) then run as one launch */
     TTS_HIP_OPT_GEMV_RSPLIT = 17, /* 1 (default): matrix-core Q4_K GEMVs with few 16-row tiles split each tile's residues over
                                      2 or 4 waves (chains joined in ggml's order: bit-identical); 0 = one wave per tile */

@@ -1705,8 +1705,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             return 0;
         }
     }
-    // lane-layout matrices with tile-layout copies: GEMVs of >= 8 columns over >= 2048 rows read the
-    // copies on the matrix-core kernels (enough 16-row tiles to fill the chip)
+    // lane-layout matrices with tile-layout copies: GEMVs of >= 8 columns over >= 2048 rows of
+    // K >= 2048 read the copies on the matrix-core kernels (enough 16-row tiles to fill the chip)
     // (a group holding a matrix stored tiled runs there whatever M is: that matrix has no other layout)
     bool all_tl = j.wtype == TTS_TYPE_Q4_K && !tmp, any_tiled = false;
     int64_t rows = 0;
@@ -1716,7 +1716,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         any_tiled |= (f & TTS_FLAG_TILED) != 0;
         rows += mm->src[0]->ne[1];
     }
-    const bool use_copy = all_tl && (any_tiled || (j.M >= 8 && rows >= 2048));
+    // (K >= 2048: for K = 1024 rows the lane-layout kernels' short prologue wins)
+    const bool use_copy = all_tl && (any_tiled || (j.M >= 8 && rows >= 2048 && j.K >= 2048));
     if (use_copy) j.tiled = 1;
     size_t k = 0;
     while (k < it.mms.size()) {
