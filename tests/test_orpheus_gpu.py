@@ -16,13 +16,22 @@ TINY = dict(n_layers=2, hidden_size=256, n_attn_heads=4, n_kv_attn_heads=2, head
 WIDE = dict(n_layers=2, max_ctx=32)
 
 
-def run_pair(hip, cfg_kw, batch, n_prompt, n_gen, tile_bytes=None):
+def run_pair(hip, cfg_kw, batch, n_prompt, n_gen, tile_bytes=None, mask=None, expect=None):
     if tile_bytes is not None:
         hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], tile_bytes)
     try:
         g = ttship.Orpheus(hip.iface(), ttship.orpheus_config(batch=batch, **cfg_kw))
     finally:
         hip.set_option(ttship.OPT["Q4K_TILE_BYTES"], 4 << 20)
+    if mask is not None:
+        hip.set_option(ttship.OPT["FUSION"], mask)
+    try:
+        _run_pair(g, cfg_kw, batch, n_prompt, n_gen, expect, ttship.FUSE_ALL if mask is None else mask)
+    finally:
+        hip.set_option(ttship.OPT["FUSION"], ttship.FUSE_ALL)
+
+
+def _run_pair(g, cfg_kw, batch, n_prompt, n_gen, expect, mask):
     c = ttship.Orpheus(py_oracle.iface(16), ttship.orpheus_config(batch=batch, **cfg_kw))
     try:
         V = c.cfg.vocab_size
@@ -36,6 +45,10 @@ def run_pair(hip, cfg_kw, batch, n_prompt, n_gen, tile_bytes=None):
         assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
         dg, dc = g.decode(tg[:, -1]), c.decode(tc[:, -1])
         assert np.abs(dg - dc).max() <= 1e-4 * np.abs(dc).max() + 1e-4
+        if expect:
+            st = g.plan_stats(mask)
+            for k, v in expect.items():
+                assert st[k] == v, f"plan {k}: {st[k]} != {v} ({st})"
     finally:
         g.close()
         c.close()
@@ -57,3 +70,20 @@ def test_orpheus_tiny_all_tiled(hip):
 def test_orpheus_wide_two_layers(hip):
     """Full Orpheus widths (tile-layout GEMVs for q/o/gate/up/down and the 156 940-row head)."""
     run_pair(hip, WIDE, 2, 4, 3)
+
+
+@pytest.mark.gpu
+def test_orpheus_wide_batch8(hip):
+    """The bench's shape (8 prompts = 8 GEMV columns): q / k / v as one launch over the stored-tiled q
+    and the tile-layout copies of k / v, the SwiGLU launch, residue-split tiles; one GEMV item per
+    (qkv, o, SwiGLU, down) and layer plus the head."""
+    run_pair(hip, WIDE, 8, 2, 2, expect={"gemv": 4 * WIDE["n_layers"] + 1})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("drop", ["none", "EPI", "CONTREAD", "MCPY", "GROUP"])
+def test_orpheus_tiny_tiled_fusion_masks(hip, drop):
+    """All matrices tiled at 8 columns (SwiGLU epilogue, residue split, mixed-row q / k / v groups) with
+    each related fusion pattern switched off in turn: tokens bit-exact, logits within the bar."""
+    mask = ttship.FUSE_ALL if drop == "none" else ttship.FUSE_ALL & ~ttship.FUSE[drop]
+    run_pair(hip, TINY, 8, 4, 6, tile_bytes=1, mask=mask)

@@ -1011,7 +1011,7 @@ class KokoroGenerator:
             self.ptr = None
 
 
-PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy", "rint"]
+PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy", "rint", "node"]
 
 
 def plan_stats(nodes_ptr, n_nodes, mask):
