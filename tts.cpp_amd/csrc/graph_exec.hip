@@ -387,6 +387,7 @@ struct Planner {
             if (act[i] != 0 || C->op != TTS_OP_CONT || !C->src[0]) continue;
             const tts_tensor * s = C->src[0];
             if (s->type != C->type || !contiguous(s) || !contiguous(C) || uses[C] != 1) continue;
+            if (C->flags & (TTS_FLAG_OUTPUT | TTS_FLAG_PERSIST)) continue;  // read after the graph: must be written
             const int r = next_real(i);
             if (r < 0 || act[r] != 0) continue;
             const tts_tensor * R = nodes[r];
