@@ -100,6 +100,8 @@ bool is_gemv(const tts_tensor * n) {
 struct GemvTarget {
     float * y;
     int64_t ycs, yrs;
+    int32_t rg = 0, nrep = 1;  // row groups of rg rows, rgs apart; nrep copies, rep apart (floats)
+    int64_t rgs = 0, rep = 0;
 };
 
 struct Item {
@@ -471,6 +473,42 @@ struct Planner {
     }
 
     // KV-store fusion: the GEMV output goes straight into the CPY destination (decode, 1 token).
+    // mm -> RESHAPE c [hd, nkv, n, B] -> CPY into each of 2-4 repeat-interleaved views of the cache
+    // (Orpheus' V store, orpheus/model.cpp:194-228): row kvh * hd + d goes to every copy
+    bool repeat_target(const tts_tensor * mm, const tts_tensor * c, int64_t N, GemvTarget & t, std::vector<int> & skips) {
+        (void)mm;
+        auto ci = consumers.find(c);
+        if (ci == consumers.end() || ci->second.size() < 2 || ci->second.size() > 4 || uses[c] != (int)ci->second.size()) return false;
+        std::vector<int> idx(ci->second.begin(), ci->second.end());
+        std::sort(idx.begin(), idx.end());
+        const tts_tensor * D0 = nodes[idx[0]];
+        int64_t rep = 0;
+        for (size_t a = 0; a < idx.size(); ++a) {
+            const tts_tensor * D = nodes[idx[a]];
+            if (D->op != TTS_OP_CPY || D->src[0] != c || act[idx[a]] != 0 || D->type != TTS_TYPE_F32 || D->nb[0] != 4) return false;
+            for (int k = 0; k < 4; ++k)
+                if (D->ne[k] != c->ne[k] || D->nb[k] != D0->nb[k]) return false;
+            const int64_t d = ((const char *)D->data - (const char *)D0->data);
+            if (d % 4) return false;
+            if (a == 1) rep = d / 4;
+            if (a > 0 && d / 4 != rep * (int64_t)a) return false;
+        }
+        // rows: ne0 x ne1 = N; columns: the n x B of the product, one of them 1
+        // the copies' runs of one row group are disjoint and fit inside the group stride
+        if (c->ne[0] * c->ne[1] != N || rep < c->ne[0] || rep * (int64_t)(idx.size() - 1) + c->ne[0] > (int64_t)(D0->nb[1] / 4))
+            return false;
+        if (c->ne[2] != 1 && c->ne[3] != 1) return false;
+        t.y = (float *)D0->data;
+        t.yrs = 1;
+        t.rg = (int32_t)c->ne[0];
+        t.rgs = (int64_t)(D0->nb[1] / 4);
+        t.ycs = (int64_t)((c->ne[2] == 1 ? D0->nb[3] : D0->nb[2]) / 4);
+        t.nrep = (int32_t)idx.size();
+        t.rep = rep;
+        for (int k : idx) skips.push_back(k);
+        return true;
+    }
+
     bool kv_target(const tts_tensor * mm, int64_t M, GemvTarget & t, std::vector<int> & skips) {
         const tts_tensor * c = sole_consumer(mm);
         if (!c) return false;
@@ -485,6 +523,9 @@ struct Planner {
             skips.push_back(index[c]);
             return true;
         }
+        // mm -> RESHAPE -> repeat copies (repeat_target; any mismatch falls through to the transpose chain below: Parler's V store starts with a
+        // RESHAPE too)
+        if (c->op == TTS_OP_RESHAPE && c->src[0] == mm && c->type == TTS_TYPE_F32 && repeat_target(mm, c, N, t, skips)) return true;
         // mm -> [RESHAPE] -> TRANSPOSE -> CONT -> CPY
         const tts_tensor * v = c;
         std::vector<int> vs;
@@ -1730,11 +1771,19 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             const tts_tensor * a = it.mms[k]->src[0];
             // matrices of another row count share a launch only on the tile-layout kernels
             if (jj.nmat > 0 && a->ne[1] != jj.N && !jj.tiled) break;
-            if (a->ne[1] != jj.N) jj.hetero = 1;
+            if (it.tgt[k].rg > 0 && jj.rep_mat >= 0) break;  // one repeat-copy target per launch
+            if (jj.nmat > 0 && a->ne[1] != jj.N) jj.hetero = 1;
             jj.W[jj.nmat] = (const uint8_t *)weight_ptr(be, a, use_copy && !(a->flags & TTS_FLAG_TILED));
             jj.Y[jj.nmat] = it.tgt[k].y;
             jj.ycs[jj.nmat] = it.tgt[k].ycs;
             jj.yrs[jj.nmat] = it.tgt[k].yrs;
+            if (it.tgt[k].rg > 0) {
+                jj.rep_mat = jj.nmat;
+                jj.yrg = it.tgt[k].rg;
+                jj.yrgs = it.tgt[k].rgs;
+                jj.nrep = it.tgt[k].nrep;
+                jj.yrep = it.tgt[k].rep;
+            }
             if (jj.nmat == 0) jj.N = a->ne[1];
             jj.roff[jj.nmat + 1] = jj.roff[jj.nmat] + a->ne[1];
             jj.nmat++;

@@ -205,6 +205,11 @@ struct GemvJob {
     // roff[m] .. roff[m + 1] - 1 (each a multiple of 16); otherwise N rows each
     int hetero = 0;
     int64_t roff[GEMV_MAX_MATS + 1] = {};
+    // matrix rep_mat (at most one per launch; -1 = none) is written straight into the GQA copies of a
+    // KV cache: row n -> (n / yrg) * yrgs + (n % yrg) * yrs, stored at +k * yrep for k < nrep.  Kept to
+    // a few scalars: the job is a kernel argument re-set in every recorded step graph.
+    int32_t rep_mat = -1, yrg = 0, nrep = 0;
+    int64_t yrgs = 0, yrep = 0;
     int dbg = 0;    // phase study (TTS_HIP_OPT_GEMV_DEBUG): 1 = skip the row phase, 2 = skip the prologue
     const float * lnw = nullptr;
     const float * lnb = nullptr;

@@ -162,6 +162,12 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
     } else if (j.epi == EPI_ADD) {
         v = __fadd_rn(v, j.res[m * j.rcs + row]);
     }
+    if (mat == j.rep_mat) {
+        const int64_t g = row / j.yrg;
+        float * y = j.Y[mat] + m * j.ycs[mat] + g * j.yrgs + (row - g * j.yrg) * j.yrs[mat];
+        for (int k = 0; k < j.nrep; ++k) y[k * j.yrep] = v;
+        return;
+    }
     j.Y[mat][m * j.ycs[mat] + row * j.yrs[mat]] = v;
 }
 
