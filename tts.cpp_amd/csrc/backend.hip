@@ -91,6 +91,8 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     for (auto e : be->pin_events) hipEventDestroy(e);
     for (auto e : be->plan_ev) hipEventDestroy(e);
     hipHostFree(be->pin);
+    for (auto & kv : be->tiled_copy) hipFree(kv.second);  // tile-layout copies of medium Q4_K weights
+    be->tiled_copy.clear();
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->argmax_keys);
