@@ -87,3 +87,12 @@ def test_orpheus_tiny_tiled_fusion_masks(hip, drop):
     each related fusion pattern switched off in turn: tokens bit-exact, logits within the bar."""
     mask = ttship.FUSE_ALL if drop == "none" else ttship.FUSE_ALL & ~ttship.FUSE[drop]
     run_pair(hip, TINY, 8, 4, 6, tile_bytes=1, mask=mask)
+
+
+@pytest.mark.gpu
+def test_orpheus_hd128_mid_context(hip):
+    """head_size 128 at 65..127 keys: the row attention kernel over Orpheus' strided (transposed-view) V
+    with every V value requested before the softmax."""
+    cfg = dict(n_layers=1, hidden_size=512, n_attn_heads=4, n_kv_attn_heads=2, head_size=128, ffn_size=512,
+               vocab_size=1000, max_ctx=160)
+    run_pair(hip, cfg, 3, 70, 12)
