@@ -10,7 +10,7 @@ decoder inside the same timed region.  value = audio-seconds produced by all ran
 (RTF^-1) of AR + DAC; the AR-only and DAC-only rates are reported beside it.
 
 Beside the headline line's fields, three more legs of BASELINE.json's configs run on the same GPU:
-"kokoro" (configs[1], Kokoro-82M end to end: durations, decoder, iSTFTNet vocoder), "dia" (configs[3], Dia-1.6B Q8_0 CFG
+"kokoro" (configs[1], Kokoro-82M fp16 end to end: durations, decoder, iSTFTNet vocoder), "dia" (configs[3], Dia-1.6B Q8_0 CFG
 decode) and "orpheus" (configs[4]'s per-GPU shard, Orpheus-3B Q4_K decode), each with its own rate; the orpheus leg carries the dequant-GEMV
 roofline at the sizes where the matrix-core GEMV streams (every Orpheus matrix is >= 4 MiB).
 
@@ -309,7 +309,7 @@ def kokoro_leg(backends, args, rank, dist, local, world):
     R-th prompt from a host thread, as the server's workers each own a runner
     (examples/server/server.cpp:316-321): one prompt's host-side graph building overlaps another's
     device work."""
-    kcfg = ttship.kokoro_config(max_tokens=64, max_total=600)
+    kcfg = ttship.kokoro_config(max_tokens=64, max_total=600, weight_type=ttship.F16)  # configs[1]: Kokoro-82M fp16
     R = len(backends)
     koks = [ttship.Kokoro(b.iface(), kcfg) for b in backends]
     try:
@@ -341,7 +341,8 @@ def kokoro_leg(backends, args, rank, dist, local, world):
                 "first_prompt_ms": {"durations": round(1000 * (t2 - t1), 3), "decode": round(1000 * (t3 - t2), 3),
                                     "frames": int(lens.sum())},
                 "graph_nodes": [koks[0].last_graph_nodes(0), koks[0].last_graph_nodes(1)],
-                "dtype": "f32 activations and weights, f16 conv operands (ggml im2col), f64 conv accumulate"}
+                "dtype": "f16 weights (F16 GGUF: matrices and conv kernels, quantize_impl.cpp:14-18), f32 activations, f16-rounded "
+                         "mul_mat / conv inputs (ggml vec_dot_type, im2col), f64 accumulate"}
     finally:
         for k in koks:
             k.close()

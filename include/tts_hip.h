@@ -292,6 +292,45 @@ int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t
  * next[h*B + b] = step + 1 > h ? (eos_seen ? eos : token) : bos. */
 int tts_hip_greedy_step(tts_hip_backend_t backend, const float * logits, int32_t B, int32_t NH, int32_t V, int32_t step,
                         int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
+/* ---- seeded sampling (sampler::sample, /root/reference/src/sampler.cpp:3-62) ----
+ * The reference draws from std::minstd_rand(std::random_device{}()) on every call (:47), so its
+ * samples cannot be reproduced; here the generator of call c for prompt b is seeded with
+ * tts_sampler_call_seed(seed, b, c) and everything else is the reference's arithmetic: repetition
+ * penalty (v / pow(penalty, count) in double, for the last token only), temperature (f32 division),
+ * max-subtracted expf softmax with a sequential f32 sum (expf = the correctly rounded value, as every
+ * transcendental of this backend), top-k by the penalised logits (or by probability after a top-p
+ * softmax), top-p trimming, one std::uniform_real_distribution<float> draw per head in head order,
+ * then the first pick whose cumulative probability reaches the draw.  Ties in the top-k order go to
+ * the lower index (std::sort leaves them unspecified).  do_sample = 0 is sampler::max. */
+typedef struct tts_sampling {
+    float temperature;        /* 1.0 (generation_configuration defaults, include/common.h:45-66) */
+    float top_p;              /* 1.0 */
+    float repetition_penalty; /* 1.0 */
+    int32_t top_k;            /* 50 */
+    int32_t do_sample;        /* 1; 0 = greedy */
+    int32_t pad_;
+    uint64_t seed;
+} tts_sampling;
+void tts_sampling_default(tts_sampling * cfg);
+/* minstd_rand seed (1 .. 2^31 - 2) of sampler call `call` of prompt `stream`. */
+uint32_t tts_sampler_call_seed(uint64_t seed, int32_t stream, int64_t call);
+/* Host sampler: one sample() call over NH heads of V logits (logits are not modified); last /
+ * count [NH] are the repetition-penalty state (last = -1, count = 0 initially; updated only when
+ * the penalty is not 1), out [NH] the tokens. */
+int tts_sampler_sample(const tts_sampling * cfg, const float * logits, int32_t NH, int32_t V, uint32_t call_seed, int32_t * last,
+                       int32_t * count, int32_t * out);
+/* The same on the device for an AR step, followed by greedy_step's EOS / next-token rule:
+ * rows [B][NH] of logits [B][NH][V], prompt b's generator seeded with tts_sampler_call_seed(seed, b,
+ * call); rep_state [B*NH][2] (last, count) in device memory.  V <= 4096 (Parler, Dia) handles every
+ * configuration; wider vocabularies (Orpheus) need 0 < top_k <= 64 and top_p >= 1, else
+ * TTS_STATUS_UNSUPPORTED (the runner then samples on the host). */
+int tts_hip_sample_step(tts_hip_backend_t backend, const float * logits, int32_t B, int32_t NH, int32_t V, const tts_sampling * cfg,
+                        int64_t call, int32_t * rep_state, int32_t step, int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist,
+                        int32_t * next);
+/* Whether tts_hip_sample_step covers (cfg, V): runners sample on the host otherwise. */
+static inline int tts_sampling_device_ok(const tts_sampling * cfg, int32_t V) {
+    return V <= 4096 || !cfg->do_sample || (cfg->top_k > 0 && cfg->top_k <= 64 && cfg->top_p >= 1.0f);
+}
 /* Diagnostic counters since creation: out[0] HIP-graph exec updates, [1] instantiations,
  * [2] fused LSTM chains, [3] fused LSTM steps.  Returns the number written (<= n). */
 int tts_hip_counters(tts_hip_backend_t backend, int64_t * out, int n);
@@ -326,6 +365,9 @@ typedef struct tts_backend_iface {
     int (*copy)(void * ctx, void * dst, const void * src, size_t size);
     int (*greedy_step)(void * ctx, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                        int32_t * hist, int32_t * next);
+    /* optional (NULL or TTS_STATUS_UNSUPPORTED = sample on the host): tts_hip_sample_step */
+    int (*sample_step)(void * ctx, const float * logits, int B, int NH, int V, const tts_sampling * cfg, int64_t call, int32_t * rep_state,
+                       int step, int bos, int eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
 } tts_backend_iface;
 
 /* Fills `out` with the HIP backend's vtable. */

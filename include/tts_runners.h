@@ -58,6 +58,9 @@ int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out);
 /* 1 (default): greedy sampling stays on the device when the backend offers greedy_step (the host
  * never waits per step); 0: logits are read back and sampled on the host every step. */
 void tts_parler_set_device_sampling(tts_parler * p, int32_t on);
+/* Seeded sampling (sampler::sample, include/tts_hip.h tts_sampling) for tts_parler_generate; NULL =
+ * greedy (the default).  Prompt b of the batch draws from its own generator (stream b). */
+void tts_parler_set_sampling(tts_parler * p, const tts_sampling * cfg);
 int32_t tts_parler_position(const tts_parler * p);
 /* Host time per phase summed over steps (us): build graph, allocate, set inputs, compute enqueue,
  * wait for logits.  Returns the step count; reset zeroes the sums. */
@@ -109,6 +112,8 @@ int tts_orpheus_decode(tts_orpheus * p, const int32_t * tokens, float * logits);
 /* Greedy loop (generate_from_batch, sampler::max): feeds first_tokens [batch], then each step's samples;
  * writes tokens [batch][n_steps].  Samples stay on the device when the backend offers greedy_step. */
 int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_tokens, int32_t n_steps, int32_t * tokens_out);
+/* Seeded sampling for tts_orpheus_generate (NULL = greedy, the default); prompt b = stream b. */
+void tts_orpheus_set_sampling(tts_orpheus * p, const tts_sampling * cfg);
 int32_t tts_orpheus_position(const tts_orpheus * p);
 int32_t tts_orpheus_last_graph_nodes(const tts_orpheus * p);
 uint64_t tts_orpheus_weight_bytes(const tts_orpheus * p);
@@ -154,6 +159,8 @@ int tts_dia_decode(tts_dia * p, const int32_t * audio, float * logits);
  * logits (both CFG rows); writes tokens [n_steps][n_output_heads].  Device-resident when the backend
  * offers plans + greedy_step. */
 int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_t n_steps, int32_t * tokens_out);
+/* Seeded sampling of the CFG heads for tts_dia_generate (NULL = greedy, the default). */
+void tts_dia_set_sampling(tts_dia * p, const tts_sampling * cfg);
 int32_t tts_dia_position(const tts_dia * p);
 int32_t tts_dia_last_graph_nodes(const tts_dia * p);
 uint64_t tts_dia_weight_bytes(const tts_dia * p);
@@ -250,6 +257,8 @@ typedef struct tts_kokoro_gen_config {
     float voice_threshold;        /* 10 */
     int32_t max_frames;           /* generator input frames per call (arena sizing) */
     int32_t debug_no_reuse;       /* 1 = every node keeps its own arena memory (node dumps) */
+    int32_t weight_type;          /* TTS_TYPE_F32 (0) or TTS_TYPE_F16 (1): the F16 GGUF's matrices / conv kernels
+                                     (examples/quantize/quantize_impl.cpp:14-18 kokoro_is_f16_compatible) */
     uint64_t seed;                /* synthetic weight seed base */
     uint64_t arena_bytes;         /* compute arena (0 = sized from max_frames) */
 } tts_kokoro_gen_config;
@@ -310,6 +319,7 @@ typedef struct tts_kokoro_config {
     float dur_bias;            /* synthetic duration_proj bias (-2.6: ~4 frames per token) */
     float f0_mean;             /* synthetic F0 projection bias (Hz) */
     int32_t debug_no_reuse;
+    int32_t weight_type;       /* TTS_TYPE_F32 (0) or TTS_TYPE_F16 (1), for the whole model (gen.weight_type follows it) */
     uint64_t seed;
     uint64_t arena_bytes;      /* 0 = sized from max_tokens / max_total */
 } tts_kokoro_config;

@@ -822,6 +822,8 @@ static void op_im2col(tts_tensor * dst, int ith, int nth) {
  * ConvTranspose1d semantics (the fork's source is absent, its converters
  * keep torch's (IC, OC/g, K) weight order): y[oc, o] = sum over ic in oc's group, k with
  * o = i*s0 - p0 + k*d0 of x[i, ic] * w[k, oc mod OC/g, ic].  f64 accumulation, one rounding.
+ * An F16 kernel takes the input rounded to f16 first, as upstream ggml's conv_transpose_1d_f16_f32
+ * converts src1 (products f16 x f16, exact in f64).
  * op_params {s0, p0, d0, output_padding, groups}. */
 static void op_conv_transpose_1d(tts_tensor * dst, int ith, int nth) {
     const tts_tensor * a = dst->src[0];
@@ -842,7 +844,9 @@ static void op_conv_transpose_1d(tts_tensor * dst, int ith, int nth) {
                 if (i >= L) continue;
                 for (int64_t icl = 0; icl < ICg; ++icl) {
                     const int64_t ic = grp * ICg + icl;
-                    acc += (ggml_float)load_elem(b, i, ic, 0, 0) * (ggml_float)load_elem(a, k, ocl, ic, 0);
+                    float xv = load_elem(b, i, ic, 0, 0);
+                    if (a->type == TTS_TYPE_F16) xv = ref_fp16_to_fp32(ref_fp32_to_fp16(xv));
+                    acc += (ggml_float)xv * (ggml_float)load_elem(a, k, ocl, ic, 0);
                 }
             }
             *PF(dst, o, oc, 0, 0) = (float)acc;
@@ -1326,5 +1330,6 @@ int oracle_backend_iface(tts_backend_iface * out, int n_threads) {
     out->set_async = NULL;
     out->copy = NULL;
     out->greedy_step = NULL;
+    out->sample_step = NULL;
     return 0;
 }

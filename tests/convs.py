@@ -7,13 +7,15 @@ import ttship
 F32, F16 = ttship.F32, ttship.F16
 
 
-def conv_transpose_1d(g, x, w, s, p, d, op, grp):
-    """x: (IC, L) f32, w: torch layout (IC, OC/g, K) -> node [OL, OC]."""
+def conv_transpose_1d(g, x, w, s, p, d, op, grp, wtype=F32):
+    """x: (IC, L) f32, w: torch layout (IC, OC/g, K) -> node [OL, OC]; wtype F16: an F16 kernel
+    (Kokoro's F16 GGUF), whose product rounds the input to f16."""
     IC, L = x.shape
     K = w.shape[2]
     OC = w.shape[1] * grp
     OL = (L - 1) * s - 2 * p + d * (K - 1) + op + 1
-    return g.node("CONV_TRANSPOSE_1D", F32, [OL, OC], [g.leaf(w), g.leaf(x)], params=[s, p, d, op, grp])
+    wl = g.leaf(w.astype(np.float16) if wtype == F16 else w, typ=wtype)
+    return g.node("CONV_TRANSPOSE_1D", F32, [OL, OC], [wl, g.leaf(x)], params=[s, p, d, op, grp])
 
 
 def conv_1d(g, x, w, s, p, d, wtype=F32):

@@ -63,13 +63,20 @@ def uv_noise(cfg, f0, rand):
     return np.broadcast_to(uv, rand.shape).astype(np.float32), (amp[None, :] * rand).astype(np.float32)
 
 
-def generator(cfg, W, x, f0, style, rand, taps=None, har_branch=None):
+def _f16(t):
+    return t.to(torch.float16).to(torch.float32)
+
+
+def generator(cfg, W, x, f0, style, rand, taps=None, har_branch=None, f16=False):
     """x: (T, C) features, f0: (T,), style: (S,), rand: (H, 300T) -> (300T,) float32 PCM.
     taps: optional dict filled with the runner's named intermediates in its memory order.
     har_branch: the runner's "har_spec" node; where a phase sits on the +-pi branch cut (a real
     negative bin, e.g. frame 0, which reflect padding makes even) the two atan2s may land on
     opposite sides, so this restatement takes the runner's side of the cut (a 2*pi shift, not
-    a substitution of values)."""
+    a substitution of values).
+    f16: the F16 model (Kokoro weight_type F16): ggml's F16 mul_mat / conv_transpose_1d round
+    their input to f16 (vec_dot_type; conv_transpose_1d_f16_f32), so the sine merge and the
+    upsamplers see f16-rounded inputs here too."""
     taps = {} if taps is None else taps
     W = {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in W.items()}
     T = x.shape[0]
@@ -86,7 +93,7 @@ def generator(cfg, W, x, f0, style, rand, taps=None, har_branch=None):
     uv, noise = uv_noise(cfg, f0, rand)
     sines = torch.sin(up) * torch.from_numpy(uv) + torch.from_numpy(noise)
     taps["sine_source"] = sines.T
-    har = torch.tanh(W["gen.m_source_weight"].reshape(1, H) @ sines + W["gen.m_source_bias"].reshape(1, 1))
+    har = torch.tanh(W["gen.m_source_weight"].reshape(1, H) @ (_f16(sines) if f16 else sines) + W["gen.m_source_bias"].reshape(1, 1))
     win = hann(n_fft)
     spec = torch.stft(har, n_fft, hop, n_fft, window=win, center=True, pad_mode="reflect", return_complex=True)  # [1, nb, F]
     # the DFT of a real signal has an exactly real DC / Nyquist bin; torch's FFT leaves +-tiny
@@ -104,7 +111,7 @@ def generator(cfg, W, x, f0, style, rand, taps=None, har_branch=None):
         xs = F.leaky_relu(xs, 0.1)
         g = f"gen.ups.{i}"
         k, r = cfg.up_kernels[i], cfg.up_rates[i]
-        xs = F.conv_transpose1d(xs, W[g + ".weight"], W[g + ".bias"].reshape(-1), stride=r, padding=(k - r) // 2)
+        xs = F.conv_transpose1d(_f16(xs) if f16 else xs, W[g + ".weight"], W[g + ".bias"].reshape(-1), stride=r, padding=(k - r) // 2)
         if i == cfg.n_ups - 1:
             xs = F.pad(xs, (1, 0), mode="reflect")
         taps[f"up.{i}"] = xs[0]

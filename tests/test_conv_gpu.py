@@ -47,12 +47,13 @@ CT_CASES = [  # IC, OC, L, K, s, p, d, op, groups
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wtype", [F32, F16])
 @pytest.mark.parametrize("case", CT_CASES)
-def test_conv_transpose_1d(hip, case):
+def test_conv_transpose_1d(hip, case, wtype):
     IC, OC, L, K, s, p, d, op, grp = case
     x = rnd(1, IC, L)
     w = rnd(2, IC, OC // grp, K, scale=0.2)
-    (gpu, ref), = run_both(hip, lambda g: [convs.conv_transpose_1d(g, x, w, s, p, d, op, grp)])
+    (gpu, ref), = run_both(hip, lambda g: [convs.conv_transpose_1d(g, x, w, s, p, d, op, grp, wtype)])
     assert_rel(gpu, ref)
 
 

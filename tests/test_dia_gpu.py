@@ -15,11 +15,37 @@ TINY = dict(n_encoder_layers=1, n_decoder_layers=2, encoder_hidden_size=64, deco
 WIDE = dict(n_encoder_layers=1, n_decoder_layers=2, max_generation_size=32)
 
 
-def run_pair(hip, kw, steps):
+HARVARD = [b"The birch canoe slid on the smooth planks.", b"Glue the sheet to the dark blue background.",
+           b"It's easy to tell the depth of a well.", b"These days a chicken leg is a rare dish.",
+           b"Rice is often served in round bowls.", b"The juice of lemons makes fine punch.",
+           b"The box was thrown beside the parked truck.", b"The hogs were fed chopped corn and garbage.",
+           b"Four hours of steady work faced us.", b"A large size in stockings is hard to sell.",
+           b"The boy was there when the sun rose.", b"A rod is used to catch pink salmon.",
+           b"The source of the huge river is the clear spring.", b"Kick the ball straight and follow through.",
+           b"Help the woman get back to her feet.", b"A pot of tea helps to pass the evening.",
+           b"Smoky fires lack flame and heat.", b"The soft cushion broke the man's fall.",
+           b"The salt breeze came across from the sea.", b"The girl at the booth sold fifty bonds.",
+           b"The small pup gnawed a hole in the sock.", b"The fish twisted and turned on the bent hook.",
+           b"Press the pants and sew a button on the vest.", b"The swan dive was far short of perfect.",
+           b"The beauty of the view stunned the young boy.", b"Two blue fish swam in the tank."]
+
+
+def dialogue(n_chars):
+    """A two-speaker dialogue (Dia's [S1] / [S2] speaker tags as the tokenizer's bytes 0x01 / 0x02)
+    of Harvard sentences, cut to n_chars bytes."""
+    out, i = b"", 0
+    while len(out) < n_chars:
+        out += (b"\x01 " if i % 2 == 0 else b" \x02 ") + HARVARD[i % len(HARVARD)]
+        i += 1
+    return np.frombuffer(out[:n_chars], dtype=np.uint8).astype(np.int32)
+
+
+def run_pair(hip, kw, steps, text=None):
     g = ttship.Dia(hip.iface(), ttship.dia_config(**kw))
     c = ttship.Dia(py_oracle.iface(16), ttship.dia_config(**kw))
     try:
-        text = np.frombuffer(b"\x01 The birch canoe slid on the smooth planks. \x02 Glue the sheet.", dtype=np.uint8).astype(np.int32)
+        if text is None:
+            text = np.frombuffer(b"\x01 The birch canoe slid on the smooth planks. \x02 Glue the sheet.", dtype=np.uint8).astype(np.int32)
         text = text[: c.cfg.max_encoder_context_length]
         audio = np.full(9, 1026, dtype=np.int32)
         for s in range(steps + 1):
@@ -59,3 +85,13 @@ def test_dia_generate_device_loop(hip):
     finally:
         g.close()
         c.close()
+
+
+@pytest.mark.gpu
+def test_dia_full_depth_long_dialogue(hip):
+    """BASELINE configs[3] as configured: Dia-1.6B at full depth (18 decoder / 12 encoder layers,
+    src/models/dia/model.h:65-85) over a long two-speaker dialogue near the 1024-byte encoder cap
+    (model.cpp:668-670), 64 CFG decoder steps: argmax identical and logits within the bar every step."""
+    text = dialogue(1000)
+    assert len(text) == 1000
+    run_pair(hip, dict(max_generation_size=80), 64, text=text)

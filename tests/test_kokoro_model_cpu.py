@@ -35,9 +35,11 @@ def close(got, ref, name, rel=5e-3):
     assert err <= rel * max(scale, 1.0), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
 
 
-@pytest.mark.parametrize("n,seed", [(7, 0), (12, 1)])
-def test_kokoro_model_oracle_matches_torch(n, seed):
-    cfg = ttship.kokoro_config(**TINY, debug_no_reuse=1, arena_bytes=1 << 30)
+@pytest.mark.parametrize("n,seed,wtype", [(7, 0, ttship.F32), (12, 1, ttship.F32), (9, 2, ttship.F16)])
+def test_kokoro_model_oracle_matches_torch(n, seed, wtype):
+    """wtype F16: the F16 GGUF (quantize -qt F16 -nqf): the torch restatement runs on the widened f16
+    weights; the oracle's F16 mul_mats / convs also round their inputs to f16, inside the same bar."""
+    cfg = ttship.kokoro_config(**TINY, debug_no_reuse=1, arena_bytes=1 << 30, weight_type=wtype)
     k = ttship.Kokoro(py_oracle.iface(8), cfg)
     try:
         W = k.weights()
@@ -67,7 +69,7 @@ def test_kokoro_model_oracle_matches_torch(n, seed):
         x = k.node("decoder_out").reshape(2 * total, cfg.gen.in_channels)
         f0 = k.node("f0_out")
         s2, _ = kokoro_front_ref.styles(W, n)
-        ref = kokoro_ref.generator(cfg.gen, W, x, f0, s2.numpy(), rand, har_branch=k.node("har_spec"))
+        ref = kokoro_ref.generator(cfg.gen, W, x, f0, s2.numpy(), rand, har_branch=k.node("har_spec"), f16=wtype == ttship.F16)
         err = float(np.max(np.abs(pcm[:-cfg.gen.hop] - ref[:-cfg.gen.hop])))
         assert err <= 2e-3 * float(np.max(np.abs(ref))), err
         assert float(np.std(pcm)) > 1e-2
@@ -129,3 +131,40 @@ def test_kokoro_model_fusion_coverage():
     assert d["lstm"] == 4 * (1 + 8 + 1), d
     assert m["lstm"] > 2 * 2 * 8 and m["adain"] > 0 and m["conv"] > 0, m
     assert d["unfused"] < nd // 8 and m["unfused"] < nm // 8, (d, m)
+
+
+def test_kokoro_model_f16_weights_follow_quantize_rule():
+    """weight_type F16 stores exactly the tensors kokoro_is_f16_compatible names (matrices and conv
+    kernels; biases, norms, gamma / beta / alpha, embeddings and the voice pack stay F32), rounded to
+    f16; durations stay close to the F32 model's."""
+    cfg32 = ttship.kokoro_config(**TINY)
+    cfg16 = ttship.kokoro_config(**TINY, weight_type=ttship.F16)
+    a = ttship.Kokoro(py_oracle.iface(8), cfg32)
+    b = ttship.Kokoro(py_oracle.iface(8), cfg16)
+    try:
+        w32, w16 = a.weights(), b.weights()
+        assert w32.keys() == w16.keys()
+        n16 = 0
+        for name, v in w32.items():
+            excluded = (any(x in name for x in ("voice_tensors", "bias", "gamma", "beta", "alpha")) or name.endswith(("embd", "norm"))
+                        or name in ("stft_window", "harmonic_sampling_norm", "sampling_factor_scalar", "n_kernels_tensor", "one",
+                                    "sqrt_tensor"))
+            if np.array_equal(w16[name], v) and (excluded or v.size == v.shape[-1] and "kernel" not in name):
+                continue  # F32 (excluded by the rule, or a 1-D tensor)
+            assert not excluded, name
+            n16 += 1
+            assert np.array_equal(w16[name], v.astype(np.float16).astype(np.float32)), name
+        assert n16 > 50
+        toks = tokens(8, 4)
+        h32, l32 = a.durations(toks)
+        h16, l16 = b.durations(toks)
+        assert np.max(np.abs(h16 - h32)) < 5e-2 * max(1.0, float(np.max(np.abs(h32))))
+        p16 = b.decode(toks, h32, l32)
+        p32 = a.decode(toks, h32, l32)
+        assert p16.shape == p32.shape and np.all(np.isfinite(p16))
+        # (the iSTFT head's phases amplify the f16 weight rounding: the two models' PCM are different
+        # signals of the same scale, not an f16-level perturbation of each other)
+        assert not np.array_equal(p16, p32) and 0.5 < float(np.std(p16)) / float(np.std(p32)) < 2.0
+    finally:
+        a.close()
+        b.close()

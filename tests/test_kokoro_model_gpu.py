@@ -19,9 +19,14 @@ CFGS = {
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,n,seed", [("tiny", 7, 0), ("tiny", 13, 1), ("kokoro82m", 6, 2)])
-def test_kokoro_model_matches_oracle(hip, name, n, seed):
-    cfg = ttship.kokoro_config(**CFGS[name])
+@pytest.mark.parametrize("name,n,seed,wtype", [("tiny", 7, 0, ttship.F32), ("tiny", 13, 1, ttship.F32), ("kokoro82m", 6, 2, ttship.F32),
+                                               ("tiny", 11, 3, ttship.F16), ("kokoro82m", 6, 2, ttship.F16),
+                                               ("kokoro82m", 40, 5, ttship.F16)])
+def test_kokoro_model_matches_oracle(hip, name, n, seed, wtype):
+    """wtype F16 = BASELINE configs[1] (Kokoro-82M fp16): the F16 GGUF's matrices and conv kernels
+    (examples/quantize/quantize_impl.cpp:14-18), F16 mul_mats / convs / conv_transpose_1d with
+    f16-rounded inputs on both sides."""
+    cfg = ttship.kokoro_config(**dict(CFGS[name], weight_type=wtype, **({"max_tokens": 48, "max_total": 256} if n > 16 else {})))
     toks = tokens(n, seed)
     g = ttship.Kokoro(hip.iface(), cfg)
     o = ttship.Kokoro(py_oracle.iface(16), cfg)

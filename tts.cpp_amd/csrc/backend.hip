@@ -103,8 +103,10 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->conv_stage);
     hipFree(be->conv_part);
     hipFree(be->gelu_table);
+    if (be->sample_cand) hipFree(be->sample_cand);
     if (be->repack_tmp) hipFree(be->repack_tmp);
-    if (be->gexec) hipGraphExecDestroy(be->gexec);
+    for (auto & ex : be->gsig_exec)
+        if (ex) hipGraphExecDestroy(ex);
     for (auto & ex : be->pexec)
         if (ex) hipGraphExecDestroy(ex);
     hipStreamDestroy(be->stream);
@@ -124,19 +126,44 @@ void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {
     hipSetDevice(be->device);
     void * p = nullptr;
     if (hipMalloc(&p, size ? size : 256) != hipSuccess) return nullptr;
+    be->buffers[p] = size ? size : 256;
     return p;
+}
+
+// Tile-layout copies of weights inside [p, p + n): freed when their weight buffer goes away or its
+// bytes are overwritten by a plain tensor_set (a stale copy must never be read: run_gemv_item aborts
+// on a TILED_COPY weight whose copy is gone instead).
+static void drop_tiled_copies(tts_hip_backend_t be, const void * p, size_t n) {
+    const char * a = (const char *)p;
+    bool synced = false;
+    for (auto it = be->tiled_copy.begin(); it != be->tiled_copy.end();) {
+        const char * k = (const char *)it->first;
+        if (k >= a && k < a + n) {
+            if (!synced) hipStreamSynchronize(be->stream), synced = true;
+            hipFree(it->second);
+            it = be->tiled_copy.erase(it);
+        } else {
+            ++it;
+        }
+    }
 }
 
 void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
     if (!be || !ptr) return;
     hipSetDevice(be->device);
     hipStreamSynchronize(be->stream);
+    auto b = be->buffers.find(ptr);
+    if (b != be->buffers.end()) {
+        drop_tiled_copies(be, ptr, b->second);
+        be->buffers.erase(b);
+    }
     hipFree(ptr);
 }
 
 int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    if (!be->tiled_copy.empty()) drop_tiled_copies(be, dst, size);
     // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
     if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
     if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
@@ -191,6 +218,13 @@ int tts_hip_greedy_step(tts_hip_backend_t be, const float * logits, int32_t B, i
     hipSetDevice(be->device);
     launch_greedy_step(be, logits, B, NH, V, step, bos, eos, eos_seen, hist, next);
     return 0;
+}
+
+int tts_hip_sample_step(tts_hip_backend_t be, const float * logits, int32_t B, int32_t NH, int32_t V, const tts_sampling * cfg, int64_t call,
+                        int32_t * rep_state, int32_t step, int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next) {
+    if (!be || !logits || !cfg || B <= 0 || NH <= 0 || V <= 0) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return launch_sample_step(be, logits, B, NH, V, cfg, call, rep_state, step, bos, eos, eos_seen, hist, next);
 }
 
 int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
@@ -298,17 +332,12 @@ int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
     if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0) {
         std::vector<uint8_t> tmp(n);
         tts_repack_q4_K(src, tmp.data(), (int64_t)(n / 144), 0);
+        t->flags &= ~TTS_FLAG_TILED_COPY;  // a re-upload replaces the copy (tensor_set drops the old one)
         int st = tts_hip_tensor_set(be, t->data, tmp.data(), n);
         if (st == 0) t->flags |= TTS_FLAG_REPACKED;
-        auto old = be->tiled_copy.find(t->data);
-        if (old != be->tiled_copy.end()) {  // a re-upload replaces the copy
-            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
-            TTS_HIP_CHECK(hipFree(old->second));
-            be->tiled_copy.erase(old);
-            t->flags &= ~TTS_FLAG_TILED_COPY;
-        }
-        if (st == 0 && be->q4k_dual_bytes > 0 && (int64_t)n >= be->q4k_dual_bytes && t->ne[1] % 16 == 0 && t->ne[2] == 1 &&
-            t->ne[3] == 1) {
+        // (K >= 2048 only: run_gemv_item reads the copies of such matrices alone)
+        if (st == 0 && be->q4k_dual_bytes > 0 && (int64_t)n >= be->q4k_dual_bytes && t->ne[0] >= 2048 && t->ne[1] % 16 == 0 &&
+            t->ne[2] == 1 && t->ne[3] == 1) {
             // medium matrix: also a tile-layout copy for the matrix-core kernels at >= 8 columns
             tts_repack_q4_K_tiled(src, tmp.data(), t->ne[1], t->ne[0] / 256, 0);
             uint8_t * cp = nullptr;
@@ -485,6 +514,10 @@ static int hb_copy(void * c, void * d, const void * s, size_t n) { return tts_hi
 static int hb_greedy(void * c, const float * l, int B, int NH, int V, int step, int bos, int eos, int32_t * seen, int32_t * hist, int32_t * next) {
     return tts_hip_greedy_step((tts_hip_backend_t)c, l, B, NH, V, step, bos, eos, seen, hist, next);
 }
+static int hb_sample(void * c, const float * l, int B, int NH, int V, const tts_sampling * cfg, int64_t call, int32_t * rep, int step, int bos,
+                     int eos, int32_t * seen, int32_t * hist, int32_t * next) {
+    return tts_hip_sample_step((tts_hip_backend_t)c, l, B, NH, V, cfg, call, rep, step, bos, eos, seen, hist, next);
+}
 
 extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * out) {
     if (!be || !out) return TTS_STATUS_BAD_ARG;
@@ -503,5 +536,6 @@ extern "C" int tts_hip_backend_iface(tts_hip_backend_t be, tts_backend_iface * o
     out->set_async = hb_set_async;
     out->copy = hb_copy;
     out->greedy_step = hb_greedy;
+    out->sample_step = hb_sample;
     return 0;
 }

@@ -47,7 +47,17 @@ struct tts_dia {
     int32_t position = 0;
     int32_t prompt_size = 0;
     int32_t last_nodes = 0;
+    // seeded sampling of the CFG heads (tts_dia_set_sampling); greedy when off
+    bool sampling = false;
+    tts_sampling samp{};
+    int64_t sample_calls = 0;
+    std::vector<int32_t> rep_last, rep_count;  // [heads]
 };
+
+extern "C" void tts_dia_set_sampling(tts_dia * p, const tts_sampling * cfg) {
+    p->sampling = cfg != nullptr;
+    if (cfg) p->samp = *cfg;
+}
 
 extern "C" void tts_dia_default_config(tts_dia_config * c) {
     // dia_model defaults (src/models/dia/model.h:62-85); FFN widths of Dia-1.6B
@@ -417,6 +427,9 @@ extern "C" int tts_dia_prefill(tts_dia * p, const int32_t * text, int32_t n_text
     if (n_text < 1 || n_text > p->cfg.max_encoder_context_length) return TTS_STATUS_BAD_ARG;
     p->position = 0;
     p->prompt_size = n_text;
+    p->sample_calls = 0;  // a new prompt: sampler::reset (dia/model.cpp:883)
+    p->rep_last.assign(p->cfg.n_output_heads, -1);
+    p->rep_count.assign(p->cfg.n_output_heads, 0);
     return run_step(p, true, text, n_text, audio, logits);
 }
 
@@ -433,12 +446,20 @@ extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_
     auto & be = p->be;
     const int NH = cf.n_output_heads;
     if (p->prompt_size == 0 || n_steps <= 0) return n_steps <= 0 ? 0 : TTS_STATUS_FAILED;
-    if (!(be.greedy_step && be.set_async && be.copy && be.prepare && be.launch)) {
+    const bool dev_sample = !p->sampling || (be.sample_step && tts_sampling_device_ok(&p->samp, cf.output_vocab_size));
+    if (!(be.greedy_step && be.set_async && be.copy && be.prepare && be.launch && dev_sample)) {
         std::vector<float> lg((size_t)NH * cf.output_vocab_size);
         std::vector<int32_t> a(first_audio, first_audio + NH);
         for (int s = 0; s < n_steps; ++s) {
-            const int st = run_step(p, false, nullptr, 0, a.data(), lg.data());
+            int st = run_step(p, false, nullptr, 0, a.data(), lg.data());
             if (st != 0) return st;
+            if (p->sampling) {  // sampler::sample over the CFG-combined heads (dia/model.cpp:855)
+                st = tts_sampler_sample(&p->samp, lg.data(), NH, cf.output_vocab_size, tts_sampler_call_seed(p->samp.seed, 0, p->sample_calls++),
+                                        p->rep_last.data(), p->rep_count.data(), a.data());
+                if (st != 0) return st;
+                for (int h = 0; h < NH; ++h) tokens_out[(size_t)s * NH + h] = a[h];
+                continue;
+            }
             for (int h = 0; h < NH; ++h) {
                 const float * l = lg.data() + (size_t)h * cf.output_vocab_size;
                 int best = 0;
@@ -453,8 +474,14 @@ extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_
     int32_t * d_seen = (int32_t *)be.alloc(be.ctx, rowi);
     int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
     int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
-    int st = (d_seen && d_next && d_hist) ? 0 : TTS_STATUS_ALLOC_FAILED;
+    int32_t * d_rep = p->sampling ? (int32_t *)be.alloc(be.ctx, 2 * rowi) : nullptr;
+    int st = (d_seen && d_next && d_hist && (!p->sampling || d_rep)) ? 0 : TTS_STATUS_ALLOC_FAILED;
     if (st == 0) st = be.memset(be.ctx, d_seen, 0, rowi);
+    std::vector<int32_t> rep(2 * (size_t)NH);
+    if (st == 0 && d_rep) {
+        for (int h = 0; h < NH; ++h) rep[2 * h] = p->rep_last[h], rep[2 * h + 1] = p->rep_count[h];
+        st = be.set(be.ctx, d_rep, rep.data(), 2 * rowi);
+    }
     std::vector<int32_t> a2((size_t)NH * 2);
     for (int h = 0; h < NH; ++h) a2[h] = a2[NH + h] = first_audio[h];
     auto launch = [&](int slot, bool host_tokens) {
@@ -481,7 +508,11 @@ extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_
             next_out = p->res->data;
         }
         // step = NH: past every head's delay, so next = the sample itself (eos -1 never matches)
-        if (st == 0) st = be.greedy_step(be.ctx, (const float *)out, 1, NH, cf.output_vocab_size, NH, 0, -1, d_seen, d_hist + (size_t)s * NH, d_next);
+        if (st == 0 && p->sampling)
+            st = be.sample_step(be.ctx, (const float *)out, 1, NH, cf.output_vocab_size, &p->samp, p->sample_calls + s, d_rep, NH, 0, -1, d_seen,
+                                d_hist + (size_t)s * NH, d_next);
+        else if (st == 0)
+            st = be.greedy_step(be.ctx, (const float *)out, 1, NH, cf.output_vocab_size, NH, 0, -1, d_seen, d_hist + (size_t)s * NH, d_next);
         if (st == 0 && s + 1 < n_steps) {
             st = be.copy(be.ctx, p->in_audio->data, d_next, rowi);
             if (st == 0) st = be.copy(be.ctx, (int32_t *)p->in_audio->data + NH, d_next, rowi);
@@ -490,6 +521,12 @@ extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_
         }
     }
     if (st == 0) st = be.get(be.ctx, tokens_out, d_hist, rowi * (size_t)n_steps);
+    if (st == 0 && d_rep) {
+        st = be.get(be.ctx, rep.data(), d_rep, 2 * rowi);
+        for (int h = 0; h < NH; ++h) p->rep_last[h] = rep[2 * h], p->rep_count[h] = rep[2 * h + 1];
+    }
+    if (st == 0 && p->sampling) p->sample_calls += n_steps;
+    if (d_rep) be.free(be.ctx, d_rep);
     if (d_seen) be.free(be.ctx, d_seen);
     if (d_next) be.free(be.ctx, d_next);
     if (d_hist) be.free(be.ctx, d_hist);

@@ -65,6 +65,16 @@ bool contiguous(const tts_tensor * t) {
            t->nb[2] == t->nb[1] * (size_t)t->ne[1] && t->nb[3] == t->nb[2] * (size_t)t->ne[2];
 }
 
+// memory that outlives the graph: a leaf (model / input tensor) or a PERSIST tensor, through views
+bool persistent_mem(const tts_tensor * t) {
+    for (int hop = 0; t && hop < 8; ++hop) {
+        if (t->op == TTS_OP_NONE || (t->flags & TTS_FLAG_PERSIST)) return true;
+        if (!is_view(t->op)) return false;
+        t = t->view_src ? t->view_src : t->src[0];
+    }
+    return false;
+}
+
 bool is_1d_f32(const tts_tensor * t, int64_t n) {
     return t->type == TTS_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 && t->nb[0] == 4;
 }
@@ -88,6 +98,11 @@ bool is_gemv(const tts_tensor * n) {
     if (a->nb[0] != tts_type_size(a->type)) return false;
     // float weights against many columns (conv_1d's im2col GEMM) belong to the matrix cores
     if ((a->type == TTS_TYPE_F16 || a->type == TTS_TYPE_F32) && b->ne[1] * b->ne[2] * b->ne[3] > 64) return false;
+    // F16 weights against more than 8 columns (Kokoro's F16 ALBERT / duration projections): the f64
+    // matrix-core GEMM (launch_gemm_f16) instead of one GEMV launch per 8 columns
+    if (a->type == TTS_TYPE_F16 && b->ne[1] * b->ne[2] * b->ne[3] > 8 && a->ne[0] % 8 == 0 && (b->nb[1] % 16) == 0 &&
+        ((uintptr_t)b->data % 16) == 0 && (a->nb[1] % 16) == 0)
+        return false;
     switch (a->type) {
         case TTS_TYPE_Q4_K: return a->ne[0] % 256 == 0;
         case TTS_TYPE_Q8_0: return a->ne[0] % 32 == 0;
@@ -389,6 +404,8 @@ struct Planner {
             if (act[i] != 0 || C->op != TTS_OP_CONT || !C->src[0]) continue;
             const tts_tensor * s = C->src[0];
             if (s->type != C->type || !contiguous(s) || !contiguous(C) || uses[C] != 1) continue;
+            // the reader indexes its source by its own shape: a reshaping cont_Nd is not skippable
+            if (s->ne[0] != C->ne[0] || s->ne[1] != C->ne[1] || s->ne[2] != C->ne[2] || s->ne[3] != C->ne[3]) continue;
             if (C->flags & (TTS_FLAG_OUTPUT | TTS_FLAG_PERSIST)) continue;  // read after the graph: must be written
             const int r = next_real(i);
             if (r < 0 || act[r] != 0) continue;
@@ -955,7 +972,12 @@ struct Planner {
             P.stash_ok = P.stash_ok && pre->type == TTS_TYPE_F32 && pre->ne[0] == Hd && pre->ne[1] == T && pre->nb[1] == (size_t)Hd * 4 &&
                          contiguous(pre);
             for (int g2 = 0; g2 < g; ++g2) P.stash_ok = P.stash_ok && P.pre[g2] != pre;
+            // a paired chain runs late: what it reads besides the stashed projections (initial h / c,
+            // the biases) must be model / persistent memory, never arena memory a later node may reuse
+            const tts_tensor * bt = s0.g[g].addb->src[1];
+            P.stash_ok = P.stash_ok && persistent_mem(bt);
         }
+        P.stash_ok = P.stash_ok && persistent_mem(s0.hprev) && persistent_mem(s0.cprev);
         for (int64_t s = 0; s < T; ++s) {
             const LStep & S = st[seq[s]];
             LstmStepArgs a;
@@ -1449,6 +1471,7 @@ struct Planner {
                 if (rs->op == TTS_OP_CONT && act[index[rs]] == 0 && uses[rs] == 1 && rs->src[0] && rs->src[0]->type == rs->type &&
                     contiguous(rs) && contiguous(rs->src[0]) && only_views(index[rs], index[src])) {
                     bool ok2 = true;
+                    for (int d = 0; d < 4; ++d) ok2 &= rs->src[0]->ne[d] == rs->ne[d];  // k_rope indexes by rs's shape
                     for (int j : idx) ok2 &= !overlap(nodes[j], rs->src[0]);
                     if (ok2) {
                         act[index[rs]] = -1;
@@ -1928,13 +1951,32 @@ extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * 
     // Recording pays off when the same graph comes back (a decode step): the first call of a
     // shape launches eagerly, so one-shot graphs (a Kokoro prompt's duration / synthesis graphs,
     // whose sizes follow the prompt) never pay for a capture and an instantiation.
-    const bool repeat = n_nodes == be->last_compute_nodes;
-    be->last_compute_nodes = n_nodes;
-    if (!repeat || !capture_worthy(be, nodes, n_nodes)) return graph_compute_launches(be, nodes, n_nodes);
+    // signature: node count + every node's op + the first and last nodes' shapes (a decode step's
+    // graph repeats with the same topology; its data pointers may move, exec update handles that)
+    uint64_t sig = 0x9E3779B97F4A7C15ull ^ (uint64_t)n_nodes;
+    for (int i = 0; i < n_nodes; ++i) sig = (sig ^ (uint64_t)nodes[i]->op) * 0x100000001B3ull;
+    if (n_nodes > 0)
+        for (int d = 0; d < 4; ++d)
+            sig = (sig ^ (uint64_t)nodes[0]->ne[d] ^ ((uint64_t)nodes[n_nodes - 1]->ne[d] << 32)) * 0x100000001B3ull;
+    sig |= 1;  // 0 = empty slot
+    int slot = -1;
+    for (int k = 0; k < tts_hip_backend::N_GSIG; ++k)
+        if (be->gsig[k] == sig) slot = k;
+    if (slot < 0) {  // first sighting: launch eagerly, remember the shape
+        slot = be->gsig_next;
+        be->gsig_next = (be->gsig_next + 1) % tts_hip_backend::N_GSIG;
+        be->gsig[slot] = sig;
+        if (be->gsig_exec[slot]) {
+            TTS_HIP_CHECK(hipGraphExecDestroy(be->gsig_exec[slot]));
+            be->gsig_exec[slot] = nullptr;
+        }
+        return graph_compute_launches(be, nodes, n_nodes);
+    }
+    if (!capture_worthy(be, nodes, n_nodes)) return graph_compute_launches(be, nodes, n_nodes);
     // the step's launches replay back to back on the device instead of at the host's launch rate
-    const int st = capture_into(be, nodes, n_nodes, be->gexec);
+    const int st = capture_into(be, nodes, n_nodes, be->gsig_exec[slot]);
     if (st != 0) return st;
-    TTS_HIP_CHECK(hipGraphLaunch(be->gexec, be->stream));
+    TTS_HIP_CHECK(hipGraphLaunch(be->gsig_exec[slot], be->stream));
     return 0;
 }
 

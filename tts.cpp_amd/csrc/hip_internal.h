@@ -285,6 +285,9 @@ struct tts_hip_backend {
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)
     int64_t q4k_dual_bytes = 1 << 20;
     std::unordered_map<const void *, uint8_t *> tiled_copy;
+    void * sample_cand = nullptr;  // wide-vocabulary sampling candidates (k_sample.hip)
+    size_t sample_cand_size = 0;
+    std::unordered_map<const void *, size_t> buffers;  // live tts_hip_buffer_alloc ranges (base -> bytes)
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;
@@ -331,10 +334,15 @@ struct tts_hip_backend {
     size_t repack_tmp_size = 0;
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
-    int last_compute_nodes = -1;  // node count of the previous tts_hip_graph_compute (repeat detection)
+    // repeat detection for tts_hip_graph_compute: signatures of the last few graphs (node count, op
+    // sequence, first / last shapes), each with its own executable graph so interleaved runners
+    // (a decode step between vocoder calls) keep replaying
+    static constexpr int N_GSIG = 4;
+    uint64_t gsig[N_GSIG] = {};
+    hipGraphExec_t gsig_exec[N_GSIG] = {};
+    int gsig_next = 0;
     bool conv_f32acc = false;  // conv GEMM on f16 MFMA with f32 accumulation (faster, misses the PCM bar)
     int conv_acc_mode = 0;     // fused conv_1d: 0 = f64 MFMA, 2 = f16 MFMA per 32-term batch + f64 accumulation
-    hipGraphExec_t gexec = nullptr;
     hipStream_t cap_stream = nullptr;  // records graphs (never runs work)
     int64_t graph_updates = 0, graph_instantiations = 0;
     int64_t lstm_chains = 0, lstm_steps = 0;
@@ -380,6 +388,8 @@ void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_te
 void launch_rope_multi(tts_hip_backend * be, const tts_tensor * rope, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,
                         int32_t * hist, int32_t * next);
+int launch_sample_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, const tts_sampling * c, int64_t call,
+                       int32_t * rep_state, int step, int bos, int eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
 constexpr int EMBED_MAX_TERMS = 16;
 void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n);
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip);

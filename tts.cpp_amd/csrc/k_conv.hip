@@ -568,8 +568,14 @@ __global__ __launch_bounds__(256) void k_conv_transpose_1d(TD y, TD x, TD w, int
         if (i >= L) continue;
         const char * xp = x.data + i * x.nb[0] + (int64_t)grp * ICg * x.nb[1];
         const char * wp = w.data + (int64_t)k * w.nb[0] + (int64_t)ocl * w.nb[1] + (int64_t)grp * ICg * w.nb[2];
-        for (int icl = 0; icl < ICg; ++icl)
-            acc = __fma_rn((double)*(const float *)(xp + icl * x.nb[1]), (double)*(const float *)(wp + icl * w.nb[2]), acc);
+        if (w.type == TTS_TYPE_F16) {  // input rounded to f16 (upstream conv_transpose_1d_f16_f32)
+            for (int icl = 0; icl < ICg; ++icl)
+                acc = __fma_rn((double)__half2float(__float2half_rn(*(const float *)(xp + icl * x.nb[1]))),
+                               (double)__half2float(*(const __half *)(wp + icl * w.nb[2])), acc);
+        } else {
+            for (int icl = 0; icl < ICg; ++icl)
+                acc = __fma_rn((double)*(const float *)(xp + icl * x.nb[1]), (double)*(const float *)(wp + icl * w.nb[2]), acc);
+        }
     }
     *(float *)(y.data + o * y.nb[0] + (int64_t)oc * y.nb[1]) = (float)acc;
 }
@@ -603,8 +609,10 @@ __global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w,
             for (int u = 0; u < 4; ++u) {
                 const int ic = ic0 + 4 * u + kq;
                 const int icc = min(ic, IC - 1);
-                const float wa = *(const float *)(wp + (int64_t)icc * w.nb[2]);
-                const float xb = *(const float *)(xp + (int64_t)icc * x.nb[1]);
+                const bool w16 = w.type == TTS_TYPE_F16;
+                const float wa = w16 ? __half2float(*(const __half *)(wp + (int64_t)icc * w.nb[2])) : *(const float *)(wp + (int64_t)icc * w.nb[2]);
+                float xb = *(const float *)(xp + (int64_t)icc * x.nb[1]);
+                if (w16) xb = __half2float(__float2half_rn(xb));
                 av[u] = ic < IC ? (double)wa : 0.0;
                 bv[u] = (ic < IC && iin) ? (double)xb : 0.0;
             }
@@ -629,7 +637,7 @@ __global__ __launch_bounds__(64) void k_conv_transpose_1d_mfma(TD y, TD x, TD w,
 // v_mfma_f64_16x16x4_f64 over (ic quad, tap j, residue, channel half): one x operand feeds 2*S
 // products.  f32 x f32 products are exact in f64; only the f64 summation order differs from the
 // oracle (tests: rel 1e-5 per layer, PCM 1e-4 end to end).
-template <int S>
+template <int S, bool W16>
 __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, double * __restrict__ part = nullptr, int icps = 0) {
     constexpr int JM = 2, K = 2 * S;  // DAC / SNAC / Kokoro upsamplers: kernel = 2 * stride
     constexpr int QT = 64, OCT = 32, ICC = 16, XW = QT + JM - 1;
@@ -657,6 +665,7 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, 
             const int64_t pos = q0 - (JM - 1) + qq;
             const bool ok = t < NX && pos >= 0 && pos < L && ic0 + ic < IC;
             xr[u] = ok ? *(const float *)(x.data + pos * x.nb[0] + (int64_t)(ic0 + ic) * x.nb[1]) : 0.f;
+            if (W16) xr[u] = __half2float(__float2half_rn(xr[u]));  // F16 kernel: the input rounded to f16
         }
 #pragma unroll
         for (int u = 0; u < WR; ++u) {
@@ -664,8 +673,14 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, 
             const int ic = t / (K * OCT / 4), rem = (t - ic * (K * OCT / 4)) * 4;
             const int oc = rem / K;
             const bool ok = t < NW4 && oc0 + oc < OC && ic0 + ic < IC;
-            wr[u] = ok ? *(const float4 *)(w.data + (int64_t)(oc0 + oc) * w.nb[1] + (int64_t)(ic0 + ic) * w.nb[2] + (rem - oc * K) * 4)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+            const char * src = w.data + (int64_t)(oc0 + oc) * w.nb[1] + (int64_t)(ic0 + ic) * w.nb[2] + (rem - oc * K) * (W16 ? 2 : 4);
+            if (W16) {  // 4 taps = 8 B (K % 4 == 0 and 8-B aligned rows, host-checked)
+                const uint2 h = ok ? *(const uint2 *)src : make_uint2(0u, 0u);
+                wr[u] = make_float4(__half2float(__ushort_as_half((unsigned short)(h.x & 0xFFFF))), __half2float(__ushort_as_half((unsigned short)(h.x >> 16))),
+                                    __half2float(__ushort_as_half((unsigned short)(h.y & 0xFFFF))), __half2float(__ushort_as_half((unsigned short)(h.y >> 16))));
+            } else {
+                wr[u] = ok ? *(const float4 *)src : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
     };
     auto stage = [&]() {
@@ -737,8 +752,10 @@ void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
     const tts_tensor * w = node->src[0];
     const tts_tensor * x = node->src[1];
     const int s = node->op_params[0], p = node->op_params[1], d = node->op_params[2], g = node->op_params[4];
-    // the LDS kernel reads whole 4-tap float4 rows of the weight: contiguous taps (nb0 = 4), 16-B rows
-    const bool wvec = w->nb[0] == 4 && w->nb[1] % 16 == 0 && w->nb[2] % 16 == 0 && ((uintptr_t)w->data % 16) == 0;
+    // the LDS kernel reads whole 4-tap rows of the weight: contiguous taps, 16-B (F16: 8-B) aligned rows
+    const bool w16 = w->type == TTS_TYPE_F16;
+    const size_t wal = w16 ? 8 : 16;
+    const bool wvec = w->nb[0] == (w16 ? 2u : 4u) && w->nb[1] % wal == 0 && w->nb[2] % wal == 0 && ((uintptr_t)w->data % 16) == 0;
     if (d == 1 && g == 1 && w->ne[1] >= 16 && x->ne[1] >= 16 && (s == 2 || s == 4 || s == 6 || s == 8 || s == 10) && w->ne[0] == 2 * s && wvec &&
         be->convt_lds && node->nb[0] == 4) {
         const int64_t nq = (node->ne[0] + p) / s + 1;
@@ -751,11 +768,17 @@ void launch_conv_transpose_1d(tts_hip_backend * be, const tts_tensor * node) {
         const int icps = nz > 1 ? (int)(((nchunk + nz - 1) / nz) * 16) : 0;
         double * part = nz > 1 ? be->conv_part : nullptr;
         grid.z = nz > 1 ? (unsigned)((IC + icps - 1) / icps) : 1u;
-        if (s == 2) hipLaunchKernelGGL((k_convt_f64_lds<2>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
-        else if (s == 4) hipLaunchKernelGGL((k_convt_f64_lds<4>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
-        else if (s == 6) hipLaunchKernelGGL((k_convt_f64_lds<6>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
-        else if (s == 8) hipLaunchKernelGGL((k_convt_f64_lds<8>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
-        else hipLaunchKernelGGL((k_convt_f64_lds<10>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);
+#define TTS_CONVT_LDS(SS)                                                                                       \
+    do {                                                                                                        \
+        if (w16) hipLaunchKernelGGL((k_convt_f64_lds<SS, true>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);  \
+        else hipLaunchKernelGGL((k_convt_f64_lds<SS, false>), grid, dim3(256), 0, be->stream, Y, X, W, p, part, icps);     \
+    } while (0)
+        if (s == 2) TTS_CONVT_LDS(2);
+        else if (s == 4) TTS_CONVT_LDS(4);
+        else if (s == 6) TTS_CONVT_LDS(6);
+        else if (s == 8) TTS_CONVT_LDS(8);
+        else TTS_CONVT_LDS(10);
+#undef TTS_CONVT_LDS
         TTS_HIP_CHECK(hipGetLastError());
         if (part) launch_split_reduce(be, (int)grid.z, OL, OC, (float *)node->data, (int64_t)(node->nb[1] / 4), nullptr, 0, nullptr, 0);
         return;

@@ -130,7 +130,8 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemvJob j, int ks, const do
 }  // namespace
 
 bool gemm_f32_ok(const GemvJob & j) {
-    return j.wtype == TTS_TYPE_F32 && j.x && j.K > 0 && j.N > 0 && j.M > 0 && j.nmat >= 1 && (j.N + GT - 1) / GT <= INT32_MAX &&
+    // the tiled GEMM stores plain (column, row) targets: no GQA repeat copies, no mixed row counts
+    return j.rep_mat < 0 && !j.hetero && j.wtype == TTS_TYPE_F32 && j.x && j.K > 0 && j.N > 0 && j.M > 0 && j.nmat >= 1 && (j.N + GT - 1) / GT <= INT32_MAX &&
            (j.M + GT - 1) / GT <= 65535 && (j.w_row_bytes % 4) == 0 && (j.xcs >= j.K);
 }
 

@@ -1579,6 +1579,8 @@ static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
             GemvJob one = j;
             one.nmat = 1;
             one.W[0] = j.W[i], one.Y[0] = j.Y[i], one.ycs[0] = j.ycs[i], one.yrs[0] = j.yrs[i];
+            one.rep_mat = i == j.rep_mat ? 0 : -1;  // the repeat-copy target follows its matrix
+            one.roff[0] = 0, one.roff[1] = j.roff[i + 1] - j.roff[i];
             launch_gemv_q4k_mc<MC>(be, one);
         }
         return;

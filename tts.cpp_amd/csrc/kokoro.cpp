@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "graph.h"
+#include "common.h"
 #include "kokoro_gen.h"
 #include "synth.h"
 #include "tts_hip.h"
@@ -92,8 +93,11 @@ extern "C" void tts_kokoro_gen_default_config(tts_kokoro_gen_config * c) {
     c->arena_bytes = 0;
 }
 
-static tts_tensor * wnew(tts_kokoro_gen * k, float scale, float offset, int64_t ne0, int64_t ne1, int64_t ne2, const std::string & name) {
-    tts_tensor * t = ne1 == 0 ? tg::new_tensor_1d(k->wctx, TTS_TYPE_F32, ne0) : tg::new_tensor_3d(k->wctx, TTS_TYPE_F32, ne0, ne1, ne2);
+// gguf = false: a constant kokoro's post_load_assign builds (model.cpp:305-392), never in the file (F32)
+static tts_tensor * wnew(tts_kokoro_gen * k, float scale, float offset, int64_t ne0, int64_t ne1, int64_t ne2, const std::string & name,
+                         bool gguf = true) {
+    const int ty = gguf && k->cfg.weight_type == TTS_TYPE_F16 && kokoro_f16_tensor(name, ne1) ? TTS_TYPE_F16 : TTS_TYPE_F32;
+    tts_tensor * t = ne1 == 0 ? tg::new_tensor_1d(k->wctx, ty, ne0) : tg::new_tensor_3d(k->wctx, ty, ne0, ne1, ne2);
     tg::set_name(t, name);
     t->flags |= tg::TG_FLAG_PERSIST;
     k->specs.push_back({t, scale, offset, k->cfg.seed ^ (k->tensor_index++)});
@@ -148,10 +152,32 @@ static bool upload(tts_kokoro_gen * k) {
         off += (tg::nbytes(s.t) + 255) & ~(size_t)255;
         host.resize(n);
         synth_f32(host.data(), n, s.seed, s.scale, s.offset);
-        if (k->be.set_tensor(k->be.ctx, s.t, host.data()) != 0) return false;
+        if (!kokoro_upload_weight(k->be, s.t, host.data(), n)) return false;
     }
     return true;
 }
+
+namespace tts {
+bool kokoro_upload_weight(const tts_backend_iface & be, tts_tensor * t, const float * host, size_t n) {
+    if (t->type != TTS_TYPE_F16) return be.set_tensor(be.ctx, t, host) == 0;
+    std::vector<uint16_t> h(n);
+    for (size_t i = 0; i < n; ++i) h[i] = fp32_to_fp16_host(host[i]);
+    return be.set_tensor(be.ctx, t, h.data()) == 0;
+}
+
+// f32 values of a weight (F16 weights widened), for the tests' float references
+uint64_t kokoro_read_weight(const tts_backend_iface & be, const tts_tensor * t, float * dst, uint64_t cap) {
+    const uint64_t n = (uint64_t)tg::nelements(t) * 4;
+    if (!dst || cap < n) return n;
+    if (t->type == TTS_TYPE_F16) {
+        std::vector<uint16_t> h((size_t)tg::nelements(t));
+        if (be.get(be.ctx, h.data(), t->data, h.size() * 2) != 0) return 0;
+        for (size_t i = 0; i < h.size(); ++i) dst[i] = fp16_to_fp32_host(h[i]);
+        return n;
+    }
+    return be.get(be.ctx, dst, t->data, n) != 0 ? 0 : n;
+}
+}  // namespace tts
 
 extern "C" tts_kokoro_gen * tts_kokoro_gen_create(const tts_backend_iface * be, const tts_kokoro_gen_config * cfg) {
     const auto & c = *cfg;
@@ -198,11 +224,11 @@ extern "C" tts_kokoro_gen * tts_kokoro_gen_create(const tts_backend_iface * be, 
     k->out_w = conv_w(k, 7, ch, 2 * (c.n_fft / 2 + 1), "gen.conv_post.weight", 0.3f);
     k->out_b = wnew(k, 0.01f, 0.f, 1, 2 * nbins, 1, "gen.conv_post.bias");
     // post_load_assign constants (model.cpp:305-392): the values are set after the synthetic fill
-    k->window = wnew(k, 0.f, 0.f, c.n_fft, 0, 0, "stft_window");
-    k->harm_norm = wnew(k, 0.f, 0.f, 1, c.harmonic_num + 1, 1, "harmonic_sampling_norm");
-    k->samp_scalar = wnew(k, 0.f, 0.f, 1, 0, 0, "sampling_factor_scalar");
-    k->nker = wnew(k, 0.f, 0.f, 1, 0, 0, "n_kernels_tensor");
-    k->one = wnew(k, 0.f, 1.0f, 1, 1, 1, "one");
+    k->window = wnew(k, 0.f, 0.f, c.n_fft, 0, 0, "stft_window", false);
+    k->harm_norm = wnew(k, 0.f, 0.f, 1, c.harmonic_num + 1, 1, "harmonic_sampling_norm", false);
+    k->samp_scalar = wnew(k, 0.f, 0.f, 1, 0, 0, "sampling_factor_scalar", false);
+    k->nker = wnew(k, 0.f, 0.f, 1, 0, 0, "n_kernels_tensor", false);
+    k->one = wnew(k, 0.f, 1.0f, 1, 1, 1, "one", false);
     if (!upload(k)) {
         tts_kokoro_gen_free(k);
         return nullptr;
@@ -429,9 +455,7 @@ extern "C" uint64_t tts_kokoro_gen_weight(tts_kokoro_gen * k, int32_t i, char * 
     }
     if (ne)
         for (int d = 0; d < 4; ++d) ne[d] = t->ne[d];
-    const uint64_t n = tg::nbytes(t);
-    if (dst && cap >= n && k->be.get(k->be.ctx, dst, t->data, n) != 0) return 0;
-    return n;
+    return kokoro_read_weight(k->be, t, dst, cap);
 }
 
 // Debug: copy the named node of the last graph to host (contiguous nodes only); returns bytes.

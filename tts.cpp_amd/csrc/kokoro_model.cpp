@@ -131,10 +131,13 @@ extern "C" void tts_kokoro_default_config(tts_kokoro_config * c) {
     c->seed = 0x6B0C0F0ull;
 }
 
-static tts_tensor * wnew(tts_kokoro * k, float scale, float offset, int64_t ne0, int64_t ne1, int64_t ne2, const std::string & name) {
-    tts_tensor * t = ne1 == 0 ? tg::new_tensor_1d(k->wctx, TTS_TYPE_F32, ne0)
-                   : ne2 == 0 ? tg::new_tensor_2d(k->wctx, TTS_TYPE_F32, ne0, ne1)
-                              : tg::new_tensor_3d(k->wctx, TTS_TYPE_F32, ne0, ne1, ne2);
+// gguf = false: a constant built at load time (post_load_assign), never in the file (F32)
+static tts_tensor * wnew(tts_kokoro * k, float scale, float offset, int64_t ne0, int64_t ne1, int64_t ne2, const std::string & name,
+                         bool gguf = true) {
+    const int ty = gguf && k->cfg.weight_type == TTS_TYPE_F16 && kokoro_f16_tensor(name, ne1) ? TTS_TYPE_F16 : TTS_TYPE_F32;
+    tts_tensor * t = ne1 == 0 ? tg::new_tensor_1d(k->wctx, ty, ne0)
+                   : ne2 == 0 ? tg::new_tensor_2d(k->wctx, ty, ne0, ne1)
+                              : tg::new_tensor_3d(k->wctx, ty, ne0, ne1, ne2);
     tg::set_name(t, name);
     t->flags |= tg::TG_FLAG_PERSIST;
     k->specs.push_back({t, scale, offset, k->cfg.seed ^ (k->tensor_index++ * 0x9E3779B97F4A7C15ull)});
@@ -206,7 +209,7 @@ static bool upload(tts_kokoro * k) {
         off += (tg::nbytes(s.t) + 255) & ~(size_t)255;
         host.resize(n);
         synth_f32(host.data(), n, s.seed, s.scale, s.offset);
-        if (k->be.set_tensor(k->be.ctx, s.t, host.data()) != 0) return false;
+        if (!kokoro_upload_weight(k->be, s.t, host.data(), n)) return false;
     }
     return true;
 }
@@ -222,6 +225,7 @@ extern "C" tts_kokoro * tts_kokoro_create(const tts_backend_iface * be, const tt
     k->be = *be;
     // the generator runs inside the main graph: its own arena is unused
     tts_kokoro_gen_config gc = c.gen;
+    gc.weight_type = c.weight_type;
     gc.max_frames = 2 * c.max_total;
     gc.arena_bytes = 256;
     k->gen = tts_kokoro_gen_create(be, &gc);
@@ -312,7 +316,7 @@ extern "C" tts_kokoro * tts_kokoro_create(const tts_backend_iface * be, const tt
                                   "decoder.decoder_blocks." + std::to_string(i)));
     }
     k->voice = wnew(k, 0.5f, 0.f, 2 * S, c.n_voice_rows, 0, "voice_tensors.synthetic");
-    k->sqrt2 = wnew(k, 0.f, (float)std::sqrt(2.0), 1, 0, 0, "sqrt_tensor");
+    k->sqrt2 = wnew(k, 0.f, (float)std::sqrt(2.0), 1, 0, 0, "sqrt_tensor", false);
     if (!upload(k)) {
         tts_kokoro_free(k);
         return nullptr;
@@ -700,9 +704,7 @@ extern "C" uint64_t tts_kokoro_weight(tts_kokoro * k, int32_t i, char * name, ui
     }
     if (ne)
         for (int d = 0; d < 4; ++d) ne[d] = t->ne[d];
-    const uint64_t nb = tg::nbytes(t);
-    if (dst && cap >= nb && k->be.get(k->be.ctx, dst, t->data, nb) != 0) return 0;
-    return nb;
+    return kokoro_read_weight(k->be, t, dst, cap);
 }
 
 extern "C" uint64_t tts_kokoro_get_node(tts_kokoro * k, int32_t which, const char * name, void * dst, uint64_t cap) {

@@ -47,7 +47,17 @@ struct tts_orpheus {
     int64_t host_steps = 0;
     std::vector<std::vector<int32_t>> output_tokens;
     uint64_t tensor_index = 0;
+    // seeded sampling (tts_orpheus_set_sampling); greedy when off
+    bool sampling = false;
+    tts_sampling samp{};
+    int64_t sample_calls = 0;
+    std::vector<int32_t> rep_last, rep_count;  // [batch]
 };
+
+extern "C" void tts_orpheus_set_sampling(tts_orpheus * p, const tts_sampling * cfg) {
+    p->sampling = cfg != nullptr;
+    if (cfg) p->samp = *cfg;
+}
 
 extern "C" void tts_orpheus_default_config(tts_orpheus_config * c) {
     // orpheus_model defaults (src/models/orpheus/model.h:31-46); Llama-3.2-3B rope scaling
@@ -202,6 +212,9 @@ extern "C" void tts_orpheus_reset(tts_orpheus * p) {
     p->position = 0;
     p->prepared = false;
     p->output_tokens.assign(p->cfg.batch, {});
+    p->sample_calls = 0;  // sampler::reset (orpheus/model.cpp:426)
+    p->rep_last.assign(p->cfg.batch, -1);
+    p->rep_count.assign(p->cfg.batch, 0);
 }
 
 static tts_tensor * rms_norm_mul(tg::context & c, tts_tensor * x, tts_tensor * w) {
@@ -395,20 +408,31 @@ extern "C" int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_token
     auto & be = p->be;
     if (n_steps <= 0) return 0;
     if (p->prepared && p->prep_n != 1) return TTS_STATUS_FAILED;
-    if (be.greedy_step && be.set_async && be.copy && be.prepare) {
+    const bool dev_sample = !p->sampling || (be.sample_step && tts_sampling_device_ok(&p->samp, (int32_t)V));
+    if (be.greedy_step && be.set_async && be.copy && be.prepare && dev_sample) {
         const size_t rowi = (size_t)B * sizeof(int32_t);
         int32_t * d_seen = (int32_t *)be.alloc(be.ctx, rowi);
         int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
         int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
-        int st = (d_seen && d_next && d_hist) ? 0 : TTS_STATUS_ALLOC_FAILED;
+        int32_t * d_rep = p->sampling ? (int32_t *)be.alloc(be.ctx, 2 * rowi) : nullptr;
+        int st = (d_seen && d_next && d_hist && (!p->sampling || d_rep)) ? 0 : TTS_STATUS_ALLOC_FAILED;
         if (st == 0) st = be.memset(be.ctx, d_seen, 0, rowi);
+        std::vector<int32_t> rep(2 * (size_t)B);
+        if (st == 0 && d_rep) {
+            for (int b = 0; b < B; ++b) rep[2 * b] = p->rep_last[b], rep[2 * b + 1] = p->rep_count[b];
+            st = be.set(be.ctx, d_rep, rep.data(), 2 * rowi);
+        }
         if (st == 0 && !p->prepared) st = prepare_step(p, 1);
         if (st == 0) st = launch_step(p, first_tokens, true);
         for (int s = 0; st == 0 && s < n_steps; ++s) {
             const float * logits = (const float *)p->launched_out;
             if (s + 1 < n_steps) st = prepare_step(p, 1);  // recorded while the device runs step s
             // one head, no BOS / EOS rule (eos -1): next = the sample itself
-            if (st == 0) st = be.greedy_step(be.ctx, logits, B, 1, (int32_t)V, 0, 0, -1, d_seen, d_hist + (size_t)s * B, d_next);
+            if (st == 0 && p->sampling)
+                st = be.sample_step(be.ctx, logits, B, 1, (int32_t)V, &p->samp, p->sample_calls + s, d_rep, 0, 0, -1, d_seen, d_hist + (size_t)s * B,
+                                    d_next);
+            else if (st == 0)
+                st = be.greedy_step(be.ctx, logits, B, 1, (int32_t)V, 0, 0, -1, d_seen, d_hist + (size_t)s * B, d_next);
             if (st == 0 && s + 1 < n_steps) {
                 st = be.copy(be.ctx, p->in_tokens->data, d_next, rowi);
                 if (st == 0) st = launch_step(p, nullptr, true);
@@ -416,6 +440,12 @@ extern "C" int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_token
         }
         std::vector<int32_t> hist((size_t)n_steps * B);
         if (st == 0) st = be.get(be.ctx, hist.data(), d_hist, hist.size() * sizeof(int32_t));
+        if (st == 0 && d_rep) {
+            st = be.get(be.ctx, rep.data(), d_rep, 2 * rowi);
+            for (int b = 0; b < B; ++b) p->rep_last[b] = rep[2 * b], p->rep_count[b] = rep[2 * b + 1];
+        }
+        if (st == 0 && p->sampling) p->sample_calls += n_steps;
+        if (d_rep) be.free(be.ctx, d_rep);
         if (d_seen) be.free(be.ctx, d_seen);
         if (d_next) be.free(be.ctx, d_next);
         if (d_hist) be.free(be.ctx, d_hist);
@@ -433,10 +463,17 @@ extern "C" int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_token
         int st = decode(p, next.data(), 1, logits.data());
         if (st != 0) return st;
         for (int b = 0; b < B; ++b) {
-            next[b] = argmax(logits.data() + (size_t)b * V, V);
+            if (p->sampling) {  // sampler::sample (orpheus/model.cpp:392), prompt b's own generator
+                st = tts_sampler_sample(&p->samp, logits.data() + (size_t)b * V, 1, (int32_t)V, tts_sampler_call_seed(p->samp.seed, b, p->sample_calls),
+                                        &p->rep_last[b], &p->rep_count[b], &next[b]);
+                if (st != 0) return st;
+            } else {
+                next[b] = argmax(logits.data() + (size_t)b * V, V);
+            }
             p->output_tokens[b].push_back(next[b]);
             if (tokens_out) tokens_out[(size_t)b * n_steps + s] = next[b];
         }
+        if (p->sampling) p->sample_calls += 1;
     }
     return 0;
 }

@@ -58,6 +58,11 @@ struct tts_parler {
     std::vector<std::vector<int32_t>> output_tokens;  // per sequence, flat [steps][heads]
     std::vector<std::vector<char>> eos_seen;
     uint64_t tensor_index = 0;
+    // seeded sampling (tts_parler_set_sampling); greedy (sampler::max) when off
+    bool sampling = false;
+    tts_sampling samp{};
+    int64_t sample_calls = 0;                 // sampler::sample calls so far (one per step)
+    std::vector<int32_t> rep_last, rep_count;  // [batch][heads] repetition-penalty state
 };
 
 extern "C" void tts_parler_default_config(tts_parler_config * c) {
@@ -281,6 +286,14 @@ extern "C" void tts_parler_reset(tts_parler * p) {
     p->prepared = false;
     p->output_tokens.assign(p->cfg.batch, {});
     p->eos_seen.assign(p->cfg.batch, std::vector<char>(p->cfg.n_output_heads, 0));
+    p->sample_calls = 0;
+    p->rep_last.assign((size_t)p->cfg.batch * p->cfg.n_output_heads, -1);  // sampler::reset
+    p->rep_count.assign((size_t)p->cfg.batch * p->cfg.n_output_heads, 0);
+}
+
+extern "C" void tts_parler_set_sampling(tts_parler * p, const tts_sampling * cfg) {
+    p->sampling = cfg != nullptr;
+    if (cfg) p->samp = *cfg;
 }
 
 // build_parler_graph for n tokens per sequence (n = 1 in audio generation).
@@ -574,7 +587,13 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
     int32_t * d_seen = (int32_t *)be.alloc(be.ctx, rowi);
     int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
     int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
-    if (!d_seen || !d_next || !d_hist) return TTS_STATUS_ALLOC_FAILED;
+    int32_t * d_rep = p->sampling ? (int32_t *)be.alloc(be.ctx, 2 * rowi) : nullptr;
+    if (!d_seen || !d_next || !d_hist || (p->sampling && !d_rep)) return TTS_STATUS_ALLOC_FAILED;
+    std::vector<int32_t> rep(2 * (size_t)B * NH);
+    if (p->sampling) {
+        for (size_t r = 0; r < (size_t)B * NH; ++r) rep[2 * r] = p->rep_last[r], rep[2 * r + 1] = p->rep_count[r];
+        if (be.set(be.ctx, d_rep, rep.data(), 2 * rowi) != 0) return TTS_STATUS_FAILED;
+    }
     std::vector<int32_t> seen((size_t)B * NH), next((size_t)B * NH);
     for (int b = 0; b < B; ++b)
         for (int h = 0; h < NH; ++h) {
@@ -588,7 +607,10 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
     for (int s = 0; st == 0 && s < n_steps; ++s) {
         const float * logits = (const float *)p->launched_out;
         if (s + 1 < n_steps) st = prepare_step(p, true, 1);  // records step s+1 while the device runs step s
-        if (st == 0)
+        if (st == 0 && p->sampling)
+            st = be.sample_step(be.ctx, logits, B, NH, V, &p->samp, p->sample_calls + s, d_rep, p->current_step + s, cf.bos_token, cf.eos_token,
+                                d_seen, d_hist + (size_t)s * B * NH, d_next);
+        else if (st == 0)
             st = be.greedy_step(be.ctx, logits, B, NH, V, p->current_step + s, cf.bos_token, cf.eos_token, d_seen,
                                 d_hist + (size_t)s * B * NH, d_next);
         if (st == 0 && s + 1 < n_steps) {
@@ -599,6 +621,11 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
     std::vector<int32_t> hist((size_t)n_steps * B * NH);
     if (st == 0) st = be.get(be.ctx, hist.data(), d_hist, hist.size() * sizeof(int32_t));
     if (st == 0) st = be.get(be.ctx, seen.data(), d_seen, rowi);
+    if (st == 0 && d_rep) {
+        st = be.get(be.ctx, rep.data(), d_rep, 2 * rowi);
+        for (size_t r = 0; r < (size_t)B * NH; ++r) p->rep_last[r] = rep[2 * r], p->rep_count[r] = rep[2 * r + 1];
+    }
+    if (d_rep) be.free(be.ctx, d_rep);
     be.free(be.ctx, d_seen);
     be.free(be.ctx, d_next);
     be.free(be.ctx, d_hist);
@@ -613,13 +640,15 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
     for (int b = 0; b < B; ++b)
         for (int h = 0; h < NH; ++h) p->eos_seen[b][h] = seen[(size_t)b * NH + h] != 0;
     p->current_step += n_steps;
+    p->sample_calls += n_steps;
     return 0;
 }
 
 extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * tokens_out) {
     const auto & cf = p->cfg;
     if (n_steps <= 0) return 0;
-    if (p->be.greedy_step && p->be.set_async && p->be.copy && p->be.prepare && p->device_sampling)
+    const bool dev_sample = !p->sampling || (p->be.sample_step && tts_sampling_device_ok(&p->samp, cf.output_vocab));
+    if (p->be.greedy_step && p->be.set_async && p->be.copy && p->be.prepare && p->device_sampling && dev_sample)
         return generate_device(p, n_steps, tokens_out);
     const int B = cf.batch, NH = cf.n_output_heads;
     std::vector<float> logits((size_t)B * NH * cf.output_vocab);
@@ -643,9 +672,20 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
         if (st == 0 && s + 1 < n_steps) st = prepare_step(p, true, 1);  // overlaps the device's step s
         if (st == 0) st = finish_step(p, logits.data());
         if (st != 0) return st;
+        std::vector<int32_t> drawn((size_t)B * NH);
+        if (p->sampling) {  // sampler::sample per prompt, its own seeded generator
+            for (int b = 0; b < B; ++b) {
+                const int st2 = tts_sampler_sample(&p->samp, logits.data() + (size_t)b * NH * cf.output_vocab, NH, cf.output_vocab,
+                                                   tts_sampler_call_seed(p->samp.seed, b, p->sample_calls), &p->rep_last[(size_t)b * NH],
+                                                   &p->rep_count[(size_t)b * NH], &drawn[(size_t)b * NH]);
+                if (st2 != 0) return st2;
+            }
+            p->sample_calls += 1;
+        }
         for (int b = 0; b < B; ++b) {
             for (int h = 0; h < NH; ++h) {
-                const int32_t t = argmax_head(logits.data() + ((size_t)b * NH + h) * cf.output_vocab, cf.output_vocab);
+                const int32_t t = p->sampling ? drawn[(size_t)b * NH + h]
+                                              : argmax_head(logits.data() + ((size_t)b * NH + h) * cf.output_vocab, cf.output_vocab);
                 p->output_tokens[b].push_back(t);
                 if (tokens_out) tokens_out[((size_t)b * n_steps + s) * NH + h] = t;
                 p->eos_seen[b][h] = p->eos_seen[b][h] || t == cf.eos_token;

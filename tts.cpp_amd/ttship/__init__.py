@@ -71,7 +71,51 @@ class BackendIface(ctypes.Structure):
         ("set_async", ctypes.c_void_p),
         ("copy", ctypes.c_void_p),
         ("greedy_step", ctypes.c_void_p),
+        ("sample_step", ctypes.c_void_p),
     ]
+
+
+class Sampling(ctypes.Structure):
+    """tts_sampling (include/tts_hip.h): sampler::sample's configuration + the seed."""
+    _fields_ = [
+        ("temperature", ctypes.c_float),
+        ("top_p", ctypes.c_float),
+        ("repetition_penalty", ctypes.c_float),
+        ("top_k", ctypes.c_int32),
+        ("do_sample", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+def sampling(**kw):
+    """tts_sampling with generation_configuration defaults (top_k 50, temperature 1, sample)."""
+    c = Sampling()
+    lib().tts_sampling_default(ctypes.byref(c))
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def call_seed(seed, stream, call):
+    return int(lib().tts_sampler_call_seed(seed, stream, call))
+
+
+def host_sample(cfg, logits, call_seed_, last=None, count=None):
+    """Host sampler (tts_sampler_sample) over logits [NH, V]; last / count: int32 arrays updated in
+    place (repetition-penalty state).  Returns the NH tokens."""
+    import numpy as np
+    lg = np.ascontiguousarray(logits, dtype=np.float32)
+    NH, V = lg.shape
+    out = np.zeros(NH, dtype=np.int32)
+    if last is None:
+        last = np.full(NH, -1, dtype=np.int32)
+    if count is None:
+        count = np.zeros(NH, dtype=np.int32)
+    st = lib().tts_sampler_sample(ctypes.byref(cfg), lg.ctypes.data, NH, V, call_seed_, last.ctypes.data, count.ctypes.data, out.ctypes.data)
+    if st != 0:
+        raise RuntimeError(f"tts_sampler_sample failed {st}")
+    return out
 
 
 class ParlerConfig(ctypes.Structure):
@@ -185,6 +229,7 @@ class KokoroGenConfig(ctypes.Structure):
         ("voice_threshold", ctypes.c_float),
         ("max_frames", ctypes.c_int32),
         ("debug_no_reuse", ctypes.c_int32),
+        ("weight_type", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("arena_bytes", ctypes.c_uint64),
     ]
@@ -215,6 +260,7 @@ class KokoroConfig(ctypes.Structure):
         ("dur_bias", ctypes.c_float),
         ("f0_mean", ctypes.c_float),
         ("debug_no_reuse", ctypes.c_int32),
+        ("weight_type", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
         ("arena_bytes", ctypes.c_uint64),
     ]
@@ -266,6 +312,14 @@ def lib():
         "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
         "tts_hip_gemv_ex": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64, i32]),
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
+        "tts_sampling_default": (None, [ctypes.POINTER(Sampling)]),
+        "tts_parler_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
+        "tts_dia_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
+        "tts_orpheus_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
+        "tts_sampler_call_seed": (ctypes.c_uint32, [ctypes.c_uint64, i32, i64]),
+        "tts_sampler_sample": (ctypes.c_int, [ctypes.POINTER(Sampling), vp, i32, i32, ctypes.c_uint32, vp, vp, vp]),
+        "tts_hip_sample_step": (ctypes.c_int, [vp, vp, i32, i32, i32, ctypes.POINTER(Sampling), i64, vp, i32, i32, i32, vp, vp, vp]),
+        "tts_hip_greedy_step": (ctypes.c_int, [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp, vp]),
         "tts_hip_backend_iface": (ctypes.c_int, [vp, ctypes.POINTER(BackendIface)]),
         "tts_hip_weight_set": (ctypes.c_int, [vp, ctypes.POINTER(TtsTensor), vp]),
         "tts_hip_quantize": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, i64, i64]),
@@ -394,6 +448,33 @@ class HipBackend:
         if st != 0:
             raise RuntimeError(f"tensor_get failed {st}")
 
+    def sample_step(self, logits, cfg, call, rep_state=None, step=100, bos=-2, eos=-3, eos_seen=None):
+        """tts_hip_sample_step on logits [B, NH, V] (host arrays staged through device buffers).
+        Returns (tokens [B, NH], next [NH, B], eos_seen, rep_state)."""
+        import numpy as np
+        lg = np.ascontiguousarray(logits, dtype=np.float32)
+        B, NH, V = lg.shape
+        rs = np.ascontiguousarray(rep_state if rep_state is not None else np.tile(np.array([-1, 0], np.int32), B * NH), dtype=np.int32)
+        es = np.ascontiguousarray(eos_seen if eos_seen is not None else np.zeros(B * NH, np.int32), dtype=np.int32)
+        bufs = [self.alloc(n) for n in (lg.nbytes, rs.nbytes, es.nbytes, B * NH * 4, B * NH * 4)]
+        try:
+            self.set(bufs[0], lg)
+            self.set(bufs[1], rs)
+            self.set(bufs[2], es)
+            st = self.L.tts_hip_sample_step(self.ptr, bufs[0], B, NH, V, ctypes.byref(cfg), call, bufs[1], step, bos, eos, bufs[2], bufs[3], bufs[4])
+            if st != 0:
+                raise RuntimeError(f"tts_hip_sample_step failed {st}")
+            hist = np.zeros((B, NH), np.int32)
+            nxt = np.zeros((NH, B), np.int32)
+            self.get(hist, bufs[3])
+            self.get(nxt, bufs[4])
+            self.get(rs, bufs[1])
+            self.get(es, bufs[2])
+            return hist, nxt, es, rs
+        finally:
+            for b in bufs:
+                self.free(b)
+
     def quantize(self, wtype, x):
         """Device quantization of f32 rows x [N][K] to ggml Q4_K / Q8_0 bytes (host array out)."""
         import numpy as np
@@ -493,6 +574,11 @@ class Dia:
             raise RuntimeError(f"generate failed {st}")
         return out
 
+    def set_sampling(self, cfg=None):
+        """Seeded sampling (ttship.sampling(...)) for generate(); None = greedy."""
+        self._samp = cfg
+        self.L.tts_dia_set_sampling(self.ptr, ctypes.byref(cfg) if cfg is not None else None)
+
     def position(self):
         return self.L.tts_dia_position(self.ptr)
 
@@ -555,6 +641,11 @@ class Orpheus:
         if st != 0:
             raise RuntimeError(f"generate failed {st}")
         return out
+
+    def set_sampling(self, cfg=None):
+        """Seeded sampling (ttship.sampling(...)) for generate(); None = greedy."""
+        self._samp = cfg
+        self.L.tts_orpheus_set_sampling(self.ptr, ctypes.byref(cfg) if cfg is not None else None)
 
     def position(self):
         return self.L.tts_orpheus_position(self.ptr)
@@ -630,6 +721,11 @@ class Parler:
     def set_device_sampling(self, on):
         """Greedy sampling on the device (default when the backend supports it) or on the host."""
         self.L.tts_parler_set_device_sampling(self.ptr, 1 if on else 0)
+
+    def set_sampling(self, cfg=None):
+        """Seeded sampling (ttship.sampling(...)) for generate(); None = greedy."""
+        self._samp = cfg
+        self.L.tts_parler_set_sampling(self.ptr, ctypes.byref(cfg) if cfg is not None else None)
 
     @property
     def position(self):
