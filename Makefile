@@ -52,3 +52,18 @@ variant-%:
 	for f in $(HIP_SRCS); do $(HIPCC) $(HIPFLAGS) $(VARIANT_DEFS_$*) -c $$f -o build/obj_$*/$$(basename $$f).o || exit 1; done
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(OUT)/$*/libtts_hip.so build/obj_$*/*.hip.o $(CPP_OBJS) -lpthread
 .PHONY: variant-%
+
+# The ggml backend adapter (src/ggml_backend), compiled against the ggml fork TTS.cpp builds with
+# (absent here): make ggml-adapter TTS_GGML_DIR=<checkout of mmwillet/ggml @ support-for-tts>
+ggml-adapter: $(OUT)/libtts_hip.so
+ifndef TTS_GGML_DIR
+	$(error set TTS_GGML_DIR to a checkout of the ggml fork (mmwillet/ggml, branch support-for-tts))
+endif
+	g++ -std=c++17 -O2 -fPIC -shared -I$(TTS_GGML_DIR)/include -I$(TTS_GGML_DIR)/src -Iinclude -Isrc/ggml_backend \
+	    src/ggml_backend/ggml-tts-hip.cpp -L$(OUT) -ltts_hip -Wl,-rpath,$(abspath $(OUT)) -o $(OUT)/libggml-tts-hip.so
+
+# syntax / API-usage check of the adapter against declaration-only stand-ins (tests/ggml_stub)
+adapter-check:
+	g++ -std=c++17 -fsyntax-only -Wall -Wextra -Itests/ggml_stub -Iinclude -Isrc/ggml_backend src/ggml_backend/ggml-tts-hip.cpp
+
+.PHONY: ggml-adapter adapter-check

@@ -184,6 +184,18 @@ const char * tts_op_name(int op);
 typedef struct tts_hip_backend * tts_hip_backend_t;
 
 int tts_hip_device_count(void);
+/* Free / total device memory of `device` (ggml_backend_device_i::get_memory). */
+int tts_hip_device_memory(int device, size_t * free_bytes, size_t * total_bytes);
+/* Stream events (ggml_backend_device_i::event_new / event_free / event_synchronize,
+ * ggml_backend_i::event_record / event_wait): an opaque hipEvent_t. */
+void * tts_hip_event_new(int device);
+void tts_hip_event_free(void * event);
+int tts_hip_event_record(tts_hip_backend_t backend, void * event);
+int tts_hip_event_wait(tts_hip_backend_t backend, void * event); /* the backend's stream waits for it */
+int tts_hip_event_synchronize(void * event);
+/* Whether `p` is device memory (UVA query): the adapter's set_tensor copies device-to-device when a
+ * caller hands it another backend's device buffer as the "host" source. */
+int tts_hip_is_device_pointer(const void * p);
 tts_hip_backend_t tts_hip_backend_init(int device); /* NULL if no device */
 void tts_hip_backend_free(tts_hip_backend_t backend);
 const char * tts_hip_backend_name(tts_hip_backend_t backend);
@@ -328,9 +340,7 @@ int tts_hip_sample_step(tts_hip_backend_t backend, const float * logits, int32_t
                         int64_t call, int32_t * rep_state, int32_t step, int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist,
                         int32_t * next);
 /* Whether tts_hip_sample_step covers (cfg, V): runners sample on the host otherwise. */
-static inline int tts_sampling_device_ok(const tts_sampling * cfg, int32_t V) {
-    return V <= 4096 || !cfg->do_sample || (cfg->top_k > 0 && cfg->top_k <= 64 && cfg->top_p >= 1.0f);
-}
+int tts_sampling_device_ok(const tts_sampling * cfg, int32_t V);
 /* Diagnostic counters since creation: out[0] HIP-graph exec updates, [1] instantiations,
  * [2] fused LSTM chains, [3] fused LSTM steps.  Returns the number written (<= n). */
 int tts_hip_counters(tts_hip_backend_t backend, int64_t * out, int n);

@@ -1,0 +1,28 @@
+// Declaration-only stand-in (compile check of the adapter; see README.md).  Not ggml.
+#pragma once
+#include "ggml.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+typedef struct ggml_backend_buffer_type * ggml_backend_buffer_type_t;
+typedef struct ggml_backend_event * ggml_backend_event_t;
+typedef struct ggml_backend * ggml_backend_t;
+typedef void * ggml_backend_graph_plan_t;
+typedef struct ggml_backend_reg * ggml_backend_reg_t;
+typedef struct ggml_backend_device * ggml_backend_dev_t;
+enum ggml_backend_buffer_usage { GGML_BACKEND_BUFFER_USAGE_ANY = 0, GGML_BACKEND_BUFFER_USAGE_WEIGHTS = 1, GGML_BACKEND_BUFFER_USAGE_COMPUTE = 2 };
+enum ggml_backend_dev_type { GGML_BACKEND_DEVICE_TYPE_CPU, GGML_BACKEND_DEVICE_TYPE_GPU, GGML_BACKEND_DEVICE_TYPE_ACCEL };
+struct ggml_backend_dev_caps { bool async; bool host_buffer; bool buffer_from_host_ptr; bool events; };
+struct ggml_backend_dev_props {
+    const char * name;
+    const char * description;
+    size_t memory_free;
+    size_t memory_total;
+    enum ggml_backend_dev_type type;
+    struct ggml_backend_dev_caps caps;
+};
+enum ggml_backend_buffer_usage ggml_backend_buffer_get_usage(ggml_backend_buffer_t buffer);
+bool ggml_backend_buffer_is_host(ggml_backend_buffer_t buffer);
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,40 @@
+"""The ggml backend adapter (src/ggml_backend/ggml-tts-hip.cpp) is a real source file:
+it compiles (syntax and API usage) against declaration-only stand-ins of the upstream ggml backend
+headers (tests/ggml_stub), uses only C-ABI entry points the library exports, fills every vtable slot
+§8(b) names, and routes weights without relying on the buffer's usage (TTS.cpp never sets it)."""
+import pathlib
+import re
+import subprocess
+
+import ttship
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+SRC = ROOT / "src" / "ggml_backend" / "ggml-tts-hip.cpp"
+
+
+def test_adapter_compiles_against_ggml_declarations():
+    r = subprocess.run(["make", "-s", "-C", str(ROOT), "adapter-check"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_adapter_uses_exported_abi_only():
+    import ctypes
+    lib = ctypes.CDLL(str(ttship.LIB_PATH))
+    used = set(re.findall(r"\b(tts_hip_[a-z_0-9]+|tts_(?:op|type)_name)\s*\(", SRC.read_text()))
+    assert len(used) > 15
+    for name in used:
+        assert hasattr(lib, name), name
+
+
+def test_adapter_fills_the_vtables():
+    s = SRC.read_text()
+    for slot in ["get_name", "get_device_count", "get_device", "get_proc_address",  # reg
+                 "get_description", "get_memory", "get_type", "get_props", "init_backend", "get_buffer_type",
+                 "supports_op", "supports_buft", "offload_op", "event_new", "event_free", "event_synchronize",  # device
+                 "alloc_buffer", "get_alignment", "get_max_size", "get_alloc_size", "is_host",  # buffer type
+                 "free_buffer", "get_base", "memset_tensor", "set_tensor", "get_tensor", "cpy_tensor", "clear",  # buffer
+                 "set_tensor_async", "get_tensor_async", "synchronize", "graph_compute", "event_record", "event_wait"]:
+        assert re.search(r"\." + slot + r"\s*=", s), slot
+    # weights are recognised by what is written, not by GGML_BACKEND_BUFFER_USAGE_WEIGHTS
+    assert "USAGE_WEIGHTS" not in s
+    assert "tts_hip_weight_set" in s and "tts_hip_weight_get" in s

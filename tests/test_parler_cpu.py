@@ -28,4 +28,22 @@ def test_parler_step_plan_coverage():
         assert st["xattn"] == L, st             # every cross-attention rides its query GEMV
         without = c.plan_stats(ttship.FUSE_ALL & ~ttship.FUSE["XATTN"])
         assert without["xattn"] == 0 and without["attn"] == 2 * L
+        # the reference's node order (parler_build_kv_store expands K / V first, Q at the attention):
+        # q / k / v still one launch per layer, the K / V cache stores in its epilogue
+        assert st["gemv_max_group"] >= 3, st
+        assert st["gemv"] == 6 * L + 1, st     # qkv, o, cross-q (+ cross-attention), cross-o, fc1, fc2; heads
+        c.close()
+
+
+def test_parler_node_order_is_the_reference_order():
+    """build_parler_graph's order: LN, K, its cache view and CPY, V, transpose, cont, view, CPY, ...,
+    then Q (model.cpp:544-548 with parler_build_kv_store :420-439): no reordering in the runner."""
+    c = _decoded(1)
+    try:
+        names = [c.node(i, cap=4)[0] for i in range(c.last_graph_nodes())]
+        mm = [i for i, o in enumerate(names) if o == "MUL_MAT"]
+        first_layer = names[mm[0]:mm[0] + 12]
+        assert first_layer[:4] == ["MUL_MAT", "VIEW", "CPY", "MUL_MAT"], first_layer
+        assert "TRANSPOSE" in first_layer and first_layer.count("CPY") == 2
+    finally:
         c.close()

@@ -119,6 +119,54 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
 
 const char * tts_hip_backend_name(tts_hip_backend_t be) { return be ? be->name : "HIP(null)"; }
 
+int tts_hip_device_memory(int device, size_t * free_bytes, size_t * total_bytes) {
+    if (device < 0 || device >= tts_hip_device_count()) return TTS_STATUS_NO_DEVICE;
+    int prev = 0;
+    hipGetDevice(&prev);
+    hipSetDevice(device);
+    size_t f = 0, t = 0;
+    const hipError_t e = hipMemGetInfo(&f, &t);
+    hipSetDevice(prev);
+    if (e != hipSuccess) return TTS_STATUS_FAILED;
+    if (free_bytes) *free_bytes = f;
+    if (total_bytes) *total_bytes = t;
+    return 0;
+}
+
+void * tts_hip_event_new(int device) {
+    if (device < 0 || device >= tts_hip_device_count()) return nullptr;
+    hipSetDevice(device);
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return (void *)ev;
+}
+void tts_hip_event_free(void * event) {
+    if (event) hipEventDestroy((hipEvent_t)event);
+}
+int tts_hip_event_record(tts_hip_backend_t be, void * event) {
+    if (!be || !event) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return hipEventRecord((hipEvent_t)event, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+int tts_hip_event_wait(tts_hip_backend_t be, void * event) {
+    if (!be || !event) return TTS_STATUS_BAD_ARG;
+    hipSetDevice(be->device);
+    return hipStreamWaitEvent(be->stream, (hipEvent_t)event, 0) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+int tts_hip_event_synchronize(void * event) {
+    if (!event) return TTS_STATUS_BAD_ARG;
+    return hipEventSynchronize((hipEvent_t)event) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+int tts_hip_is_device_pointer(const void * p) {
+    if (!p) return 0;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return a.type == hipMemoryTypeDevice ? 1 : 0;
+}
+
 size_t tts_hip_buffer_alignment(void) { return 256; }
 
 void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {

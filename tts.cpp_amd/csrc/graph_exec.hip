@@ -492,19 +492,21 @@ struct Planner {
     // KV-store fusion: the GEMV output goes straight into the CPY destination (decode, 1 token).
     // mm -> RESHAPE c [hd, nkv, n, B] -> CPY into each of 2-4 repeat-interleaved views of the cache
     // (Orpheus' V store, orpheus/model.cpp:194-228): row kvh * hd + d goes to every copy
+    // (c = the product itself or a RESHAPE of it; the copies may view another shape of the same
+    // elements -- the reference copies Orpheus' [H, n] V product into [hd, nkv, n] cache views)
     bool repeat_target(const tts_tensor * mm, const tts_tensor * c, int64_t N, GemvTarget & t, std::vector<int> & skips) {
-        (void)mm;
         auto ci = consumers.find(c);
         if (ci == consumers.end() || ci->second.size() < 2 || ci->second.size() > 4 || uses[c] != (int)ci->second.size()) return false;
         std::vector<int> idx(ci->second.begin(), ci->second.end());
         std::sort(idx.begin(), idx.end());
         const tts_tensor * D0 = nodes[idx[0]];
+        if (D0->ne[0] * D0->ne[1] * D0->ne[2] * D0->ne[3] != mm->ne[0] * mm->ne[1] * mm->ne[2] * mm->ne[3]) return false;
         int64_t rep = 0;
         for (size_t a = 0; a < idx.size(); ++a) {
             const tts_tensor * D = nodes[idx[a]];
             if (D->op != TTS_OP_CPY || D->src[0] != c || act[idx[a]] != 0 || D->type != TTS_TYPE_F32 || D->nb[0] != 4) return false;
             for (int k = 0; k < 4; ++k)
-                if (D->ne[k] != c->ne[k] || D->nb[k] != D0->nb[k]) return false;
+                if (D->ne[k] != D0->ne[k] || D->nb[k] != D0->nb[k]) return false;
             const int64_t d = ((const char *)D->data - (const char *)D0->data);
             if (d % 4) return false;
             if (a == 1) rep = d / 4;
@@ -512,14 +514,14 @@ struct Planner {
         }
         // rows: ne0 x ne1 = N; columns: the n x B of the product, one of them 1
         // the copies' runs of one row group are disjoint and fit inside the group stride
-        if (c->ne[0] * c->ne[1] != N || rep < c->ne[0] || rep * (int64_t)(idx.size() - 1) + c->ne[0] > (int64_t)(D0->nb[1] / 4))
+        if (D0->ne[0] * D0->ne[1] != N || rep < D0->ne[0] || rep * (int64_t)(idx.size() - 1) + D0->ne[0] > (int64_t)(D0->nb[1] / 4))
             return false;
-        if (c->ne[2] != 1 && c->ne[3] != 1) return false;
+        if (D0->ne[2] != 1 && D0->ne[3] != 1) return false;
         t.y = (float *)D0->data;
         t.yrs = 1;
-        t.rg = (int32_t)c->ne[0];
+        t.rg = (int32_t)D0->ne[0];
         t.rgs = (int64_t)(D0->nb[1] / 4);
-        t.ycs = (int64_t)((c->ne[2] == 1 ? D0->nb[3] : D0->nb[2]) / 4);
+        t.ycs = (int64_t)((D0->ne[2] == 1 ? D0->nb[3] : D0->nb[2]) / 4);
         t.nrep = (int32_t)idx.size();
         t.rep = rep;
         for (int k : idx) skips.push_back(k);
@@ -527,10 +529,12 @@ struct Planner {
     }
 
     bool kv_target(const tts_tensor * mm, int64_t M, GemvTarget & t, std::vector<int> & skips) {
-        const tts_tensor * c = sole_consumer(mm);
-        if (!c) return false;
         const int64_t N = mm->ne[0];
         if (mm->ne[1] != 1 && M != 1) return false;  // one token per column (decode)
+        // the product copied straight into 2-4 repeat-interleaved cache views
+        if (mm->type == TTS_TYPE_F32 && contiguous(mm) && repeat_target(mm, mm, N, t, skips)) return true;
+        const tts_tensor * c = sole_consumer(mm);
+        if (!c) return false;
         if (c->op == TTS_OP_CPY && c->src[0] == mm) {
             const tts_tensor * D = c;  // view of the K cache: [N] or [N, B] with row stride per sequence
             if (D->type != TTS_TYPE_F32 || D->nb[0] != 4 || D->ne[0] != N || D->ne[1] != M || D->ne[2] * D->ne[3] != 1) return false;
@@ -616,29 +620,87 @@ struct Planner {
         Item it;
         it.kind = Item::GEMV;
         std::vector<int> skips;
-        // group adjacent MUL_MATs sharing src1 and weight type/shape
-        int j = i;
-        while (j < n && (int)it.mms.size() < ((mask & TTS_FUSE_GROUP) ? GEMV_MAX_MATS : 1)) {
-            const tts_tensor * mm = nodes[j];
-            if (mm->op != TTS_OP_MUL_MAT || mm->src[1] != x || !is_gemv(mm)) break;
+        // Group MUL_MATs sharing src1 and weight type / shape into one launch at the first one's
+        // position.  The reference's node order separates them (parler_build_kv_store and
+        // orpheus_build_kv_store pull K and V -- and K's rope and cache copies -- in before Q), so the
+        // scan passes over views, the KV-store nodes of members already taken, and other nodes; a later
+        // product is hoisted over those only if its output (or cache target) overlaps nothing they read
+        // or write, and none of them writes src1.
+        auto compatible = [&](const tts_tensor * mm) {
             const tts_tensor * a = mm->src[0];
             // another row count: only Q4_K matrices the tile-layout kernels can read (stored tiled, or
             // with a tile-layout copy), each a multiple of 16 rows; run_gemv_item splits the launch
             // when it ends up on a lane-layout kernel
             const bool tl = a->type == TTS_TYPE_Q4_K && (a->flags & (TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) &&
                             (a0->flags & (TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) && a->ne[1] % 16 == 0 && a0->ne[1] % 16 == 0;
-            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->nb[1] != a0->nb[1] || (a->ne[1] != a0->ne[1] && !tl)) break;
-            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED)) && !tl) break;
-            GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
-            GemvTarget kt;
-            std::vector<int> ks;
-            if ((mask & TTS_FUSE_KV) && mm->ne[1] * mm->ne[2] * mm->ne[3] == M && kv_target(mm, M, kt, ks)) {
-                t = kt;
-                for (int s : ks) skips.push_back(s);
+            if (a->type != a0->type || a->ne[0] != a0->ne[0] || a->nb[1] != a0->nb[1] || (a->ne[1] != a0->ne[1] && !tl)) return false;
+            if (a->type == TTS_TYPE_Q4_K && ((a->flags ^ a0->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED)) && !tl) return false;
+            return true;
+        };
+        auto target_span = [&](const tts_tensor * mm, const GemvTarget & t, const char *& y0, const char *& y1) {
+            const int64_t Mm = mm->ne[1] * mm->ne[2] * mm->ne[3], rows = mm->ne[0];
+            int64_t last;
+            if (t.rg > 0) {
+                const int64_t g = (rows - 1) / t.rg;
+                last = (Mm - 1) * t.ycs + g * t.rgs + (rows - 1 - g * t.rg) * t.yrs + (int64_t)(t.nrep - 1) * t.rep;
+            } else {
+                last = (Mm - 1) * t.ycs + (rows - 1) * t.yrs;
             }
-            it.mms.push_back(mm);
-            it.tgt.push_back(t);
-            if (j > i) act[j] = -1;
+            y0 = (const char *)t.y;
+            y1 = y0 + 4 * (size_t)(last + 1);
+        };
+        auto hits = [&](const char * y0, const char * y1, const tts_tensor * u) {
+            if (!u || !u->data) return false;
+            const char * u0 = (const char *)u->data;
+            return y0 < u0 + tbytes(u) && u0 < y1;
+        };
+        std::vector<const tts_tensor *> passed;  // nodes the later members are hoisted over
+        const int max_mats = (mask & TTS_FUSE_GROUP) ? GEMV_MAX_MATS : 1;
+        const int jend = std::min(n, i + 96);
+        int j = i;
+        while (j < jend && (int)it.mms.size() < max_mats) {
+            const tts_tensor * mm = nodes[j];
+            const bool member = j == i || (act[j] == 0 && mm->op == TTS_OP_MUL_MAT && mm->src[1] == x && is_gemv(mm) && compatible(mm));
+            if (member) {
+                GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
+                GemvTarget kt;
+                std::vector<int> ks;
+                if ((mask & TTS_FUSE_KV) && mm->ne[1] * mm->ne[2] * mm->ne[3] == M && kv_target(mm, M, kt, ks)) t = kt;
+                else ks.clear();
+                bool ok = true;
+                if (j > i) {
+                    const char *y0, *y1;
+                    target_span(mm, t, y0, y1);
+                    for (const tts_tensor * u : passed) ok = ok && !hits(y0, y1, u);
+                    for (size_t k = 0; k < it.mms.size() && ok; ++k) {
+                        const char *z0, *z1;
+                        target_span(it.mms[k], it.tgt[k], z0, z1);
+                        ok = !(y0 < z1 && z0 < y1);
+                    }
+                }
+                if (ok) {
+                    for (int s2 : ks) skips.push_back(s2);
+                    it.mms.push_back(mm);
+                    it.tgt.push_back(t);
+                    if (j > i) act[j] = -1;
+                    ++j;
+                    continue;
+                }
+                // not hoistable: it stays where it is, as a node passed over
+            }
+            if (!(mask & TTS_FUSE_GROUP)) break;
+            if (std::find(skips.begin(), skips.end(), j) != skips.end()) {  // a member's KV store: absorbed
+                ++j;
+                continue;
+            }
+            if (act[j] == 0 && is_view(mm->op)) {
+                ++j;
+                continue;
+            }
+            if (act[j] != 0 || overlap(mm, x) || (int)passed.size() > 64) break;
+            passed.push_back(mm);
+            for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
+                if (mm->src[s2]) passed.push_back(mm->src[s2]);
             ++j;
         }
         if (it.mms.size() == 1 && (mask & TTS_FUSE_EPI)) {
@@ -1447,8 +1509,10 @@ struct Planner {
             for (size_t b = a + 1; b < idx.size(); ++b)
                 if (overlap(nodes[idx[a]], nodes[idx[b]]) && !interleaved(nodes[idx[a]], nodes[idx[b]])) return;
         }
+        // between the copies: views, copies, or nodes a GEMV item planned before this one absorbed
+        // (it ran earlier: act -1 with the product's launch at a lower position)
         for (int j = idx.front() + 1; j < idx.back(); ++j)
-            if (!is_view(nodes[j]->op) && nodes[j]->op != TTS_OP_CPY) return;
+            if (!is_view(nodes[j]->op) && nodes[j]->op != TTS_OP_CPY && act[j] != -1) return;
         Item m;
         m.kind = Item::MCPY;
         m.x = src;
@@ -2015,8 +2079,9 @@ extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
 }
 
 // Fusion coverage of a graph without a device (tests, tooling): counts[k] = items of kind k
-// (Item::Kind order), counts[14] = attention items folded into their query GEMV (TTS_FUSE_XATTN),
-// counts[15] = nodes still launched one by one.  Returns the item count.
+// (Item::Kind order), counts[12] = MUL_MATs inside GEMV items, counts[13] = the most in one item,
+// counts[14] = attention items folded into their query GEMV (TTS_FUSE_XATTN), counts[15] = nodes still
+// launched one by one.  Returns the item count.
 extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int mask, int32_t * counts) {
     Planner pl;
     pl.mask = mask;
@@ -2035,6 +2100,10 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     for (const Item & it : pl.items) {
         counts[(int)it.kind]++;
         if (it.xattn >= 0) counts[14]++;
+        if (it.kind == Item::GEMV) {
+            counts[12] += (int32_t)it.mms.size();  // products in GEMV launches
+            if ((int32_t)it.mms.size() > counts[13]) counts[13] = (int32_t)it.mms.size();
+        }
     }
     for (int i = 0; i < n_nodes; ++i)
         if (pl.act[i] == 0 && !is_view(nodes[i]->op)) counts[15]++;

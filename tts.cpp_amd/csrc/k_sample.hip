@@ -99,7 +99,7 @@ __device__ __forceinline__ float temper(const SampleArgs & a, const RowState & r
 // repetition-penalty update and greedy_step's EOS / next-token rule (thread 0 only)
 __device__ void finish_row(const SampleArgs & a, RowState & r, int row, int tok) {
     const int b = row / a.NH, h = row % a.NH;
-    if (r.rep) {
+    if (r.rep && a.do_sample) {  // sampler::max (do_sample = 0) leaves the penalty state alone
         if (r.last != tok) r.count = 0;
         r.last = tok;
         r.count += 1;

@@ -260,13 +260,12 @@ static tts_tensor * build_graph(tts_orpheus * p, int n) {
             tts_tensor * Qcur = tg::mul_mat(c, L.q, cur);
             tts_tensor * Kcur = tg::mul_mat(c, L.k, cur);
             tts_tensor * Vcur = tg::mul_mat(c, L.v, cur);
-            tg::build_forward_expand(c, Qcur);
-            tg::build_forward_expand(c, Kcur);
-            tg::build_forward_expand(c, Vcur);
-            // orpheus_build_kv_store (model.cpp:194-228): rope K, then `repeat` strided copies each of K and V
+            // orpheus_build_kv_store (model.cpp:194-228): rope K, then `repeat` strided copies each of K and
+            // V (V copied as the [H, n] product itself); the node order is the reference's (K's chain,
+            // then V, Q only at the attention), which the planner groups across (try_gemv)
             tts_tensor * kr = B == 1 ? tg::reshape_3d(c, Kcur, hd, nkv, n) : tg::reshape_4d(c, Kcur, hd, nkv, n, B);
             kr = rope(p, c, tg::cont(c, kr));
-            tts_tensor * vr = B == 1 ? tg::reshape_3d(c, Vcur, hd, nkv, n) : tg::reshape_4d(c, Vcur, hd, nkv, n, B);
+            tts_tensor * vr = Vcur;
             for (int i = 0; i < repeat; ++i) {
                 const size_t off = es * (size_t)H * p->position + (size_t)i * es * hd;
                 tts_tensor *kv, *vv;

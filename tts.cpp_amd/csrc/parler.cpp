@@ -362,12 +362,9 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
             tts_tensor * Qcur = tg::mul_mat(c, L.q, cur);
             tts_tensor * Kcur = tg::mul_mat(c, L.k, cur);
             tts_tensor * Vcur = tg::mul_mat(c, L.v, cur);
-            // node order: the three projections adjacent (same values as the reference's order,
-            // where the KV-store expands pull K and V in first; lets graph_compute fuse them)
-            tg::build_forward_expand(c, Qcur);
-            tg::build_forward_expand(c, Kcur);
-            tg::build_forward_expand(c, Vcur);
-            // parler_build_kv_store (model.cpp:420-439)
+            // parler_build_kv_store (model.cpp:420-439): its expands pull K and V into the node list
+            // first, Q follows at the attention -- the reference's order, which the planner groups
+            // across (graph_exec.hip try_gemv)
             if (B == 1) {
                 tts_tensor * kv = tg::view_1d(c, p->k_l[l], (int64_t)n * H, tts_row_size(TTS_TYPE_F32, H) * p->position);
                 tg::build_forward_expand(c, tg::cpy(c, Kcur, kv));

@@ -23,6 +23,10 @@ extern "C" void tts_sampling_default(tts_sampling * c) {
     c->seed = 0x5EED;
 }
 
+extern "C" int tts_sampling_device_ok(const tts_sampling * cfg, int32_t V) {
+    return V <= 4096 || !cfg->do_sample || (cfg->top_k > 0 && cfg->top_k <= 64 && cfg->top_p >= 1.0f);
+}
+
 extern "C" uint32_t tts_sampler_call_seed(uint64_t seed, int32_t stream, int64_t call) {
     uint64_t z = seed ^ ((uint64_t)(uint32_t)stream << 40) ^ ((uint64_t)call * 0x9E3779B97F4A7C15ull);
     z += 0x9E3779B97F4A7C15ull;  // splitmix64 finaliser
@@ -35,11 +39,6 @@ extern "C" uint32_t tts_sampler_call_seed(uint64_t seed, int32_t stream, int64_t
 namespace {
 
 inline float cr_expf_host(float x) { return (float)std::exp((double)x); }
-
-struct Head {
-    const float * l;  // logits of this head (read only)
-    std::vector<float> p;  // softmax output where the reference overwrites logits
-};
 
 }  // namespace
 

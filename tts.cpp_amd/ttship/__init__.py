@@ -1115,6 +1115,8 @@ def plan_stats(nodes_ptr, n_nodes, mask):
     counts = (ctypes.c_int32 * 16)()
     lib().tts_hip_plan_stats(nodes_ptr, n_nodes, mask, counts)
     out = {k: int(counts[i]) for i, k in enumerate(PLAN_KINDS)}
+    out["gemv_products"] = int(counts[12])
+    out["gemv_max_group"] = int(counts[13])
     out["xattn"] = int(counts[14])
     out["unfused"] = int(counts[15])
     return out
