@@ -152,38 +152,46 @@ def gather_audio(dist, rank, world, local, pcms):
 
 
 def cpu_baseline(args, n_threads):
-    """Oracle (C restatement of ggml-cpu) running the same Parler step graph and the same DAC graph
-    on host cores; end-to-end rate = 1 / (1/AR + 1/DAC) per audio-second."""
+    """Oracle (C restatement of ggml-cpu) on the GPU leg's workload shape, on host cores: the same
+    Parler step graph at the same batch (all of this GPU's prompts in one runner) and the same KV
+    length when timing starts (tts_parler_set_position: the prefill is skipped, the step's work is
+    the same), then the same DAC graph over a few frames per prompt; rates per audio-second,
+    end to end = 1 / (1/AR + 1/DAC)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import py_oracle
-    cfg = ttship.parler_config(batch=1, max_ctx=args.ctx + 64)
+    B = args.batch
+    cfg = ttship.parler_config(batch=B, max_ctx=args.ctx + 64)
     p = ttship.Parler(py_oracle.iface(n_threads), cfg)
     try:
-        p.prefill(prompt_tokens(1, 8, cfg.prompt_vocab))
+        p.prefill(prompt_tokens(B, 8, cfg.prompt_vocab))
+        p.set_position(args.ctx)
         p.generate(1)
         steps, t0 = 0, time.perf_counter()
         while steps < args.cpu_steps and (steps < 2 or time.perf_counter() - t0 < args.cpu_seconds):
             p.generate(1)
             steps += 1
         dt_ar = time.perf_counter() - t0
-        toks = p.generate(2)[0]
+        toks = p.generate(2)
     finally:
         p.close()
-    dcfg = ttship.dac_config(max_frames=2)
+    frames = 2
+    dcfg = ttship.dac_config(max_frames=frames)
     dac = ttship.Dac(py_oracle.iface(n_threads), dcfg)
     try:
         t0 = time.perf_counter()
-        dac.decode(dac_codes(toks, dcfg.codebook_size))
+        for b in range(B):
+            dac.decode(dac_codes(toks[b], dcfg.codebook_size))
         dt_dac = time.perf_counter() - t0
     finally:
         dac.close()
-    ar = steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt_ar
-    dac_rate = 2 * SAMPLES_PER_STEP / SAMPLE_RATE / dt_dac
+    ar = B * steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt_ar
+    dac_rate = B * frames * SAMPLES_PER_STEP / SAMPLE_RATE / dt_dac
     return {"value": 1.0 / (1.0 / ar + 1.0 / dac_rate), "unit": "audio-sec/wall-sec", "cores": n_threads, "kind": "port",
-            "sample": f"{steps} Parler-mini Q4_K decode steps (batch 1, KV length ~10) + DAC-44k decode of 2 frames "
-                      f"(oracle/ggml_ref.c, C restatement of ggml-cpu scalar paths; reference ggml-cpu unbuildable offline)",
+            "sample": f"{steps} Parler-mini Q4_K decode steps of {B} prompts at KV length {args.ctx} (the GPU leg's batch and KV "
+                      f"length; prefill skipped) + DAC-44k decode of {frames} frames per prompt (oracle/ggml_ref.c, C restatement "
+                      f"of ggml-cpu scalar paths; reference ggml-cpu unbuildable offline)",
             "ar_audio_sec_per_s": round(ar, 5), "dac_audio_sec_per_s": round(dac_rate, 5),
-            "codec_tokens_per_s": steps * HEADS / dt_ar}
+            "codec_tokens_per_s": B * steps * HEADS / dt_ar}
 
 
 def gemv_roofline(be, runner, steps):
@@ -294,6 +302,38 @@ def dia_leg(be, args):
         d.close()
 
 
+def parler_b1_leg(args, rank, local, new_backend):
+    """TTS.cpp's serving shape (examples/server/server.cpp:316-321,885-895): one prompt per runner,
+    `b1_replicas` runners, each on its own backend (HIP stream) driven by its own host thread, all
+    prefilled to the same KV length; beside the headline's lock-step batches."""
+    R, steps = args.b1_replicas, args.b1_steps
+    cfg = ttship.parler_config(batch=1, max_ctx=args.ctx + steps + args.warmup + 64)
+    bes = [new_backend() for _ in range(R)]
+    runs = [ttship.Parler(b.iface(), cfg) for b in bes]
+    try:
+        for r, (b, p) in enumerate(zip(bes, runs)):
+            p.prefill(prompt_tokens(1, args.ctx, cfg.prompt_vocab, offset=rank * R + r))
+            p.generate(args.warmup)
+            b.sync()
+
+        def one(r):
+            runs[r].generate(steps)
+            bes[r].sync()
+
+        t0 = time.perf_counter()
+        run_replicas(one, R)
+        dt = time.perf_counter() - t0
+        return {"workload": f"Parler-mini Q4_K AR decode, {R} runners x 1 prompt (TTS.cpp's server model), KV {args.ctx} -> "
+                            f"{args.ctx + steps}", "replicas": R, "batch_per_replica": 1,
+                "ms_per_step": round(1000 * dt / steps, 4),
+                "ar_audio_sec_per_s": round(R * steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3)}
+    finally:
+        for p in runs:
+            p.close()
+        for b in bes:
+            b.close()
+
+
 def kokoro_prompt(g, vocab):
     """Synthetic phoneme ids for global prompt g: a Harvard sentence's bytes mapped into the
     phoneme vocabulary, wrapped in the boundary id 0 as the phonemizer wraps a prompt."""
@@ -358,6 +398,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=400)
+    ap.add_argument("--b1-replicas", type=int, default=8, help="the B=1 leg: this many runners of one prompt each, as "
+                    "TTS.cpp's server workers run (0 = skip)")
+    ap.add_argument("--b1-steps", type=int, default=100)
     ap.add_argument("--no-fusion", action="store_true")
     ap.add_argument("--no-dac", action="store_true", help="AR decode only")
     ap.add_argument("--attn-split", type=int, default=None, help="TTS_HIP_OPT_ATTN_SPLIT: min KV length for split attention (0 = off)")
@@ -372,6 +415,8 @@ def main():
     ap.add_argument("--gemv-ks", type=int, default=None, help="TTS_HIP_OPT_GEMV_KS: max 16-row tiles of a tile-layout GEMV on the K-split matrix-core kernel (0 = never)")
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
+    ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
+                    "replica on all CUs, 1 = replica r on the r-th contiguous CU set, 2 = on CUs c with c %% R == r")
     ap.add_argument("--dac-workers", type=int, default=8, help="concurrent DAC decoders per GPU (each its own backend / "
                     "stream; the AR replicas' backends first): short codec sequences fill few CUs, so several "
                     "prompts decode side by side")
@@ -425,6 +470,8 @@ def main():
         # a replica = one backend (its own HIP stream) + its own runners, as a server worker owns its
         # runners (examples/server/server.cpp:316-321); replicas run concurrently from host threads
         rb = new_backend()
+        if args.cu_partition and R > 1:
+            rb.set_option(ttship.OPT["CU_PARTITION"], (r << 8) | R | ((args.cu_partition - 1) << 16))
         rr = ttship.Parler(rb.iface(), cfg)
         rd = None if args.no_dac else new_dac(rb)
         reps.append((rb, rr, rd))
@@ -474,6 +521,13 @@ def main():
     # parts of compute_enqueue: waiting on the device for the plan slot, planner, launches under
     # capture (incl. planner), exec update
     host.update({k.replace("_ns", "_us"): round(v, 1) for k, v in cdelta.items()})
+    b1 = None
+    if args.b1_replicas > 0:
+        barrier_sync(dist, be)
+        b1 = parler_b1_leg(args, rank, local, new_backend)
+        t = max_over_ranks(dist, local, b1["ms_per_step"])
+        b1["ms_per_step"] = t
+        b1["ar_audio_sec_per_s"] = round(world * args.b1_replicas * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
     kres = None
     if args.kokoro_prompts > 0:
         barrier_sync(dist, be)
@@ -542,6 +596,7 @@ def main():
             "audio_gather": None if gathered is None else {
                 "prompts": len(gathered), "audio_sec": round(sum(len(p) for p in gathered) / SAMPLE_RATE, 3),
                 "ms": round(1000.0 * t_gather, 3), "transport": "RCCL send/recv (gatherv) to rank 0" if world > 1 else "local"},
+            "parler_b1": b1,
             "kokoro": kres,
             "orpheus": ores,
             "dia": dres,

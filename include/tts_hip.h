@@ -271,6 +271,14 @@ enum tts_hip_option {
     TTS_HIP_OPT_ATTN_FUSED = 14,  /* decode attention over P >= value keys (hd 64 / 128, 16-B K and V rows) runs as
                                      ONE 1024-thread launch per attention (k_attn_fused; default 0 = off: the split pair,
                                      TTS_HIP_OPT_ATTN_SPLIT; tests and studies use 128) */
+    TTS_HIP_OPT_GEMM_Q8 = 18,     /* 1 (default) = Q8_0 products of more than 8 columns run the int8 matrix-core GEMM
+                                     (k_gemm_q8_0, bit-identical); 0 = one GEMV launch per 8 columns */
+    TTS_HIP_OPT_BGEMM_F32 = 19,   /* 1 (default) = batched float products (attention over many queries: encoders,
+                                     prefill) run the tiled f64-accumulating GEMM; 0 = the one-wave-per-output kernel */
+    TTS_HIP_OPT_CU_PARTITION = 20, /* (index << 8) | count, count > 1: the backend's stream runs on partition `index` of
+                                     `count` equal CU sets (hipExtStreamCreateWithCUMask; bit 16 set = interleaved CU
+                                     numbers, else contiguous), and kernel grids are sized to that share -- concurrent
+                                     replica backends then stop competing for CUs.  0 = all CUs */
     TTS_HIP_OPT_Q4K_DUAL_BYTES = 16, /* tts_hip_weight_set keeps a tile-layout copy of lane-layout Q4_K matrices of >= value
                                         bytes (default 1 MiB; 0 = never); a GEMV of >= 8 columns over >= 2048 rows (K >= 2048)
                                         of such matrices runs on the matrix-core kernels, and matrices of different row counts

@@ -61,6 +61,8 @@ void tts_parler_set_device_sampling(tts_parler * p, int32_t on);
 /* Seeded sampling (sampler::sample, include/tts_hip.h tts_sampling) for tts_parler_generate; NULL =
  * greedy (the default).  Prompt b of the batch draws from its own generator (stream b). */
 void tts_parler_set_sampling(tts_parler * p, const tts_sampling * cfg);
+/* Timing harness only (bench.py's cpu_baseline): continue as if `position` tokens were decoded. */
+int tts_parler_set_position(tts_parler * p, int32_t position);
 int32_t tts_parler_position(const tts_parler * p);
 /* Host time per phase summed over steps (us): build graph, allocate, set inputs, compute enqueue,
  * wait for logits.  Returns the step count; reset zeroes the sums. */

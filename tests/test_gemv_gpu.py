@@ -62,8 +62,9 @@ def test_q4_K(hip, K, N, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,N", [(2048, 2048), (2048, 512), (8192, 64), (1024, 1024), (64, 7)])
-@pytest.mark.parametrize("M", [1, 2, 8])
+@pytest.mark.parametrize("M", [1, 2, 8, 9, 64, 300])
 def test_q8_0(hip, K, N, M):
+    """M > 8: the int8 matrix-core GEMM (k_gemm_q8_0): per-block exact int dots, ggml's f32 chain."""
     rng = np.random.default_rng(K + N * 3 + M)
     w = helpers.rand_q8_0(rng, N, K)
     x = rng.standard_normal((M, K)).astype(np.float32)

@@ -100,8 +100,11 @@ def test_soft_max(hip, rows, nc, heads, masked):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,N,M,B", [(64, 450, 1, 16), (450, 1, 64, 16), (128, 33, 2, 4)])
+@pytest.mark.parametrize("K,N,M,B", [(64, 450, 1, 16), (450, 1, 64, 16), (128, 33, 2, 4),
+                                     (128, 1024, 1024, 2), (1024, 128, 1024, 2), (64, 448, 448, 3), (37, 70, 19, 2)])
 def test_mul_mat_f32_batched(hip, K, N, M, B):
+    """3-D float products: decode shapes on the generic kernel, many-query shapes (Dia's encoder
+    attention, prompt prefill) on the tiled batched GEMM; both bit-identical to the oracle."""
     a = rnd(7, B, N, K)
     b = rnd(8, B, M, K)
 
@@ -109,6 +112,18 @@ def test_mul_mat_f32_batched(hip, K, N, M, B):
         ta, tb = g.leaf(a), g.leaf(b)
         return [g.node("MUL_MAT", F32, [N, M, B], [ta, tb])]
     assert_bits(run_both(hip, build), "mul_mat")
+
+
+@pytest.mark.gpu
+def test_mul_mat_f32_batched_broadcast(hip):
+    """src0 broadcast over src1's batch dims (GQA-style: r2 = 4, r3 = 2)."""
+    K, N, M = 64, 40, 48
+    a = rnd(31, 1, 2, N, K)
+    b = rnd(32, 2, 8, M, K)
+
+    def build(g):
+        return [g.node("MUL_MAT", F32, [N, M, 8, 2], [g.leaf(a), g.leaf(b)])]
+    assert_bits(run_both(hip, build), "mul_mat broadcast")
 
 
 @pytest.mark.gpu

@@ -6,6 +6,7 @@
 #include <thread>
 
 #include "hip_internal.h"
+#include <hip/hip_ext.h>
 
 using namespace tts;
 
@@ -51,10 +52,14 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     hipDeviceProp_t prop;
     TTS_HIP_CHECK(hipGetDeviceProperties(&prop, device));
     snprintf(be->name, sizeof(be->name), "HIP%d(%s)", device, prop.gcnArchName);
+    be->cu_total = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    be->cus = be->cu_total;
     TTS_HIP_CHECK(hipMalloc((void **)&be->scratch, kScratchBytes));
     be->scratch_size = kScratchBytes;
     TTS_HIP_CHECK(hipMalloc((void **)&be->shadow, kShadowBytes));
     be->shadow_size = kShadowBytes;
+    be->hoist_size = (size_t)8 << 20;
+    TTS_HIP_CHECK(hipMalloc(&be->hoist, be->hoist_size));
     TTS_HIP_CHECK(hipMalloc((void **)&be->lstm_buf, kLstmFloats * sizeof(float)));
     TTS_HIP_CHECK(hipMalloc((void **)&be->attn_buf, kAttnFloats * sizeof(float)));
     be->attn_floats = kAttnFloats;
@@ -98,6 +103,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->argmax_keys);
     hipFree(be->argmax_counts);
     hipFree(be->lstm_buf);
+    hipFree(be->hoist);
     hipFree(be->attn_buf);
     hipFree(be->vec_scratch);
     hipFree(be->conv_stage);
@@ -489,6 +495,37 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_Q4K_TILE_BYTES: be->q4k_tile_bytes = value; return 0;
         case TTS_HIP_OPT_Q4K_DUAL_BYTES: be->q4k_dual_bytes = value; return 0;
         case TTS_HIP_OPT_GEMV_RSPLIT: be->gemv_mf_rsplit = value != 0; return 0;
+        case TTS_HIP_OPT_GEMM_Q8: be->gemm_q8 = value != 0; return 0;
+        case TTS_HIP_OPT_CU_PARTITION: {
+            const int count = value & 0xFF, index = (value >> 8) & 0xFF;
+            const bool inter = (value >> 16) & 1;
+            hipSetDevice(be->device);
+            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+            hipStream_t ns = nullptr;
+            if (count <= 1) {
+                TTS_HIP_CHECK(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+                be->cus = be->cu_total;
+            } else {
+                if (index >= count) return TTS_STATUS_BAD_ARG;
+                std::vector<uint32_t> mask((be->cu_total + 31) / 32, 0u);
+                const int per = be->cu_total / count;
+                int n = 0;
+                for (int c = 0; c < be->cu_total; ++c) {
+                    const bool on = inter ? (c % count == index) : (c / per == index && c < per * count);
+                    if (on) mask[c / 32] |= 1u << (c % 32), ++n;
+                }
+                if (hipExtStreamCreateWithCUMask(&ns, (uint32_t)mask.size(), mask.data()) != hipSuccess) return TTS_STATUS_FAILED;
+                be->cus = n;
+            }
+            TTS_HIP_CHECK(hipStreamDestroy(be->stream));
+            be->stream = ns;
+            // executable graphs were recorded for the old stream's launches: drop them
+            for (auto & ex : be->gsig_exec)
+                if (ex) hipGraphExecDestroy(ex), ex = nullptr;
+            for (auto & g : be->gsig) g = 0;
+            return 0;
+        }
+        case TTS_HIP_OPT_BGEMM_F32: be->bgemm_f32 = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;

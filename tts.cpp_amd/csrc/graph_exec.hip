@@ -120,7 +120,12 @@ struct GemvTarget {
 };
 
 struct Item {
-    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT, NODE } kind;
+    enum Kind { GEMV, ATTN, LN, LSTM, SNAKE, EMBED, CONV, ADAIN, MCPY, RINT, NODE, COPY } kind;
+    // COPY: a grouped product hoisted into an earlier launch wrote its output to backend scratch;
+    // at the product's own position it is copied to its tensor (cp_src -> cp_dst, cp_bytes)
+    const void * cp_src = nullptr;
+    void * cp_dst = nullptr;
+    size_t cp_bytes = 0;
     // NODE: a node run with a rewritten source (TTS_FUSE_CONTREAD)
     tts_tensor node{};
     // MCPY: the ROPE node producing the copies' source, applied on the way (x = the rope's source)
@@ -271,6 +276,8 @@ struct Planner {
     size_t vec_cap = 0;          // floats of the backend's vector scratch (fused AdaIN staging)
     float * conv_stage = nullptr;  // backend scratch for fused conv outputs that cannot stage in their im2col buffer
     size_t conv_stage_cap = 0;
+    char * hoist_buf = nullptr;  // backend scratch for hoisted products whose own memory is still in use (try_gemv)
+    size_t hoist_cap = 0, hoist_used = 0;
     size_t lstm_cap = 0, lstm_used = 0;
 
     const tts_tensor * sole_consumer(const tts_tensor * t) {
@@ -668,14 +675,32 @@ struct Planner {
                 if ((mask & TTS_FUSE_KV) && mm->ne[1] * mm->ne[2] * mm->ne[3] == M && kv_target(mm, M, kt, ks)) t = kt;
                 else ks.clear();
                 bool ok = true;
-                if (j > i) {
+                auto clear_of = [&](const GemvTarget & tt) {
                     const char *y0, *y1;
-                    target_span(mm, t, y0, y1);
-                    for (const tts_tensor * u : passed) ok = ok && !hits(y0, y1, u);
-                    for (size_t k = 0; k < it.mms.size() && ok; ++k) {
+                    target_span(mm, tt, y0, y1);
+                    bool c = true;
+                    for (const tts_tensor * u : passed) c = c && !hits(y0, y1, u);
+                    for (size_t k = 0; k < it.mms.size() && c; ++k) {
                         const char *z0, *z1;
                         target_span(it.mms[k], it.tgt[k], z0, z1);
-                        ok = !(y0 < z1 && z0 < y1);
+                        c = !(y0 < z1 && z0 < y1);
+                    }
+                    return c;
+                };
+                if (j > i) ok = clear_of(t);
+                // The product's own memory is still in use by what it is hoisted over (the graph
+                // allocator reuses the memory of tensors dead at its original position -- Orpheus' Q on
+                // K's): it writes backend scratch instead, copied to its tensor at its own position.
+                int copy_back = -1;
+                const size_t obytes = 4 * (size_t)(mm->ne[0] * mm->ne[1] * mm->ne[2] * mm->ne[3]);
+                if (!ok && t.y == (float *)mm->data && t.rg == 0 && contiguous(mm) && hoist_buf &&
+                    hoist_used + ((obytes + 255) & ~(size_t)255) <= hoist_cap) {
+                    GemvTarget ht{(float *)(hoist_buf + hoist_used), (int64_t)(mm->nb[1] / 4), 1};
+                    if (clear_of(ht)) {
+                        t = ht;
+                        copy_back = j;
+                        hoist_used += (obytes + 255) & ~(size_t)255;
+                        ok = true;
                     }
                 }
                 if (ok) {
@@ -683,6 +708,14 @@ struct Planner {
                     it.mms.push_back(mm);
                     it.tgt.push_back(t);
                     if (j > i) act[j] = -1;
+                    if (copy_back >= 0) {
+                        Item cp;
+                        cp.kind = Item::COPY;
+                        cp.cp_src = t.y;
+                        cp.cp_dst = mm->data;
+                        cp.cp_bytes = obytes;
+                        act[j] = add_item(std::move(cp));
+                    }
                     ++j;
                     continue;
                 }
@@ -1932,6 +1965,9 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             return 0;
         case Item::NODE:
             return run_node(be, &it.node);
+        case Item::COPY:
+            TTS_HIP_CHECK(hipMemcpyAsync(it.cp_dst, it.cp_src, it.cp_bytes, hipMemcpyDeviceToDevice, be->stream));
+            return 0;
         case Item::LSTM:
             if (it.lkind & 4)
                 for (int g = 0; g < 4; ++g)
@@ -2094,6 +2130,9 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     static float conv_stand_in alignas(256);
     pl.conv_stage = &conv_stand_in;
     pl.conv_stage_cap = (size_t)8 << 20;
+    static char hoist_stand_in alignas(256);
+    pl.hoist_buf = &hoist_stand_in;
+    pl.hoist_cap = (size_t)8 << 20;
     if (mask) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
     for (int k = 0; k < 16; ++k) counts[k] = 0;  // (NODE items count under counts[10])
@@ -2122,6 +2161,8 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     pl.vec_cap = be->vec_scratch ? (1u << 18) : 0;
     pl.conv_stage = be->conv_stage;
     pl.conv_stage_cap = be->conv_stage_floats;
+    pl.hoist_buf = (char *)be->hoist;
+    pl.hoist_cap = be->hoist_size;
     if (be->fusion) pl.build(nodes, n_nodes);
     be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
     // long-context attention items in launch order: each one's K/V is prefetched into MALL on the

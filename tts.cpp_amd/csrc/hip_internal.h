@@ -261,6 +261,9 @@ struct tts_hip_backend {
     // allocator has placed that GEMV's output on the attention output's memory
     float * shadow = nullptr;
     size_t shadow_size = 0;
+    // outputs of grouped products hoisted over nodes that still use their memory (graph_exec try_gemv)
+    void * hoist = nullptr;
+    size_t hoist_size = 0;
     // split decode attention: masked, scaled scores [B][n][H][P] and per-chunk maxima between the
     // scores kernel and the softmax + P.V kernel (consumed by the very next launch on the stream)
     float * attn_buf = nullptr;
@@ -277,6 +280,10 @@ struct tts_hip_backend {
     int gemv_dbg = 0;
     // Q4_K GEMVs in the lane layout run the unique-load kernel (k_gemv_q4_K_u) where the shape fits
     int gemv_unique = 1;
+    int gemm_q8 = 1;    // TTS_HIP_OPT_GEMM_Q8
+    int64_t cus = 256;  // compute units this backend's stream may use (TTS_HIP_OPT_CU_PARTITION); grids are sized to it
+    int cu_total = 256;
+    int bgemm_f32 = 1;  // TTS_HIP_OPT_BGEMM_F32
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;
@@ -362,6 +369,7 @@ namespace tts {
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job);
 // F32 weights x many columns (k_gemm.hip): bit-identical to the sequential-f64 float dot
+bool launch_bgemm_f32(tts_hip_backend * be, const tts_tensor * node);
 bool gemm_f32_ok(const GemvJob & j);
 void launch_gemm_f32(tts_hip_backend * be, const GemvJob & j);
 void launch_copy_cols(tts_hip_backend * be, float * dst, const float * src, int64_t K, int64_t scs, int64_t M);

@@ -127,7 +127,106 @@ __global__ __launch_bounds__(256) void k_gemm_reduce(GemvJob j, int ks, const do
     }
 }
 
+// Batched form for ggml's 3-D / 4-D float MUL_MAT (attention over many queries: Dia's 1024-position
+// encoder, prompt prefills): dst[i0, i1, i2, i3] = dot(src0[:, i0, i2 / r2, i3 / r3], src1[:, i1, i2, i3]),
+// the same f32 products, ascending-k f64 sums and single rounding per output as the 2-D kernel
+// (no K split: equal to the oracle's sequential sum up to f64 rounding).  blockIdx.z = i2 + ne2 * i3.
+struct BGemm {
+    const char *a, *b;
+    char * y;
+    int64_t K, N, M, ne2, ne3, r2, r3;
+    int64_t a1, a2, a3, b1, b2, b3, y0, y1, y2, y3;  // byte strides
+};
+
+__global__ __launch_bounds__(256) void k_bgemm_f32(BGemm g) {
+    __shared__ float As[GK][GLD];
+    __shared__ float Bs[GK][GLD];
+    const int tid = threadIdx.x;
+    const int64_t i2 = blockIdx.z % g.ne2, i3 = blockIdx.z / g.ne2;
+    const int64_t row0 = (int64_t)blockIdx.x * GT, col0 = (int64_t)blockIdx.y * GT;
+    const int64_t N = g.N, M = g.M, K = g.K;
+    const char * A = g.a + (i2 / g.r2) * g.a2 + (i3 / g.r3) * g.a3;
+    const char * B = g.b + i2 * g.b2 + i3 * g.b3;
+    const int tm = tid & 15, tn = tid >> 4;
+    double acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = 0.0;
+    const int lr = tid >> 2, kq = (tid & 3) * 4;
+    const int64_t wr = row0 + lr, xc = col0 + lr;
+    const float * wp = (const float *)(A + (wr < N ? wr : N - 1) * g.a1);
+    const float * xp = (const float *)(B + (xc < M ? xc : M - 1) * g.b1);
+    for (int64_t k0 = 0; k0 < K; k0 += GK) {
+        const int64_t k = k0 + kq;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            As[kq + e][lr] = k + e < K ? wp[k + e] : 0.0f;
+            Bs[kq + e][lr] = k + e < K ? xp[k + e] : 0.0f;
+        }
+        __syncthreads();
+        const int kn = K - k0 < GK ? (int)(K - k0) : GK;
+        if (kn == GK) {
+#pragma unroll 4
+            for (int kk = 0; kk < GK; ++kk) {
+                float a[4], b[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[i] = As[kk][tm + 16 * i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) b[i] = Bs[kk][tn + 16 * i];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[i][c] += (double)__fmul_rn(a[i], b[c]);
+            }
+        } else {
+            for (int kk = 0; kk < kn; ++kk) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc[i][c] += (double)__fmul_rn(As[kk][tm + 16 * i], Bs[kk][tn + 16 * c]);
+            }
+        }
+        __syncthreads();
+    }
+    char * Y = g.y + i2 * g.y2 + i3 * g.y3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int64_t col = col0 + tn + 16 * c;
+        if (col >= M) continue;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t row = row0 + tm + 16 * i;
+            if (row < N) *(float *)(Y + row * g.y0 + col * g.y1) = (float)acc[i][c];
+        }
+    }
+}
+
 }  // namespace
+
+// Batched float MUL_MAT on the tiled kernel; false when the node does not fit it (the caller then
+// uses the one-wave-per-output kernel).
+bool launch_bgemm_f32(tts_hip_backend * be, const tts_tensor * node) {
+    const tts_tensor * a = node->src[0];
+    const tts_tensor * b = node->src[1];
+    if (!be->bgemm_f32 || a->type != TTS_TYPE_F32 || b->type != TTS_TYPE_F32 || node->type != TTS_TYPE_F32) return false;
+    if (a->nb[0] != 4 || b->nb[0] != 4 || a->ne[0] < 32 || a->ne[1] < 16 || b->ne[1] < 16) return false;
+    if (b->ne[2] % a->ne[2] || b->ne[3] % a->ne[3]) return false;
+    if ((a->nb[1] | b->nb[1] | node->nb[1] | node->nb[0]) % 4) return false;
+    const int64_t batches = node->ne[2] * node->ne[3];
+    if (batches > 65535 || (node->ne[1] + GT - 1) / GT > 65535) return false;
+    BGemm g;
+    g.a = (const char *)a->data, g.b = (const char *)b->data, g.y = (char *)node->data;
+    g.K = a->ne[0], g.N = a->ne[1], g.M = b->ne[1], g.ne2 = node->ne[2], g.ne3 = node->ne[3];
+    g.r2 = b->ne[2] / a->ne[2], g.r3 = b->ne[3] / a->ne[3];
+    g.a1 = (int64_t)a->nb[1], g.a2 = (int64_t)a->nb[2], g.a3 = (int64_t)a->nb[3];
+    g.b1 = (int64_t)b->nb[1], g.b2 = (int64_t)b->nb[2], g.b3 = (int64_t)b->nb[3];
+    g.y0 = (int64_t)node->nb[0], g.y1 = (int64_t)node->nb[1], g.y2 = (int64_t)node->nb[2], g.y3 = (int64_t)node->nb[3];
+    const dim3 grid((unsigned)((g.N + GT - 1) / GT), (unsigned)((g.M + GT - 1) / GT), (unsigned)batches);
+    hipLaunchKernelGGL(k_bgemm_f32, grid, dim3(256), 0, be->stream, g);
+    TTS_HIP_CHECK(hipGetLastError());
+    return true;
+}
 
 bool gemm_f32_ok(const GemvJob & j) {
     // the tiled GEMM stores plain (column, row) targets: no GQA repeat copies, no mixed row counts

@@ -1523,12 +1523,12 @@ static void launch_q4k(tts_hip_backend * be, const GemvJob & j, unsigned gx, int
 
 // Unique-load geometry (k_gemv_q4_K_u): R rows per 512-thread workgroup with R * nb <= 64 octets,
 // as few rows per workgroup as spreads the matrix over every CU.  False when the shape does not fit.
-static bool q4k_u_geometry(const GemvJob & j, int MC, int & R, int & NCG, int64_t & gx, size_t & lds) {
+static bool q4k_u_geometry(const GemvJob & j, int MC, int & R, int & NCG, int64_t & gx, size_t & lds, int64_t cus) {
     const int64_t nb = j.K / QK_K;
     if (nb < 1 || nb > 64) return false;
     const int64_t NR = (int64_t)j.nmat * j.N;
     const int64_t rmax = 64 / nb;
-    int64_t r = (NR + 255) / 256;
+    int64_t r = (NR + cus - 1) / cus;
     r = r > rmax ? rmax : r < 1 ? 1 : r;
     R = (int)r;
     gx = (NR + r - 1) / r;
@@ -1562,7 +1562,7 @@ static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
         int R, NCG;
         int64_t gx;
         size_t lds;
-        if (q4k_u_geometry(j, MC, R, NCG, gx, lds)) {
+        if (q4k_u_geometry(j, MC, R, NCG, gx, lds, be->cus)) {
             const bool wide = j.K > 4 * QK_K;  // LN prologue: NP = NCH / 4 chunk passes per lane
             if (j.pro == PRO_LN) {
                 if (wide) launch_q4k_u<MC, PRO_LN, 16>(be, j, (unsigned)gx, R, NCG, lds);
@@ -1592,7 +1592,7 @@ static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
     const bool small = j.K <= 4 * QK_K;
     const int nw_max = small ? 16 : 8;
     const int64_t G = ((int64_t)j.nmat * j.N + S - 1) / S;
-    int64_t nw = (G + 255) / 256;
+    int64_t nw = (G + be->cus - 1) / be->cus;
     if (j.pro == PRO_LN && nw < j.M) nw = j.M;
     nw = nw < 1 ? 1 : nw > nw_max ? nw_max : nw;
     int64_t gx = (G + nw - 1) / nw;
@@ -1643,7 +1643,7 @@ static void launch_q4k_mf_rs(tts_hip_backend * be, const GemvJob & j, unsigned g
 template <int PRO, int NCH>
 static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
     const int64_t T = (job_rows(j) + 15) / 16;
-    const unsigned gx = (unsigned)(T < 256 ? T : 256);
+    const unsigned gx = (unsigned)(T < be->cus ? T : be->cus);
     // residue split when every tile fits one slot of RS waves (8 waves per workgroup)
     const int rs = j.epi == EPI_SWIGLU || !be->gemv_mf_rsplit ? 1 : T <= (int64_t)gx * 2 ? 4 : T <= (int64_t)gx * 4 ? 2 : 1;
     if (rs == 4) launch_q4k_mf_rs<PRO, NCH, 4>(be, j, gx);
@@ -1716,6 +1716,103 @@ static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Q8_0 x Q8_0 GEMM for many columns (Dia's 1024-position encoder, prompt prefills) on the int8
+// matrix cores.  ggml_vec_dot_q8_0_q8_0 per (row, column): sumf += sumi_b * (d_w,b * d_x,b) over the
+// 32-element blocks b in ascending order, sumi_b the exact int32 dot of the block.  One
+// v_mfma_i32_16x16x32_i8 computes sumi_b for a 16 x 16 tile exactly (K = 32 = one block; A[i = l&15]
+// [k = 8(l>>4)..+7], B[k][j = l&15], D col l&15, rows 4(l>>4)+e), and each lane then folds its
+// outputs' terms into f32 sums in block order with ggml's roundings: bit-identical to the GEMV.
+// Workgroup: 4 waves over a 64-row x 64-column tile (2 x 2 MFMA tiles per wave); the next block's
+// operands are loaded before the current block's MFMAs.  Native Q8_0 rows (34-B blocks, 2-B
+// aligned): a lane's 8 weight bytes come as four 16-bit loads; activations are the Q8_0 copy
+// (int8 [M][K], fp16-rounded d [M][K/32]) prepare_act made.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_gemm_q8_0(GemvJob j) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int mat = blockIdx.z;
+    const int nb = (int)(j.K / QK8_0);
+    const int64_t r0 = (int64_t)blockIdx.x * 64 + (wave & 1) * 32;
+    const int64_t c0 = (int64_t)blockIdx.y * 64 + (wave >> 1) * 32;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const uint8_t * W = j.W[mat];
+    const uint8_t * wrow[2];
+    const int8_t * xcol[2];
+    const float * xd[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int64_t r = min(r0 + 16 * t + r16, j.N - 1);
+        const int64_t c = min(c0 + 16 * t + r16, j.M - 1);
+        wrow[t] = W + r * j.w_row_bytes;
+        xcol[t] = j.aq.qs + c * j.K;
+        xd[t] = j.aq.d + c * nb;
+    }
+    // rows of this lane's accumulator elements (t, e): r0 + 16 t + 4 kq + e
+    const uint8_t * drow[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) drow[t][e] = W + min(r0 + 16 * t + 4 * kq + e, j.N - 1) * j.w_row_bytes;
+    float acc[2][2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[a][b][e] = 0.0f;
+    long av[2], bv[2], an[2], bn[2];
+    float dwv[2][4], dxv[2], dwn[2][4], dxn[2];
+    auto load = [&](int b, long (&fa)[2], long (&fb)[2], float (&fw)[2][4], float (&fx)[2]) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint16_t * q = (const uint16_t *)(wrow[t] + (int64_t)b * 34 + 2 + 8 * kq);
+            const uint64_t w = (uint64_t)q[0] | ((uint64_t)q[1] << 16) | ((uint64_t)q[2] << 32) | ((uint64_t)q[3] << 48);
+            fa[t] = (long)w;
+            fb[t] = *(const long *)(xcol[t] + (int64_t)b * QK8_0 + 8 * kq);
+            fx[t] = xd[t][b];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) fw[t][e] = dev_fp16_to_fp32(*(const uint16_t *)(drow[t][e] + (int64_t)b * 34));
+        }
+    };
+    load(0, av, bv, dwv, dxv);
+    for (int b = 0; b < nb; ++b) {
+        if (b + 1 < nb) load(b + 1, an, bn, dwn, dxn);
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+            for (int tj = 0; tj < 2; ++tj) {
+                const i32x4_t z = {0, 0, 0, 0};
+                const i32x4_t s = __builtin_amdgcn_mfma_i32_16x16x32_i8(av[ti], bv[tj], z, 0, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[ti][tj][e] = __fadd_rn(acc[ti][tj][e], __fmul_rn((float)s[e], __fmul_rn(dwv[ti][e], dxv[tj])));
+            }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            av[t] = an[t], bv[t] = bn[t], dxv[t] = dxn[t];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dwv[t][e] = dwn[t][e];
+        }
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 2; ++tj) {
+            const int64_t col = c0 + 16 * tj + r16;
+            if (col >= j.M) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t row = r0 + 16 * ti + 4 * kq + e;
+                if (row < j.N) gemv_store<1>(j, mat, row, (int)col, acc[ti][tj][e]);
+            }
+        }
+}
+
+static void launch_gemm_q8_0(tts_hip_backend * be, const GemvJob & j) {
+    const dim3 grid((unsigned)((j.N + 63) / 64), (unsigned)((j.M + 63) / 64), (unsigned)j.nmat);
+    hipLaunchKernelGGL(k_gemm_q8_0, grid, dim3(256), 0, be->stream, j);
+}
+
 template <int MC>
 static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
     const unsigned nmat = (unsigned)j.nmat;
@@ -1764,6 +1861,15 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
     const int64_t K = job.K;
     if (job.wtype == TTS_TYPE_F32 && job.M > 8 && gemm_f32_ok(job)) {
         launch_gemm_f32(be, job);  // one tiled pass instead of a GEMV launch per 8 columns
+        if (prof) {
+            TTS_HIP_CHECK(hipEventRecord(e1, be->stream));
+            profile_push(be, e0, e1, gemv_bytes(job), job.wtype);
+        }
+        return;
+    }
+    if (job.wtype == TTS_TYPE_Q8_0 && job.M > 8 && job.aq.vtype == TTS_TYPE_Q8_0 && !job.hetero && be->gemm_q8) {
+        launch_gemm_q8_0(be, job);  // one matrix-core pass instead of a GEMV launch per 8 columns
+        TTS_HIP_CHECK(hipGetLastError());
         if (prof) {
             TTS_HIP_CHECK(hipEventRecord(e1, be->stream));
             profile_push(be, e0, e1, gemv_bytes(job), job.wtype);

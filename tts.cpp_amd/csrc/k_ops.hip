@@ -681,6 +681,7 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
                     return 0;
                 }
             }
+            if (launch_bgemm_f32(be, node)) return 0;  // batched float products over many queries
             if (s0->ne[0] <= 32) {
                 hipLaunchKernelGGL(k_mul_mat_smallk, dim3((unsigned)((nout + 255) / 256)), dim3(256), 0, st, d, make_td(s0), make_td(s1), nout);
                 break;

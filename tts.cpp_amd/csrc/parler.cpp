@@ -694,6 +694,16 @@ extern "C" int tts_parler_generate(tts_parler * p, int32_t n_steps, int32_t * to
 }
 
 extern "C" int32_t tts_parler_position(const tts_parler * p) { return p->position; }
+
+// Timing harness (bench.py's cpu_baseline): continue as if the KV cache held `position` tokens, the
+// rows in between keeping whatever they hold, so a slow backend can time decode steps at the GPU
+// bench's KV length without running its prompt prefill.  Not for generating audio.
+extern "C" int tts_parler_set_position(tts_parler * p, int32_t position) {
+    if (position < p->position || position >= p->cfg.max_ctx) return TTS_STATUS_BAD_ARG;
+    p->position = position;
+    p->prepared = false;
+    return 0;
+}
 extern "C" void tts_parler_set_device_sampling(tts_parler * p, int32_t on) { p->device_sampling = on != 0; }
 
 extern "C" int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset) {

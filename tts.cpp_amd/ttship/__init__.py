@@ -26,7 +26,7 @@ FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17, "GEMM_Q8": 18, "BGEMM_F32": 19, "CU_PARTITION": 20}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 ATTN_FUSED_ON = 128  # P >= 128 keys -> one 1024-thread launch (k_attn_fused; backend default 0 = off)
 
@@ -314,6 +314,7 @@ def lib():
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_sampling_default": (None, [ctypes.POINTER(Sampling)]),
         "tts_parler_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
+        "tts_parler_set_position": (ctypes.c_int, [vp, i32]),
         "tts_dia_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
         "tts_orpheus_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
         "tts_sampler_call_seed": (ctypes.c_uint32, [ctypes.c_uint64, i32, i64]),
@@ -722,6 +723,11 @@ class Parler:
         """Greedy sampling on the device (default when the backend supports it) or on the host."""
         self.L.tts_parler_set_device_sampling(self.ptr, 1 if on else 0)
 
+    def set_position(self, position):
+        """Timing harness only: continue as if `position` tokens had been decoded."""
+        if self.L.tts_parler_set_position(self.ptr, position) != 0:
+            raise RuntimeError("set_position failed")
+
     def set_sampling(self, cfg=None):
         """Seeded sampling (ttship.sampling(...)) for generate(); None = greedy."""
         self._samp = cfg
@@ -1107,7 +1113,7 @@ class KokoroGenerator:
             self.ptr = None
 
 
-PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy", "rint", "node"]
+PLAN_KINDS = ["gemv", "attn", "ln", "lstm", "snake", "embed", "conv", "adain", "mcpy", "rint", "node", "copy"]
 
 
 def plan_stats(nodes_ptr, n_nodes, mask):
