@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/tts_gguf.h"
 #include "graph.h"
 #include "synth.h"
 #include "tts_hip.h"
@@ -56,6 +57,7 @@ struct tts_dac {
     tts_tensor * in_codes = nullptr;
     uint64_t tensor_index = 0;
     std::vector<wspec> specs;
+    const tts_gguf * gguf = nullptr;  // weight source while creating from a file (else synthetic)
 };
 
 extern "C" void tts_dac_default_config(tts_dac_config * c) {
@@ -88,6 +90,23 @@ static tts_tensor * conv_w(tts_dac * d, int K, int IC, int OC, const std::string
     return wnew(d, gain * std::sqrt(3.0f / (float)(K * IC)), 0.f, K, IC, OC, name);
 }
 
+// GGUF name of a weight: the reference's (dac_gguf_encoder.py's mapping, read back by
+// dac_model.cpp:58-98 / general_neural_audio_codec.cpp:36-127); the runner's own constant has none.
+static std::string gguf_name(const tts_tensor * t) { return std::string("audio_encoder.") + t->name; }
+
+static bool same_squeezed_shape(const int64_t * a, const int64_t * b) {
+    int64_t x[4], y[4];
+    int nx = 0, ny = 0;
+    for (int k = 0; k < 4; ++k) {
+        if (a[k] != 1) x[nx++] = a[k];
+        if (b[k] != 1) y[ny++] = b[k];
+    }
+    if (nx != ny) return false;
+    for (int k = 0; k < nx; ++k)
+        if (x[k] != y[k]) return false;
+    return true;
+}
+
 static bool upload(tts_dac * d) {
     size_t total = 0;
     for (auto & s : d->specs) total += (tg::nbytes(s.t) + 255) & ~(size_t)255;
@@ -99,56 +118,78 @@ static bool upload(tts_dac * d) {
         const size_t n = (size_t)tg::nelements(s.t);
         s.t->data = (char *)d->wbuf + off;
         off += (tg::nbytes(s.t) + 255) & ~(size_t)255;
-        host.resize(n);
-        synth_f32(host.data(), n, s.seed, s.scale, s.offset);
-        if (d->be.set_tensor(d->be.ctx, s.t, host.data()) != 0) return false;
+        const void * src = nullptr;
+        if (d->gguf && s.t != d->one) {  // assign_weight: the mapped file bytes
+            const std::string fname = gguf_name(s.t);
+            const int64_t i = tts_gguf_find_tensor(d->gguf, fname.c_str());
+            int64_t ne[4] = {1, 1, 1, 1};
+            if (i >= 0) tts_gguf_tensor_ndims(d->gguf, i, ne);
+            if (i < 0 || tts_gguf_tensor_type(d->gguf, i) != TTS_TYPE_F32 || !same_squeezed_shape(ne, s.t->ne)) {
+                fprintf(stderr, "gguf: DAC tensor '%s' %s (the decoder takes F32 [%lld %lld %lld])\n", fname.c_str(),
+                        i < 0 ? "is missing" : "has another type or shape", (long long)s.t->ne[0], (long long)s.t->ne[1], (long long)s.t->ne[2]);
+                return false;
+            }
+            src = tts_gguf_tensor_data(d->gguf, i);
+        } else {
+            host.resize(n);
+            synth_f32(host.data(), n, s.seed, s.scale, s.offset);
+            src = host.data();
+        }
+        if (d->be.set_tensor(d->be.ctx, s.t, src) != 0) return false;
     }
     return true;
 }
 
-extern "C" tts_dac * tts_dac_create(const tts_backend_iface * be, const tts_dac_config * cfg) {
-    auto * d = new tts_dac();
-    d->cfg = *cfg;
-    d->be = *be;
+// Declares every weight in the reference's order (synthetic seeds follow this order).
+static void declare_weights(tts_dac * d) {
     const auto & c = d->cfg;
     for (int i = 0; i < c.n_codebooks; ++i) {
         dac_quant q;
-        q.codebook = wnew(d, 1.0f, 0.f, c.codebook_dim, c.codebook_size, 1, "quantizer." + std::to_string(i) + ".codebook");
-        q.out_kernel = conv_w(d, 1, c.codebook_dim, c.latent_dim, "quantizer." + std::to_string(i) + ".out_proj.weight");
-        q.out_bias = wnew(d, 0.01f, 0.f, 1, c.latent_dim, 1, "quantizer." + std::to_string(i) + ".out_proj.bias");
+        q.codebook = wnew(d, 1.0f, 0.f, c.codebook_dim, c.codebook_size, 1, "quantizers." + std::to_string(i) + ".codebook.weight");
+        q.out_kernel = conv_w(d, 1, c.codebook_dim, c.latent_dim, "quantizers." + std::to_string(i) + ".out_proj.weight");
+        q.out_bias = wnew(d, 0.01f, 0.f, 1, c.latent_dim, 1, "quantizers." + std::to_string(i) + ".out_proj.bias");
         d->quant.push_back(q);
     }
-    d->in_kernel = conv_w(d, 7, c.latent_dim, c.decoder_dim, "decoder.in.weight");
-    d->in_bias = wnew(d, 0.01f, 0.f, 1, c.decoder_dim, 1, "decoder.in.bias");
+    d->in_kernel = conv_w(d, 7, c.latent_dim, c.decoder_dim, "initial.weight");
+    d->in_bias = wnew(d, 0.01f, 0.f, 1, c.decoder_dim, 1, "initial.bias");
     int ch = c.decoder_dim;
     for (int l = 0; l < c.n_layers; ++l) {
         const int s = c.rates[l], oc = ch / 2;
         dac_layer L;
-        const std::string pre = "decoder.layer." + std::to_string(l);
+        const std::string pre = "decoder_block." + std::to_string(l + 1);
         L.stride = s;
         L.padding = (s + 1) / 2;  // DAC: ceil(stride / 2)
-        L.in_alpha = wnew(d, 0.5f, 1.0f, 1, ch, 1, pre + ".alpha");
-        L.kernel = wnew(d, std::sqrt(3.0f / (float)(2 * ch)), 0.f, 2 * s, oc, ch, pre + ".convT.weight");
-        L.bias = wnew(d, 0.01f, 0.f, 1, oc, 1, pre + ".convT.bias");
+        L.in_alpha = wnew(d, 0.5f, 1.0f, 1, ch, 1, pre + ".final.alpha");
+        L.kernel = wnew(d, std::sqrt(3.0f / (float)(2 * ch)), 0.f, 2 * s, oc, ch, pre + ".final.weight");
+        L.bias = wnew(d, 0.01f, 0.f, 1, oc, 1, pre + ".final.bias");
         for (int r = 0; r < 3; ++r) {
             dac_ru & u = L.ru[r];
-            const std::string rp = pre + ".res." + std::to_string(r);
+            const std::string rp = pre + ".residual_unit." + std::to_string(r);
             u.dilation = (int)std::pow(3, r);
             u.padding = 3 * u.dilation;
-            u.in_alpha = wnew(d, 0.5f, 1.0f, 1, oc, 1, rp + ".alpha1");
-            u.in_kernel = conv_w(d, 7, oc, oc, rp + ".conv1.weight", 0.5f);
-            u.in_bias = wnew(d, 0.01f, 0.f, 1, oc, 1, rp + ".conv1.bias");
-            u.out_alpha = wnew(d, 0.5f, 1.0f, 1, oc, 1, rp + ".alpha2");
-            u.out_kernel = conv_w(d, 1, oc, oc, rp + ".conv2.weight", 0.5f);
-            u.out_bias = wnew(d, 0.01f, 0.f, 1, oc, 1, rp + ".conv2.bias");
+            u.in_alpha = wnew(d, 0.5f, 1.0f, 1, oc, 1, rp + ".res.initial.alpha");
+            u.in_kernel = conv_w(d, 7, oc, oc, rp + ".res.initial.weight", 0.5f);
+            u.in_bias = wnew(d, 0.01f, 0.f, 1, oc, 1, rp + ".res.initial.bias");
+            u.out_alpha = wnew(d, 0.5f, 1.0f, 1, oc, 1, rp + ".res.final.alpha");
+            u.out_kernel = conv_w(d, 1, oc, oc, rp + ".res.final.weight", 0.5f);
+            u.out_bias = wnew(d, 0.01f, 0.f, 1, oc, 1, rp + ".res.final.bias");
         }
         d->layers.push_back(L);
         ch = oc;
     }
-    d->out_alpha = wnew(d, 0.5f, 1.0f, 1, ch, 1, "decoder.out.alpha");
-    d->out_kernel = conv_w(d, 7, ch, 1, "decoder.out.weight", 0.3f);
-    d->out_bias = wnew(d, 0.01f, 0.f, 1, 1, 1, "decoder.out.bias");
+    d->out_alpha = wnew(d, 0.5f, 1.0f, 1, ch, 1, "final.alpha");
+    d->out_kernel = conv_w(d, 7, ch, 1, "final.weight", 0.3f);
+    d->out_bias = wnew(d, 0.01f, 0.f, 1, 1, 1, "final.bias");
     d->one = wnew(d, 0.f, 1.0f, 1, 1, 1, "one");
+}
+
+static tts_dac * dac_create(const tts_backend_iface * be, const tts_dac_config * cfg, const tts_gguf * g) {
+    auto * d = new tts_dac();
+    d->cfg = *cfg;
+    d->be = *be;
+    d->gguf = g;
+    const auto & c = d->cfg;
+    declare_weights(d);
     if (!upload(d)) {
         tts_dac_free(d);
         return nullptr;
@@ -164,8 +205,11 @@ extern "C" tts_dac * tts_dac_create(const tts_backend_iface * be, const tts_dac_
         tts_dac_free(d);
         return nullptr;
     }
+    d->gguf = nullptr;
     return d;
 }
+
+extern "C" tts_dac * tts_dac_create(const tts_backend_iface * be, const tts_dac_config * cfg) { return dac_create(be, cfg, nullptr); }
 
 extern "C" void tts_dac_free(tts_dac * d) {
     if (!d) return;
@@ -248,3 +292,89 @@ extern "C" int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, flo
 }
 
 extern "C" int32_t tts_dac_last_graph_nodes(const tts_dac * d) { return (int32_t)d->gctx.nodes.size(); }
+
+// ---- GGUF loader path (dac_model::prep_constants / prep_layers / assign_weight) ----
+static bool key_u32(const tts_gguf * g, std::initializer_list<const char *> keys, uint32_t * out) {
+    for (const char * k : keys) {
+        const int64_t i = tts_gguf_find_key(g, k);
+        if (i >= 0 && tts_gguf_get_u32(g, i, out)) return true;
+    }
+    return false;
+}
+
+static int64_t tdim(const tts_gguf * g, const std::string & name, int k) {
+    const int64_t i = tts_gguf_find_tensor(g, name.c_str());
+    if (i < 0) return -1;
+    int64_t ne[4];
+    tts_gguf_tensor_ndims(g, i, ne);
+    return ne[k];
+}
+
+extern "C" int tts_dac_config_from_gguf(const tts_gguf * g, tts_dac_config * c) {
+    if (!g || !c) return TTS_STATUS_BAD_ARG;
+    uint32_t v = 0;
+    if (key_u32(g, {"parler-tts.decoder.output_heads", "output_heads", "dia.decoder.output_heads"}, &v)) c->n_codebooks = (int32_t)v;
+    int n_layers = 0;
+    for (int l = 0; l < 8; ++l) {  // prep_layers: dac_layer_stride_{l} / dac_layer_padding_{l} per block
+        const std::string sk = "dac_layer_stride_" + std::to_string(l), pk = "dac_layer_padding_" + std::to_string(l);
+        uint32_t s = 0, pd = 0;
+        if (!key_u32(g, {("dac." + sk).c_str(), sk.c_str()}, &s)) break;
+        if (!key_u32(g, {("dac." + pk).c_str(), pk.c_str()}, &pd)) {
+            fprintf(stderr, "gguf: key %s must be specified for the DAC decoder\n", pk.c_str());
+            return TTS_STATUS_BAD_ARG;
+        }
+        if (pd != (s + 1) / 2) {
+            fprintf(stderr, "gguf: DAC block %d padding %u, the decoder assumes ceil(stride / 2) = %u\n", l, pd, (s + 1) / 2);
+            return TTS_STATUS_UNSUPPORTED;
+        }
+        c->rates[l] = (int32_t)s;
+        n_layers = l + 1;
+    }
+    if (n_layers == 0) {
+        fprintf(stderr, "gguf: key dac_layer_stride_0 must be specified for the DAC decoder\n");
+        return TTS_STATUS_BAD_ARG;
+    }
+    c->n_layers = n_layers;
+    const int64_t cd = tdim(g, "audio_encoder.quantizers.0.codebook.weight", 0), cs = tdim(g, "audio_encoder.quantizers.0.codebook.weight", 1);
+    const int64_t lat = tdim(g, "audio_encoder.initial.weight", 1), dd = tdim(g, "audio_encoder.initial.weight", 2);
+    if (cd < 0 || cs < 0 || lat < 0 || dd < 0) {
+        fprintf(stderr, "gguf: DAC tensors missing\n");
+        return TTS_STATUS_BAD_ARG;
+    }
+    c->codebook_dim = (int32_t)cd;
+    c->codebook_size = (int32_t)cs;
+    c->latent_dim = (int32_t)lat;
+    c->decoder_dim = (int32_t)dd;
+    return TTS_STATUS_SUCCESS;
+}
+
+extern "C" tts_dac * tts_dac_create_from_gguf(const tts_backend_iface * be, const tts_dac_config * cfg, const tts_gguf * g) {
+    if (!be || !cfg || !g) return nullptr;
+    return dac_create(be, cfg, g);
+}
+
+namespace tts {
+// The synthetic DAC-44k decoder as "audio_encoder.*" tensors + dac.* keys (dac_gguf_encoder.py:99-110).
+void dac_write_synthetic(const tts_dac_config * cfg, tts_gguf_writer * w) {
+    tts_dac d;  // declarations only
+    d.cfg = *cfg;
+    declare_weights(&d);
+    int64_t hop = 1;
+    for (int l = 0; l < cfg->n_layers; ++l) {
+        hop *= cfg->rates[l];
+        tts_gguf_set_u32(w, ("dac.dac_layer_stride_" + std::to_string(l)).c_str(), (uint32_t)cfg->rates[l]);
+        tts_gguf_set_u32(w, ("dac.dac_layer_padding_" + std::to_string(l)).c_str(), (uint32_t)((cfg->rates[l] + 1) / 2));
+    }
+    tts_gguf_set_u32(w, "dac.up_scaling_factor", (uint32_t)hop);
+    std::vector<float> host;
+    for (auto & s : d.specs) {
+        if (s.t == d.one) continue;
+        const size_t n = (size_t)tg::nelements(s.t);
+        host.resize(n);
+        synth_f32(host.data(), n, s.seed, s.scale, s.offset);
+        int nd = 3;
+        while (nd > 1 && s.t->ne[nd - 1] == 1) --nd;
+        tts_gguf_add_tensor(w, gguf_name(s.t).c_str(), TTS_TYPE_F32, nd, s.t->ne, host.data(), n * 4);
+    }
+}
+}  // namespace tts

@@ -14,6 +14,7 @@
 #include <string>
 #include <vector>
 
+#include "../../include/tts_gguf.h"
 #include "../../include/tts_runners.h"
 #include "graph.h"
 #include "synth.h"
@@ -63,6 +64,7 @@ struct tts_parler {
     tts_sampling samp{};
     int64_t sample_calls = 0;                 // sampler::sample calls so far (one per step)
     std::vector<int32_t> rep_last, rep_count;  // [batch][heads] repetition-penalty state
+    const tts_gguf * gguf = nullptr;  // weight source while creating from a file (else synthetic)
 };
 
 extern "C" void tts_parler_default_config(tts_parler_config * c) {
@@ -96,13 +98,68 @@ struct wspec {
     uint64_t seed;
 };
 
+// Tensor names are the GGUF names without the "decoder." prefix (parler/model.cpp:4-27, :501-505).
+static std::string gguf_name(const tts_tensor * t) { return std::string("decoder.") + t->name; }
+
 static tts_tensor * wnew(tts_parler * p, std::vector<wspec> & specs, int type, int64_t ne0, int64_t ne1, int kind,
                          const std::string & name) {
+    if (p->gguf) {  // the file decides the storage type (quantize_impl.cpp's per-tensor rules)
+        const int64_t i = tts_gguf_find_tensor(p->gguf, ("decoder." + name).c_str());
+        if (i >= 0) type = tts_gguf_tensor_type(p->gguf, i);
+    }
     tts_tensor * t = ne1 > 1 ? tg::new_tensor_2d(p->wctx, type, ne0, ne1) : tg::new_tensor_1d(p->wctx, type, ne0);
     tg::set_name(t, name);
     t->flags |= tg::TG_FLAG_PERSIST;
     specs.push_back({t, kind, p->cfg.seed ^ (p->tensor_index++)});
     return t;
+}
+
+// The synthetic bytes tts_parler_create uploads for a spec (host).
+static void synth_host(const wspec & s, std::vector<char> & host) {
+    const tts_tensor * t = s.t;
+    host.resize(tg::nbytes(t));
+    const int64_t K = t->ne[0], rows = tg::nelements(t) / t->ne[0];
+    const int kind = (t->type == TTS_TYPE_F32) ? s.kind : 0;
+    const float std = s.kind == 3 ? 0.25f : 0.02f;
+    switch (kind) {
+        case 1: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.1f, 1.0f); break;
+        case 2: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.02f, 0.0f); break;
+        case 3: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.5f, 0.0f); break;
+        default: synth_fill(t->type, host.data(), rows, K, s.seed, std); break;
+    }
+}
+
+// Same elements in the same order: equal after dropping the 1-sized dimensions (a GGUF bias [C]
+// against a [1, C] tensor, assign_to_layer's transposed dup).
+static bool same_squeezed_shape(const int64_t * a, const int64_t * b) {
+    int64_t x[4], y[4];
+    int nx = 0, ny = 0;
+    for (int d = 0; d < 4; ++d) {
+        if (a[d] != 1) x[nx++] = a[d];
+        if (b[d] != 1) y[ny++] = b[d];
+    }
+    if (nx != ny) return false;
+    for (int d = 0; d < nx; ++d)
+        if (x[d] != y[d]) return false;
+    return true;
+}
+
+// File tensor for t: present, same type and element layout; NULL (reason on stderr) otherwise.
+static const void * gguf_source(const tts_gguf * g, const std::string & fname, const tts_tensor * t) {
+    const int64_t i = tts_gguf_find_tensor(g, fname.c_str());
+    if (i < 0) {
+        fprintf(stderr, "gguf: tensor '%s' is missing\n", fname.c_str());
+        return nullptr;
+    }
+    int64_t ne[4];
+    tts_gguf_tensor_ndims(g, i, ne);
+    if (tts_gguf_tensor_type(g, i) != t->type || !same_squeezed_shape(ne, t->ne) || tts_gguf_tensor_size(g, i) != tg::nbytes(t)) {
+        fprintf(stderr, "gguf: tensor '%s' has type %d [%lld %lld %lld %lld], the runner needs type %d [%lld %lld %lld %lld]\n", fname.c_str(),
+                tts_gguf_tensor_type(g, i), (long long)ne[0], (long long)ne[1], (long long)ne[2], (long long)ne[3], t->type, (long long)t->ne[0],
+                (long long)t->ne[1], (long long)t->ne[2], (long long)t->ne[3]);
+        return nullptr;
+    }
+    return tts_gguf_tensor_data(g, i);
 }
 
 static bool upload_weights(tts_parler * p, std::vector<wspec> & specs) {
@@ -118,18 +175,16 @@ static bool upload_weights(tts_parler * p, std::vector<wspec> & specs) {
         const size_t nb = tg::nbytes(t);
         t->data = (char *)p->wbuf + off;
         off += (nb + 255) & ~(size_t)255;
-        host.resize(nb);
-        const int64_t K = t->ne[0], rows = tg::nelements(t) / t->ne[0];
-        const int kind = (t->type == TTS_TYPE_F32) ? s.kind : 0;
-        const float std = s.kind == 3 ? 0.25f : 0.02f;
-        switch (kind) {
-            case 1:synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.1f, 1.0f); break;
-            case 2: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.02f, 0.0f); break;
-            case 3: synth_f32((float *)host.data(), (size_t)(K * rows), s.seed, 0.5f, 0.0f); break;
-            default: synth_fill(t->type, host.data(), rows, K, s.seed, std); break;
+        const void * src;
+        if (p->gguf) {  // assign_weight: the mapped file bytes, uploaded whole
+            src = gguf_source(p->gguf, gguf_name(t), t);
+            if (!src) return false;
+        } else {
+            synth_host(s, host);
+            src = host.data();
         }
         // whole-tensor upload: the backend may keep its own layout (HIP: Q4_K lane layout)
-        if (p->be.set_tensor(p->be.ctx, t, host.data()) != 0) return false;
+        if (p->be.set_tensor(p->be.ctx, t, src) != 0) return false;
     }
     return true;
 }
@@ -177,21 +232,17 @@ static bool prep_cross_key_values(tts_parler * p) {
     return p->be.synchronize(p->be.ctx) == 0;
 }
 
-extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tts_parler_config * cfg) {
-    auto * p = new tts_parler();
-    p->cfg = *cfg;
-    p->be = *be;
+extern "C" void tts_parler_free(tts_parler * p);
+
+// Declares every weight tensor in the reference's order (synthetic seeds follow this order).
+static void declare_weights(tts_parler * p, std::vector<wspec> & specs) {
     const auto & cf = p->cfg;
     const int64_t H = cf.hidden_size;
-    const int hd = cf.hidden_size / cf.n_attn_heads;
-    const int B = cf.batch < 1 ? 1 : cf.batch;
-    p->cfg.batch = B;
-    std::vector<wspec> specs;
     // decoder.embed_tokens.{i} (Q4_K when quantized), decoder.lm_heads.{i}.weight.head (F32)
     for (int i = 0; i < cf.n_output_heads; ++i)
-        p->embds.push_back(wnew(p, specs, cf.weight_type, H, cf.output_vocab, 3, "embd_" + std::to_string(i)));
+        p->embds.push_back(wnew(p, specs, cf.weight_type, H, cf.output_vocab, 3, "embed_tokens." + std::to_string(i) + ".weight"));
     for (int i = 0; i < cf.n_output_heads; ++i)
-        p->heads.push_back(wnew(p, specs, cf.head_type, H, cf.output_vocab, 0, "head_" + std::to_string(i)));
+        p->heads.push_back(wnew(p, specs, cf.head_type, H, cf.output_vocab, 0, "lm_heads." + std::to_string(i) + ".weight.head"));
     p->pos_embd = wnew(p, specs, TTS_TYPE_F32, H, cf.max_positions, 3, "positional_embed");
     p->prompt_embd = wnew(p, specs, TTS_TYPE_F32, H, cf.prompt_vocab, 3, "embed_prompts");
     p->text_encoding = wnew(p, specs, TTS_TYPE_F32, H, cf.n_encode, 3, "text_encoding");
@@ -201,27 +252,41 @@ extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tt
     for (int l = 0; l < cf.n_layers; ++l) {
         parler_layer & L = p->layers[l];
         const std::string pre = "layers." + std::to_string(l);
-        L.q = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.q_proj");
-        L.k = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.k_proj");
-        L.v = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.v_proj");
-        L.o = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.out_proj");
+        L.q = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.q_proj.weight");
+        L.k = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.k_proj.weight");
+        L.v = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.v_proj.weight");
+        L.o = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".self_attn.out_proj.weight");
         L.sa_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".self_attn_layer_norm.weight");
         L.sa_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".self_attn_layer_norm.bias");
-        L.aq = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.q_proj");
+        L.aq = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.q_proj.weight");
         // encoder_attn k/v stay F32 (quantize_impl.cpp: quantize_cross_attn_kv off by default)
-        L.ak = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.k_proj");
-        L.av = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.v_proj");
-        L.ao = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.out_proj");
+        L.ak = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.k_proj.weight");
+        L.av = wnew(p, specs, TTS_TYPE_F32, H, H, 0, pre + ".encoder_attn.v_proj.weight");
+        L.ao = wnew(p, specs, cf.weight_type, H, H, 0, pre + ".encoder_attn.out_proj.weight");
         L.a_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".encoder_attn_layer_norm.weight");
         L.a_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".encoder_attn_layer_norm.bias");
-        L.fc1 = wnew(p, specs, cf.weight_type, H, cf.ffn_size, 0, pre + ".fc1");
-        L.fc2 = wnew(p, specs, cf.weight_type, cf.ffn_size, H, 0, pre + ".fc2");
+        L.fc1 = wnew(p, specs, cf.weight_type, H, cf.ffn_size, 0, pre + ".fc1.weight");
+        L.fc2 = wnew(p, specs, cf.weight_type, cf.ffn_size, H, 0, pre + ".fc2.weight");
         L.f_norm = wnew(p, specs, TTS_TYPE_F32, H, 1, 1, pre + ".final_layer_norm.weight");
         L.f_norm_b = wnew(p, specs, TTS_TYPE_F32, H, 1, 2, pre + ".final_layer_norm.bias");
     }
+}
+
+static tts_parler * parler_create(const tts_backend_iface * be, const tts_parler_config * cfg, const tts_gguf * g) {
+    auto * p = new tts_parler();
+    p->cfg = *cfg;
+    p->be = *be;
+    p->gguf = g;
+    const auto & cf = p->cfg;
+    const int64_t H = cf.hidden_size;
+    const int hd = cf.hidden_size / cf.n_attn_heads;
+    const int B = cf.batch < 1 ? 1 : cf.batch;
+    p->cfg.batch = B;
+    std::vector<wspec> specs;
+    declare_weights(p, specs);
     if (!upload_weights(p, specs)) {
         fprintf(stderr, "parler: weight allocation/upload failed\n");
-        delete p;
+        tts_parler_free(p);
         return nullptr;
     }
     // cross K/V + KV caches in one persistent buffer
@@ -231,7 +296,7 @@ extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tt
     p->kvbytes = (size_t)cf.n_layers * (((ck + 255) & ~(size_t)255) + ((cv + 255) & ~(size_t)255) + 2 * kvl);
     p->kvbuf = p->be.alloc(p->be.ctx, p->kvbytes);
     if (!p->kvbuf) {
-        delete p;
+        tts_parler_free(p);
         return nullptr;
     }
     p->be.memset(p->be.ctx, p->kvbuf, 0, p->kvbytes);  // ggml_backend_buffer_clear(buf, 0)
@@ -260,17 +325,20 @@ extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tt
     p->arena_size = cf.arena_bytes ? cf.arena_bytes : (256ull << 20);
     p->arena = (char *)p->be.alloc(p->be.ctx, p->arena_size);
     if (!p->arena) {
-        delete p;
+        tts_parler_free(p);
         return nullptr;
     }
     if (cf.use_cross_attn && !prep_cross_key_values(p)) {
         fprintf(stderr, "parler: cross K/V precompute failed\n");
-        delete p;
+        tts_parler_free(p);
         return nullptr;
     }
+    p->gguf = nullptr;
     tts_parler_reset(p);
     return p;
 }
+
+extern "C" tts_parler * tts_parler_create(const tts_backend_iface * be, const tts_parler_config * cfg) { return parler_create(be, cfg, nullptr); }
 
 extern "C" void tts_parler_free(tts_parler * p) {
     if (!p) return;
@@ -749,4 +817,112 @@ extern "C" uint64_t tts_parler_get_node(tts_parler * p, const char * name, void 
         }
     }
     return 0;
+}
+
+// ---- GGUF loader path (runner_from_file + parler_tts_model::prep_constants / assign_weight) ----
+namespace tts {
+void dac_write_synthetic(const tts_dac_config * cfg, tts_gguf_writer * w);
+}
+
+static bool gguf_u32(const tts_gguf * g, std::initializer_list<const char *> keys, int32_t * out) {
+    for (const char * k : keys) {  // search_for_gguf_keys: first key present wins
+        const int64_t i = tts_gguf_find_key(g, k);
+        uint32_t v;
+        if (i >= 0 && tts_gguf_get_u32(g, i, &v)) {
+            *out = (int32_t)v;
+            return true;
+        }
+    }
+    return false;
+}
+
+static int64_t gguf_dim(const tts_gguf * g, const char * name, int d) {
+    const int64_t i = tts_gguf_find_tensor(g, name);
+    if (i < 0) return -1;
+    int64_t ne[4];
+    tts_gguf_tensor_ndims(g, i, ne);
+    return ne[d];
+}
+
+extern "C" int tts_parler_config_from_gguf(const tts_gguf * g, tts_parler_config * c) {
+    if (!g || !c) return TTS_STATUS_BAD_ARG;
+    const int64_t ak = tts_gguf_find_key(g, "general.architecture");
+    if (ak >= 0 && (!tts_gguf_get_str(g, ak) || strcmp(tts_gguf_get_str(g, ak), "parler-tts") != 0)) {
+        fprintf(stderr, "gguf: not a parler-tts file\n");
+        return TTS_STATUS_BAD_ARG;
+    }
+    // prep_constants (model.cpp:51-108); encode_length is the one required key
+    if (!gguf_u32(g, {"parler-tts.decoder.encode_length", "encode_length"}, &c->n_encode)) {
+        fprintf(stderr, "gguf: key 'parler-tts.decoder.encode_length' must be specified\n");
+        return TTS_STATUS_BAD_ARG;
+    }
+    gguf_u32(g, {"parler-tts.decoder.hidden_size", "hidden_size"}, &c->hidden_size);
+    gguf_u32(g, {"parler-tts.decoder.output_heads", "output_heads"}, &c->n_output_heads);
+    gguf_u32(g, {"parler-tts.decoder.attention.head_count", "attn_heads"}, &c->n_attn_heads);
+    gguf_u32(g, {"parler-tts.decoder.out_vocab_size", "out_vocab_size"}, &c->output_vocab);
+    gguf_u32(g, {"parler-tts.decoder.audio_vocab_size", "audio_vocab_size"}, &c->audio_vocab);
+    gguf_u32(g, {"parler-tts.decoder.num_hidden_layers", "num_hidden_layers"}, &c->n_layers);
+    gguf_u32(g, {"audio.bos_token_id", "bos_token_id"}, &c->bos_token);
+    gguf_u32(g, {"audio.eos_token_id", "eos_token_id"}, &c->eos_token);
+    // sizes the reference takes from the tensors themselves
+    const int64_t ffn = gguf_dim(g, "decoder.layers.0.fc1.weight", 1);
+    const int64_t pv = gguf_dim(g, "decoder.embed_prompts", 1);
+    const int64_t mp = gguf_dim(g, "decoder.positional_embed", 1);
+    const int64_t wt = tts_gguf_find_tensor(g, "decoder.layers.0.self_attn.q_proj.weight");
+    const int64_t ht = tts_gguf_find_tensor(g, "decoder.lm_heads.0.weight.head");
+    if (ffn < 0 || pv < 0 || mp < 0 || wt < 0 || ht < 0) {
+        fprintf(stderr, "gguf: decoder tensors missing\n");
+        return TTS_STATUS_BAD_ARG;
+    }
+    c->ffn_size = (int32_t)ffn;
+    c->prompt_vocab = (int32_t)pv;
+    c->max_positions = (int32_t)mp;
+    c->weight_type = tts_gguf_tensor_type(g, wt);
+    c->head_type = tts_gguf_tensor_type(g, ht);
+    c->use_cross_attn = tts_gguf_find_tensor(g, "decoder.layers.0.encoder_attn.q_proj.weight") >= 0 ? 1 : 0;
+    if (!c->use_cross_attn) {
+        fprintf(stderr, "gguf: parler files without cross attention are not supported\n");
+        return TTS_STATUS_UNSUPPORTED;
+    }
+    return TTS_STATUS_SUCCESS;
+}
+
+extern "C" tts_parler * tts_parler_create_from_gguf(const tts_backend_iface * be, const tts_parler_config * cfg, const tts_gguf * g) {
+    if (!be || !cfg || !g) return nullptr;
+    return parler_create(be, cfg, g);
+}
+
+extern "C" int tts_parler_write_synthetic_gguf(const tts_parler_config * cfg, const tts_dac_config * dac_cfg, const char * path) {
+    if (!cfg || !path) return TTS_STATUS_BAD_ARG;
+    tts_parler p;  // declarations only: no backend, no buffers
+    p.cfg = *cfg;
+    std::vector<wspec> specs;
+    declare_weights(&p, specs);
+    tts_gguf_writer * w = tts_gguf_writer_new();
+    const auto & c = *cfg;
+    // the keys prep_constants reads (parler_tts_gguf_encoder.py writes them)
+    tts_gguf_set_str(w, "general.architecture", "parler-tts");
+    tts_gguf_set_u32(w, "parler-tts.decoder.encode_length", (uint32_t)c.n_encode);
+    tts_gguf_set_u32(w, "parler-tts.decoder.hidden_size", (uint32_t)c.hidden_size);
+    tts_gguf_set_u32(w, "parler-tts.decoder.output_heads", (uint32_t)c.n_output_heads);
+    tts_gguf_set_u32(w, "parler-tts.decoder.context_length", (uint32_t)c.max_ctx);
+    tts_gguf_set_u32(w, "parler-tts.decoder.attention.head_count", (uint32_t)c.n_attn_heads);
+    tts_gguf_set_u32(w, "parler-tts.decoder.out_vocab_size", (uint32_t)c.output_vocab);
+    tts_gguf_set_u32(w, "parler-tts.decoder.audio_vocab_size", (uint32_t)c.audio_vocab);
+    tts_gguf_set_u32(w, "parler-tts.decoder.max_generation", (uint32_t)c.max_ctx);
+    tts_gguf_set_u32(w, "parler-tts.decoder.num_hidden_layers", (uint32_t)c.n_layers);
+    tts_gguf_set_u32(w, "audio.bos_token_id", (uint32_t)c.bos_token);
+    tts_gguf_set_u32(w, "audio.eos_token_id", (uint32_t)c.eos_token);
+    int st = TTS_STATUS_SUCCESS;
+    std::vector<char> host;
+    for (auto & s : specs) {
+        synth_host(s, host);
+        const int nd = s.t->ne[1] > 1 ? 2 : 1;
+        st = tts_gguf_add_tensor(w, gguf_name(s.t).c_str(), s.t->type, nd, s.t->ne, host.data(), host.size());
+        if (st != TTS_STATUS_SUCCESS) break;
+    }
+    if (st == TTS_STATUS_SUCCESS && dac_cfg) dac_write_synthetic(dac_cfg, w);
+    if (st == TTS_STATUS_SUCCESS) st = tts_gguf_writer_write(w, path);
+    tts_gguf_writer_free(w);
+    return st;
 }

@@ -269,6 +269,18 @@ class KokoroConfig(ctypes.Structure):
 _lib = None
 
 
+class QuantizeParams(ctypes.Structure):
+    """tts_quantize_params (quantize_impl.h quantization_params without n_threads)."""
+    _fields_ = [("quantize_type", ctypes.c_int32), ("quantize_output_heads", ctypes.c_int32),
+                ("quantize_text_embeddings", ctypes.c_int32), ("quantize_cross_attn_kv", ctypes.c_int32),
+                ("convert_dac_to_f16", ctypes.c_int32), ("convert_non_quantizable_to_f16", ctypes.c_int32)]
+
+
+# tts_quantize_rows_fn(ctx, type, x, dst, rows, K)
+QUANTIZE_ROWS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_int64, ctypes.c_int64)
+
+
 def row_size(t, ne0):
     return TYPE_SIZE[t] * (ne0 // BLCK_SIZE[t])
 
@@ -402,6 +414,55 @@ def lib():
         "tts_kokoro_gen_graph": (vp, [vp, ctypes.POINTER(i32)]),
         "tts_hip_plan_stats": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i32)]),
         "tts_kokoro_gen_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(ctypes.c_int64), vp, u64]),
+        # GGUF files (include/tts_gguf.h)
+        "tts_gguf_open": (vp, [ctypes.c_char_p]),
+        "tts_gguf_close": (None, [vp]),
+        "tts_gguf_version": (ctypes.c_uint32, [vp]),
+        "tts_gguf_alignment": (u64, [vp]),
+        "tts_gguf_data_offset": (u64, [vp]),
+        "tts_gguf_n_kv": (i64, [vp]),
+        "tts_gguf_find_key": (i64, [vp, ctypes.c_char_p]),
+        "tts_gguf_key": (ctypes.c_char_p, [vp, i64]),
+        "tts_gguf_kv_type": (i32, [vp, i64]),
+        "tts_gguf_get_u32": (ctypes.c_int, [vp, i64, ctypes.POINTER(ctypes.c_uint32)]),
+        "tts_gguf_get_i64": (ctypes.c_int, [vp, i64, ctypes.POINTER(i64)]),
+        "tts_gguf_get_f64": (ctypes.c_int, [vp, i64, ctypes.POINTER(ctypes.c_double)]),
+        "tts_gguf_get_str": (ctypes.c_char_p, [vp, i64]),
+        "tts_gguf_arr_type": (i32, [vp, i64]),
+        "tts_gguf_arr_n": (i64, [vp, i64]),
+        "tts_gguf_arr_data": (vp, [vp, i64]),
+        "tts_gguf_arr_str": (ctypes.c_char_p, [vp, i64, i64]),
+        "tts_gguf_n_tensors": (i64, [vp]),
+        "tts_gguf_find_tensor": (i64, [vp, ctypes.c_char_p]),
+        "tts_gguf_tensor_name": (ctypes.c_char_p, [vp, i64]),
+        "tts_gguf_tensor_type": (i32, [vp, i64]),
+        "tts_gguf_tensor_ndims": (i32, [vp, i64, ctypes.POINTER(i64)]),
+        "tts_gguf_tensor_offset": (u64, [vp, i64]),
+        "tts_gguf_tensor_size": (u64, [vp, i64]),
+        "tts_gguf_tensor_data": (vp, [vp, i64]),
+        "tts_gguf_type_size": (sz, [i32]),
+        "tts_gguf_blck_size": (i64, [i32]),
+        "tts_gguf_writer_new": (vp, []),
+        "tts_gguf_writer_free": (None, [vp]),
+        "tts_gguf_set_u32": (None, [vp, ctypes.c_char_p, ctypes.c_uint32]),
+        "tts_gguf_set_i32": (None, [vp, ctypes.c_char_p, i32]),
+        "tts_gguf_set_f32": (None, [vp, ctypes.c_char_p, ctypes.c_float]),
+        "tts_gguf_set_u64": (None, [vp, ctypes.c_char_p, u64]),
+        "tts_gguf_set_bool": (None, [vp, ctypes.c_char_p, ctypes.c_int]),
+        "tts_gguf_set_str": (None, [vp, ctypes.c_char_p, ctypes.c_char_p]),
+        "tts_gguf_set_arr": (None, [vp, ctypes.c_char_p, i32, vp, i64]),
+        "tts_gguf_set_arr_str": (None, [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), i64]),
+        "tts_gguf_copy_kv": (None, [vp, vp]),
+        "tts_gguf_add_tensor": (ctypes.c_int, [vp, ctypes.c_char_p, i32, i32, ctypes.POINTER(i64), vp, u64]),
+        "tts_gguf_writer_write": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "tts_gguf_tensor_rule": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(QuantizeParams)]),
+        "tts_gguf_quantize": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(QuantizeParams), vp, vp]),
+        "tts_hip_gguf_quantize": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(QuantizeParams)]),
+        "tts_parler_config_from_gguf": (ctypes.c_int, [vp, ctypes.POINTER(ParlerConfig)]),
+        "tts_parler_create_from_gguf": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(ParlerConfig), vp]),
+        "tts_parler_write_synthetic_gguf": (ctypes.c_int, [ctypes.POINTER(ParlerConfig), ctypes.POINTER(DacConfig), ctypes.c_char_p]),
+        "tts_dac_config_from_gguf": (ctypes.c_int, [vp, ctypes.POINTER(DacConfig)]),
+        "tts_dac_create_from_gguf": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(DacConfig), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -680,12 +741,16 @@ def parler_config(**kw):
 class Parler:
     """Parler-TTS decoder runner over a backend vtable (HIP, or the oracle in tests)."""
 
-    def __init__(self, iface, cfg):
+    def __init__(self, iface, cfg, gguf=None):
+        """gguf: a Gguf file whose "decoder.*" tensors are the weights (cfg from parler_config_from_gguf)."""
         import numpy as np  # noqa: F401
         self.L = lib()
         self.cfg = cfg
         self._iface = iface  # keep alive
-        self.ptr = self.L.tts_parler_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if gguf is None:
+            self.ptr = self.L.tts_parler_create(ctypes.byref(iface), ctypes.byref(cfg))
+        else:
+            self.ptr = self.L.tts_parler_create_from_gguf(ctypes.byref(iface), ctypes.byref(cfg), gguf.ptr)
         if not self.ptr:
             raise RuntimeError("tts_parler_create failed")
 
@@ -787,11 +852,15 @@ def dac_config(**kw):
 class Dac:
     """DAC decoder runner (codec tokens -> PCM) over a backend vtable (HIP, or the oracle in tests)."""
 
-    def __init__(self, iface, cfg):
+    def __init__(self, iface, cfg, gguf=None):
+        """gguf: a Gguf file whose "audio_encoder.*" tensors are the weights (cfg from dac_config_from_gguf)."""
         self.L = lib()
         self.cfg = cfg
         self._iface = iface
-        self.ptr = self.L.tts_dac_create(ctypes.byref(iface), ctypes.byref(cfg))
+        if gguf is None:
+            self.ptr = self.L.tts_dac_create(ctypes.byref(iface), ctypes.byref(cfg))
+        else:
+            self.ptr = self.L.tts_dac_create_from_gguf(ctypes.byref(iface), ctypes.byref(cfg), gguf.ptr)
         if not self.ptr:
             raise RuntimeError("tts_dac_create failed")
 
@@ -1126,3 +1195,204 @@ def plan_stats(nodes_ptr, n_nodes, mask):
     out["xattn"] = int(counts[14])
     out["unfused"] = int(counts[15])
     return out
+
+
+# ---- GGUF files (include/tts_gguf.h) ----
+GGUF_TYPES = {"u8": 0, "i8": 1, "u16": 2, "i16": 3, "u32": 4, "i32": 5, "f32": 6, "bool": 7, "str": 8, "arr": 9, "u64": 10,
+              "i64": 11, "f64": 12}
+_GGUF_NP = {0: "u1", 1: "i1", 2: "<u2", 3: "<i2", 4: "<u4", 5: "<i4", 6: "<f4", 7: "u1", 10: "<u8", 11: "<i8", 12: "<f8"}
+
+
+class Gguf:
+    """A GGUF file mapped read-only (gguf_init_from_file + llama_mmap)."""
+
+    def __init__(self, path):
+        self.L = lib()
+        self.ptr = self.L.tts_gguf_open(str(path).encode())
+        if not self.ptr:
+            raise RuntimeError(f"cannot read GGUF file {path}")
+
+    @property
+    def version(self):
+        return self.L.tts_gguf_version(self.ptr)
+
+    @property
+    def alignment(self):
+        return self.L.tts_gguf_alignment(self.ptr)
+
+    @property
+    def data_offset(self):
+        return self.L.tts_gguf_data_offset(self.ptr)
+
+    def keys(self):
+        return [self.L.tts_gguf_key(self.ptr, i).decode() for i in range(self.L.tts_gguf_n_kv(self.ptr))]
+
+    def get(self, key, default=None):
+        """Value of a key: int / float / bool / str, or a list / numpy array for arrays."""
+        import numpy as np
+        L, g = self.L, self.ptr
+        i = L.tts_gguf_find_key(g, key.encode())
+        if i < 0:
+            return default
+        t = L.tts_gguf_kv_type(g, i)
+        if t == 8:
+            return L.tts_gguf_get_str(g, i).decode()
+        if t == 9:
+            at, n = L.tts_gguf_arr_type(g, i), L.tts_gguf_arr_n(g, i)
+            if at == 8:
+                return [L.tts_gguf_arr_str(g, i, j).decode() for j in range(n)]
+            dt = np.dtype(_GGUF_NP[at])
+            buf = (ctypes.c_char * (n * dt.itemsize)).from_address(L.tts_gguf_arr_data(g, i)) if n else b""
+            return np.frombuffer(bytes(buf), dtype=dt).copy()
+        if t in (6, 12):
+            v = ctypes.c_double()
+            L.tts_gguf_get_f64(g, i, ctypes.byref(v))
+            return v.value
+        v = ctypes.c_int64()
+        L.tts_gguf_get_i64(g, i, ctypes.byref(v))
+        return bool(v.value) if t == 7 else v.value
+
+    def tensors(self):
+        """[(name, type, ne (4), offset, nbytes)] in file order."""
+        L, g = self.L, self.ptr
+        out = []
+        for i in range(L.tts_gguf_n_tensors(g)):
+            ne = (ctypes.c_int64 * 4)()
+            nd = L.tts_gguf_tensor_ndims(g, i, ne)
+            out.append((L.tts_gguf_tensor_name(g, i).decode(), L.tts_gguf_tensor_type(g, i), tuple(ne[:nd]),
+                        L.tts_gguf_tensor_offset(g, i), L.tts_gguf_tensor_size(g, i)))
+        return out
+
+    def tensor_bytes(self, name):
+        """The tensor's bytes (a copy of the mapping) as uint8."""
+        import numpy as np
+        i = self.L.tts_gguf_find_tensor(self.ptr, name.encode())
+        if i < 0:
+            raise KeyError(name)
+        n = self.L.tts_gguf_tensor_size(self.ptr, i)
+        return np.frombuffer(bytes((ctypes.c_char * n).from_address(self.L.tts_gguf_tensor_data(self.ptr, i))), dtype=np.uint8)
+
+    def tensor_type(self, name):
+        i = self.L.tts_gguf_find_tensor(self.ptr, name.encode())
+        return None if i < 0 else self.L.tts_gguf_tensor_type(self.ptr, i)
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_gguf_close(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class GgufWriter:
+    """gguf_init_empty / gguf_set_* / gguf_add_tensor / gguf_write_to_file."""
+
+    def __init__(self):
+        self.L = lib()
+        self.ptr = self.L.tts_gguf_writer_new()
+
+    def set(self, key, value, kind=None):
+        """kind: u32 (int default), i32, u64, f32 (float default), bool, str, or ("arr", elem kind) for lists."""
+        import numpy as np
+        k, L, w = key.encode(), self.L, self.ptr
+        if isinstance(value, (list, tuple, np.ndarray)):
+            ek = kind[1] if isinstance(kind, tuple) else ("str" if value and isinstance(value[0], str) else "i32")
+            if ek == "str":
+                arr = (ctypes.c_char_p * len(value))(*[v.encode() for v in value])
+                L.tts_gguf_set_arr_str(w, k, arr, len(value))
+            else:
+                a = np.ascontiguousarray(value, dtype=np.dtype(_GGUF_NP[GGUF_TYPES[ek]]))
+                L.tts_gguf_set_arr(w, k, GGUF_TYPES[ek], a.ctypes.data, a.size)
+            return
+        kind = kind or ("bool" if isinstance(value, bool) else "str" if isinstance(value, str) else
+                        "f32" if isinstance(value, float) else "u32")
+        fn = {"u32": L.tts_gguf_set_u32, "i32": L.tts_gguf_set_i32, "u64": L.tts_gguf_set_u64, "f32": L.tts_gguf_set_f32,
+              "bool": L.tts_gguf_set_bool, "str": L.tts_gguf_set_str}[kind]
+        fn(w, k, value.encode() if kind == "str" else value)
+
+    def copy_kv(self, g):
+        self.L.tts_gguf_copy_kv(self.ptr, g.ptr)
+
+    def add_tensor(self, name, ttype, ne, data):
+        import numpy as np
+        d = np.ascontiguousarray(data)
+        ne_a = (ctypes.c_int64 * len(ne))(*ne)
+        st = self.L.tts_gguf_add_tensor(self.ptr, name.encode(), ttype, len(ne), ne_a, d.ctypes.data, d.nbytes)
+        if st != 0:
+            raise ValueError(f"add_tensor({name}) failed {st}")
+
+    def write(self, path):
+        if self.L.tts_gguf_writer_write(self.ptr, str(path).encode()) != 0:
+            raise RuntimeError(f"writing {path} failed")
+
+    def close(self):
+        if self.ptr:
+            self.L.tts_gguf_writer_free(self.ptr)
+            self.ptr = None
+
+
+def quantize_params(quantize_type=Q4_K, **kw):
+    p = QuantizeParams()
+    p.quantize_type = quantize_type
+    for k, v in kw.items():
+        setattr(p, k, int(v))
+    return p
+
+
+def gguf_tensor_rule(arch, name, params=None):
+    """1 = quantize, 2 = convert to F16, 0 = copy (quantize_impl.cpp's is_quantizable / F16 rules)."""
+    p = params or quantize_params()
+    return lib().tts_gguf_tensor_rule(arch.encode() if arch else None, name.encode(), ctypes.byref(p))
+
+
+def quantize_gguf(src, dst, params=None, backend=None, rows_fn=None):
+    """examples/quantize's quantize_gguf.  The rows are quantized by the device (backend: HipBackend) or by
+    rows_fn(type, x[rows][K] float32) -> bytes (tests: the CPU oracle)."""
+    import numpy as np
+    L = lib()
+    p = params or quantize_params()
+    if backend is not None:
+        st = L.tts_hip_gguf_quantize(backend.ptr, str(src).encode(), str(dst).encode(), ctypes.byref(p))
+    else:
+        def cb(_ctx, ttype, x, dst_p, rows, K):
+            try:
+                xa = np.ctypeslib.as_array(ctypes.cast(x, ctypes.POINTER(ctypes.c_float)), shape=(rows, K))
+                q = np.ascontiguousarray(rows_fn(ttype, xa.copy()), dtype=np.uint8)
+                ctypes.memmove(dst_p, q.ctypes.data, q.nbytes)
+                return 0
+            except Exception:  # noqa: BLE001 -- reported as a failed conversion
+                import traceback
+                traceback.print_exc()
+                return -1
+        fn = QUANTIZE_ROWS_FN(cb)
+        st = L.tts_gguf_quantize(str(src).encode(), str(dst).encode(), ctypes.byref(p), ctypes.cast(fn, ctypes.c_void_p), None)
+    if st != 0:
+        raise RuntimeError(f"quantize_gguf failed {st}")
+
+
+def parler_config_from_gguf(g, **kw):
+    cfg = parler_config(**kw)
+    if lib().tts_parler_config_from_gguf(g.ptr, ctypes.byref(cfg)) != 0:
+        raise RuntimeError("not a usable parler-tts GGUF file")
+    for k, v in kw.items():  # caller overrides (batch, max_ctx, arena) win
+        setattr(cfg, k, v)
+    return cfg
+
+
+def dac_config_from_gguf(g, **kw):
+    cfg = dac_config(**kw)
+    if lib().tts_dac_config_from_gguf(g.ptr, ctypes.byref(cfg)) != 0:
+        raise RuntimeError("no usable DAC decoder in the GGUF file")
+    return cfg
+
+
+def write_parler_synthetic_gguf(path, cfg, dac_cfg=None):
+    """The runner's synthetic weights for cfg (and a DAC decoder) as a GGUF file with the reference's names."""
+    st = lib().tts_parler_write_synthetic_gguf(ctypes.byref(cfg), ctypes.byref(dac_cfg) if dac_cfg is not None else None,
+                                               str(path).encode())
+    if st != 0:
+        raise RuntimeError(f"writing {path} failed {st}")
