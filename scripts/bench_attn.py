@@ -1,4 +1,5 @@
-"""Decode-attention micro-benchmark at Parler (hd 64, H 16, B 8) and Orpheus (hd 128, H 24/8, B 1)
+"""Decode-attention micro-benchmark at Parler (hd 64, H 16, B 8) and Orpheus (hd 128, H 24, B 1; the
+Orpheus runner hands attention its GQA copies of K / V, so Hk = H here)
 shapes: the unfused reference chain (tests/test_attn_gpu.py `build`) through tts_hip_graph_compute,
 which the planner fuses into one attention item, repeated `reps` times with the split kernels on and
 off.  Wall time per call after a device sync; run under rocprofv3 --kernel-trace for kernel times.
@@ -43,12 +44,16 @@ def run(hip, P, hd, H, Hk, B, reps, split):
     hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split == "split" else 0)
     ptrs = g.node_ptrs()
     L = ttship.lib()
+    def compute():
+        st = L.tts_hip_graph_compute(hip.ptr, ptrs, len(g.nodes))
+        if st != 0:
+            raise RuntimeError(f"tts_hip_graph_compute failed {st} (P {P}, hd {hd}, H {H}, Hk {Hk}, B {B}, {split})")
     for _ in range(3):
-        L.tts_hip_graph_compute(hip.ptr, ptrs, len(g.nodes))
+        compute()
     hip.sync()
     t0 = time.perf_counter()
     for _ in range(reps):
-        L.tts_hip_graph_compute(hip.ptr, ptrs, len(g.nodes))
+        compute()
     hip.sync()
     dt = (time.perf_counter() - t0) / reps
     for d in dev.values():
@@ -63,7 +68,7 @@ def run(hip, P, hd, H, Hk, B, reps, split):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     hip = ttship.HipBackend(0)
-    for (hd, H, Hk, B) in [(64, 16, 16, 8), (128, 24, 8, 1)]:
+    for (hd, H, Hk, B) in [(64, 16, 16, 8), (128, 24, 24, 1)]:
         for P in (448, 900, 1309, 2048):
             for split in ("rows", "split", "fused"):
                 print(json.dumps(run(hip, P, hd, H, Hk, B, reps, split)), flush=True)
