@@ -316,7 +316,139 @@ void ref_quantize_row_q4_K(const float * x, ref_block_q4_K * y, int64_t k) {
     }
 }
 
+/* ---- SIMD accumulation order (oracle_set_simd_mode(1)) -------------------------------------------
+ * A stock x86-64 ggml-cpu build (AVX2 + FMA + F16C, GGML_SIMD) does not run the generic loops above:
+ *  - ggml_vec_dot_f16 / _f32: GGML_F16_STEP = GGML_F32_STEP = 32 elements per iteration in
+ *    GGML_F32_ARR = 4 accumulators of 8 f32 lanes, sum[j] = fma(x, y, sum[j]) (_mm256_fmadd_ps),
+ *    then GGML_F32x8_REDUCE: sum0 += sum2, sum1 += sum3, sum0 += sum1, the two 128-bit halves added,
+ *    two horizontal adds; the tail (n % 32) is added after, in ggml_float for f16 and in f32 (fused
+ *    multiply-add, -ffp-contract=fast) for f32.
+ *  - ggml_vec_dot_q4_K_q8_K (__AVX2__): per super-block the integer sums land in 8 int32 lanes, lane k
+ *    holding bytes 4k..4k+3 of every 32-byte chunk (maddubs + madd with the 6-bit scales); then
+ *    acc[k] = fma(d, (float)sumi[k], acc[k]) with d = y.d * x.d, the mins term in 4 lanes
+ *    acc_m = fma(-y.d * x.dmin, (float)prod, acc_m), and *s = hsum_float_8(acc) + hsum(acc_m).
+ *  - ggml_vec_dot_q8_0_q8_0 (__AVX2__): per block the 32 products in 8 int32 lanes (4 bytes each),
+ *    acc = fma(x.d * y.d, (float)lane, acc), *s = hsum_float_8(acc).
+ *  - conv_transpose_1d (upstream's loop, which the fork extends with padding / dilation / groups): for
+ *    each output channel, input position i and tap k, v = vec_dot over the input channels, then
+ *    dst[i*s0 + k*d0 - p0] += v in f32.
+ * Restated from the published upstream ggml-cpu sources (ggml-cpu.c / vec.cpp / ggml-quants.c /
+ * simd-mappings.h of early 2025, the fork's base); the fork itself is absent, so this mode
+ * bounds the scalar-vs-SIMD gap rather than reproducing a pinned binary. */
+static int g_simd_mode = 0;
+void oracle_set_simd_mode(int mode) { g_simd_mode = mode; }
+int oracle_simd_mode(void) { return g_simd_mode; }
+
+/* GGML_F32x8_REDUCE over four 8-lane accumulators */
+static float simd_reduce4x8(float acc[4][8]) {
+    for (int e = 0; e < 8; ++e) acc[0][e] = acc[0][e] + acc[2][e];
+    for (int e = 0; e < 8; ++e) acc[1][e] = acc[1][e] + acc[3][e];
+    for (int e = 0; e < 8; ++e) acc[0][e] = acc[0][e] + acc[1][e];
+    float t0[4];
+    for (int e = 0; e < 4; ++e) t0[e] = acc[0][e] + acc[0][4 + e];  /* low half + high half */
+    const float h0 = t0[0] + t0[1], h1 = t0[2] + t0[3];              /* _mm_hadd_ps(t0, t0) */
+    return h0 + h1;                                                   /* _mm_hadd_ps(t1, t1)[0] */
+}
+
+/* hsum_float_8 */
+static float simd_hsum8(const float x[8]) {
+    float r[4];
+    for (int e = 0; e < 4; ++e) r[e] = x[4 + e] + x[e];
+    const float a = r[0] + r[2], b = r[1] + r[3];
+    return a + b;
+}
+
+static void simd_vec_dot_f16(int n, float * s, const ref_fp16_t * x, const ref_fp16_t * y) {
+    const int np = n & ~31;
+    float acc[4][8];
+    memset(acc, 0, sizeof(acc));
+    for (int i = 0; i < np; i += 32)
+        for (int j = 0; j < 4; ++j)
+            for (int e = 0; e < 8; ++e)
+                acc[j][e] = fmaf(ref_fp16_to_fp32(x[i + 8 * j + e]), ref_fp16_to_fp32(y[i + 8 * j + e]), acc[j][e]);
+    ggml_float sumf = (ggml_float)simd_reduce4x8(acc);
+    for (int i = np; i < n; ++i) sumf += (ggml_float)(ref_fp16_to_fp32(x[i]) * ref_fp16_to_fp32(y[i]));
+    *s = (float)sumf;
+}
+
+static void simd_vec_dot_f32(int n, float * s, const float * x, const float * y) {
+    const int np = n & ~31;
+    float acc[4][8];
+    memset(acc, 0, sizeof(acc));
+    for (int i = 0; i < np; i += 32)
+        for (int j = 0; j < 4; ++j)
+            for (int e = 0; e < 8; ++e) acc[j][e] = fmaf(x[i + 8 * j + e], y[i + 8 * j + e], acc[j][e]);
+    float sumf = simd_reduce4x8(acc);
+    for (int i = np; i < n; ++i) sumf = fmaf(x[i], y[i], sumf);
+    *s = sumf;
+}
+
+static void simd_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy) {
+    const ref_block_q4_K * x = (const ref_block_q4_K *)vx;
+    const ref_block_q8_K * y = (const ref_block_q8_K *)vy;
+    const int nb = n / QK_K;
+    static const uint32_t kmask1 = 0x3f3f3f3f, kmask2 = 0x0f0f0f0f, kmask3 = 0x03030303;
+    uint32_t utmp[4];
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, acc_m[4] = {0, 0, 0, 0};
+    for (int i = 0; i < nb; ++i) {
+        const float d = y[i].d * ref_fp16_to_fp32(x[i].d);
+        const float dmin = -y[i].d * ref_fp16_to_fp32(x[i].dmin);
+        memcpy(utmp, x[i].scales, 12);
+        utmp[3] = ((utmp[2] >> 4) & kmask2) | (((utmp[1] >> 6) & kmask3) << 4);
+        const uint32_t uaux = utmp[1] & kmask1;
+        utmp[1] = (utmp[2] & kmask2) | (((utmp[0] >> 6) & kmask3) << 4);
+        utmp[2] = uaux;
+        utmp[0] &= kmask1;
+        const uint8_t * sc = (const uint8_t *)&utmp[0];  /* scales[0..7] */
+        const uint8_t * mn = (const uint8_t *)&utmp[2];  /* mins[0..7] */
+        /* mins: q8s[p] = bsums[2p] + bsums[2p+1] (hadd), prod lane q = mn[2q]*q8s[2q] + mn[2q+1]*q8s[2q+1] */
+        for (int q = 0; q < 4; ++q) {
+            const int32_t s0 = y[i].bsums[4 * q] + y[i].bsums[4 * q + 1], s1 = y[i].bsums[4 * q + 2] + y[i].bsums[4 * q + 3];
+            const int32_t prod = (int32_t)mn[2 * q] * s0 + (int32_t)mn[2 * q + 1] * s1;
+            acc_m[q] = fmaf(dmin, (float)prod, acc_m[q]);
+        }
+        int32_t sumi[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint8_t * q4 = x[i].qs;
+        const int8_t * q8 = y[i].qs;
+        for (int j = 0; j < QK_K / 64; ++j) {
+            for (int k = 0; k < 8; ++k) {
+                int32_t lo = 0, hi = 0;
+                for (int b = 4 * k; b < 4 * k + 4; ++b) {
+                    lo += (int32_t)(q4[b] & 0xF) * q8[b];
+                    hi += (int32_t)(q4[b] >> 4) * q8[32 + b];
+                }
+                sumi[k] += (int32_t)sc[2 * j] * lo + (int32_t)sc[2 * j + 1] * hi;
+            }
+            q4 += 32;
+            q8 += 64;
+        }
+        for (int k = 0; k < 8; ++k) acc[k] = fmaf(d, (float)sumi[k], acc[k]);
+    }
+    const float m0 = acc_m[0] + acc_m[2], m1 = acc_m[1] + acc_m[3];
+    *s = simd_hsum8(acc) + (m0 + m1);
+}
+
+static void simd_vec_dot_q8_0_q8_0(int n, float * s, const void * vx, const void * vy) {
+    const ref_block_q8_0 * x = (const ref_block_q8_0 *)vx;
+    const ref_block_q8_0 * y = (const ref_block_q8_0 *)vy;
+    const int nb = n / QK8_0;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ib = 0; ib < nb; ++ib) {
+        const float d = ref_fp16_to_fp32(x[ib].d) * ref_fp16_to_fp32(y[ib].d);
+        for (int k = 0; k < 8; ++k) {
+            int32_t l = 0;
+            for (int b = 4 * k; b < 4 * k + 4; ++b) l += (int32_t)x[ib].qs[b] * y[ib].qs[b];
+            acc[k] = fmaf(d, (float)l, acc[k]);
+        }
+    }
+    *s = simd_hsum8(acc);
+}
+
 void ref_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy) {
+    if (g_simd_mode) {
+        simd_vec_dot_q4_K_q8_K(n, s, vx, vy);
+        return;
+    }
     const ref_block_q4_K * x = (const ref_block_q4_K *)vx;
     const ref_block_q8_K * y = (const ref_block_q8_K *)vy;
     const int nb = n / QK_K;
@@ -373,6 +505,10 @@ void ref_vec_dot_q4_K_q8_K(int n, float * s, const void * vx, const void * vy) {
 }
 
 void ref_vec_dot_q8_0_q8_0(int n, float * s, const void * vx, const void * vy) {
+    if (g_simd_mode) {
+        simd_vec_dot_q8_0_q8_0(n, s, vx, vy);
+        return;
+    }
     const ref_block_q8_0 * x = (const ref_block_q8_0 *)vx;
     const ref_block_q8_0 * y = (const ref_block_q8_0 *)vy;
     const int nb = n / QK8_0;
@@ -386,12 +522,20 @@ void ref_vec_dot_q8_0_q8_0(int n, float * s, const void * vx, const void * vy) {
 }
 
 void ref_vec_dot_f16(int n, float * s, const ref_fp16_t * x, const ref_fp16_t * y) {
+    if (g_simd_mode) {
+        simd_vec_dot_f16(n, s, x, y);
+        return;
+    }
     ggml_float sumf = 0.0;
     for (int i = 0; i < n; ++i) sumf += (ggml_float)(ref_fp16_to_fp32(x[i]) * ref_fp16_to_fp32(y[i]));
     *s = (float)sumf;
 }
 
 void ref_vec_dot_f32(int n, float * s, const float * x, const float * y) {
+    if (g_simd_mode) {
+        simd_vec_dot_f32(n, s, x, y);
+        return;
+    }
     ggml_float sumf = 0.0;
     for (int i = 0; i < n; ++i) sumf += (ggml_float)(x[i] * y[i]);
     *s = (float)sumf;
@@ -781,6 +925,10 @@ static void op_mul_mat(tts_tensor * dst, int ith, int nth) {
                 case TTS_TYPE_Q8_0: ref_vec_dot_q8_0_q8_0((int)K, &s, wr, xq); break;
                 case TTS_TYPE_F16: ref_vec_dot_f16((int)K, &s, (const ref_fp16_t *)wr, (const ref_fp16_t *)xq); break;
                 default: {
+                    if (g_simd_mode) {
+                        ref_vec_dot_f32((int)K, &s, (const float *)wr, xr);
+                        break;
+                    }
                     /* src0 rows may be strided in ne0 only if nb[0]==4 (ggml requires it) */
                     ggml_float sum = 0.0;
                     const float * w = (const float *)wr;
@@ -833,6 +981,39 @@ static void op_conv_transpose_1d(tts_tensor * dst, int ith, int nth) {
     const int64_t OL = dst->ne[0], OC = dst->ne[1], ICg = IC / g;
     const int64_t dr = (OC + nth - 1) / nth;
     const int64_t c0 = dr * ith, c1 = MIN(c0 + dr, OC);
+    if (g_simd_mode) { /* upstream's loop: per (input position, tap) a vec_dot over the channels, f32 += */
+        const int w16 = a->type == TTS_TYPE_F16;
+        float * xs = (float *)malloc(ICg * sizeof(float));
+        float * ws = (float *)malloc(ICg * sizeof(float));
+        ref_fp16_t * xh = (ref_fp16_t *)malloc(ICg * sizeof(ref_fp16_t));
+        ref_fp16_t * wh = (ref_fp16_t *)malloc(ICg * sizeof(ref_fp16_t));
+        for (int64_t oc = c0; oc < c1; ++oc) {
+            const int64_t grp = oc / OCg, ocl = oc % OCg;
+            for (int64_t o = 0; o < OL; ++o) *PF(dst, o, oc, 0, 0) = 0.f;
+            for (int64_t i = 0; i < L; ++i) {
+                for (int64_t icl = 0; icl < ICg; ++icl) xs[icl] = load_elem(b, i, grp * ICg + icl, 0, 0);
+                if (w16) for (int64_t icl = 0; icl < ICg; ++icl) xh[icl] = ref_fp32_to_fp16(xs[icl]);
+                for (int64_t k = 0; k < K; ++k) {
+                    const int64_t o = i * s0 + k * d0 - p0;
+                    if (o < 0 || o >= OL) continue;
+                    float v = 0.f;
+                    if (w16) {
+                        for (int64_t icl = 0; icl < ICg; ++icl) wh[icl] = ref_fp32_to_fp16(load_elem(a, k, ocl, grp * ICg + icl, 0));
+                        ref_vec_dot_f16((int)ICg, &v, xh, wh);
+                    } else {
+                        for (int64_t icl = 0; icl < ICg; ++icl) ws[icl] = load_elem(a, k, ocl, grp * ICg + icl, 0);
+                        ref_vec_dot_f32((int)ICg, &v, xs, ws);
+                    }
+                    *PF(dst, o, oc, 0, 0) += v;
+                }
+            }
+        }
+        free(xs);
+        free(ws);
+        free(xh);
+        free(wh);
+        return;
+    }
     for (int64_t oc = c0; oc < c1; ++oc) {
         const int64_t grp = oc / OCg, ocl = oc % OCg;
         for (int64_t o = 0; o < OL; ++o) {

@@ -77,6 +77,10 @@ void ref_gemv(int type, const void * w, const float * x, float * y, int64_t K, i
 int oracle_graph_compute(tts_tensor * const * nodes, int n_nodes, int n_threads);
 /* Single node, single thread. */
 int oracle_compute_node(tts_tensor * node);
+/* 0 (default): ggml-cpu's generic scalar loops; 1: the x86 AVX2/FMA/F16C accumulation order of
+ * vec_dot_f16 / _f32 / q4_K_q8_K / q8_0_q8_0 and upstream's conv_transpose_1d loop (ggml_ref.c). */
+void oracle_set_simd_mode(int mode);
+int oracle_simd_mode(void);
 
 /* Backend vtable (host memory) for the C++ runners. */
 int oracle_backend_iface(tts_backend_iface * out, int n_threads);

@@ -39,6 +39,10 @@ def lib():
         "oracle_graph_compute": (ctypes.c_int, [ctypes.POINTER(ctypes.POINTER(ttship.TtsTensor)), ctypes.c_int, ctypes.c_int]),
         "oracle_compute_node": (ctypes.c_int, [ctypes.POINTER(ttship.TtsTensor)]),
         "oracle_backend_iface": (ctypes.c_int, [ctypes.POINTER(ttship.BackendIface), ctypes.c_int]),
+        "oracle_set_simd_mode": (None, [ctypes.c_int]),
+        "oracle_simd_mode": (ctypes.c_int, []),
+        "ref_vec_dot_f16": (None, [ctypes.c_int, vp, vp, vp]),
+        "ref_vec_dot_f32": (None, [ctypes.c_int, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -46,6 +50,21 @@ def lib():
         fn.argtypes = args
     _lib = L
     return L
+
+
+class simd_mode:
+    """with simd_mode(1): the oracle accumulates like an x86 AVX2/FMA/F16C ggml-cpu build (ggml_ref.c)."""
+
+    def __init__(self, mode=1):
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = lib().oracle_simd_mode()
+        lib().oracle_set_simd_mode(self.mode)
+        return self
+
+    def __exit__(self, *a):
+        lib().oracle_set_simd_mode(self.prev)
 
 
 def iface(n_threads=8):

@@ -16,12 +16,13 @@ import ttship  # noqa: E402
 
 
 def main():
-    frames = [int(a) for a in sys.argv[1:]] or [50, 861]
+    frames = [int(a) for a in sys.argv[1:] if not a.startswith("--")] or [50, 861]
+    modes = ((0, 1),) if "--default-only" in sys.argv else ((0, 1), (0, 0), (1, 1))
     be = ttship.HipBackend(0)
     cfg = ttship.dac_config(max_frames=max(frames))
     dac = ttship.Dac(be.iface(), cfg)
     rng = np.random.default_rng(0)
-    for f32acc, convt in ((0, 1), (0, 0), (1, 1)):
+    for f32acc, convt in modes:
         be.set_option(3, f32acc)
         be.set_option(4, convt)
         for T in frames:
