@@ -417,6 +417,8 @@ def main():
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
                     "replica on all CUs, 1 = replica r on the r-th contiguous CU set, 2 = on CUs c with c %% R == r")
+    ap.add_argument("--dac-conv-split", type=int, default=None, help="TTS_HIP_OPT_CONV_SPLIT on the DAC workers' backends "
+                    "(split convs over extra workgroups; default: the backend's default, on)")
     ap.add_argument("--dac-workers", type=int, default=8, help="concurrent DAC decoders per GPU (each its own backend / "
                     "stream; the AR replicas' backends first): short codec sequences fill few CUs, so several "
                     "prompts decode side by side")
@@ -461,6 +463,8 @@ def main():
     dcfg = ttship.dac_config(max_frames=args.steps)
 
     def new_dac(rb):
+        if args.dac_conv_split is not None:  # concurrent decoders each sizing split convs for the whole chip
+            rb.set_option(ttship.OPT["CONV_SPLIT"], args.dac_conv_split)
         rd = ttship.Dac(rb.iface(), dcfg)
         rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
         return rd

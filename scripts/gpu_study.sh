@@ -46,6 +46,12 @@ case "$1" in
     timeout -k 10 300 python3 scripts/bench_dac.py $F > "$O/dac_bench.jsonl" 2>&1 &&
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/profd" -o run --output-format csv -- python3 "$R/scripts/bench_dac.py" 200 > "$O/profd.log" 2>&1) &&
     cat "$O/dac_bench.jsonl" ;;
+  dac_short)   # the driver's short line (20 frames): DAC workers x conv split
+    for w in 8 4 2; do for sp in 1 0; do
+      timeout -k 10 200 python3 bench.py --steps 20 --no-cpu-baseline --kokoro-prompts 0 --orpheus-steps 0 --dia-steps 0 --b1-replicas 0 \
+          --dac-workers $w --dac-conv-split $sp > "$O/ds_${w}_$sp.log" 2>&1 &&
+      python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('workers $w split $sp', d['value'], d['ar_ms_per_step'], d['dac_audio_sec_per_s'])" "$O/ds_${w}_$sp.log" || exit 1
+    done; done ;;
   tests)       # selected GPU test files, e.g. scripts/gpu_study.sh tests tests/test_dia_gpu.py
     shift
     timeout -k 10 900 python -u -m pytest "$@" $T > "$O/tests.log" 2>&1; rc=$?; tail -3 "$O/tests.log"; exit $rc ;;
@@ -54,5 +60,5 @@ case "$1" in
   mfma_f64)    # the f64 MFMA ceiling
     hipcc --offload-arch=gfx950 -O3 scripts/mfma_f64_peak.hip -o build/mfma_f64_peak && timeout -k 10 120 build/mfma_f64_peak > "$O/mfma_f64.log" 2>&1 && cat "$O/mfma_f64.log" ;;
   *)
-    echo "usage: $0 {ar|replicas|cu_partition|kernarg|gemv_phase|attn|dac|tests|sync|mfma_f64} [args]"; exit 2 ;;
+    echo "usage: $0 {ar|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
 esac
