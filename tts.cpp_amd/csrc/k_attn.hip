@@ -926,7 +926,7 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
     hipLaunchKernelGGL(k_attn_decode, dim3((unsigned)H, (unsigned)n, (unsigned)B), dim3(ATTN_THREADS), 0, be->stream, a);
     TTS_HIP_CHECK(hipGetLastError());
     if (out2)
-        TTS_HIP_CHECK(hipMemcpyAsync(out2, out, sizeof(float) * (size_t)hd * H * n * B, hipMemcpyDeviceToDevice, be->stream));
+        launch_copy_bytes(be, out2, out, sizeof(float) * (size_t)hd * H * n * B);
 }
 
 }  // namespace tts

@@ -543,7 +543,7 @@ void launch_conv1d_fused(tts_hip_backend * be, Conv1dArgs a) {
     TTS_HIP_CHECK(hipGetLastError());
     if (a.part) launch_split_reduce(be, (int)grid.z, a.OL, a.OC, e.y, e.ycs, e.bias, e.bcs, e.res, e.rcs);
     if (a.copy_dst)  // the output aliased the input: the kernel wrote a staging buffer
-        TTS_HIP_CHECK(hipMemcpyAsync(a.copy_dst, a.y, (size_t)a.OL * (size_t)a.OC * 4, hipMemcpyDeviceToDevice, be->stream));
+        launch_copy_bytes(be, a.copy_dst, a.y, (size_t)a.OL * (size_t)a.OC * 4);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -154,6 +154,12 @@ __device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc
 
 __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
 
+// A kernel argument indexed by a matrix index the compiler cannot prove wave-uniform compiles to a
+// VECTOR load of the kernarg segment, and the s_waitcnt vmcnt(0) that guards its use also waits for
+// every weight and activation load already in flight (it serialised a GEMV's first weight loads
+// behind its prologue's activation loads).  Callers pass indices that are uniform by construction
+// through readfirstlane, and single-matrix jobs index 0.
+
 template <int MC>
 __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t row, int m, float v) {
     if (j.epi == EPI_GELU) {
@@ -162,13 +168,15 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
     } else if (j.epi == EPI_ADD) {
         v = __fadd_rn(v, j.res[m * j.rcs + row]);
     }
+    float * const Y = j.Y[mat];
+    const int64_t ycs = j.ycs[mat], yrs = j.yrs[mat];
     if (mat == j.rep_mat) {
         const int64_t g = row / j.yrg;
-        float * y = j.Y[mat] + m * j.ycs[mat] + g * j.yrgs + (row - g * j.yrg) * j.yrs[mat];
+        float * y = Y + m * ycs + g * j.yrgs + (row - g * j.yrg) * yrs;
         for (int k = 0; k < j.nrep; ++k) y[k * j.yrep] = v;
         return;
     }
-    j.Y[mat][m * j.ycs[mat] + row * j.yrs[mat]] = v;
+    Y[m * ycs + row * yrs] = v;
 }
 
 // quantize_row_q8_K_ref for four 256-element blocks per wave: the 16-lane row r = lane >> 4 owns
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
     u32x4 hdr[NBMAX], q[NBMAX];
     auto load_row = [&](int64_t gg, int b0) {
         const int64_t flat0 = gg * S;
-        const int mat = mat_of(flat0);
+        const int mat = __builtin_amdgcn_readfirstlane(mat_of(flat0));  // gg is the wave's: uniform
         int64_t row = flat0 - (int64_t)mat * j.N + s;
         row = row < j.N ? row : j.N - 1;
         const uint8_t * wr = j.W[mat] + row * j.w_row_bytes;
@@ -547,7 +555,7 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
         }
         const float tot = q4k_octet_total(sumf, sums);
         const int64_t flat0 = g * S;
-        const int mat = mat_of(flat0);
+        const int mat = __builtin_amdgcn_readfirstlane(mat_of(flat0));
         const int64_t row = flat0 - (int64_t)mat * j.N + s;
         TTS_TS(j, 4);
         if (l == 0 && m < j.M && row < j.N && mat < j.nmat) gemv_store<MC>(j, mat, row, m, tot);
@@ -638,18 +646,12 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) 
     const int64_t NR = (int64_t)j.nmat * j.N;
     const int64_t row0 = (int64_t)blockIdx.x * R;
     const bool own = cg < NCG && m0 < M && row0 + r < NR;  // this octet has (row, block, columns) work
-    auto mat_of = [&](int64_t flat) {
-        int mt = 0;
-        while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
-        return mt;
-    };
     u32x4 hdr, qw;
     TTS_TS(j, 0);
     auto mid = [&]() {
         int64_t flat = row0 + r;
         flat = flat < NR ? flat : NR - 1;  // clamped: every lane loads, unused results are dropped
-        const int mat = mat_of(flat);
-        const uint8_t * bp = j.W[mat] + (flat - (int64_t)mat * j.N) * j.w_row_bytes + (int64_t)b * 144;
+        const uint8_t * bp = j.W[0] + flat * j.w_row_bytes + (int64_t)b * 144;  // single-matrix jobs (launcher)
         if (cg < NCG) {
             hdr = TTS_WLOAD((const u32x4 *)bp);
             qw = TTS_WLOAD((const u32x4 *)(bp + 16 + l * 16));
@@ -724,9 +726,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) 
         }
         const float tot = q4k_octet_total(sumf, sums);
         if (ok && l == 0) {
-            const int64_t flat = row0 + rr;
-            const int mat = mat_of(flat);
-            gemv_store<8>(j, mat, flat - (int64_t)mat * j.N, m, tot);
+            gemv_store<8>(j, 0, row0 + rr, m, tot);
         }
     }
     TTS_TS(j, 5);
@@ -820,7 +820,9 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         const int c = (int)(i % nch);
         int64_t flat = t * 16 + r;
         flat = flat < NR ? flat : NR - 1;
-        const int mat = xpair ? xmat : swiglu ? (int)(ti & 1) : mat_of(flat);
+        // a 16-row tile never straddles two matrices (row counts are multiples of 16): the tile's
+        // matrix is wave-uniform, and readfirstlane keeps W[mat] / roff[mat] scalar loads
+        const int mat = __builtin_amdgcn_readfirstlane(xpair ? xmat : swiglu ? (int)(ti & 1) : mat_of(flat));
         const int64_t row = swiglu ? flat : flat - job_roff(j, mat);
         const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
         const int ri = (int)(row & 3);
@@ -936,7 +938,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
                     if ((ti & 1) == 0) gate[q] = tot;  // gate row; the up row follows in this wave
                     else if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gate[q]), tot);
                 } else if (r < M && flat < NR) {
-                    const int mat = mat_of(flat);
+                    const int mat = __builtin_amdgcn_readfirstlane(mat_of(t * 16));  // the tile's matrix
                     gemv_store<8>(j, mat, flat - job_roff(j, mat), r, tot);
                 }
             }
@@ -983,7 +985,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
                 for (int l = 0; l < LPW; ++l) tot = __fadd_rn(tot, sums[l][q >> 1][q & 1]);
                 const int64_t flat = t0 * 16 + 4 * kg + q;
                 if (r < M && flat < NR) {
-                    const int mat = mat_of(flat);
+                    const int mat = __builtin_amdgcn_readfirstlane(mat_of(t0 * 16));  // the tile's matrix
                     gemv_store<8>(j, mat, flat - job_roff(j, mat), r, tot);
                 }
             }
@@ -1558,6 +1560,19 @@ static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
     constexpr int S = 8 / MC;
     // unique loads pay off once a row holds >= 8 blocks (Parler fc2: 14.0 -> 11.1 us in the decode
     // graph at M = 8); at K = 1024 the octet-per-column kernel is faster (6.1 vs 7.7 us)
+    if (be->gemv_unique && j.K >= 8 * QK_K && j.nmat > 1) {  // the unique-load kernel takes one matrix per launch
+        for (int i = 0; i < j.nmat; ++i) {
+            GemvJob one = j;
+            one.nmat = 1;
+            one.hetero = 0;
+            one.W[0] = j.W[i], one.Y[0] = j.Y[i], one.ycs[0] = j.ycs[i], one.yrs[0] = j.yrs[i];
+            one.rep_mat = i == j.rep_mat ? 0 : -1;
+            one.N = j.hetero ? j.roff[i + 1] - j.roff[i] : j.N;
+            one.roff[0] = 0, one.roff[1] = one.N;
+            launch_gemv_q4k_mc<MC>(be, one);
+        }
+        return;
+    }
     if (be->gemv_unique && j.K >= 8 * QK_K) {
         int R, NCG;
         int64_t gx;

@@ -22,6 +22,26 @@ __global__ void k_cpy(TD dst, TD src, int64_t n) {
     }
 }
 
+// Contiguous device-to-device byte copy.  Every copy inside a step's launch sequence goes through
+// this kernel rather than hipMemcpyAsync, so a recorded step is a graph of kernel nodes only
+// (memcpy nodes were the one node kind the profiler's graph replay could not walk).
+__global__ void k_copy_bytes(char * __restrict__ dst, const char * __restrict__ src, int64_t n) {
+    const int64_t n16 = (((uintptr_t)dst | (uintptr_t)src) & 15) == 0 ? n >> 4 : 0;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t k = t; k < n16; k += stride) ((uint4 *)dst)[k] = ((const uint4 *)src)[k];
+    for (int64_t k = (n16 << 4) + t; k < n; k += stride) dst[k] = src[k];
+}
+
+void launch_copy_bytes(tts_hip_backend * be, void * dst, const void * src, size_t bytes) {
+    if (bytes == 0 || dst == src) return;
+    const int64_t units = (int64_t)(bytes >> 4) + 1;
+    int64_t g = (units + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_copy_bytes, dim3((unsigned)g), dim3(256), 0, be->stream, (char *)dst, (const char *)src, (int64_t)bytes);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 // One source copied into up to 4 destination views of the same shape (the planner's MCPY item:
 // Orpheus' repeat-interleaved KV store); each element is read once.
 struct CpyMulti {
@@ -557,7 +577,7 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
             const int64_t n = nel(s0);
             if (n == 0) return 0;
             if (is_cont(s0) && is_cont(node) && s0->type == node->type) {
-                TTS_HIP_CHECK(hipMemcpyAsync(node->data, s0->data, n * tts_type_size(s0->type), hipMemcpyDeviceToDevice, st));
+                launch_copy_bytes(be, node->data, s0->data, n * tts_type_size(s0->type));
                 return 0;
             }
             hipLaunchKernelGGL(k_cpy, dim3(grid_for(n)), dim3(256), 0, st, d, make_td(s0), n);
