@@ -287,6 +287,9 @@ enum tts_hip_option {
                                      2 or 4 waves (chains joined in ggml's order: bit-identical); 0 = one wave per tile */
     TTS_HIP_OPT_ATTN_PV16 = 15,   /* 1: the split P.V kernel requests a lane's whole V slice (16 x 16 B) before the
                                      softmax when P <= 1024; 0 (default): two 8-chunk batches (measured equal) */
+    TTS_HIP_OPT_GEMV_PREQUANT = 21, /* 1 (default): a matrix-core Q4_K GEMV's activation is normed / quantized once, by a
+                                     pass writing its MFMA operands to backend scratch, which every workgroup copies into
+                                     LDS by LDS-DMA; 0 = every workgroup quantizes the whole activation itself */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

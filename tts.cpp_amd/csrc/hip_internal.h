@@ -61,10 +61,17 @@ __device__ __forceinline__ float dev_silu(float x) { return cr_divf(x, __fadd_rn
 // Cache policy of the two big decode streams (build-time, for the MALL-residency study):
 // TTS_WLOAD = quantized weight rows (default non-temporal), TTS_KVLOAD = K/V cache rows of decode
 // attention (default plain).
+// Loads through an explicitly global (address space 1) pointer: a pointer the compiler cannot trace
+// to a kernel argument would otherwise be a FLAT load, and flat loads complete out of order, so every
+// later wait on any vector load becomes vmcnt(0) -- a wait for the weight stream in the prologue.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T * gptr(const T * p) {
+    return (const __attribute__((address_space(1))) T *)p;
+}
 #ifdef TTS_W_PLAIN
-#define TTS_WLOAD(p) (*(p))
+#define TTS_WLOAD(p) (*gptr(p))
 #else
-#define TTS_WLOAD(p) __builtin_nontemporal_load(p)
+#define TTS_WLOAD(p) __builtin_nontemporal_load(gptr(p))
 #endif
 __device__ __forceinline__ float4 kv_ld4(const float4 * p) {
 #ifdef TTS_KV_NT
@@ -217,6 +224,11 @@ struct GemvJob {
     int rms = 0;
     float * lnout = nullptr;
     int64_t locs = 0;
+    // PRO_COPY (matrix-core kernels): the Q8_K activation already in the kernel's LDS operand layout
+    // ([M*nb + 1][256] f16, [M*nb + 1][16] f16 bsum halves, [M*nb + 1] f32 d; bq_bytes, a multiple of
+    // 1 KiB), written by k_quant_mf
+    const char * bq = nullptr;
+    int64_t bq_bytes = 0;
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
 };
 __host__ __device__ inline int64_t job_roff(const GemvJob & j, int m) { return j.hetero ? j.roff[m] : (int64_t)m * j.N; }
@@ -236,7 +248,7 @@ __host__ __device__ inline int64_t job_rows(const GemvJob & j) { return job_roff
     do {               \
     } while (0)
 #endif
-enum { PRO_QUANT = 1, PRO_LN = 2 };
+enum { PRO_QUANT = 1, PRO_LN = 2, PRO_COPY = 3 };  // PRO_COPY: operands pre-quantized at GemvJob::bq
 // Cross-attention over a short context folded into the Q4_K GEMV that produces its query
 // (k_gemv_q4K_xattn): K view [hd, P, H, B], V view [P, hd, H, B] (f32), out [hd, H, 1, B].
 struct XAttnArgs {
@@ -287,6 +299,7 @@ struct tts_hip_backend {
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;
+    int gemv_mf_prequant = 1;  // TTS_HIP_OPT_GEMV_PREQUANT
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)

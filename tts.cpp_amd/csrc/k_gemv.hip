@@ -259,7 +259,7 @@ __device__ __forceinline__ void q8k_row_block_mf(const float (&v)[16], int lane,
 // L2 round trip (measured: 0.4 us per block).  The launcher guarantees 16-B aligned x / lnw / lnb
 // and, for PRO_QUANT, contiguous columns (xcs == K).
 __device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
-    const float4 t = *(const float4 *)p;
+    const f32x4 t = *gptr((const f32x4 *)p);
     v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
 }
 
@@ -274,17 +274,35 @@ __device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
 struct NoMid {
     __device__ void operator()() const {}
 };
+// Per-call overrides of the prologue (defaults: the whole workgroup, j.x's M columns, LDS slots from 0)
+struct ProOv {
+    int nwaves = 0;               // waves taking part (0 = the whole workgroup)
+    const float * xcol = nullptr; // quantize this single column instead of j.x's M columns ...
+    float * lncol = nullptr;      // ... and write its LN output here (or nowhere)
+    int slot0 = 0;                // first output slot
+    int trash = -1;               // slot absorbing padding writes (-1: M * nb)
+};
 template <int PRO, int NCH, bool MF = false, typename Mid = NoMid>
 __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s,
-                                             _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr, Mid mid = Mid{}) {
+                                             _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr, Mid mid = Mid{},
+                                             ProOv ov = ProOv{}) {
+    // ov.xcol: quantize one column instead of j.x's M columns.  Overriding fields here instead of
+    // copying the job keeps every pointer a kernel argument, so the compiler keeps them in the global
+    // address space (a copied job's pointers turned into flat loads, which complete out of order and
+    // make every later wait a vmcnt(0))
+    const int nwaves = ov.nwaves;
+    const float * const xcol = ov.xcol;
+    float * const lncol = ov.lncol;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nwaves ? nwaves : blockDim.x >> 6;
+    const int r = lane >> 4, t = lane & 15;
+    const int M = xcol ? 1 : (int)j.M;
+    const float * const X = xcol ? xcol : j.x;
+    const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
     auto put = [&](const float (&v)[16], int lane, int slot) {
+        slot = slot == trash ? (ov.trash >= 0 ? ov.trash : slot) : ov.slot0 + slot;
         if constexpr (MF) q8k_row_block_mf(v, lane, mf_b16 + (int64_t)slot * QK_K, mf_sb + slot * 16, xd_s + slot);
         else q8k_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
     };
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int r = lane >> 4, t = lane & 15;
-    const int M = (int)j.M;
-    const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
     if (PRO == PRO_QUANT) {
         // pass p quantizes blocks 4p..4p+3 (block qb = column m, chunk b at x + qb*256)
         constexpr int QP = NCH <= 4 ? 2 : 4;  // passes whose loads a wave keeps in flight
@@ -294,7 +312,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 #pragma unroll
             for (int u = 0; u < QP; ++u) {
                 const int qb = min(4 * min(p0 + u * nw, npass - 1) + r, nq - 1);
-                const float * src = j.x + (int64_t)qb * QK_K + 16 * t;
+                const float * src = X + (int64_t)qb * QK_K + 16 * t;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) ld4(src + 4 * k, *(float (*)[4]) & v[u][4 * k]);
             }
@@ -318,7 +336,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         constexpr int NP = (NCH + 3) / 4;
         constexpr bool PRE = NCH <= 4;
         const double Kd = (double)j.K;
-        const bool write = j.lnout && blockIdx.x == 0;
+        float * const lno = xcol ? lncol : j.lnout;
+        const bool write = lno && (xcol || blockIdx.x == 0);
         const float * lnb = j.lnb ? j.lnb : j.lnw;
         float wp[PRE ? NP : 1][16], bp[PRE ? NP : 1][16];
         if (PRE) {
@@ -332,8 +351,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
                 }
             }
         }
-        auto column = [&](int m, bool first) {
-            const float * xr = j.x + m * j.xcs;
+        auto column = [&](int m, bool first, bool live = true) {
+            const float * xr = X + m * j.xcs;
             float v[NP][16];
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
@@ -390,9 +409,9 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
                     if (j.lnb) y = __fadd_rn(y, b16[e]);
                     v[p][e] = y;
                 }
-                const bool valid = 4 * p + r < nb;
+                const bool valid = live && 4 * p + r < nb;
                 if (write && valid) {
-                    float * o = j.lnout + m * j.locs + off;
+                    float * o = lno + m * j.locs + off;
 #pragma unroll
                     for (int k = 0; k < 4; ++k) *(float4 *)(o + 4 * k) = make_float4(v[p][4 * k], v[p][4 * k + 1], v[p][4 * k + 2], v[p][4 * k + 3]);
                 }
@@ -529,7 +548,10 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
     // need more registers than it leaves, so they start after it)
     TTS_TS(j, 0);
     auto mid = [&]() {
-        if ((NBMAX <= 4 || (TTS_GEMV_EARLY16 && PRO == PRO_QUANT)) && g < G) load_row(g, 0);
+        // unconditional (an idle wave loads the last row group): a load under a branch leaves the
+        // paths after it with different numbers of loads in flight, and the compiler then guards the
+        // prologue's first use of the activation with vmcnt(0) -- a wait for these weight loads too
+        if (NBMAX <= 4 || (TTS_GEMV_EARLY16 && PRO == PRO_QUANT)) load_row(g < G ? g : G - 1, 0);
         TTS_TS(j, 1);
     };
     q4k_prologue<PRO, NBMAX>(j, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid);
@@ -652,10 +674,9 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) 
         int64_t flat = row0 + r;
         flat = flat < NR ? flat : NR - 1;  // clamped: every lane loads, unused results are dropped
         const uint8_t * bp = j.W[0] + flat * j.w_row_bytes + (int64_t)b * 144;  // single-matrix jobs (launcher)
-        if (cg < NCG) {
-            hdr = TTS_WLOAD((const u32x4 *)bp);
-            qw = TTS_WLOAD((const u32x4 *)(bp + 16 + l * 16));
-        }
+        // unconditional (spare octets load a valid block and drop it): see k_gemv_q4_K's first loads
+        hdr = TTS_WLOAD((const u32x4 *)bp);
+        qw = TTS_WLOAD((const u32x4 *)(bp + 16 + l * 16));
         TTS_PIN_LOADS();
         TTS_TS(j, 1);
     };
@@ -951,8 +972,24 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
         if (nmine > 0) load(I0{}, 0);
         TTS_TS(j, 1);
     };
-    if (!(j.dbg & 2)) q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
-    else mid();
+    if constexpr (PRO == PRO_COPY) {
+        // the operands k_quant_mf wrote, in this kernel's LDS layout: 1 KiB per wave instruction by
+        // LDS-DMA (no registers), the weight loads behind them
+        const int nck = (int)(j.bq_bytes >> 10);
+        for (int i = wave; i < nck; i += nw)
+            __builtin_amdgcn_global_load_lds(gptr(j.bq + (size_t)i * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
+        TTS_PIN_LOADS();
+        load(I0{}, 0);  // unconditional (clamped): the wait below counts exactly these loads
+        TTS_PIN_LOADS();
+        // this wave's DMA has landed once at most the weight loads issued after it are outstanding
+        constexpr int NWL = (RS == 1 ? 3 : 2) * CH;
+        __builtin_amdgcn_s_waitcnt((NWL & 15) | (7 << 4) | (15 << 8) | (((NWL >> 4) & 3) << 14));
+    } else if (!(j.dbg & 2)) {
+        q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
+    } else {
+        mid();
+    }
     TTS_TS(j, 2);
     __syncthreads();
     TTS_TS(j, 3);
@@ -1127,7 +1164,16 @@ __global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
         if (t < T) load(t);
         TTS_TS(j, 1);
     };
-    q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
+    if constexpr (PRO == PRO_COPY) {  // operands from k_quant_mf (see k_gemv_q4K_mf)
+        const int nck = (int)(j.bq_bytes >> 10);
+        for (int i = wave; i < nck; i += nw)
+            __builtin_amdgcn_global_load_lds(gptr(j.bq + (size_t)i * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
+        TTS_PIN_LOADS();
+        load(t < T ? t : T - 1);
+    } else {
+        q4k_prologue<PRO, NCH, true>(j, nb, nullptr, xd_s, nullptr, b16, sbs, mid);
+    }
     TTS_TS(j, 2);
     __syncthreads();
     TTS_TS(j, 3);
@@ -1174,24 +1220,20 @@ __global__ __launch_bounds__(64 * NWMAX) void k_gemv_q4K_ks(GemvJob j) {
 // the launch and the attention kernel's whole latency chain disappear.  The attention's K, V and
 // mask are requested at kernel entry, next to the weight rows.
 template <int PRO>
-__global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) {
+__global__ __launch_bounds__(576) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) {
+    // waves 0..7: the query GEMV (8 rows each); wave 8: the attention, whose K / V loads are issued at
+    // entry and never share a code path with the prologue's activation loads (a join of paths with
+    // unequal loads in flight makes the compiler wait for all of them before the activation's use)
     constexpr int HD = 64, NW = 8, F = HD / 4, VB = 8;
     __shared__ __attribute__((aligned(16))) int8_t xq_s[5 * QK_K];  // nb <= 4 blocks + trash slot
     __shared__ float xd_s[8];
     __shared__ __attribute__((aligned(16))) int16_t xs_s[5 * 8];
     __shared__ float s_q[HD];
     const int h = blockIdx.x, b = blockIdx.y;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int l = lane & 7, s = lane >> 3;
     const int nb = (int)(j.K / QK_K);
-    GemvJob jb = j;  // this workgroup's column
-    jb.M = 1;
-    jb.x = j.x + (int64_t)b * j.xcs;
-    jb.lnout = j.lnout && h == 0 ? j.lnout + (int64_t)b * j.locs : nullptr;
-    const int64_t row = (int64_t)h * HD + wave * 8 + s;
-    const uint8_t * wr = j.W[0] + row * j.w_row_bytes;
-    u32x4 hdr[4], q[4];
-    // attention operands for the last wave (position p = lane)
+    // attention operands for the attention wave (position p = lane)
     const int P = a.P;
     const int p = min(lane, P - 1);
     float4 kr[F];
@@ -1200,31 +1242,42 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
     const int bk = b / (a.B / (int)a.k.ne[3]), bv = b / (a.B / (int)a.v.ne[3]);  // K/V shared across prompts or not
     const char * kbase = a.k.data + (int64_t)h * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
     const char * vbase = a.v.data + (int64_t)h * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
-    // weight rows and attention operands are requested behind the prologue's activation loads
-    auto mid = [&]() {
+    u32x4 hdr[4], q[4];
+    if (wave < NW) {
+        const int64_t row = (int64_t)h * HD + wave * 8 + s;
+        const uint8_t * wr = j.W[0] + row * j.w_row_bytes;
+        // weight rows are requested behind the prologue's activation loads
+        auto mid = [&]() {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t bo = (int64_t)min(u, nb - 1) * 144;
-            hdr[u] = TTS_WLOAD((const u32x4 *)(wr + bo));
-            q[u] = TTS_WLOAD((const u32x4 *)(wr + bo + 16 + l * 16));
-        }
-        if (wave == NW - 1) {
+            for (int u = 0; u < 4; ++u) {
+                const int64_t bo = (int64_t)min(u, nb - 1) * 144;
+                hdr[u] = TTS_WLOAD((const u32x4 *)(wr + bo));
+                q[u] = TTS_WLOAD((const u32x4 *)(wr + bo + 16 + l * 16));
+            }
+        };
+        // this workgroup's column b (head 0's workgroup writes its LN output)
+        ProOv ov;
+        ov.nwaves = NW;
+        ov.xcol = j.x + (int64_t)b * j.xcs;
+        ov.lncol = j.lnout && h == 0 ? j.lnout + (int64_t)b * j.locs : nullptr;
+        q4k_prologue<PRO, 4>(j, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid, ov);
+    } else {
 #pragma unroll
-            for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
+        for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
 #pragma unroll
-            for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
-            if (a.mask) mk = a.mask[p];
-        }
-    };
-    q4k_prologue<PRO, 4>(jb, nb, xq_s, xd_s, xs_s, nullptr, nullptr, mid);
+        for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
+        mk = *(a.mask ? a.mask + p : (const float *)kbase);  // unconditional: no branch join before the barrier
+    }
     __syncthreads();
-    float sums = 0.f, sumf = 0.f;
+    if (wave < NW) {
+        float sums = 0.f, sumf = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) q4k_block(hdr[u], q[u], xq_s, xs_s, xd_s, min(u, nb - 1), l, u < nb, sums, sumf);
-    const float tot = q4k_octet_total(sumf, sums);
-    if (l == 0) s_q[wave * 8 + s] = tot;
+        for (int u = 0; u < 4; ++u) q4k_block(hdr[u], q[u], xq_s, xs_s, xd_s, min(u, nb - 1), l, u < nb, sums, sumf);
+        const float tot = q4k_octet_total(sumf, sums);
+        if (l == 0) s_q[wave * 8 + s] = tot;
+    }
     __syncthreads();
-    if (wave != NW - 1) return;
+    if (wave != NW) return;
     // ---- k_attn_small<64> on (h, b) with q from LDS ----
     double acc = 0.0;
 #pragma unroll
@@ -1271,8 +1324,8 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
 // columns with 16-B aligned, 16-B strided x; K rows 16-B vectors; P <= 64.
 void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnArgs & a) {
     const dim3 grid((unsigned)a.H, (unsigned)a.B);
-    if (j.pro == PRO_LN) hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_LN>, grid, dim3(512), 0, be->stream, j, a);
-    else hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_QUANT>, grid, dim3(512), 0, be->stream, j, a);
+    if (j.pro == PRO_LN) hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_LN>, grid, dim3(576), 0, be->stream, j, a);
+    else hipLaunchKernelGGL(k_gemv_q4K_xattn<PRO_QUANT>, grid, dim3(576), 0, be->stream, j, a);
     TTS_HIP_CHECK(hipGetLastError());
 }
 
@@ -1635,6 +1688,93 @@ static int64_t q4k_mf_max_cols(int64_t K) {
     const int64_t c = ((int64_t)(160 * 1024 - 16384 - 16) / (2 * QK_K + 32 + 4) - 1) / (K / QK_K);
     return c >= 16 ? 16 : c >= 8 ? 8 : c;
 }
+// The matrix-core GEMV's prologue as a pass of its own (TTS_HIP_OPT_GEMV_PREQUANT): one workgroup per
+// column norms (PRO_LN) and quantizes it, writing the operands in the GEMV's LDS layout to j.bq; the
+// GEMV's workgroups then copy them instead of each loading and quantizing the whole activation
+// (Orpheus down: 256 KB of f32 and 64 k quantizations per workgroup).  Same arithmetic, same layout:
+// bit-identical.
+// Grid (ceil(nb / 4), M) single-wave workgroups: the 16-lane row r of wave (c, m) quantizes block
+// 4c + r of column m (q8k_row_block_mf).  PRO_LN: every wave first reduces the whole column (f64 sums,
+// then mean, variance and scale exactly as the in-kernel prologue: ggml's NORM / RMS_NORM), then
+// applies the affine to its blocks and writes them to the LN output as well (K <= 4096).
+template <int PRO>
+__global__ __launch_bounds__(64) void k_quant_mf(GemvJob j) {
+    const int m = blockIdx.y, lane = threadIdx.x, r = lane >> 4, t = lane & 15;
+    const int nb = (int)(j.K / QK_K);
+    const int nslot = (int)j.M * nb + 1;
+    _Float16 * b16 = (_Float16 *)j.bq;
+    _Float16 * sb = b16 + (size_t)nslot * QK_K;
+    float * xd = (float *)(sb + (size_t)nslot * 16);
+    const float * x = j.x + (int64_t)m * j.xcs;
+    const int b = blockIdx.x * 4 + r;
+    const int bc = b < nb ? b : nb - 1;
+    const int off = bc * QK_K + 16 * t;
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ld4(x + off + 4 * k, *(float (*)[4]) & v[4 * k]);
+    if (PRO == PRO_LN) {
+        // the whole column, 16 floats per lane per pass (passes of 1024 elements)
+        const int K = (int)j.K;
+        const double Kd = (double)K;
+        float w[16], bb[16];
+        const float * lnb = j.lnb ? j.lnb : j.lnw;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ld4(j.lnw + off + 4 * k, *(float (*)[4]) & w[4 * k]);
+            ld4(lnb + off + 4 * k, *(float (*)[4]) & bb[4 * k]);
+        }
+        constexpr int PMAX = 4;  // K <= 4096 (the planner's LN fusion)
+        float c[PMAX][16];
+#pragma unroll
+        for (int p = 0; p < PMAX; ++p) {  // unconditional (clamped) loads
+            const int e0 = p * 1024 + 16 * lane;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ld4(x + min(e0 + 4 * k, K - 4), *(float (*)[4]) & c[p][4 * k]);
+        }
+        float mean = 0.f;
+        if (!j.rms) {
+            double s = 0.0;
+#pragma unroll
+            for (int p = 0; p < PMAX; ++p) {
+                if (p * 1024 >= K) break;
+                double sp = 0.0;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sp += (double)c[p][e];
+                s += p * 1024 + 16 * lane < K ? sp : 0.0;
+            }
+            mean = (float)(wave_sum_f64(s) / Kd);
+        }
+        double s2 = 0.0;
+#pragma unroll
+        for (int p = 0; p < PMAX; ++p) {
+            if (p * 1024 >= K) break;
+            double sp = 0.0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const float d = j.rms ? c[p][e] : __fsub_rn(c[p][e], mean);
+                sp += (double)__fmul_rn(d, d);
+            }
+            s2 += p * 1024 + 16 * lane < K ? sp : 0.0;
+        }
+        const float var = (float)(wave_sum_f64(s2) / Kd);
+        const float scale = cr_divf(1.0f, cr_sqrtf(__fadd_rn(var, j.eps)));
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            float y = j.rms ? __fmul_rn(v[e], scale) : __fmul_rn(__fsub_rn(v[e], mean), scale);
+            y = __fmul_rn(y, w[e]);
+            if (j.lnb) y = __fadd_rn(y, bb[e]);
+            v[e] = y;
+        }
+        if (j.lnout && b < nb) {
+            float * o = j.lnout + (int64_t)m * j.locs + off;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *(float4 *)(o + 4 * k) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+        }
+    }
+    const int slot = b < nb ? m * nb + b : nslot - 1;
+    q8k_row_block_mf(v, lane, b16 + (size_t)slot * QK_K, sb + (size_t)slot * 16, xd + slot);
+}
+
 static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
     (void)be;
     // at least one column's Q8_K operands must fit LDS (K <= ~76k); wider rows would make
@@ -1681,6 +1821,21 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
             fprintf(stderr, "tts_hip: LN-fused Q4_K GEMV with K = %lld > 4096\n", (long long)j.K);
             abort();
         }
+        const int64_t nb = j.K / QK_K;
+        const int64_t bq = (((j.M * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+        if (be->gemv_mf_prequant && !j.dbg && (size_t)(bq + 4 * j.K * j.M) <= be->scratch_size) {
+            // operands to the top of scratch (its bottom may hold this GEMV's staged input columns)
+            j.bq = be->scratch + be->scratch_size - bq;
+            j.bq_bytes = bq;
+            const dim3 qg((unsigned)((nb + 3) / 4), (unsigned)j.M);
+            if (j.pro == PRO_LN) hipLaunchKernelGGL(k_quant_mf<PRO_LN>, qg, dim3(64), 0, be->stream, j);
+            else hipLaunchKernelGGL(k_quant_mf<PRO_QUANT>, qg, dim3(64), 0, be->stream, j);
+            TTS_HIP_CHECK(hipGetLastError());
+            j.pro = PRO_COPY;
+            j.lnout = nullptr;  // written by the pass
+            launch_q4k_mf_pro<PRO_COPY, 16>(be, j);
+            continue;
+        }
         if (j.pro == PRO_LN) launch_q4k_mf_pro<PRO_LN, 16>(be, j);
         else launch_q4k_mf_pro<PRO_QUANT, 16>(be, j);
     }
@@ -1718,10 +1873,30 @@ static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
     // units (block, residue half) per wave: one for nb <= 4 (<= 8 waves); above, two (<= 16 waves)
     // after a quantize-only prologue, four (<= 8 waves) after an LN prologue, whose K / 256 chunks
     // per lane need the registers of a 512-thread workgroup
-    const int upw = nb <= 4 ? 1 : j.pro == PRO_LN ? 4 : 2;
-    const int nw = (int)((2 * nb + upw - 1) / upw);
     const unsigned gx = (unsigned)(T < 2048 ? T : 2048);
     const size_t lds = q4k_ks_lds(j.M, nb);
+    const int64_t bq = (((j.M * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+    if (be->gemv_mf_prequant && !j.dbg && (size_t)(bq + 4 * j.K * j.M) <= be->scratch_size &&
+        (size_t)bq <= lds) {
+        // the prologue as a pass of its own (k_quant_mf), the GEMV copying its operands (k_gemv_q4K_mf);
+        // the DMA's rounding up to 1 KiB lands in the term area, written only after the barrier
+        GemvJob jc = j;
+        jc.bq = be->scratch + be->scratch_size - bq;
+        jc.bq_bytes = bq;
+        const dim3 qg((unsigned)((nb + 3) / 4), (unsigned)j.M);
+        if (j.pro == PRO_LN) hipLaunchKernelGGL(k_quant_mf<PRO_LN>, qg, dim3(64), 0, be->stream, jc);
+        else hipLaunchKernelGGL(k_quant_mf<PRO_QUANT>, qg, dim3(64), 0, be->stream, jc);
+        TTS_HIP_CHECK(hipGetLastError());
+        jc.pro = PRO_COPY;
+        jc.lnout = nullptr;
+        const int upw = nb <= 4 ? 1 : 2;
+        const int nw = (int)((2 * nb + upw - 1) / upw);
+        if (nb <= 4) launch_q4k_ks_t<PRO_COPY, 4, 1, 8>(be, jc, gx, nw, lds);
+        else launch_q4k_ks_t<PRO_COPY, 16, 2, 16>(be, jc, gx, nw, lds);
+        return;
+    }
+    const int upw = nb <= 4 ? 1 : j.pro == PRO_LN ? 4 : 2;
+    const int nw = (int)((2 * nb + upw - 1) / upw);
     if (nb <= 4) {
         if (j.pro == PRO_LN) launch_q4k_ks_t<PRO_LN, 4, 1, 8>(be, j, gx, nw, lds);
         else launch_q4k_ks_t<PRO_QUANT, 4, 1, 8>(be, j, gx, nw, lds);
