@@ -56,6 +56,10 @@ case "$1" in
     shift
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/proft" -o run --output-format csv -- python3 "$R/bench.py" $AR --steps 60 "$@" > "$O/ar_trace.log" 2>&1) &&
     f=$(find "$O/proft" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 5 30 > "$O/ar_breakdown.txt" && cat "$O/ar_breakdown.txt" | cut -c1-150 ;;
+  orph_trace)  # kernel trace of the Orpheus leg + per-step breakdown (markers: the wide-vocabulary greedy step)
+    shift
+    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/profo" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --dia-steps 0 --no-cpu-baseline --b1-replicas 0 --orpheus-steps 40 "$@" > "$O/orph_trace.log" 2>&1) &&
+    f=$(find "$O/profo" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 10 25 - k_greedy_step_wide > "$O/orph_breakdown.txt" && cut -c1-150 "$O/orph_breakdown.txt" ;;
   tests)       # selected GPU test files, e.g. scripts/gpu_study.sh tests tests/test_dia_gpu.py
     shift
     timeout -k 10 900 python -u -m pytest "$@" $T > "$O/tests.log" 2>&1; rc=$?; tail -3 "$O/tests.log"; exit $rc ;;
@@ -64,5 +68,5 @@ case "$1" in
   mfma_f64)    # the f64 MFMA ceiling
     hipcc --offload-arch=gfx950 -O3 scripts/mfma_f64_peak.hip -o build/mfma_f64_peak && timeout -k 10 120 build/mfma_f64_peak > "$O/mfma_f64.log" 2>&1 && cat "$O/mfma_f64.log" ;;
   *)
-    echo "usage: $0 {ar|ar_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
+    echo "usage: $0 {ar|ar_trace|orph_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
 esac

@@ -1,5 +1,5 @@
 """Per-decode-step kernel breakdown from a rocprofv3 kernel trace of bench.py.
-Usage: step_breakdown.py trace.csv [first_step] [n_steps] [marker_grid]
+Usage: step_breakdown.py trace.csv [first_step] [n_steps] [marker_grid|-] [marker_name]
 
 Steps are delimited by the device greedy-sampling launches (k_greedy_step*).  The bench runs the
 Parler leg first, then Orpheus / Dia; `marker_grid` (Grid_Size_X of the Parler leg's sampling
@@ -15,8 +15,9 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
     first = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 30
-    grid = sys.argv[4] if len(sys.argv) > 4 else None
-    g = [i for i, r in enumerate(rows) if "k_greedy_step" in r["Kernel_Name"] and (grid is None or r["Grid_Size_X"] == grid)]
+    grid = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] != "-" else None
+    name = sys.argv[5] if len(sys.argv) > 5 else "k_greedy_step"
+    g = [i for i, r in enumerate(rows) if name in r["Kernel_Name"] and (grid is None or r["Grid_Size_X"] == grid)]
     if len(g) < first + n:
         print(f"only {len(g)} step markers")
         n = len(g) - first - 1

@@ -787,7 +787,27 @@ __device__ __forceinline__ f16x2 byte2_f16_biased(uint32_t w, uint32_t sel) {
 // (sumf + sums[0] + ... + sums[7]), so after one barrier the last part adds the others' sums from LDS
 // in residue order: the same additions as the one-wave kernel.  Few-tile matrices (Orpheus down:
 // 192 tiles of 32 blocks) then keep all four SIMDs of a CU busy instead of one.
-template <int PRO, int NCH, int RS = 1>
+// Compile-time sequence C = B..E-1 of calls f(integral_constant<C>) (an unrolled chunk loop whose
+// register buffers are indexed by constants)
+template <int B, int E>
+struct ChunkSeq {
+    template <class F>
+    __device__ __forceinline__ static void run(F && f) {
+        f(std::integral_constant<int, B>{});
+        ChunkSeq<B + 1, E>::run(f);
+    }
+};
+template <int E>
+struct ChunkSeq<E, E> {
+    template <class F>
+    __device__ __forceinline__ static void run(F &&) {}
+};
+
+// NCK > 0: every row tile is NCK chunks of 4 blocks (K = 1024 NCK) and the chunk loop is unrolled:
+// straight-line code in which the compiler's wait counting stays exact (in the runtime loop it put
+// address temporaries into the registers of the next chunk's in-flight loads and then had to wait
+// for every load, the prefetch included, before each chunk)
+template <int PRO, int NCH, int RS = 1, int NCK = 0>
 __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
@@ -798,11 +818,14 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     float * xd_s = (float *)(sbs + (size_t)nslot * 16);    // [nslot]      Q8_K d
 
     TTS_TS(j, 0);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // wave-uniform by construction (readfirstlane): branches on the wave's part / slot are then scalar,
+    // and the compiler's wait counting stays exact across them (exec-masked branches made it wait for
+    // every load in flight, the next chunk's prefetch included, inside the row loop)
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
     const int r = lane & 15, kg = lane >> 4;
     const int cc = r < M ? r : M - 1;  // B / C column (padding columns compute and are dropped)
     constexpr int CH = 4;
-    const int nch = (nb + CH - 1) / CH;
+    const int nch = NCK > 0 ? NCK : (nb + CH - 1) / CH;
     // EPI_SWIGLU: a wave runs tile t of gate, then tile t of up (units = tile pairs), and keeps the
     // gate results in registers until the up tile is done
     // When every pair fits one wave slot of the first half of the workgroups' waves (xpair), wave w
@@ -834,7 +857,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     // tile layout (tts_repack_q4_K_tiled): lane (r, kg) reads its row's header and the two 16-B
     // pieces of chunk c = kg (residues 0..3, 4..7); a quarter wave covers four 64-B runs
     u32x4 hd[2][CH], qa[2][CH], qb[2][RS == 1 ? CH : 1];  // RS > 1: qa holds this wave's 16-B piece
-    auto load = [&](auto BS, int64_t i) {
+    auto load = [&](auto BS, int64_t i) __attribute__((always_inline)) {
         constexpr int bs = decltype(BS)::value;
         const int64_t ti = i / nch;
         const int64_t t = t0 + (ti / per) * tstride;
@@ -872,7 +895,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     typedef float f2v __attribute__((ext_vector_type(2)));
     f2v sums[LPW][2], sumf[2];
     float gate[4];
-    auto compute = [&](auto BS, int64_t i) {
+    auto compute = [&](auto BS, int64_t i) __attribute__((always_inline)) {
         constexpr int bs = decltype(BS)::value;
         const int64_t ti = i / nch;
         const int64_t t = t0 + (ti / per) * tstride;
@@ -993,12 +1016,24 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
     TTS_TS(j, 2);
     __syncthreads();
     TTS_TS(j, 3);
-    for (int64_t i = 0; i < nmine; i += 2) {
-        load(I1{}, min(i + 1, nmine - 1));
-        compute(I0{}, i);
-        if (i + 1 >= nmine) break;
-        load(I0{}, min(i + 2, nmine - 1));
-        compute(I1{}, i + 1);
+    if constexpr (NCK > 0) {
+        const int64_t units = nmine / NCK;  // tiles (SwiGLU: gate / up tiles) of this wave
+        for (int64_t u = 0; u < units; ++u) {
+            if (u > 0) load(I0{}, u * NCK);
+            ChunkSeq<0, NCK>::run([&](auto CI) __attribute__((always_inline)) {
+                constexpr int C = decltype(CI)::value;
+                if constexpr (C + 1 < NCK) load(std::integral_constant<int, (C + 1) & 1>{}, u * NCK + C + 1);
+                compute(std::integral_constant<int, C & 1>{}, u * NCK + C);
+            });
+        }
+    } else {
+        for (int64_t i = 0; i < nmine; i += 2) {
+            load(I1{}, min(i + 1, nmine - 1));
+            compute(I0{}, i);
+            if (i + 1 >= nmine) break;
+            load(I0{}, min(i + 2, nmine - 1));
+            compute(I1{}, i + 1);
+        }
     }
     if (RS > 1) {  // one tile per wave at most: join the parts' chains in residue order
         float * xs = xg;  // [RS - 1 parts][nws slots][64 lanes][LPW * 4]
@@ -1781,19 +1816,29 @@ static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
     // launch_q4k_mf's column loop step by 0
     return j.wtype == TTS_TYPE_Q4_K && j.tiled && q4k_mf_max_cols(j.K) >= 1;
 }
-template <int PRO, int NCH, int RS>
+template <int PRO, int NCH, int RS, int NCK = 0>
 static void launch_q4k_mf_rs(tts_hip_backend * be, const GemvJob & j, unsigned gx) {
+    if constexpr (PRO == PRO_COPY && NCK == 0) {  // unrolled chunk loop for the common row lengths
+        switch ((j.K / QK_K + 3) / 4 * (j.K % (4 * QK_K) == 0 ? 1 : 0)) {
+            case 1: launch_q4k_mf_rs<PRO, NCH, RS, 1>(be, j, gx); return;
+            case 2: launch_q4k_mf_rs<PRO, NCH, RS, 2>(be, j, gx); return;
+            case 3: launch_q4k_mf_rs<PRO, NCH, RS, 3>(be, j, gx); return;
+            case 4: launch_q4k_mf_rs<PRO, NCH, RS, 4>(be, j, gx); return;
+            case 8: launch_q4k_mf_rs<PRO, NCH, RS, 8>(be, j, gx); return;
+            default: break;
+        }
+    }
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH, RS>);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_mf<PRO, NCH, RS, NCK>);
     const size_t lds = q4k_mf_lds(j.M, j.K);
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS, NCK>), dim3(gx), dim3(512), (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS>), dim3(gx), dim3(512), lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_mf<PRO, NCH, RS, NCK>), dim3(gx), dim3(512), lds, be->stream, j);
 }
 template <int PRO, int NCH>
 static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
