@@ -290,6 +290,9 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_PREQUANT = 21, /* 1 (default): a matrix-core Q4_K GEMV's activation is normed / quantized once, by a
                                      pass writing its MFMA operands to backend scratch, which every workgroup copies into
                                      LDS by LDS-DMA; 0 = every workgroup quantizes the whole activation itself */
+    TTS_HIP_OPT_GEMV_KRELAY = 22, /* 1 (default): pre-quantized matrix-core Q4_K GEMVs of K = 1024 / 2048 / 3072 / 4096 /
+                                     8192 run the K-relay kernel (a 16-row tile's blocks split over 4-8 waves, ggml's
+                                     chain handed from wave to wave in block order); 0 = k_gemv_q4K_mf */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

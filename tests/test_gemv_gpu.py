@@ -116,14 +116,27 @@ def run_gpu_tiled(hip, w, x, N):
 KS_DEFAULT = 256  # backend default of TTS_HIP_OPT_GEMV_KS
 
 
-@pytest.fixture(params=[0, KS_DEFAULT, 1 << 20], ids=["mf", "ks", "ks_loop"])
+# (GEMV_KS tile cap, GEMV_KRELAY, GEMV_PREQUANT)
+MF_PATHS = {"mf": (0, 0, 1), "ks": (KS_DEFAULT, 0, 1), "ks_loop": (1 << 20, 0, 1), "kr": (KS_DEFAULT, 1, 1),
+            "mf_inkernel": (0, 0, 0), "ks_inkernel": (KS_DEFAULT, 0, 0)}
+
+
+@pytest.fixture(params=list(MF_PATHS), ids=list(MF_PATHS))
 def ks_tiles(request, hip):
-    """Tile-layout GEMVs on k_gemv_q4K_mf (0), on the K-split kernel k_gemv_q4K_ks where it applies
-    (M <= 8, K <= 4096, N % 16 == 0) with the default tile cap, and on the K-split kernel for every
-    tile count (grids of more than 2048 tiles loop over tiles)."""
-    assert ttship.lib().tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], request.param) == 0
+    """Tile-layout GEMVs on k_gemv_q4K_mf, on the K-split kernel k_gemv_q4K_ks where it applies
+    (M <= 8, K <= 4096, N % 16 == 0) with the default tile cap and for every tile count (grids of more
+    than 2048 tiles loop over tiles), on the K-relay kernel k_gemv_q4K_kr (M <= 8, K = 1024 * {1, 2,
+    3, 4, 8}, N % 16 == 0; the default), each after the quantize pass (k_quant_mf, default) or with
+    the operands quantized inside every workgroup."""
+    lib = ttship.lib()
+    ks, kr, pre = MF_PATHS[request.param]
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], ks) == 0
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KRELAY"], kr) == 0
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_PREQUANT"], pre) == 0
     yield request.param
-    ttship.lib().tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], KS_DEFAULT)
+    lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], KS_DEFAULT)
+    lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KRELAY"], 1)
+    lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_PREQUANT"], 1)
 
 
 @pytest.mark.gpu

@@ -83,6 +83,20 @@ def test_orpheus_wide_batch8(hip):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("path", ["mf", "inkernel"])
+def test_orpheus_wide_batch8_gemv_paths(hip, path):
+    """The bench shape on the older matrix-core paths: k_gemv_q4K_mf after the quantize pass (K relay
+    off), and every workgroup quantizing its own operands (quantize pass off); tokens bit-exact either way
+    (the default, K relay after the pass, is test_orpheus_wide_batch8)."""
+    opt = "GEMV_KRELAY" if path == "mf" else "GEMV_PREQUANT"
+    hip.set_option(ttship.OPT[opt], 0)
+    try:
+        run_pair(hip, WIDE, 8, 2, 2)
+    finally:
+        hip.set_option(ttship.OPT[opt], 1)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("drop", ["none", "EPI", "CONTREAD", "MCPY", "GROUP"])
 def test_orpheus_tiny_tiled_fusion_masks(hip, drop):
     """All matrices tiled at 8 columns (SwiGLU epilogue, residue split, mixed-row q / k / v groups) with

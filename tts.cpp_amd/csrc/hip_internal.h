@@ -300,6 +300,7 @@ struct tts_hip_backend {
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;
     int gemv_mf_prequant = 1;  // TTS_HIP_OPT_GEMV_PREQUANT
+    int gemv_kr = 1;           // TTS_HIP_OPT_GEMV_KRELAY
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)

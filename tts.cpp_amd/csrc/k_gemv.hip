@@ -1081,6 +1081,198 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Matrix-core Q4_K GEMV, "K relay" (k_gemv_q4K_kr): one workgroup per 16-row tile (SwiGLU: per gate /
+// up tile pair), its waves splitting the tile's blocks: wave w owns the BPW consecutive blocks
+// w*BPW .. (w+1)*BPW-1.  Every weight byte is loaded once (header + both 16-B residue pieces per
+// lane, all of the wave's blocks requested at entry behind the operand DMA), the integer dots are
+// the MFMAs of k_gemv_q4K_mf (8 residue MFMAs + the mins MFMA per block, exact), and each lane
+// turns them into ggml's per-block terms p_l = (d*yd)*aux32[l], q = (dmin*yd)*sumi for its 4 rows x
+// 1 column, kept in registers.  ggml's chain (sums[l] += p_l, sumf -= q over the blocks in
+// ascending order) then runs as a relay: wave 0 folds its blocks, hands the 36 running sums per lane
+// to wave 1 through LDS, and so on; the last wave adds sumf + sums[0..7] and stores.  Same additions
+// in the same order as vec_dot_q4_K_q8_K: bit-identical.  A tile's weights stream through all its
+// waves at once instead of one chunk at a time through one wave (k_gemv_q4K_mf's row phase).
+// Operands: PRO_COPY (k_quant_mf's layout, DMA'd into LDS).
+template <int BPW, bool SW, int NWT>
+__global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
+    constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int nb = (int)(j.K / QK_K);
+    const int M = (int)j.M;
+    const int nslot = M * nb + 1;
+    _Float16 * b16 = (_Float16 *)smem;
+    _Float16 * sbs = b16 + (size_t)nslot * QK_K;
+    float * xd_s = (float *)(sbs + (size_t)nslot * 16);
+    float * relay = (float *)(smem + ((j.bq_bytes + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
+
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+    const int r = lane & 15, kg = lane >> 4;
+    const int cc = r < M ? r : M - 1;
+    const int sub = SW ? wave / nwt : 0;    // SwiGLU: 0 = gate tile, 1 = up tile
+    const int w = wave - sub * nwt;         // position in the relay
+    const int64_t t = blockIdx.x;           // the tile (pair)
+    const int64_t NR = SW ? j.N : job_rows(j);
+    auto mat_of = [&](int64_t flat) {
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
+        return mt;
+    };
+    const int mat = __builtin_amdgcn_readfirstlane(SW ? sub : mat_of(t * 16));
+    const int64_t row0 = SW ? t * 16 : t * 16 - job_roff(j, mat);  // the tile's first row in its matrix
+
+    // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
+    {
+        const int nck = (int)(j.bq_bytes >> 10);
+        for (int i = wave; i < nck; i += nw)
+            __builtin_amdgcn_global_load_lds(gptr(j.bq + (size_t)i * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
+    }
+    TTS_PIN_LOADS();
+    u32x4 hd[BPW], qa[BPW], qb[BPW];
+    {
+        int64_t row = row0 + r;
+        const int64_t rows_m = SW ? j.N : job_roff(j, mat + 1) - job_roff(j, mat);
+        row = row < rows_m ? row : rows_m - 1;
+        const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
+        const int ri = (int)(row & 3);
+#pragma unroll
+        for (int u = 0; u < BPW; ++u) {
+            const uint8_t * bp = wt + (int64_t)min(w * BPW + u, nb - 1) * 576;
+            hd[u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+            qa[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+            qb[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+        }
+    }
+    TTS_PIN_LOADS();
+    __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
+
+    // the terms of this wave's blocks: tp[u][l][q], tq[u][q] for rows 4kg + q, column r
+    float tp[BPW][8][4], tq[BPW][4];
+#pragma unroll
+    for (int u = 0; u < BPW; ++u) {
+        const int b = min(w * BPW + u, nb - 1);
+        const u32x4 h = hd[u];
+        const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
+        const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+        const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+        const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
+        const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
+        const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
+        const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
+        const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
+        const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8;
+        f32x4 acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const uint32_t D = l < 4 ? qa[u][l & 3] : qb[u][l & 3];
+            const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+            const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
+            const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
+            const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
+            const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
+            const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+            const f16x8 B = *(const f16x8 *)(bsl + l * 32);
+            acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+        const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
+        const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
+        const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
+        const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
+        const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
+        const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
+        const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+        const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
+        const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const float yd = xd_s[cc * nb + b];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
+            const float dy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+            const float dmy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+#pragma unroll
+            for (int l = 0; l < 8; ++l) tp[u][l][q] = __fmul_rn(dy, acc[l][q]);
+            tq[u][q] = __fmul_rn(dmy, si[q]);
+        }
+    }
+
+    // the relay: wave w' folds its blocks into the running sums in block order, then hands them on
+    float sums[8][4], sumf[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        sumf[q] = 0.f;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) sums[l][q] = 0.f;
+    }
+    float * rl = relay + ((size_t)sub * 64 + lane) * 36;
+    const int nblk = nb - w * BPW < BPW ? nb - w * BPW : BPW;  // the last wave may own fewer blocks
+    for (int step = 0; step < nwt; ++step) {
+        if (step == w) {
+            if (w > 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 a = *(const float4 *)(rl + 8 * q), c = *(const float4 *)(rl + 8 * q + 4);
+                    sums[0][q] = a.x, sums[1][q] = a.y, sums[2][q] = a.z, sums[3][q] = a.w;
+                    sums[4][q] = c.x, sums[5][q] = c.y, sums[6][q] = c.z, sums[7][q] = c.w;
+                }
+                const float4 f = *(const float4 *)(rl + 32);
+                sumf[0] = f.x, sumf[1] = f.y, sumf[2] = f.z, sumf[3] = f.w;
+            }
+#pragma unroll
+            for (int u = 0; u < BPW; ++u) {
+                if (u >= nblk) break;  // wave-uniform
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                    for (int l = 0; l < 8; ++l) sums[l][q] = __fadd_rn(sums[l][q], tp[u][l][q]);
+                    sumf[q] = __fsub_rn(sumf[q], tq[u][q]);
+                }
+            }
+            if (w < nwt - 1) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    *(float4 *)(rl + 8 * q) = make_float4(sums[0][q], sums[1][q], sums[2][q], sums[3][q]);
+                    *(float4 *)(rl + 8 * q + 4) = make_float4(sums[4][q], sums[5][q], sums[6][q], sums[7][q]);
+                }
+                *(float4 *)(rl + 32) = make_float4(sumf[0], sumf[1], sumf[2], sumf[3]);
+            }
+        }
+        if (step < nwt - 1) __syncthreads();
+    }
+    if (w != nwt - 1) {
+        if (SW) __syncthreads();  // the gate / up exchange below
+        return;
+    }
+    float tot[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        tot[q] = sumf[q];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) tot[q] = __fadd_rn(tot[q], sums[l][q]);
+    }
+    if constexpr (SW) {  // out = silu(gate) * up, by the up tile's last wave
+        float * xg = relay + 2 * 64 * 36;  // [64 lanes][4] after both relays
+        if (sub == 0) *(float4 *)(xg + lane * 4) = make_float4(tot[0], tot[1], tot[2], tot[3]);
+        __syncthreads();
+        if (sub == 1) {
+            const float4 g4 = *(const float4 *)(xg + lane * 4);
+            const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t flat = t * 16 + 4 * kg + q;
+                if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), tot[q]);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int64_t rr = row0 + 4 * kg + q;
+            const int64_t rows_m = job_roff(j, mat + 1) - job_roff(j, mat);
+            if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, r, tot[q]);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // Matrix-core Q4_K GEMV for latency-bound decode matrices (k_gemv_q4K_ks).  Parler's matrices are
 // 0.6-2.4 MB: the row phase of the VALU kernels is ~1.2-2.5 us of dependent integer dots at one wave
 // per SIMD, and k_gemv_q4K_mf streams a tile's blocks through ONE wave.  Here a workgroup owns one
@@ -1850,6 +2042,7 @@ static void launch_q4k_mf_pro(tts_hip_backend * be, const GemvJob & j) {
     else if (rs == 2) launch_q4k_mf_rs<PRO, NCH, 2>(be, j, gx);
     else launch_q4k_mf_rs<PRO, NCH, 1>(be, j, gx);
 }
+static bool launch_q4k_kr(tts_hip_backend * be, const GemvJob & j);
 static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
     const int64_t cmax = q4k_mf_max_cols(job.K);
     for (int64_t m0 = 0; m0 < job.M; m0 += cmax) {
@@ -1878,11 +2071,52 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
             TTS_HIP_CHECK(hipGetLastError());
             j.pro = PRO_COPY;
             j.lnout = nullptr;  // written by the pass
-            launch_q4k_mf_pro<PRO_COPY, 16>(be, j);
+            if (!launch_q4k_kr(be, j)) launch_q4k_mf_pro<PRO_COPY, 16>(be, j);
             continue;
         }
         if (j.pro == PRO_LN) launch_q4k_mf_pro<PRO_LN, 16>(be, j);
         else launch_q4k_mf_pro<PRO_QUANT, 16>(be, j);
+    }
+}
+
+// ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
+static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
+template <int BPW, bool SW, int NWT>
+static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx) {
+    static std::atomic<uint32_t> attr_done{0};
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT>);
+    const size_t lds = q4k_kr_lds(j.bq_bytes, SW);
+    const dim3 blk(64 * NWT * (SW ? 2 : 1));
+    if (be->profile_gemv) {
+        hipEvent_t e0, e1;
+        profile_pair(be, e0, e1);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT>), dim3(gx), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
+        return;
+    }
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT>), dim3(gx), blk, lds, be->stream, j);
+}
+// PRO_COPY jobs (operands in j.bq) whose row length has an instantiation; false otherwise
+static bool launch_q4k_kr(tts_hip_backend * be, const GemvJob & j) {
+    if (!be->gemv_kr || j.pro != PRO_COPY || j.M > 8) return false;
+    const bool sw = j.epi == EPI_SWIGLU;
+    if (!sw) {
+        for (int m = 0; m <= j.nmat; ++m)
+            if (job_roff(j, m) % 16) return false;
+    } else if (j.N % 16) {
+        return false;
+    }
+    if (q4k_kr_lds(j.bq_bytes, sw) > 160 * 1024) return false;
+    const int64_t T = sw ? j.N / 16 : job_rows(j) / 16;
+    if (T < 1 || T > 0x7fffffff) return false;
+    const unsigned gx = (unsigned)T;
+    switch (j.K / QK_K) {
+        case 4: sw ? launch_q4k_kr_t<1, true, 4>(be, j, gx) : launch_q4k_kr_t<1, false, 4>(be, j, gx); return true;
+        case 8: sw ? launch_q4k_kr_t<2, true, 4>(be, j, gx) : launch_q4k_kr_t<2, false, 4>(be, j, gx); return true;
+        case 12: sw ? launch_q4k_kr_t<3, true, 4>(be, j, gx) : launch_q4k_kr_t<3, false, 4>(be, j, gx); return true;
+        case 16: sw ? launch_q4k_kr_t<4, true, 4>(be, j, gx) : launch_q4k_kr_t<4, false, 4>(be, j, gx); return true;
+        case 32: if (sw) return false; launch_q4k_kr_t<4, false, 8>(be, j, gx); return true;
+        default: return false;
     }
 }
 
@@ -1934,6 +2168,7 @@ static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
         TTS_HIP_CHECK(hipGetLastError());
         jc.pro = PRO_COPY;
         jc.lnout = nullptr;
+        if (launch_q4k_kr(be, jc)) return;
         const int upw = nb <= 4 ? 1 : 2;
         const int nw = (int)((2 * nb + upw - 1) / upw);
         if (nb <= 4) launch_q4k_ks_t<PRO_COPY, 4, 1, 8>(be, jc, gx, nw, lds);
