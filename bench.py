@@ -414,6 +414,8 @@ def main():
     ap.add_argument("--attn-fused", type=int, default=None, help="TTS_HIP_OPT_ATTN_FUSED: decode attention over >= value keys as one 1024-thread launch (0 = off)")
     ap.add_argument("--gemv-ks", type=int, default=None, help="TTS_HIP_OPT_GEMV_KS: max 16-row tiles of a tile-layout GEMV on the K-split matrix-core kernel (0 = never)")
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
+    ap.add_argument("--attn-ks", type=int, default=None, help="TTS_HIP_OPT_ATTN_KS: 128 * value key positions per split-scores workgroup")
+    ap.add_argument("--attn-pv8", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV8: 8 output dims per split P.V workgroup (1) or 16 (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
                     "replica on all CUs, 1 = replica r on the r-th contiguous CU set, 2 = on CUs c with c %% R == r")
@@ -456,6 +458,10 @@ def main():
             rb.set_option(ttship.OPT["ATTN_FUSED"], args.attn_fused)
         if args.attn_pv16 is not None:
             rb.set_option(ttship.OPT["ATTN_PV16"], args.attn_pv16)
+        if args.attn_ks is not None:
+            rb.set_option(ttship.OPT["ATTN_KS"], args.attn_ks)
+        if args.attn_pv8 is not None:
+            rb.set_option(ttship.OPT["ATTN_PV8"], args.attn_pv8)
         if args.kv_prefetch_blocks is not None:
             rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
         return rb

@@ -60,6 +60,11 @@ case "$1" in
     shift
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/profo" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --dia-steps 0 --no-cpu-baseline --b1-replicas 0 --orpheus-steps 40 "$@" > "$O/orph_trace.log" 2>&1) &&
     f=$(find "$O/profo" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 10 25 - k_greedy_step_wide > "$O/orph_breakdown.txt" && cut -c1-150 "$O/orph_breakdown.txt" ;;
+  attn_opts)   # split-attention geometry (scores positions per workgroup x P.V dims per workgroup), AR-only
+    for cfg in "--attn-ks 2 --attn-pv8 0" "--attn-ks 1 --attn-pv8 0" "--attn-ks 2 --attn-pv8 1" "--attn-ks 1 --attn-pv8 1" "--attn-ks 4 --attn-pv8 0" "--attn-ks 2 --attn-pv8 0"; do
+      n=$(echo $cfg | tr -d ' -')
+      timeout -k 10 200 python3 bench.py $AR $cfg > "$O/at_$n.log" 2>&1 && ar_line "$O/at_$n.log" "$cfg" || exit 1
+    done ;;
   tests)       # selected GPU test files, e.g. scripts/gpu_study.sh tests tests/test_dia_gpu.py
     shift
     timeout -k 10 900 python -u -m pytest "$@" $T > "$O/tests.log" 2>&1; rc=$?; tail -3 "$O/tests.log"; exit $rc ;;

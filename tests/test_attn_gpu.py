@@ -45,7 +45,7 @@ def build(g, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx):
                                          (37, 128, 16, 16, 2), (430, 128, 8, 8, 1), (1, 64, 4, 4, 1),
                                          (1309, 64, 16, 16, 8), (2100, 128, 24, 24, 1), (128, 64, 16, 16, 3),
                                          (257, 128, 16, 16, 2), (4096, 64, 16, 16, 2)])
-@pytest.mark.parametrize("mode", ["fused", "split", "rows"])
+@pytest.mark.parametrize("mode", ["fused", "split", "split_ks1", "split_ks4_pv8", "rows"])
 def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, mode):
     set_mode(hip, mode)
     rng = np.random.default_rng(P * 7 + hd)
@@ -70,8 +70,13 @@ def test_fused_attention_matches_unfused_chain(hip, P, hd, H, Hk, B, mode):
 
 
 def set_mode(hip, mode):
+    """split_ks1 / split_ks4_pv8: the split pair with 128 / 512 positions per scores workgroup and 8
+    output dims per P.V workgroup (TTS_HIP_OPT_ATTN_KS / _PV8); the same sums per element."""
+    split = mode.startswith("split") or mode == "default"
     hip.set_option(ttship.OPT["ATTN_FUSED"], ttship.ATTN_FUSED_ON if mode == "fused" else 0)
-    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if mode in ("split", "default") else 0)
+    hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
+    hip.set_option(ttship.OPT["ATTN_KS"], 1 if mode == "split_ks1" else 4 if mode == "split_ks4_pv8" else 2)
+    hip.set_option(ttship.OPT["ATTN_PV8"], 1 if mode == "split_ks4_pv8" else 0)
 
 
 @pytest.mark.gpu

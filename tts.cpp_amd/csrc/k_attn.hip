@@ -459,12 +459,13 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float 
 
 constexpr int PV_THREADS = 256;
 
-template <bool VVEC, int UV>
-__global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float * __restrict__ sbuf, int pstride,
-                                                       const float * __restrict__ mxbuf, int nch) {
+template <bool VVEC, int UV, int NW = PV_THREADS / 64>
+__global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * __restrict__ sbuf, int pstride,
+                                                    const float * __restrict__ mxbuf, int nch) {
+    // NW waves x 4 output dims each (4 NW dims per workgroup)
+    constexpr int NTH = 64 * NW;
     __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
-    __shared__ double s_wd[PV_THREADS / 64];
-    constexpr int NW = PV_THREADS / 64;
+    __shared__ double s_wd[NW];
     const int h = blockIdx.y, z = blockIdx.z;
     const int b = z / a.n, tq = z - b * a.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float 
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
     const int64_t vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
-    const int d = blockIdx.x * 16 + wave * 4 + r;
+    const int d = blockIdx.x * 4 * NW + wave * 4 + r;
     const char * vrow = vbase + (int64_t)min(d, a.hd - 1) * vnb1;
     const int ilast = ((P - 1) >> 2) << 2;
     float4 w4[VVEC ? UV : 1];
@@ -492,7 +493,7 @@ __global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float 
     float mx = -INFINITY;
     for (int k = 0; k < nch; ++k) mx = fmaxf(mx, mrow[k]);
     double sum = 0.0;
-    for (int i = tid; i < P; i += PV_THREADS) {
+    for (int i = tid; i < P; i += NTH) {
         const float e = cr_expf(__fsub_rn(srow[i], mx));
         s_p[i] = e;
         sum += (double)e;
@@ -505,7 +506,7 @@ __global__ __launch_bounds__(PV_THREADS) void k_attn_pv(AttnArgs a, const float 
     for (int w = 0; w < NW; ++w) sum += s_wd[w];
     const float inv = (float)(1.0 / sum);
     const int P64 = (P + 63) & ~63;
-    for (int i = tid; i < P64; i += PV_THREADS) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    for (int i = tid; i < P64; i += NTH) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
     __syncthreads();
 
     double acc = 0.0;
@@ -889,7 +890,7 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
         return;
     }
     if (krows && be->attn_split_minp > 0 && P >= be->attn_split_minp && P <= ATTN_MAXP && hd % 16 == 0) {
-        constexpr int KS = 2;
+        const int KS = be->attn_ks == 1 ? 1 : be->attn_ks == 4 ? 4 : 2;  // 128 * KS positions per scores workgroup
         const int nch = (P + 128 * KS - 1) / (128 * KS);
         const int pstride = (P + 63) & ~63;
         const size_t rows = (size_t)H * n * B;
@@ -897,14 +898,23 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             float * sbuf = be->attn_buf;
             float * mxbuf = be->attn_buf + rows * pstride;
             const dim3 g1((unsigned)nch, (unsigned)H, (unsigned)(n * B));
-            if (hd == 64) hipLaunchKernelGGL((k_attn_scores<1, KS>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
-            else hipLaunchKernelGGL((k_attn_scores<2, KS>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            auto scores = [&](auto DPR, auto KSc) {
+                hipLaunchKernelGGL((k_attn_scores<decltype(DPR)::value, decltype(KSc)::value>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride,
+                                   mxbuf, nch);
+            };
+            using C1 = std::integral_constant<int, 1>;
+            using C2 = std::integral_constant<int, 2>;
+            using C4 = std::integral_constant<int, 4>;
+            if (hd == 64) KS == 1 ? scores(C1{}, C1{}) : KS == 4 ? scores(C1{}, C4{}) : scores(C1{}, C2{});
+            else KS == 1 ? scores(C2{}, C1{}) : KS == 4 ? scores(C2{}, C4{}) : scores(C2{}, C2{});
             TTS_HIP_CHECK(hipGetLastError());
             const bool vvec = v.nb[0] == 4 && (v.nb[1] % 16) == 0 && (v.nb[2] % 16) == 0 && (v.nb[3] % 16) == 0 &&
                               (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
             const dim3 g2((unsigned)(hd / 16), (unsigned)H, (unsigned)(n * B));
+            const dim3 g2h((unsigned)(hd / 8), (unsigned)H, (unsigned)(n * B));  // 8 dims per workgroup
             // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
             if (vvec && P <= 1024 && be->attn_pv_uv16) hipLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            else if (vvec && be->attn_pv8) hipLaunchKernelGGL((k_attn_pv<true, 8, 2>), g2h, dim3(128), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
             else if (vvec) hipLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
             else hipLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
             TTS_HIP_CHECK(hipGetLastError());
