@@ -416,6 +416,8 @@ def main():
     ap.add_argument("--gemv-unique", type=int, default=None, help="TTS_HIP_OPT_GEMV_UNIQUE: unique-load Q4_K GEMV (1, default) or octet per (row, column) (0)")
     ap.add_argument("--attn-ks", type=int, default=None, help="TTS_HIP_OPT_ATTN_KS: 128 * value key positions per split-scores workgroup")
     ap.add_argument("--attn-pv8", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV8: 8 output dims per split P.V workgroup (1) or 16 (0)")
+    ap.add_argument("--gemv-krelay", type=int, default=None, help="TTS_HIP_OPT_GEMV_KRELAY: K-relay matrix-core GEMV / prefill GEMM (1) or not (0)")
+    ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
                     "replica on all CUs, 1 = replica r on the r-th contiguous CU set, 2 = on CUs c with c %% R == r")
@@ -458,6 +460,10 @@ def main():
             rb.set_option(ttship.OPT["ATTN_FUSED"], args.attn_fused)
         if args.attn_pv16 is not None:
             rb.set_option(ttship.OPT["ATTN_PV16"], args.attn_pv16)
+        if args.gemv_krelay is not None:
+            rb.set_option(ttship.OPT["GEMV_KRELAY"], args.gemv_krelay)
+        if args.gemv_nw_min is not None:
+            rb.set_option(ttship.OPT["GEMV_NW_MIN"], args.gemv_nw_min)
         if args.attn_ks is not None:
             rb.set_option(ttship.OPT["ATTN_KS"], args.attn_ks)
         if args.attn_pv8 is not None:
@@ -492,9 +498,15 @@ def main():
     while len(dac_workers) < W:
         xb = new_backend()
         dac_workers.append((xb, new_dac(xb)))
-    # text-prompt pass to reach the measured KV length
+    # text-prompt pass to reach the measured KV length (timed on its own: the prompt prefill, batch x ctx
+    # columns per Q4_K product, on the matrix-core GEMM; not part of the headline's timed region)
+    prefill_ms = []
     for r, (rb, rr, rd) in enumerate(reps):
+        rb.sync()
+        tp0 = time.perf_counter()
         rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * args.batch + r * bl))
+        rb.sync()
+        prefill_ms.append(1000.0 * (time.perf_counter() - tp0))
         rr.generate(args.warmup)
         rb.sync()
     barrier_sync(dist, be)
@@ -603,6 +615,8 @@ def main():
             "dac_audio_sec_per_s": round(audio_s / dt_dac, 3) if dac is not None else None,
             "codec_tokens_per_s": round(total_prompts * args.steps * HEADS / dt_ar, 1),
             "host_us_per_step": host,
+            "prefill_ms": {"per_replica": [round(v, 2) for v in prefill_ms], "prompts": bl, "tokens_per_prompt": args.ctx,
+                           "note": "prompt pass to the KV start length (untimed by the headline)"},
             "audio_gather": None if gathered is None else {
                 "prompts": len(gathered), "audio_sec": round(sum(len(p) for p in gathered) / SAMPLE_RATE, 3),
                 "ms": round(1000.0 * t_gather, 3), "transport": "RCCL send/recv (gatherv) to rank 0" if world > 1 else "local"},

@@ -295,6 +295,8 @@ enum tts_hip_option {
                                      chain handed from wave to wave in block order); 0 = k_gemv_q4K_mf */
     TTS_HIP_OPT_ATTN_KS = 23,     /* split decode attention: 128 * value key positions per scores workgroup (1, 2 default, 4) */
     TTS_HIP_OPT_ATTN_PV8 = 24,    /* 1: the split P.V kernel covers 8 output dims per workgroup (twice the workgroups); 0 = 16 */
+    TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
+                                     0 = default geometry, about one row group per wave over every CU) */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,

@@ -9,8 +9,8 @@ mkdir -p "$O"
 cd "$R"
 AR="--no-dac --kokoro-prompts 0 --orpheus-steps 0 --dia-steps 0 --no-cpu-baseline --b1-replicas 0 --steps 200"
 T="-x -v --timeout 300 --timeout-method thread"
-ar_line() {  # bench.py AR-only line: ms/step, audio-s/s, average GEMV launch
-  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2], d['ar_ms_per_step'], d['ar_audio_sec_per_s'], d['roofline']['avg_launch_us'])" "$1" "$2"
+ar_line() {  # bench.py AR-only line: ms/step, audio-s/s, average GEMV launch, prefill ms per replica
+  python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print(sys.argv[2], d['ar_ms_per_step'], d['ar_audio_sec_per_s'], d['roofline']['avg_launch_us'], d.get('prefill_ms', {}).get('per_replica'))" "$1" "$2"
 }
 case "$1" in
   ar)          # Parler AR decode only, bench.py options appended (e.g. --replicas 1)

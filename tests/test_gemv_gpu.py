@@ -61,6 +61,22 @@ def test_q4_K(hip, K, N, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("K,N", [(1024, 1024), (1024, 3072), (2048, 160), (3072, 512), (4096, 1024), (1024, 1000)])
+@pytest.mark.parametrize("M", [9, 16, 17, 100, 448])
+def test_q4_K_prefill_gemm(hip, tiled, K, N, M):
+    """Many-column Q4_K products (prompt prefill): the operand pass over all columns, then the K-relay
+    kernel over (16-row tile, 16-column tile) pairs, on lane-layout and tile-layout weights; N = 1000
+    (not whole tiles) falls back to the 8-column GEMV loop.  Bit-identical to ggml's order."""
+    rng = np.random.default_rng(K * 13 + N + M + tiled)
+    w = helpers.rand_q4_K(rng, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+    got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,N", [(2048, 2048), (2048, 512), (8192, 64), (1024, 1024), (64, 7)])
 @pytest.mark.parametrize("M", [1, 2, 8, 9, 64, 300])
 def test_q8_0(hip, K, N, M):

@@ -229,6 +229,7 @@ struct GemvJob {
     // 1 KiB), written by k_quant_mf
     const char * bq = nullptr;
     int64_t bq_bytes = 0;
+    int64_t bq_tile = 0;  // > 0: columns in tiles of 16, tile c's operands at bq + c * bq_tile (its own slot layout)
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
 };
 __host__ __device__ inline int64_t job_roff(const GemvJob & j, int m) { return j.hetero ? j.roff[m] : (int64_t)m * j.N; }
@@ -303,6 +304,7 @@ struct tts_hip_backend {
     int64_t gemv_ks_tiles = 256;
     int gemv_mf_prequant = 1;  // TTS_HIP_OPT_GEMV_PREQUANT
     int gemv_kr = 1;           // TTS_HIP_OPT_GEMV_KRELAY
+    int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)

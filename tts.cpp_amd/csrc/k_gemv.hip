@@ -1093,17 +1093,25 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 // in the same order as vec_dot_q4_K_q8_K: bit-identical.  A tile's weights stream through all its
 // waves at once instead of one chunk at a time through one wave (k_gemv_q4K_mf's row phase).
 // Operands: PRO_COPY (k_quant_mf's layout, DMA'd into LDS).
-template <int BPW, bool SW, int NWT>
+// LANE: weights in the lane layout (tts_repack_q4_K: residue l's 16 bytes of a block at 16 + 16 l,
+// chunk c's dword at + 4 c -- the tile layout's piece dword for (c, l)), read as 8 dwords per block;
+// otherwise the 4-row tile layout.  blockIdx.y = column tile (j.bq_tile > 0: 16 columns per tile,
+// the many-column prefill GEMM).
+template <int BPW, bool SW, int NWT, bool LANE = false>
 __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
     constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
-    const int M = (int)j.M;
+    const int ct = blockIdx.y;                 // column tile
+    const int c0 = j.bq_tile ? 16 * ct : 0;    // its first column
+    const int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;
+    const char * const bqt = j.bq + (size_t)ct * j.bq_tile;
+    const int64_t bqb = j.bq_tile ? j.bq_tile : j.bq_bytes;
     const int nslot = M * nb + 1;
     _Float16 * b16 = (_Float16 *)smem;
     _Float16 * sbs = b16 + (size_t)nslot * QK_K;
     float * xd_s = (float *)(sbs + (size_t)nslot * 16);
-    float * relay = (float *)(smem + ((j.bq_bytes + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
+    float * relay = (float *)(smem + ((bqb + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
 
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
     const int r = lane & 15, kg = lane >> 4;
@@ -1122,9 +1130,9 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
 
     // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
     {
-        const int nck = (int)(j.bq_bytes >> 10);
+        const int nck = (int)(bqb >> 10);
         for (int i = wave; i < nck; i += nw)
-            __builtin_amdgcn_global_load_lds(gptr(j.bq + (size_t)i * 1024 + lane * 16),
+            __builtin_amdgcn_global_load_lds(gptr(bqt + (size_t)i * 1024 + lane * 16),
                                              (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
     }
     TTS_PIN_LOADS();
@@ -1133,14 +1141,28 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
         int64_t row = row0 + r;
         const int64_t rows_m = SW ? j.N : job_roff(j, mat + 1) - job_roff(j, mat);
         row = row < rows_m ? row : rows_m - 1;
-        const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
-        const int ri = (int)(row & 3);
+        if constexpr (LANE) {
+            const uint8_t * wr = j.W[mat] + row * j.w_row_bytes;
 #pragma unroll
-        for (int u = 0; u < BPW; ++u) {
-            const uint8_t * bp = wt + (int64_t)min(w * BPW + u, nb - 1) * 576;
-            hd[u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
-            qa[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-            qb[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+            for (int u = 0; u < BPW; ++u) {
+                const uint8_t * bp = wr + (int64_t)min(w * BPW + u, nb - 1) * 144;
+                hd[u] = TTS_WLOAD((const u32x4 *)bp);
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    qa[u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
+                    qb[u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
+                }
+            }
+        } else {
+            const uint8_t * wt = j.W[mat] + (row >> 2) * nb * 576;
+            const int ri = (int)(row & 3);
+#pragma unroll
+            for (int u = 0; u < BPW; ++u) {
+                const uint8_t * bp = wt + (int64_t)min(w * BPW + u, nb - 1) * 576;
+                hd[u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+                qa[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+                qb[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+            }
         }
     }
     TTS_PIN_LOADS();
@@ -1259,7 +1281,7 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int64_t flat = t * 16 + 4 * kg + q;
-                if (r < M && flat < NR) j.Y[0][r * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), tot[q]);
+                if (r < M && flat < NR) j.Y[0][(c0 + r) * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), tot[q]);
             }
         }
     } else {
@@ -1267,7 +1289,7 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
         for (int q = 0; q < 4; ++q) {
             const int64_t rr = row0 + 4 * kg + q;
             const int64_t rows_m = job_roff(j, mat + 1) - job_roff(j, mat);
-            if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, r, tot[q]);
+            if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, c0 + r, tot[q]);
         }
     }
 }
@@ -1888,6 +1910,7 @@ static void launch_gemv_q4k_mc(tts_hip_backend * be, const GemvJob & j) {
     const int nw_max = small ? 16 : 8;
     const int64_t G = ((int64_t)j.nmat * j.N + S - 1) / S;
     int64_t nw = (G + be->cus - 1) / be->cus;
+    if (nw < be->gemv_nw_min) nw = be->gemv_nw_min;  // fewer, fuller workgroups (TTS_HIP_OPT_GEMV_NW_MIN)
     if (j.pro == PRO_LN && nw < j.M) nw = j.M;
     nw = nw < 1 ? 1 : nw > nw_max ? nw_max : nw;
     int64_t gx = (G + nw - 1) / nw;
@@ -1928,8 +1951,11 @@ template <int PRO>
 __global__ __launch_bounds__(64) void k_quant_mf(GemvJob j) {
     const int m = blockIdx.y, lane = threadIdx.x, r = lane >> 4, t = lane & 15;
     const int nb = (int)(j.K / QK_K);
-    const int nslot = (int)j.M * nb + 1;
-    _Float16 * b16 = (_Float16 *)j.bq;
+    // column tiles of 16 (bq_tile > 0) each hold their own slot layout; otherwise one tile of M columns
+    const int ct = j.bq_tile ? m >> 4 : 0, lm = j.bq_tile ? m & 15 : m;
+    const int Mt = j.bq_tile ? min(16, (int)j.M - 16 * ct) : (int)j.M;
+    const int nslot = Mt * nb + 1;
+    _Float16 * b16 = (_Float16 *)(j.bq + (size_t)ct * j.bq_tile);
     _Float16 * sb = b16 + (size_t)nslot * QK_K;
     float * xd = (float *)(sb + (size_t)nslot * 16);
     const float * x = j.x + (int64_t)m * j.xcs;
@@ -1998,7 +2024,7 @@ __global__ __launch_bounds__(64) void k_quant_mf(GemvJob j) {
             for (int k = 0; k < 4; ++k) *(float4 *)(o + 4 * k) = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
         }
     }
-    const int slot = b < nb ? m * nb + b : nslot - 1;
+    const int slot = b < nb ? lm * nb + b : nslot - 1;
     q8k_row_block_mf(v, lane, b16 + (size_t)slot * QK_K, sb + (size_t)slot * 16, xd + slot);
 }
 
@@ -2081,20 +2107,62 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 
 // ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
-template <int BPW, bool SW, int NWT>
-static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx) {
+template <int BPW, bool SW, int NWT, bool LANE = false>
+static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT>);
-    const size_t lds = q4k_kr_lds(j.bq_bytes, SW);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE>);
+    const size_t lds = q4k_kr_lds(j.bq_tile ? j.bq_tile : j.bq_bytes, SW);
     const dim3 blk(64 * NWT * (SW ? 2 : 1));
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT>), dim3(gx), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT>), dim3(gx), blk, lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE>), dim3(gx, gy), blk, lds, be->stream, j);
+}
+
+// Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
+// (16-column tiles), then the K-relay kernel over (row tile, column tile) -- the same per-(row,
+// column) arithmetic as the GEMV, so bit-identical to ggml's order, in two launches instead of one
+// 8-column GEMV launch per 8 columns.  Lane-layout or tile-layout weights, K = 1024 x {1, 2, 3, 4}.
+static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job) {
+    if (!be->gemv_kr || !be->gemv_mf_prequant || job.wtype != TTS_TYPE_Q4_K || job.M <= 8 || job.epi == EPI_SWIGLU || job.dbg) return false;
+    if (job.pro != PRO_QUANT && job.pro != PRO_LN) return false;
+    if (job.pro == PRO_LN && job.K > 4 * 1024) return false;
+    const int64_t nb = job.K / QK_K;
+    if (nb != 4 && nb != 8 && nb != 12 && nb != 16) return false;
+    for (int m = 0; m <= job.nmat; ++m)
+        if (job_roff(job, m) % 16) return false;
+    const int64_t tile = (((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+    const int64_t nct = (job.M + 15) / 16;
+    if (q4k_kr_lds(tile, false) > 160 * 1024) return false;
+    if ((size_t)(tile * nct + 4 * job.K * job.M) > be->scratch_size || nct > 65535) return false;
+    GemvJob j = job;
+    j.bq_tile = tile;
+    j.bq_bytes = tile * nct;
+    j.bq = be->scratch + be->scratch_size - j.bq_bytes;
+    const dim3 qg((unsigned)((nb + 3) / 4), (unsigned)j.M);
+    if (j.pro == PRO_LN) hipLaunchKernelGGL(k_quant_mf<PRO_LN>, qg, dim3(64), 0, be->stream, j);
+    else hipLaunchKernelGGL(k_quant_mf<PRO_QUANT>, qg, dim3(64), 0, be->stream, j);
+    TTS_HIP_CHECK(hipGetLastError());
+    j.pro = PRO_COPY;
+    j.lnout = nullptr;
+    const unsigned gx = (unsigned)(job_rows(j) / 16), gy = (unsigned)nct;
+    auto go = [&](auto LANE) {
+        constexpr bool L = decltype(LANE)::value;
+        switch (nb) {
+            case 4: launch_q4k_kr_t<1, false, 4, L>(be, j, gx, gy); break;
+            case 8: launch_q4k_kr_t<2, false, 4, L>(be, j, gx, gy); break;
+            case 12: launch_q4k_kr_t<3, false, 4, L>(be, j, gx, gy); break;
+            default: launch_q4k_kr_t<4, false, 4, L>(be, j, gx, gy); break;
+        }
+    };
+    if (j.tiled) go(std::false_type{});
+    else go(std::true_type{});
+    TTS_HIP_CHECK(hipGetLastError());
+    return true;
 }
 // PRO_COPY jobs (operands in j.bq) whose row length has an instantiation; false otherwise
 static bool launch_q4k_kr(tts_hip_backend * be, const GemvJob & j) {
@@ -2346,6 +2414,7 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
         }
         return;
     }
+    if (job.M > 8 && launch_gemm_q4k_kr(be, job)) return;  // prefill: matrix-core GEMM over column tiles
     if (q4k_ks_eligible(be, job)) {
         launch_q4k_ks(be, job);
         TTS_HIP_CHECK(hipGetLastError());
