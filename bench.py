@@ -270,7 +270,8 @@ def orpheus_leg(be, args, rank):
                 "tokens_per_s": round(B * steps / dt, 1), "audio_sec_per_s": round(B * steps / dt / ORPHEUS_TOK_PER_AUDIO_S, 3),
                 "ms_per_step": round(1000 * dt / steps, 3), "graph_nodes": o.last_graph_nodes(),
                 "weight_bytes": o.weight_bytes(),
-                "roofline": {"bound": "hbm", "kernel": "k_gemv_q4K_mf (tile layout, >= 4 MiB) + k_gemv_q4_K",
+                "roofline": {"bound": "hbm", "kernel": "k_gemv_q4K_kr (K relay, tile layout, >= 4 MiB; its operand pass k_quant_mf "
+                                                      "not included) + k_gemv_q4_K (k / v lane layout)",
                              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                              "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(nbytes / max(launches, 1), 1),
                              "launches_sampled": launches}}

@@ -295,6 +295,8 @@ enum tts_hip_option {
                                      chain handed from wave to wave in block order); 0 = k_gemv_q4K_mf */
     TTS_HIP_OPT_ATTN_KS = 23,     /* split decode attention: 128 * value key positions per scores workgroup (1, 2 default, 4) */
     TTS_HIP_OPT_ATTN_PV8 = 24,    /* 1: the split P.V kernel covers 8 output dims per workgroup (twice the workgroups); 0 = 16 */
+    TTS_HIP_OPT_GEMV_KRELAY_LOOP = 26, /* 1 (default): K-relay SwiGLU launches with more tile pairs than CUs run one workgroup
+                                     per CU over its pairs (operands copied once, next pair prefetched); 0 = one per pair */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
 };

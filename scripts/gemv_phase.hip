@@ -46,6 +46,10 @@ int main() {
     be.gemv_unique = getenv("GEMV_UNIQUE") ? atoi(getenv("GEMV_UNIQUE")) : 1;
     if (getenv("GEMV_KS")) be.gemv_ks_tiles = atoi(getenv("GEMV_KS"));
     TTS_HIP_CHECK(hipStreamCreate(&be.stream));
+    be.scratch_size = (size_t)64 << 20;  // the operand pass (GEMV_PREQUANT) writes the top of scratch
+    TTS_HIP_CHECK(hipMalloc((void **)&be.scratch, be.scratch_size));
+    if (getenv("GEMV_PREQUANT")) be.gemv_mf_prequant = atoi(getenv("GEMV_PREQUANT"));
+    if (getenv("GEMV_KRELAY")) be.gemv_kr = atoi(getenv("GEMV_KRELAY"));
     std::mt19937 rng(1);
     const size_t wbytes = 3ull * 4096 * 4096 / 256 * 144;
     std::vector<uint8_t> hw(wbytes);

@@ -1097,9 +1097,14 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 // chunk c's dword at + 4 c -- the tile layout's piece dword for (c, l)), read as 8 dwords per block;
 // otherwise the 4-row tile layout.  blockIdx.y = column tile (j.bq_tile > 0: 16 columns per tile,
 // the many-column prefill GEMM).
-template <int BPW, bool SW, int NWT, bool LANE = false>
+// LOOP: a workgroup per CU walks tiles t = blockIdx.x + k * gridDim.x (the operands are copied once,
+// the next tile's weights are requested before the current tile's relay); otherwise one tile per
+// workgroup.  Terms and running sums are kept as row pairs (packed f32 ops, each element still one
+// rounded multiply / add).
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false>
 __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
     constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
+    typedef float f2v __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
     const int ct = blockIdx.y;                 // column tile
@@ -1118,16 +1123,17 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     const int cc = r < M ? r : M - 1;
     const int sub = SW ? wave / nwt : 0;    // SwiGLU: 0 = gate tile, 1 = up tile
     const int w = wave - sub * nwt;         // position in the relay
-    const int64_t t = blockIdx.x;           // the tile (pair)
     const int64_t NR = SW ? j.N : job_rows(j);
+    const int64_t T = NR / 16;              // launcher: whole tiles
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
         while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
         return mt;
     };
-    const int mat = __builtin_amdgcn_readfirstlane(SW ? sub : mat_of(t * 16));
-    const int64_t row0 = SW ? t * 16 : t * 16 - job_roff(j, mat);  // the tile's first row in its matrix
+    auto tile_mat = [&](int64_t t) { return __builtin_amdgcn_readfirstlane(SW ? sub : mat_of(t * 16)); };
+    auto tile_row0 = [&](int64_t t, int mat) { return SW ? t * 16 : t * 16 - job_roff(j, mat); };
 
+    TTS_TS(j, 0);
     // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
     {
         const int nck = (int)(bqb >> 10);
@@ -1136,9 +1142,12 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
                                              (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
     }
     TTS_PIN_LOADS();
-    u32x4 hd[BPW], qa[BPW], qb[BPW];
-    {
-        int64_t row = row0 + r;
+    u32x4 hd[LOOP ? 2 : 1][BPW], qa[LOOP ? 2 : 1][BPW], qb[LOOP ? 2 : 1][BPW];
+    auto load_w = [&](auto BUF, int64_t t) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
+        t = t < T ? t : T - 1;
+        const int mat = tile_mat(t);
+        int64_t row = tile_row0(t, mat) + r;
         const int64_t rows_m = SW ? j.N : job_roff(j, mat + 1) - job_roff(j, mat);
         row = row < rows_m ? row : rows_m - 1;
         if constexpr (LANE) {
@@ -1146,11 +1155,11 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
 #pragma unroll
             for (int u = 0; u < BPW; ++u) {
                 const uint8_t * bp = wr + (int64_t)min(w * BPW + u, nb - 1) * 144;
-                hd[u] = TTS_WLOAD((const u32x4 *)bp);
+                hd[bf][u] = TTS_WLOAD((const u32x4 *)bp);
 #pragma unroll
                 for (int l = 0; l < 4; ++l) {
-                    qa[u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
-                    qb[u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
+                    qa[bf][u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
+                    qb[bf][u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
                 }
             }
         } else {
@@ -1159,139 +1168,181 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
 #pragma unroll
             for (int u = 0; u < BPW; ++u) {
                 const uint8_t * bp = wt + (int64_t)min(w * BPW + u, nb - 1) * 576;
-                hd[u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
-                qa[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-                qb[u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+                hd[bf][u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
+                qa[bf][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+                qb[bf][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
             }
         }
-    }
-    TTS_PIN_LOADS();
+        TTS_PIN_LOADS();
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, LOOP ? 1 : 0>;
+    int64_t t = blockIdx.x;
+    load_w(B0{}, t);
+    TTS_TS(j, 1);
     __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
+    TTS_TS(j, 2);
 
-    // the terms of this wave's blocks: tp[u][l][q], tq[u][q] for rows 4kg + q, column r
-    float tp[BPW][8][4], tq[BPW][4];
+    // the terms of this wave's blocks for rows 4kg + q (pairs h: q = 2h, 2h + 1), column r
+    f2v tp[BPW][8][2], tq[BPW][2];
+    auto terms = [&](auto BUF) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
 #pragma unroll
-    for (int u = 0; u < BPW; ++u) {
-        const int b = min(w * BPW + u, nb - 1);
-        const u32x4 h = hd[u];
-        const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
-        const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
-        const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
-        const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
-        const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
-        const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
-        const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
-        const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
-        const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8;
-        f32x4 acc[8];
+        for (int u = 0; u < BPW; ++u) {
+            const int b = min(w * BPW + u, nb - 1);
+            const u32x4 h = hd[bf][u];
+            const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
+            const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+            const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+            const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
+            const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
+            const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
+            const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
+            const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
+            const _Float16 * bsl = b16 + (size_t)(cc * nb + b) * QK_K + kg * 8;
+            f32x4 acc[8];
 #pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const uint32_t D = l < 4 ? qa[u][l & 3] : qb[u][l & 3];
-            const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
-            const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
-            const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
-            const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
-            const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
-            const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
-            const f16x8 B = *(const f16x8 *)(bsl + l * 32);
-            acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        }
-        const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
-        const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
-        const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
-        const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
-        const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
-        const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
-        const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
-        const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
-        const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        const float yd = xd_s[cc * nb + b];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
-            const float dy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
-            const float dmy = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
-#pragma unroll
-            for (int l = 0; l < 8; ++l) tp[u][l][q] = __fmul_rn(dy, acc[l][q]);
-            tq[u][q] = __fmul_rn(dmy, si[q]);
-        }
-    }
-
-    // the relay: wave w' folds its blocks into the running sums in block order, then hands them on
-    float sums[8][4], sumf[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        sumf[q] = 0.f;
-#pragma unroll
-        for (int l = 0; l < 8; ++l) sums[l][q] = 0.f;
-    }
-    float * rl = relay + ((size_t)sub * 64 + lane) * 36;
-    const int nblk = nb - w * BPW < BPW ? nb - w * BPW : BPW;  // the last wave may own fewer blocks
-    for (int step = 0; step < nwt; ++step) {
-        if (step == w) {
-            if (w > 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const float4 a = *(const float4 *)(rl + 8 * q), c = *(const float4 *)(rl + 8 * q + 4);
-                    sums[0][q] = a.x, sums[1][q] = a.y, sums[2][q] = a.z, sums[3][q] = a.w;
-                    sums[4][q] = c.x, sums[5][q] = c.y, sums[6][q] = c.z, sums[7][q] = c.w;
-                }
-                const float4 f = *(const float4 *)(rl + 32);
-                sumf[0] = f.x, sumf[1] = f.y, sumf[2] = f.z, sumf[3] = f.w;
+            for (int l = 0; l < 8; ++l) {
+                const uint32_t D = l < 4 ? qa[bf][u][l & 3] : qb[bf][u][l & 3];
+                const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+                const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
+                const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
+                const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
+                const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
+                const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+                const f16x8 B = *(const f16x8 *)(bsl + l * 32);
+                acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             }
-#pragma unroll
-            for (int u = 0; u < BPW; ++u) {
-                if (u >= nblk) break;  // wave-uniform
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-#pragma unroll
-                    for (int l = 0; l < 8; ++l) sums[l][q] = __fadd_rn(sums[l][q], tp[u][l][q]);
-                    sumf[q] = __fsub_rn(sumf[q], tq[u][q]);
-                }
-            }
-            if (w < nwt - 1) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    *(float4 *)(rl + 8 * q) = make_float4(sums[0][q], sums[1][q], sums[2][q], sums[3][q]);
-                    *(float4 *)(rl + 8 * q + 4) = make_float4(sums[4][q], sums[5][q], sums[6][q], sums[7][q]);
-                }
-                *(float4 *)(rl + 32) = make_float4(sumf[0], sumf[1], sumf[2], sumf[3]);
-            }
-        }
-        if (step < nwt - 1) __syncthreads();
-    }
-    if (w != nwt - 1) {
-        if (SW) __syncthreads();  // the gate / up exchange below
-        return;
-    }
-    float tot[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        tot[q] = sumf[q];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) tot[q] = __fadd_rn(tot[q], sums[l][q]);
-    }
-    if constexpr (SW) {  // out = silu(gate) * up, by the up tile's last wave
-        float * xg = relay + 2 * 64 * 36;  // [64 lanes][4] after both relays
-        if (sub == 0) *(float4 *)(xg + lane * 4) = make_float4(tot[0], tot[1], tot[2], tot[3]);
-        __syncthreads();
-        if (sub == 1) {
-            const float4 g4 = *(const float4 *)(xg + lane * 4);
-            const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+            const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
+            const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
+            const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
+            const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
+            const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+            const f16x8 Bs = *(const f16x8 *)(sbs + (size_t)(cc * nb + b) * 16 + (kg & 1) * 8);
+            const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            const float yd = xd_s[cc * nb + b];
+            float dy[4], dmy[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int64_t flat = t * 16 + 4 * kg + q;
-                if (r < M && flat < NR) j.Y[0][(c0 + r) * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), tot[q]);
+                const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
+                dy[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+                dmy[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+            }
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const f2v d2 = {dy[2 * hq], dy[2 * hq + 1]}, dm2 = {dmy[2 * hq], dmy[2 * hq + 1]};
+#pragma unroll
+                for (int l = 0; l < 8; ++l) tp[u][l][hq] = d2 * f2v{acc[l][2 * hq], acc[l][2 * hq + 1]};
+                tq[u][hq] = dm2 * f2v{si[2 * hq], si[2 * hq + 1]};
             }
         }
-    } else {
+    };
+
+    // the relay: wave w' folds its blocks into the running sums in block order, hands them on; the
+    // last wave of the relay adds sumf + sums[0..7] and stores
+    float * rl = relay + ((size_t)sub * 64 + lane) * 36;
+    const int nblk = nb - w * BPW < BPW ? nb - w * BPW : BPW;  // the last wave may own fewer blocks
+    auto relay_store = [&](int64_t tt) __attribute__((always_inline)) {
+        f2v sums[8][2], sumf[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int64_t rr = row0 + 4 * kg + q;
-            const int64_t rows_m = job_roff(j, mat + 1) - job_roff(j, mat);
-            if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, c0 + r, tot[q]);
+        for (int hq = 0; hq < 2; ++hq) {
+            sumf[hq] = f2v{0.f, 0.f};
+#pragma unroll
+            for (int l = 0; l < 8; ++l) sums[l][hq] = f2v{0.f, 0.f};
         }
+        for (int step = 0; step < nwt; ++step) {
+            if (step == w) {
+                if (w > 0) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {  // sums[2k], sums[2k + 1]: 4 floats
+                        const float4 a = *(const float4 *)(rl + 4 * k);
+                        const float4 c = *(const float4 *)(rl + 16 + 4 * k);
+                        sums[2 * k][0] = f2v{a.x, a.y}, sums[2 * k][1] = f2v{a.z, a.w};
+                        sums[2 * k + 1][0] = f2v{c.x, c.y}, sums[2 * k + 1][1] = f2v{c.z, c.w};
+                    }
+                    const float4 f = *(const float4 *)(rl + 32);
+                    sumf[0] = f2v{f.x, f.y}, sumf[1] = f2v{f.z, f.w};
+                }
+#pragma unroll
+                for (int u = 0; u < BPW; ++u) {
+                    if (u >= nblk) break;  // wave-uniform
+#pragma unroll
+                    for (int hq = 0; hq < 2; ++hq) {
+#pragma unroll
+                        for (int l = 0; l < 8; ++l) sums[l][hq] = sums[l][hq] + tp[u][l][hq];
+                        sumf[hq] = sumf[hq] - tq[u][hq];
+                    }
+                }
+                if (w < nwt - 1) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        *(float4 *)(rl + 4 * k) = make_float4(sums[2 * k][0].x, sums[2 * k][0].y, sums[2 * k][1].x, sums[2 * k][1].y);
+                        *(float4 *)(rl + 16 + 4 * k) =
+                            make_float4(sums[2 * k + 1][0].x, sums[2 * k + 1][0].y, sums[2 * k + 1][1].x, sums[2 * k + 1][1].y);
+                    }
+                    *(float4 *)(rl + 32) = make_float4(sumf[0].x, sumf[0].y, sumf[1].x, sumf[1].y);
+                }
+            }
+            if (step < nwt - 1) __syncthreads();
+        }
+        float tot[4];
+        if (w == nwt - 1) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                tot[q] = sumf[q >> 1][q & 1];
+#pragma unroll
+                for (int l = 0; l < 8; ++l) tot[q] = __fadd_rn(tot[q], sums[l][q >> 1][q & 1]);
+            }
+        }
+        if constexpr (SW) {  // out = silu(gate) * up, by the up tile's last wave
+            float * xg = relay + 2 * 64 * 36;  // [64 lanes][4] after both relays
+            if (w == nwt - 1 && sub == 0) *(float4 *)(xg + lane * 4) = make_float4(tot[0], tot[1], tot[2], tot[3]);
+            __syncthreads();
+            if (w == nwt - 1 && sub == 1) {
+                const float4 g4 = *(const float4 *)(xg + lane * 4);
+                const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int64_t flat = tt * 16 + 4 * kg + q;
+                    if (r < M && flat < NR) j.Y[0][(c0 + r) * j.ycs[0] + flat * j.yrs[0]] = __fmul_rn(dev_silu(gv[q]), tot[q]);
+                }
+            }
+        } else if (w == nwt - 1) {
+            const int mat = tile_mat(tt);
+            const int64_t row0 = tile_row0(tt, mat);
+            const int64_t rows_m = job_roff(j, mat + 1) - job_roff(j, mat);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int64_t rr = row0 + 4 * kg + q;
+                if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, c0 + r, tot[q]);
+            }
+        }
+    };
+
+    if constexpr (LOOP) {
+        const int64_t G = gridDim.x;
+        for (; t < T; t += 2 * G) {
+            terms(B0{});
+            load_w(B1{}, t + G);  // clamped: the loads are unconditional
+            TTS_TS(j, 3);
+            relay_store(t);
+            TTS_TS(j, 4);
+            __syncthreads();  // the relay buffer is reused by the next tile
+            if (t + G >= T) break;
+            terms(B1{});
+            load_w(B0{}, t + 2 * G);
+            relay_store(t + G);
+            __syncthreads();
+        }
+    } else {
+        terms(B0{});
+        TTS_TS(j, 3);
+        relay_store(t);
+        TTS_TS(j, 4);
     }
+    TTS_TS(j, 5);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2107,20 +2158,28 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 
 // ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
-template <int BPW, bool SW, int NWT, bool LANE = false>
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false>
 static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
+    if constexpr (SW && !LOOP && BPW <= 3) {  // (BPW 4: the prefetch registers would spill)
+        // SwiGLU pairs (8 waves, ~170 VGPRs: one workgroup per CU): more pairs than CUs run as one
+        // workgroup per CU walking its pairs, operands copied once, the next pair's weights prefetched
+        if (be->gemv_kr_loop && gx > (unsigned)be->cus && gy == 1) {
+            launch_q4k_kr_t<BPW, SW, NWT, LANE, true>(be, j, (unsigned)be->cus, gy);
+            return;
+        }
+    }
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE>);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>);
     const size_t lds = q4k_kr_lds(j.bq_tile ? j.bq_tile : j.bq_bytes, SW);
     const dim3 blk(64 * NWT * (SW ? 2 : 1));
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE>), dim3(gx, gy), blk, lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>), dim3(gx, gy), blk, lds, be->stream, j);
 }
 
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
