@@ -37,6 +37,8 @@ HEADS = 9
 HBM_PEAK_GBS = 8000.0           # MI355X spec (MI355X_MICROARCH.md chip table)
 # offline rocprofv3 --pmc result (scripts/gpu_pmc.sh): the newest round's
 PMC_FILE = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k.json"), default=ROOT / "profiles" / "r01" / "pmc_gemv_q4k.json")
+# PMC traffic of the Orpheus leg's matrix-core GEMV (scripts/gpu_pmc_orpheus.sh), newest round first
+PMC_FILE_ORPH = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k_kr_orpheus.json"), default=None)
 
 HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), token ids derived from bytes
     "The birch canoe slid on the smooth planks.",
@@ -274,7 +276,9 @@ def orpheus_leg(be, args, rank):
                                                       "not included) + k_gemv_q4_K (k / v lane layout)",
                              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                              "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(nbytes / max(launches, 1), 1),
-                             "launches_sampled": launches}}
+                             "launches_sampled": launches,
+                             "traffic_kr": (json.loads(PMC_FILE_ORPH.read_text()).get("hbm_bytes_per_launch") if PMC_FILE_ORPH else None),
+                             "traffic_source": str(PMC_FILE_ORPH.relative_to(ROOT)) if PMC_FILE_ORPH else None}}
     finally:
         o.close()
 
