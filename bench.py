@@ -422,6 +422,9 @@ def main():
     ap.add_argument("--attn-ks", type=int, default=None, help="TTS_HIP_OPT_ATTN_KS: 128 * value key positions per split-scores workgroup")
     ap.add_argument("--attn-pv8", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV8: 8 output dims per split P.V workgroup (1) or 16 (0)")
     ap.add_argument("--gemv-krelay", type=int, default=None, help="TTS_HIP_OPT_GEMV_KRELAY: K-relay matrix-core GEMV / prefill GEMM (1) or not (0)")
+    ap.add_argument("--gemv-q80-pro", type=int, default=None, help="TTS_HIP_OPT_GEMV_Q80_PRO: Q8_0 GEMVs of <= 8 columns quantize / normalize in every workgroup")
+    ap.add_argument("--gemv-q80-slab", type=int, default=None, help="TTS_HIP_OPT_GEMV_Q80_SLAB: slab-form Q8_0 GEMV (1) or the row-block kernel (0)")
+    ap.add_argument("--gemv-q80-rw", type=int, default=None, help="TTS_HIP_OPT_GEMV_Q80_RW: rows per slab Q8_0 GEMV workgroup (0 = auto)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
@@ -469,6 +472,12 @@ def main():
             rb.set_option(ttship.OPT["GEMV_KRELAY"], args.gemv_krelay)
         if args.gemv_nw_min is not None:
             rb.set_option(ttship.OPT["GEMV_NW_MIN"], args.gemv_nw_min)
+        if args.gemv_q80_pro is not None:
+            rb.set_option(ttship.OPT["GEMV_Q80_PRO"], args.gemv_q80_pro)
+        if args.gemv_q80_slab is not None:
+            rb.set_option(ttship.OPT["GEMV_Q80_SLAB"], args.gemv_q80_slab)
+        if args.gemv_q80_rw is not None:
+            rb.set_option(ttship.OPT["GEMV_Q80_RW"], args.gemv_q80_rw)
         if args.attn_ks is not None:
             rb.set_option(ttship.OPT["ATTN_KS"], args.attn_ks)
         if args.attn_pv8 is not None:

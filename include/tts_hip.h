@@ -297,6 +297,13 @@ enum tts_hip_option {
     TTS_HIP_OPT_ATTN_PV8 = 24,    /* 1: the split P.V kernel covers 8 output dims per workgroup (twice the workgroups); 0 = 16 */
     TTS_HIP_OPT_GEMV_KRELAY_LOOP = 26, /* 1 (default): K-relay SwiGLU launches with more tile pairs than CUs run one workgroup
                                      per CU over its pairs (operands copied once, next pair prefetched); 0 = one per pair */
+    TTS_HIP_OPT_GEMV_Q80_PRO = 27, /* 1 (default): Q8_0 GEMVs of <= 8 columns with K % 256 == 0 quantize (and, fused with a
+                                     preceding LayerNorm / RMSNorm of K <= 4096, normalize) the activation in every
+                                     workgroup: one launch instead of norm + quantize + GEMV; 0 = separate launches */
+    TTS_HIP_OPT_GEMV_Q80_SLAB = 28, /* 1 (default): Q8_0 GEMVs with K % 256 == 0 run the slab kernel (a workgroup's rows
+                                     fetched whole by LDS-DMA, terms then ggml's block-order chain from LDS);
+                                     0 = the (row, block)-per-thread kernel */
+    TTS_HIP_OPT_GEMV_Q80_RW = 29,  /* slab Q8_0 GEMV rows per workgroup (0 = auto: the most that still fills every CU) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
 };

@@ -65,6 +65,17 @@ case "$1" in
       n=$(echo $cfg | tr -d ' -')
       timeout -k 10 200 python3 bench.py $AR $cfg > "$O/at_$n.log" 2>&1 && ar_line "$O/at_$n.log" "$cfg" || exit 1
     done ;;
+  dia)         # Dia leg only (100 CFG steps), one bench run per option set, e.g. dia "--gemv-q80-pro 0" "--gemv-q80-pro 1"
+    shift
+    for cfg in "$@"; do
+      n=$(echo $cfg | tr -d ' -')
+      timeout -k 10 300 python3 bench.py --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --orpheus-steps 0 --no-cpu-baseline --b1-replicas 0 --dia-steps 100 $cfg > "$O/dia_$n.log" 2>&1 &&
+      python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['dia'];print(sys.argv[2], d['ms_per_step'], d['encoder_step_ms'])" "$O/dia_$n.log" "$cfg" || exit 1
+    done ;;
+  dia_trace)   # kernel trace of the Dia leg + per-step breakdown (markers: the greedy step)
+    shift
+    (cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/profdia" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --orpheus-steps 0 --no-cpu-baseline --b1-replicas 0 --dia-steps 40 "$@" > "$O/dia_trace.log" 2>&1) &&
+    f=$(find "$O/profdia" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 3 25 - k_greedy_step > "$O/dia_breakdown.txt" && cut -c1-150 "$O/dia_breakdown.txt" ;;
   tests)       # selected GPU test files, e.g. scripts/gpu_study.sh tests tests/test_dia_gpu.py
     shift
     timeout -k 10 900 python -u -m pytest "$@" $T > "$O/tests.log" 2>&1; rc=$?; tail -3 "$O/tests.log"; exit $rc ;;
@@ -73,5 +84,5 @@ case "$1" in
   mfma_f64)    # the f64 MFMA ceiling
     hipcc --offload-arch=gfx950 -O3 scripts/mfma_f64_peak.hip -o build/mfma_f64_peak && timeout -k 10 120 build/mfma_f64_peak > "$O/mfma_f64.log" 2>&1 && cat "$O/mfma_f64.log" ;;
   *)
-    echo "usage: $0 {ar|ar_trace|orph_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
+    echo "usage: $0 {ar|ar_trace|orph_trace|dia|dia_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
 esac

@@ -95,3 +95,33 @@ def test_dia_full_depth_long_dialogue(hip):
     text = dialogue(1000)
     assert len(text) == 1000
     run_pair(hip, dict(max_generation_size=80), 64, text=text)
+
+
+@pytest.mark.gpu
+def test_dia_q80_paths_bit_identical(hip):
+    """Dia's decode GEMVs (Q8_0, 2 CFG columns) on every Q8_0 path: the (row, block)-per-thread kernel
+    after separate norm + quantize launches (the reference point), the slab kernel after them, and the
+    slab kernel quantizing -- after the RMS norms, normalizing -- the activation inside every workgroup
+    (TTS_HIP_OPT_GEMV_Q80_PRO / _SLAB, the defaults).  Same arithmetic, so every logit is bit-identical."""
+    text = np.frombuffer(b"\x01 The birch canoe slid on the smooth planks.", dtype=np.uint8).astype(np.int32)
+    lib = ttship.lib()
+    outs = []
+    for pro, slab in ((0, 0), (0, 1), (1, 1), (1, 0)):
+        assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], pro) == 0
+        assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], slab) == 0
+        g = ttship.Dia(hip.iface(), ttship.dia_config(**WIDE))
+        try:
+            audio = np.full(9, 1026, dtype=np.int32)
+            seq = []
+            for s in range(4):
+                lg = g.prefill(text, audio) if s == 0 else g.decode(audio)
+                seq.append(lg.copy())
+                audio = lg.argmax(axis=1).astype(np.int32)
+            outs.append(seq)
+        finally:
+            g.close()
+            lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], 1)
+            lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], 1)
+    for c in range(1, len(outs)):
+        for s, (a, b) in enumerate(zip(outs[0], outs[c])):
+            assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (c, s, np.abs(a - b).max())

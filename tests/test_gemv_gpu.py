@@ -76,17 +76,39 @@ def test_q4_K_prefill_gemm(hip, tiled, K, N, M):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
 
 
+Q80_PATHS = {"slab_pro": (1, 1, 0), "slab": (1, 0, 0), "rows_pro": (0, 1, 0), "rows": (0, 0, 0), "slab_rw1": (1, 1, 1),
+             "slab_rw32": (1, 0, 32)}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("K,N", [(2048, 2048), (2048, 512), (8192, 64), (1024, 1024), (64, 7)])
-@pytest.mark.parametrize("M", [1, 2, 8, 9, 64, 300])
-def test_q8_0(hip, K, N, M):
-    """M > 8: the int8 matrix-core GEMM (k_gemm_q8_0): per-block exact int dots, ggml's f32 chain."""
-    rng = np.random.default_rng(K + N * 3 + M)
-    w = helpers.rand_q8_0(rng, N, K)
-    x = rng.standard_normal((M, K)).astype(np.float32)
-    ref = py_oracle.gemv(ttship.Q8_0, w, x, N)
-    got = run_gpu(hip, ttship.Q8_0, w, x, N)
-    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()  # exact ggml order
+@pytest.mark.parametrize("path", list(Q80_PATHS))
+@pytest.mark.parametrize("K,N", [(2048, 2048), (2048, 512), (8192, 64), (1024, 1024), (64, 7), (768, 33), (4096, 1000)])
+@pytest.mark.parametrize("M", [1, 2, 3, 8, 9, 64, 300])
+def test_q8_0(hip, path, K, N, M):
+    """M > 8: the int8 matrix-core GEMM (k_gemm_q8_0): per-block exact int dots, ggml's f32 chain.
+    M <= 8, K % 256 == 0: the slab kernel (TTS_HIP_OPT_GEMV_Q80_SLAB = 1; rows per workgroup auto, 1 or
+    32, partial last workgroups) or the (row, block)-per-thread kernel, each with the activation quantized
+    to Q8_0 inside every workgroup (TTS_HIP_OPT_GEMV_Q80_PRO = 1: quantize_row_q8_0 per 32 elements) or by
+    the separate quantize launch."""
+    slab, pro, rw = Q80_PATHS[path]
+    if M > 8 and path != "slab_pro":
+        pytest.skip("M > 8 runs the matrix-core GEMM on every path")
+    lib = ttship.lib()
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], pro) == 0
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], slab) == 0
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_RW"], rw) == 0
+    try:
+        rng = np.random.default_rng(K + N * 3 + M)
+        w = helpers.rand_q8_0(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        x[0, :32] = 0.0  # an all-zero block: d = 0, id = 0
+        ref = py_oracle.gemv(ttship.Q8_0, w, x, N)
+        got = run_gpu(hip, ttship.Q8_0, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()  # exact ggml order
+    finally:
+        lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], 1)
+        lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], 1)
+        lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_RW"], 0)
 
 
 @pytest.mark.gpu

@@ -499,6 +499,12 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_GEMV_PREQUANT: be->gemv_mf_prequant = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KRELAY: be->gemv_kr = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KRELAY_LOOP: be->gemv_kr_loop = value != 0; return 0;
+        case TTS_HIP_OPT_GEMV_Q80_PRO: be->gemv_q80_pro = value != 0; return 0;
+        case TTS_HIP_OPT_GEMV_Q80_SLAB: be->gemv_q80_slab = value != 0; return 0;
+        case TTS_HIP_OPT_GEMV_Q80_RW:
+            if (value < 0 || value > 32 || (value & (value - 1))) return TTS_STATUS_BAD_ARG;
+            be->gemv_q80_rw = value;
+            return 0;
         case TTS_HIP_OPT_ATTN_KS: be->attn_ks = value; return 0;
         case TTS_HIP_OPT_GEMV_NW_MIN: be->gemv_nw_min = value; return 0;
         case TTS_HIP_OPT_ATTN_PV8: be->attn_pv8 = value != 0; return 0;

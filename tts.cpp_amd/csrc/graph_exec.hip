@@ -272,6 +272,7 @@ struct Planner {
     std::vector<Item> items;
     std::deque<tts_tensor> derived;  // strided stand-ins for folded CONT nodes (stable addresses)
     int mask = 0xFF;
+    bool q80pro = true;  // Q8_0 GEMVs of <= 8 columns take LN prologues too (TTS_HIP_OPT_GEMV_Q80_PRO)
     float * lstm_buf = nullptr;  // backend scratch for fused LSTM chains (hidden history + cell)
     size_t vec_cap = 0;          // floats of the backend's vector scratch (fused AdaIN staging)
     float * conv_stage = nullptr;  // backend scratch for fused conv outputs that cannot stage in their im2col buffer
@@ -434,9 +435,9 @@ struct Planner {
         }
     }
 
-    // An LN item directly followed by the Q4_K GEMV item that reads its output becomes that
-    // GEMV's prologue (every workgroup normalizes + quantizes the activation itself; workgroup 0
-    // still writes the LN output tensor).
+    // An LN item directly followed by the Q4_K GEMV item (or Q8_0 GEMV item of <= 8 columns) that
+    // reads its output becomes that GEMV's prologue (every workgroup normalizes + quantizes the
+    // activation itself; workgroup 0 still writes the LN output tensor).
     void fuse_ln_into_gemv() {
         for (int i = 0; i < n; ++i) {
             const int a = act[i];
@@ -445,7 +446,10 @@ struct Planner {
             if (nx < 0 || act[nx] <= 0) continue;
             Item & L = items[a - 1];
             Item & G = items[act[nx] - 1];
-            if (G.kind != Item::GEMV || G.ln || G.mms[0]->src[0]->type != TTS_TYPE_Q4_K || G.mms[0]->src[1] != L.dst) continue;
+            if (G.kind != Item::GEMV || G.ln || G.mms[0]->src[1] != L.dst) continue;
+            const int wt = G.mms[0]->src[0]->type;
+            const tts_tensor * B = G.mms[0]->src[1];
+            if (wt != TTS_TYPE_Q4_K && !(wt == TTS_TYPE_Q8_0 && q80pro && B->ne[1] * B->ne[2] * B->ne[3] <= 8)) continue;
             const int64_t K = L.dst->ne[0];
             if (K % 256 || K > 4096) continue;
             if (((uintptr_t)L.w->data & 15) || (L.b && ((uintptr_t)L.b->data & 15)) || (L.dst->nb[1] & 15)) continue;
@@ -1781,7 +1785,9 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         j.res = (const float *)it.res->data;
         j.rcs = (int64_t)(it.res->nb[1] / 4);
     }
-    if (j.wtype == TTS_TYPE_Q4_K) {
+    // Q8_0 with <= 8 columns (K % 256 == 0): the same prologue, writing Q8_0 blocks (k_gemv_q8_0<MC, PRO>)
+    const bool q80pro = j.wtype == TTS_TYPE_Q8_0 && j.K % QK_K == 0 && j.M <= 8 && (it.ln || be->gemv_q80_pro);
+    if (j.wtype == TTS_TYPE_Q4_K || q80pro) {
         // the kernel quantizes (and normalizes) src1 itself in every workgroup
         j.pro = it.ln ? PRO_LN : PRO_QUANT;
         j.tiled = (a0->flags & TTS_FLAG_TILED) ? 1 : 0;
@@ -1828,6 +1834,7 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             j.xcs = j.K;
         }
     } else {
+        if (it.ln) return TTS_STATUS_UNSUPPORTED;  // planner invariant: a fused LN always runs as a prologue
         int st = prepare_act(be, j.wtype, b, j.K, j.M, j.aq);
         if (st) return st;
     }
@@ -2156,6 +2163,7 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     const auto tp0 = std::chrono::steady_clock::now();
     Planner pl;
     pl.mask = be->fusion;
+    pl.q80pro = be->gemv_q80_pro != 0;
     pl.lstm_buf = be->lstm_buf;
     pl.lstm_cap = be->lstm_floats;
     pl.vec_cap = be->vec_scratch ? (1u << 18) : 0;
@@ -2263,7 +2271,8 @@ extern "C" int tts_hip_gemv_ex(tts_hip_backend_t be, int type, const void * w, c
     j.yrs[0] = 1;
     j.x = x;
     j.xcs = K;
-    if (type == TTS_TYPE_Q4_K) {
+    const bool q80pro = type == TTS_TYPE_Q8_0 && K % QK_K == 0 && M <= 8 && be->gemv_q80_pro;
+    if (type == TTS_TYPE_Q4_K || q80pro) {
         j.pro = PRO_QUANT;
         j.tiled = (wflags & TTS_FLAG_TILED) ? 1 : 0;
         if ((uintptr_t)x & 15) {  // the prologue reads 16-B vectors

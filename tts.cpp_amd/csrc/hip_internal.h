@@ -305,6 +305,9 @@ struct tts_hip_backend {
     int gemv_mf_prequant = 1;  // TTS_HIP_OPT_GEMV_PREQUANT
     int gemv_kr = 1;           // TTS_HIP_OPT_GEMV_KRELAY
     int gemv_kr_loop = 1;      // TTS_HIP_OPT_GEMV_KRELAY_LOOP
+    int gemv_q80_pro = 1;      // TTS_HIP_OPT_GEMV_Q80_PRO
+    int gemv_q80_slab = 1;     // TTS_HIP_OPT_GEMV_Q80_SLAB
+    int gemv_q80_rw = 0;       // TTS_HIP_OPT_GEMV_Q80_RW
     int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a

@@ -254,6 +254,29 @@ __device__ __forceinline__ void q8k_row_block_mf(const float (&v)[16], int lane,
     if (t == 0) *xd = d;
 }
 
+// quantize_row_q8_0 (k_quantize_q8_0's arithmetic) of the 16 elements a lane holds: lanes 2k and 2k+1
+// hold one 32-element block (amax by DPP over the pair); int8 values to xq (elements 16t .. 16t+15 of
+// the 256-element chunk), the fp16-rounded d of block t/2 to xd[t/2].
+__device__ __forceinline__ void q80_row_block(const float (&v)[16], int lane, int8_t * xq, float * xd) {
+    const int t = lane & 15;
+    float a = 0.f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) a = fmaxf(a, fabsf(v[e]));
+    a = fmaxf(a, dpp_f32<DPP_XOR1>(a));
+    const float d = cr_divf(a, 127.f);
+    const float id = d != 0.f ? cr_divf(1.f, d) : 0.f;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t u = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) u |= ((uint32_t)(int)roundf(__fmul_rn(v[4 * k + e], id)) & 0xFFu) << (8 * e);
+        w[k] = u;
+    }
+    *(uint4 *)(xq + 16 * t) = make_uint4(w[0], w[1], w[2], w[3]);
+    if ((t & 1) == 0) xd[t >> 1] = __half2float(__float2half_rn(d));
+}
+
 // Loads are unconditional (addresses clamped into range) so that a wave issues all of them before
 // the first use: a load under a guard is sunk next to its use, and every block then pays a full
 // L2 round trip (measured: 0.4 us per block).  The launcher guarantees 16-B aligned x / lnw / lnb
@@ -282,7 +305,7 @@ struct ProOv {
     int slot0 = 0;                // first output slot
     int trash = -1;               // slot absorbing padding writes (-1: M * nb)
 };
-template <int PRO, int NCH, bool MF = false, typename Mid = NoMid>
+template <int PRO, int NCH, bool MF = false, typename Mid = NoMid, bool Q80 = false>
 __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s,
                                              _Float16 * mf_b16 = nullptr, _Float16 * mf_sb = nullptr, Mid mid = Mid{},
                                              ProOv ov = ProOv{}) {
@@ -300,7 +323,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
     const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
     auto put = [&](const float (&v)[16], int lane, int slot) {
         slot = slot == trash ? (ov.trash >= 0 ? ov.trash : slot) : ov.slot0 + slot;
-        if constexpr (MF) q8k_row_block_mf(v, lane, mf_b16 + (int64_t)slot * QK_K, mf_sb + slot * 16, xd_s + slot);
+        if constexpr (Q80) q80_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + (int64_t)slot * (QK_K / QK8_0));
+        else if constexpr (MF) q8k_row_block_mf(v, lane, mf_b16 + (int64_t)slot * QK_K, mf_sb + slot * 16, xd_s + slot);
         else q8k_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
     };
     if (PRO == PRO_QUANT) {
@@ -1633,7 +1657,11 @@ void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnA
 // blocks in ascending order, sumf += (float)sumi * (d_w * d_x).  Phase 1: a thread per
 // (row, block) computes the exact int dots for every column -> LDS; phase 2: a lane per
 // (row, column) folds its blocks in order.
-template <int MC>
+// PRO (PRO_QUANT / PRO_LN): the workgroup quantizes (after RMS / LayerNorm) the f32 activation itself
+// (q4k_prologue with Q8_0 output: quantize_row_q8_0 per 32 elements, K % 256 == 0), with this thread's
+// first (row, block) weights requested before it; PRO = 0: the activation was quantized by
+// k_quantize_q8_0 (j.aq).  One launch instead of norm + quantize + GEMV.
+template <int MC, int PRO = 0>
 __global__ __launch_bounds__(256) void k_gemv_q8_0(GemvJob j, int RW) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK8_0);
@@ -1644,10 +1672,25 @@ __global__ __launch_bounds__(256) void k_gemv_q8_0(GemvJob j, int RW) {
     const int rows = (int)((j.N - row0) < RW ? (j.N - row0) : RW);
     const int M = j.M;
     int8_t * xq_s = (int8_t *)smem;
-    float * xd_s = (float *)(smem + al16((size_t)MC * j.K));
-    int * s_s = (int *)((char *)xd_s + al16(sizeof(float) * MC * nb));
+    float * xd_s = (float *)(smem + al16((size_t)MC * j.K + (PRO ? QK_K : 0)));  // + the prologue's trash slot
+    int * s_s = (int *)((char *)xd_s + al16(sizeof(float) * (MC * nb + (PRO ? QK_K / QK8_0 : 0))));
     float * f_s = (float *)((char *)s_s + al16(sizeof(int) * (size_t)RW * nb * MC));
+    const int npairs = rows * nb;
+    // this thread's first (row, block): weights in registers before the prologue (clamped, unconditional)
+    int wv0[8];
+    uint16_t dw0;
     {
+        const int p = min((int)threadIdx.x, npairs - 1);
+        const int r = p / nb, b = p % nb;
+        const uint16_t * bp = (const uint16_t *)(W + (row0 + r) * j.w_row_bytes + (int64_t)b * 34);
+        dw0 = *gptr(bp);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) wv0[k] = (int)*gptr(bp + 1 + 2 * k) | ((int)*gptr(bp + 2 + 2 * k) << 16);
+    }
+    TTS_PIN_LOADS();
+    if constexpr (PRO != 0) {
+        q4k_prologue<PRO, 16, false, NoMid, true>(j, (int)(j.K / QK_K), xq_s, xd_s, nullptr);
+    } else {
         const int4 * src = (const int4 *)j.aq.qs;
         int4 * dst = (int4 *)xq_s;
         const int n16 = (int)((int64_t)M * j.K / 16);
@@ -1655,14 +1698,20 @@ __global__ __launch_bounds__(256) void k_gemv_q8_0(GemvJob j, int RW) {
         for (int i = threadIdx.x; i < M * nb; i += 256) xd_s[i] = j.aq.d[i];
     }
     __syncthreads();
-    const int npairs = rows * nb;
     for (int p = threadIdx.x; p < npairs; p += 256) {
         const int r = p / nb, b = p % nb;
-        const uint16_t * bp = (const uint16_t *)(W + (row0 + r) * j.w_row_bytes + (int64_t)b * 34);
-        const float dw = dev_fp16_to_fp32(bp[0]);
+        float dw;
         int wv[8];
+        if (p == (int)threadIdx.x) {
+            dw = dev_fp16_to_fp32(dw0);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
+            for (int k = 0; k < 8; ++k) wv[k] = wv0[k];
+        } else {
+            const uint16_t * bp = (const uint16_t *)(W + (row0 + r) * j.w_row_bytes + (int64_t)b * 34);
+            dw = dev_fp16_to_fp32(bp[0]);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) wv[k] = (int)bp[1 + 2 * k] | ((int)bp[2 + 2 * k] << 16);
+        }
 #pragma unroll
         for (int m = 0; m < MC; ++m) {
             if (m >= M) break;
@@ -1688,6 +1737,119 @@ __global__ __launch_bounds__(256) void k_gemv_q8_0(GemvJob j, int RW) {
         float a = 0.f;
         const int o = (r * MC + m) * nb;
         for (int b = 0; b < nb; ++b) a = __fadd_rn(a, __fmul_rn((float)s_s[o + b], f_s[o + b]));
+        gemv_store<MC>(j, mat, row0 + r, m, a);
+    }
+}
+
+// Q8_0 GEMV, slab form (K % 256 == 0, 16-B aligned weights; decode, <= 8 columns).  A workgroup owns RW
+// consecutive rows, i.e. one contiguous RW * row_bytes slab of the matrix: the whole slab is requested
+// up front by LDS-DMA (16 B per lane, fully coalesced, no registers held), so each CU has tens of KB in
+// flight and the launch costs about one memory latency plus slab / per-CU bandwidth, instead of one
+// dependent 34-B block fetch per (row, block) round.  Then, from LDS:
+//   terms: a thread per (row, block pair) -- the pair (2k, 2k+1) spans 68 B at a 4-B aligned offset
+//          (17 dwords; block 2k's quants are the funnel-shifted dwords) -- eight sdot4 per block and
+//          column, term = (float)sumi * (d_w * d_x) as ggml_vec_dot_q8_0_q8_0 rounds it;
+//   chain: a thread per (row, column) adds the nb terms in block order (sumf += term, from 0).
+// So the result is bit-identical to ggml's generic order.  The activation's Q8_0 blocks come from the
+// quantize launch (PRO = 0, DMA'd with the slab) or from the prologue (PRO_QUANT / PRO_LN, whose
+// activation loads are issued before the slab DMA so they do not queue behind it).
+// LDS: slab al1K(RW*row_bytes) | xq al1K(MC*K + 256) | xd al1K(4*(MC*nb + 8)) | terms 4*RW*MC*nb.
+__host__ __device__ constexpr int64_t al1k(int64_t v) { return (v + 1023) & ~(int64_t)1023; }
+// LDS-DMA of `bytes` (a multiple of 16) from 16-B aligned global `src` to LDS `dst`; lanes past the end
+// re-read the last 16 B and land in the 1 KB slack after dst + bytes
+__device__ __forceinline__ void dma_span(char * dst, const char * src, int64_t bytes, int wave, int nw, int lane) {
+    const int nck = (int)((bytes + 1023) >> 10);
+    for (int i = wave; i < nck; i += nw) {
+        int64_t off = (int64_t)i * 1024 + lane * 16;
+        off = off < bytes - 16 ? off : bytes - 16;
+        __builtin_amdgcn_global_load_lds(gptr(src + off), (__attribute__((address_space(3))) void *)(dst + (size_t)i * 1024), 16, 0, 0);
+    }
+}
+static size_t q80s_lds(int MC, int64_t K, int RW) {
+    const int64_t nb = K / QK8_0, rb = nb * 34;
+    return (size_t)(al1k(RW * rb) + al1k(MC * K + QK_K) + al1k(4 * (MC * nb + 8)) + 4 * (int64_t)RW * MC * nb);
+}
+template <int MC, int PRO = 0>
+__global__ __launch_bounds__(256) void k_gemv_q8_0s(GemvJob j, int RW) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nb = (int)(j.K / QK8_0), nbp = nb >> 1;
+    const int64_t rb = j.w_row_bytes;
+    const int mat = blockIdx.y;
+    const int64_t row0 = (int64_t)blockIdx.x * RW;
+    const int rows = (int)((j.N - row0) < RW ? (j.N - row0) : RW);
+    const int M = j.M;
+    char * ws = smem;
+    int8_t * xq_s = (int8_t *)(smem + al1k(RW * rb));
+    float * xd_s = (float *)((char *)xq_s + al1k(MC * j.K + QK_K));
+    float * T = (float *)((char *)xd_s + al1k(4 * (MC * nb + 8)));
+    const char * slab = (const char *)j.W[mat] + row0 * rb;
+    auto dma_slab = [&]() { dma_span(ws, slab, rows * rb, wave, 4, lane); };
+    if constexpr (PRO != 0) {
+        struct Mid {
+            decltype(dma_slab) & f;
+            __device__ void operator()() const { f(); }
+        };
+        q4k_prologue<PRO, 16, false, Mid, true>(j, (int)(j.K / QK_K), xq_s, xd_s, nullptr, nullptr, nullptr, Mid{dma_slab});
+    } else {
+        dma_slab();
+        dma_span((char *)xq_s, (const char *)j.aq.qs, (int64_t)M * j.K, wave, 4, lane);
+        dma_span((char *)xd_s, (const char *)j.aq.d, (int64_t)4 * M * nb, wave, 4, lane);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's DMA has landed (vmcnt, lgkmcnt 0)
+    __syncthreads();
+    for (int u = threadIdx.x; u < rows * nbp; u += 256) {
+        const int r = u / nbp, k = u - r * nbp;
+        const uint32_t * wl = (const uint32_t *)(ws + r * rb + 68 * k);
+        uint32_t w[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) w[i] = wl[i];
+        const float d0 = dev_fp16_to_fp32((uint16_t)(w[0] & 0xFFFFu));
+        const float d1 = dev_fp16_to_fp32((uint16_t)(w[8] >> 16));
+        int q0[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q0[i] = (int)__builtin_amdgcn_alignbit(w[i + 1], w[i], 16);
+#pragma unroll
+        for (int m = 0; m < MC; ++m) {
+            if (m >= M) break;
+            const int4 * xb = (const int4 *)(xq_s + (m * nb + 2 * k) * QK8_0);
+            const int4 x0 = xb[0], x1 = xb[1], x2 = xb[2], x3 = xb[3];
+            int s0 = __builtin_amdgcn_sdot4(q0[0], x0.x, 0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[1], x0.y, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[2], x0.z, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[3], x0.w, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[4], x1.x, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[5], x1.y, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[6], x1.z, s0, false);
+            s0 = __builtin_amdgcn_sdot4(q0[7], x1.w, s0, false);
+            int s1 = __builtin_amdgcn_sdot4((int)w[9], x2.x, 0, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[10], x2.y, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[11], x2.z, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[12], x2.w, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[13], x3.x, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[14], x3.y, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[15], x3.z, s1, false);
+            s1 = __builtin_amdgcn_sdot4((int)w[16], x3.w, s1, false);
+            const float2 xd = *(const float2 *)(xd_s + m * nb + 2 * k);
+            float2 t;
+            t.x = __fmul_rn((float)s0, __fmul_rn(d0, xd.x));
+            t.y = __fmul_rn((float)s1, __fmul_rn(d1, xd.y));
+            *(float2 *)(T + (r * MC + m) * nb + 2 * k) = t;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < rows * MC; t += 256) {
+        const int r = t / MC, m = t % MC;
+        if (m >= M) continue;
+        const float4 * tr = (const float4 *)(T + (r * MC + m) * nb);
+        float a = 0.f;
+        for (int b = 0; b < (nb >> 2); ++b) {
+            const float4 v = tr[b];
+            a = __fadd_rn(a, v.x);
+            a = __fadd_rn(a, v.y);
+            a = __fadd_rn(a, v.z);
+            a = __fadd_rn(a, v.w);
+        }
         gemv_store<MC>(j, mat, row0 + r, m, a);
     }
 }
@@ -2410,17 +2572,47 @@ static void launch_gemm_q8_0(tts_hip_backend * be, const GemvJob & j) {
     hipLaunchKernelGGL(k_gemm_q8_0, grid, dim3(256), 0, be->stream, j);
 }
 
+// slab-form Q8_0 GEMV: whole 16-B aligned rows (K % 256 == 0), activation quantized by the prologue or
+// by the quantize launch (Q8_0 blocks at j.aq)
+static bool q80s_ok(const tts_hip_backend * be, const GemvJob & j) {
+    if (!be->gemv_q80_slab || j.K % QK_K || j.hetero || j.dbg) return false;
+    if (!j.pro && (j.aq.vtype != TTS_TYPE_Q8_0 || ((uintptr_t)j.aq.qs & 15) || ((uintptr_t)j.aq.d & 15))) return false;
+    for (int m = 0; m < j.nmat; ++m)
+        if ((uintptr_t)j.W[m] & 15) return false;
+    return q80s_lds(8, j.K, 1) <= 160 * 1024;
+}
+template <int MC>
+static void launch_q80s(tts_hip_backend * be, const GemvJob & j) {
+    // rows per workgroup: the largest of 32 / 16 / 8 / 4 / 2 / 1 that still gives every CU a workgroup
+    // and fits LDS (option TTS_HIP_OPT_GEMV_Q80_RW overrides)
+    int RW = be->gemv_q80_rw > 0 ? be->gemv_q80_rw : 32;
+    if (be->gemv_q80_rw <= 0)
+        while (RW > 1 && (j.N + RW - 1) / RW * j.nmat < be->cus) RW /= 2;
+    while (RW > 1 && q80s_lds(MC, j.K, RW) > (be->gemv_q80_rw > 0 ? 160 : 80) * 1024) RW /= 2;  // auto: 2+ workgroups per CU
+    const size_t lds = q80s_lds(MC, j.K, RW);
+    const dim3 grid((unsigned)((j.N + RW - 1) / RW), (unsigned)j.nmat);
+    if (j.pro == PRO_LN) hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_LN>), grid, dim3(256), lds, be->stream, j, RW);
+    else if (j.pro == PRO_QUANT) hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_QUANT>), grid, dim3(256), lds, be->stream, j, RW);
+    else hipLaunchKernelGGL(k_gemv_q8_0s<MC>, grid, dim3(256), lds, be->stream, j, RW);
+}
+
 template <int MC>
 static void launch_gemv_mc(tts_hip_backend * be, const GemvJob & j) {
     const unsigned nmat = (unsigned)j.nmat;
     switch (j.wtype) {
         case TTS_TYPE_Q4_K: launch_gemv_q4k_mc<MC>(be, j); break;
         case TTS_TYPE_Q8_0: {
+            if (q80s_ok(be, j)) {
+                launch_q80s<MC>(be, j);
+                break;
+            }
             int RW = 8;
             while (RW > 1 && q80_lds(MC, j.K, RW) > 64 * 1024) RW /= 2;
-            const size_t lds = q80_lds(MC, j.K, RW);
+            const size_t lds = q80_lds(MC, j.K, RW) + (j.pro ? QK_K + 64 : 0);
             const unsigned grid = (unsigned)((j.N + RW - 1) / RW);
-            hipLaunchKernelGGL(k_gemv_q8_0<MC>, dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
+            if (j.pro == PRO_LN) hipLaunchKernelGGL((k_gemv_q8_0<MC, PRO_LN>), dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
+            else if (j.pro == PRO_QUANT) hipLaunchKernelGGL((k_gemv_q8_0<MC, PRO_QUANT>), dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
+            else hipLaunchKernelGGL(k_gemv_q8_0<MC>, dim3(grid, nmat), dim3(256), lds, be->stream, j, RW);
         } break;
         case TTS_TYPE_F16: {
             const unsigned grid = (unsigned)((j.N + 3) / 4);
