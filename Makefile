@@ -22,9 +22,13 @@ CPP_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.cpp.o,$(CPP_SRCS))
 
 all: $(OUT)/libtts_hip.so oracle/_build/liboracle.so
 
+# k_gemv: MFMA results straight into VGPRs (the Q8_0 GEMM issues a block's MFMAs back to back instead of
+# funnelling each through one AGPR quad)
+HIPFLAGS_k_gemv := -mllvm -amdgpu-mfma-vgpr-form
+
 $(OBJ)/%.hip.o: $(SRC)/%.hip $(wildcard $(SRC)/*.h) include/tts_hip.h
 	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPFLAGS_$*) -c $< -o $@
 
 $(OBJ)/%.cpp.o: $(SRC)/%.cpp $(wildcard $(SRC)/*.h) include/tts_hip.h include/tts_runners.h
 	@mkdir -p $(OBJ)

@@ -102,13 +102,17 @@ def test_dia_q80_paths_bit_identical(hip):
     """Dia's decode GEMVs (Q8_0, 2 CFG columns) on every Q8_0 path: the (row, block)-per-thread kernel
     after separate norm + quantize launches (the reference point), the slab kernel after them, and the
     slab kernel quantizing -- after the RMS norms, normalizing -- the activation inside every workgroup
-    (TTS_HIP_OPT_GEMV_Q80_PRO / _SLAB, the defaults).  Same arithmetic, so every logit is bit-identical."""
+    (TTS_HIP_OPT_GEMV_Q80_PRO / _SLAB, the defaults), with the MLP's SILU * up folded into the up
+    product's epilogue (TTS_FUSE_EPI) or not.  Same arithmetic, so every logit is bit-identical.  The
+    prefill step runs the encoder's many-column Q8_0 GEMMs (the same epilogue at M = 2 x 32)."""
     text = np.frombuffer(b"\x01 The birch canoe slid on the smooth planks.", dtype=np.uint8).astype(np.int32)
     lib = ttship.lib()
     outs = []
-    for pro, slab in ((0, 0), (0, 1), (1, 1), (1, 0)):
+    no_epi = ttship.FUSE_ALL & ~8  # TTS_FUSE_EPI off: the MLP's SILU and MUL run as their own launches
+    for pro, slab, fuse in ((0, 0, no_epi), (0, 1, no_epi), (1, 1, ttship.FUSE_ALL), (1, 0, ttship.FUSE_ALL), (0, 1, ttship.FUSE_ALL)):
         assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], pro) == 0
         assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], slab) == 0
+        hip.set_option(0, fuse)
         g = ttship.Dia(hip.iface(), ttship.dia_config(**WIDE))
         try:
             audio = np.full(9, 1026, dtype=np.int32)
@@ -122,6 +126,7 @@ def test_dia_q80_paths_bit_identical(hip):
             g.close()
             lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], 1)
             lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], 1)
+            hip.set_option(0, ttship.FUSE_ALL)
     for c in range(1, len(outs)):
         for s, (a, b) in enumerate(zip(outs[0], outs[c])):
             assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (c, s, np.abs(a - b).max())

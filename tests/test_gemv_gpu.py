@@ -112,6 +112,29 @@ def test_q8_0(hip, path, K, N, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("staged", [2, 1, 0])
+@pytest.mark.parametrize("K,N", [(1024, 1024), (4096, 1024), (1024, 4096), (2048, 200), (256, 64), (8192, 96), (96, 40)])
+@pytest.mark.parametrize("M", [9, 64, 130, 1000])
+def test_q8_0_gemm(hip, staged, K, N, M):
+    """Many-column Q8_0 products (Dia's encoder, prefills) on the int8 matrix cores: the staged kernel
+    (TTS_HIP_OPT_GEMM_Q8_STAGED = 2: 64 x 128 output tiles, 1: 64 x 64; operands of 8 blocks per stage
+    through two LDS buffers) and the direct-load kernel (0; also K % 256 != 0).  Partial row and column
+    tiles.  Bit-identical to ggml's block order."""
+    lib = ttship.lib()
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMM_Q8_STAGED"], staged) == 0
+    try:
+        rng = np.random.default_rng(K * 7 + N * 3 + M + staged)
+        w = helpers.rand_q8_0(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        x[1, 32:64] = 0.0
+        ref = py_oracle.gemv(ttship.Q8_0, w, x, N)
+        got = run_gpu(hip, ttship.Q8_0, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMM_Q8_STAGED"], 2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("wtype", [ttship.F32, ttship.F16])
 @pytest.mark.parametrize("K,N", [(1024, 1088), (768, 768), (640, 1024), (4, 9)])
 @pytest.mark.parametrize("M", [1, 3, 9])

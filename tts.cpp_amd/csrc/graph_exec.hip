@@ -621,6 +621,45 @@ struct Planner {
         return true;
     }
 
+    // SwiGLU MLP on Q8_0 weights (Dia model.cpp:358): MUL(UNARY SILU(MUL_MAT(gate, x)), MUL_MAT(up, y)).
+    // The gate product runs alone and is stored; the up product's epilogue reads it back and writes
+    // silu(gate) * up to the MUL's output (EPI_SILU_MUL), so the SILU and MUL launches and their
+    // tensors disappear.  Needs the gate product first in node order, every node between the up
+    // product and the MUL a view (the MUL's output is written at the up product's position), and the
+    // MUL's output disjoint from (or exactly) the gate product and disjoint from the up product's src1.
+    bool try_silu_mul(int i) {
+        const tts_tensor * G = nodes[i];
+        if (G->src[0]->type != TTS_TYPE_Q8_0) return false;
+        const tts_tensor * S = sole_consumer(G);
+        if (!S || S->op != TTS_OP_UNARY || S->op_params[0] != TTS_UNARY_SILU || S->src[0] != G) return false;
+        const tts_tensor * E = sole_consumer(S);
+        if (!E || E->op != TTS_OP_MUL || E->src[0] != S) return false;
+        const tts_tensor * U = E->src[1];
+        if (!U || U->op != TTS_OP_MUL_MAT || uses[U] != 1 || !is_gemv(U) || U->src[0]->type != TTS_TYPE_Q8_0) return false;
+        if (E->type != TTS_TYPE_F32 || !contiguous(E) || !contiguous(G) || !contiguous(S) || !contiguous(U)) return false;
+        for (int d = 0; d < 4; ++d)
+            if (E->ne[d] != G->ne[d] || U->ne[d] != G->ne[d] || S->ne[d] != G->ne[d]) return false;
+        if ((overlap(E, G) && E->data != G->data) || overlap(E, U->src[1])) return false;
+        const int iS = index[S], iU = index[U], iE = index[E];
+        if (iS <= i || iU <= i || iE <= iS || iE <= iU || act[iS] || act[iU] || act[iE]) return false;
+        for (int k = iU + 1; k < iE; ++k)
+            if (k != iS && !(is_view(nodes[k]->op) && act[k] == 0)) return false;
+        Item g;
+        g.kind = Item::GEMV;
+        g.mms = {G};
+        g.tgt = {GemvTarget{(float *)G->data, (int64_t)(G->nb[1] / 4), 1}};
+        Item u;
+        u.kind = Item::GEMV;
+        u.mms = {U};
+        u.tgt = {GemvTarget{(float *)E->data, (int64_t)(E->nb[1] / 4), 1}};
+        u.epi = EPI_SILU_MUL;
+        u.res = G;
+        act[iS] = act[iE] = -1;
+        act[i] = add_item(std::move(g));
+        act[iU] = add_item(std::move(u));
+        return true;
+    }
+
     void try_gemv(int i) {
         const tts_tensor * mm0 = nodes[i];
         if (!is_gemv(mm0)) return;
@@ -628,6 +667,7 @@ struct Planner {
         const tts_tensor * x = mm0->src[1];
         const int64_t M = x->ne[1] * x->ne[2] * x->ne[3];
         if ((mask & TTS_FUSE_EPI) && try_swiglu(i)) return;
+        if ((mask & TTS_FUSE_EPI) && try_silu_mul(i)) return;
         Item it;
         it.kind = Item::GEMV;
         std::vector<int> skips;

@@ -188,7 +188,9 @@ struct ActQuant {
 // optional fused epilogue (GELU table, or + residual(row n, column m) = res[m*rcs + n]).
 // EPI_SWIGLU (matrix-core Q4_K kernel only, nmat == 2: gate, up): Y[0] = silu(gate) * up, the
 // UNARY SILU and MUL of the SwiGLU MLP (Orpheus model.cpp:296-300); gate / up are never stored.
-enum { EPI_NONE = 0, EPI_GELU = 1, EPI_ADD = 2, EPI_SWIGLU = 3 };
+// EPI_SILU_MUL (Q8_0 kernels): y = silu(res) * product -- the up product's epilogue reading the gate
+// product stored by the previous launch (Dia's MLP: MUL(SILU(gate x), up x)), as UNARY SILU then MUL round.
+enum { EPI_NONE = 0, EPI_GELU = 1, EPI_ADD = 2, EPI_SWIGLU = 3, EPI_SILU_MUL = 4 };
 constexpr int GEMV_MAX_MATS = 16;
 struct GemvJob {
     int wtype = 0;
@@ -308,6 +310,7 @@ struct tts_hip_backend {
     int gemv_q80_pro = 1;      // TTS_HIP_OPT_GEMV_Q80_PRO
     int gemv_q80_slab = 1;     // TTS_HIP_OPT_GEMV_Q80_SLAB
     int gemv_q80_rw = 0;       // TTS_HIP_OPT_GEMV_Q80_RW
+    int gemm_q8_staged = 2;    // TTS_HIP_OPT_GEMM_Q8_STAGED
     int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a

@@ -167,6 +167,8 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
         else if (v < 10.0f) v = __half2float(__ushort_as_half(j.gelu[__half_as_ushort(__float2half_rn(v))]));
     } else if (j.epi == EPI_ADD) {
         v = __fadd_rn(v, j.res[m * j.rcs + row]);
+    } else if (j.epi == EPI_SILU_MUL) {
+        v = __fmul_rn(dev_silu(j.res[m * j.rcs + row]), v);
     }
     float * const Y = j.Y[mat];
     const int64_t ycs = j.ycs[mat], yrs = j.yrs[mat];
@@ -2567,7 +2569,174 @@ __global__ __launch_bounds__(256) void k_gemm_q8_0(GemvJob j) {
         }
 }
 
+// The staged form (K % 256 == 0, 16-B aligned weight rows and activation copy): a workgroup owns a
+// 64-row x TC-column output tile; the K dimension runs in stages of 8 blocks (256 elements), each
+// stage's operands fetched into registers while the previous stage computes, then stored to the other
+// of two LDS buffers:
+//   A: the 64 rows' native 272-B stage spans, row-major (17 x 16 B per row; row stride 68 dwords puts
+//      the 16 rows an MFMA reads on distinct banks), read as 3 dwords + funnel shift (quants start
+//      2 B into a block) and the block's fp16 d as one u16;
+//   B: the TC columns' 256 int8, 16-B chunks XOR-swizzled by column (chunk q of column c at slot
+//      q ^ (c & 15)) so the 16 columns of an MFMA read different banks;
+//   dx: the TC columns' 8 block scales.
+// Per block and 16 x 16 tile one v_mfma_i32_16x16x32_i8 gives the exact block dots; each lane folds
+// its four outputs' terms into f32 in block order with ggml's roundings, as k_gemm_q8_0: bit-identical.
+template <int TC>
+struct Q8s {
+    static constexpr int A_BYTES = 20 * 1024;  // 64 rows x 272 B (1088 chunks) as 20 x 64 uniform 16-B chunks
+    static constexpr int B_BYTES = TC * 256;
+    static constexpr int D_BYTES = TC * 32;
+    static constexpr int STAGE = A_BYTES + B_BYTES + D_BYTES;
+};
+template <int TC>
+__global__ __launch_bounds__(256) void k_gemm_q8_0s(GemvJob j) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int NT = TC / 32;  // 16-column tiles per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int l16 = lane & 15, kq = lane >> 4;
+    const int mat = blockIdx.z;
+    const int64_t row0 = (int64_t)blockIdx.x * 64, col0 = (int64_t)blockIdx.y * TC;
+    const int64_t rb = j.w_row_bytes, K = j.K;
+    const int nb = (int)(K / QK8_0), nst = nb / 8;
+    const char * W = (const char *)j.W[mat];
+    const char * xq = (const char *)j.aq.qs;
+    const char * xdg = (const char *)j.aq.d;
+    // a wave's share of one stage: 5 A chunks, TC / 16 B chunks, <= 1 dx chunk (16 B each), fetched into
+    // registers while the previous stage computes, then stored to LDS (a lane's chunk of instruction
+    // `ins` at slot ins * 64 + lane).  Register staging, not LDS-DMA: the compiler cannot tell a DMA's
+    // LDS target from the buffer being read and would wait for the DMA before every LDS read.
+    constexpr int NB_ = TC / 16;
+    u32x4 ra[5], rbv[NB_], rd;
+    auto stage_load = [&](int st) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            // A: linear chunk n = r * 17 + q (n < 1088; the rest re-read the last chunk into the slack)
+            int n = (wave * 5 + i) * 64 + lane;
+            n = n < 1088 ? n : 1087;
+            const int r = n / 17, q = n - 17 * (n / 17);
+            const int64_t row = row0 + r < j.N ? row0 + r : j.N - 1;
+            ra[i] = *gptr((const u32x4 *)(W + row * rb + (int64_t)st * 272 + 16 * q));
+        }
+#pragma unroll
+        for (int i = 0; i < NB_; ++i) {
+            // B: slot idx = c * 16 + q' holds chunk q = q' ^ (c & 15) of column c
+            const int idx = (wave * NB_ + i) * 64 + lane, c = idx >> 4, q = (idx & 15) ^ (c & 15);
+            const int64_t col = col0 + c < j.M ? col0 + c : j.M - 1;
+            rbv[i] = *gptr((const u32x4 *)(xq + col * K + (int64_t)st * 256 + 16 * q));
+        }
+        {
+            // dx: column c's 8 scales as chunks 2c, 2c + 1 (waves 0 .. TC/32 - 1)
+            const int idx = (wave < TC / 32 ? wave : 0) * 64 + lane, c = idx >> 1, h = idx & 1;
+            const int64_t col = col0 + c < j.M ? col0 + c : j.M - 1;
+            rd = *gptr((const u32x4 *)(xdg + col * (int64_t)nb * 4 + (int64_t)st * 32 + 16 * h));
+        }
+    };
+    auto stage_store = [&](int buf) __attribute__((always_inline)) {
+        char * base = smem + buf * Q8s<TC>::STAGE;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) *(u32x4 *)(base + (wave * 5 + i) * 1024 + 16 * lane) = ra[i];
+        char * bb = base + Q8s<TC>::A_BYTES;
+#pragma unroll
+        for (int i = 0; i < NB_; ++i) *(u32x4 *)(bb + (wave * NB_ + i) * 1024 + 16 * lane) = rbv[i];
+        if (wave < TC / 32) *(u32x4 *)(bb + Q8s<TC>::B_BYTES + wave * 1024 + 16 * lane) = rd;
+    };
+    const int wr = (wave & 1) * 32, wc = (wave >> 1) * (TC / 2);
+    float acc[2][NT][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < NT; ++b)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[a][b][e] = 0.0f;
+    stage_load(0);
+    stage_store(0);
+    __syncthreads();
+    for (int st = 0; st < nst; ++st) {
+        stage_load(st + 1 < nst ? st + 1 : st);  // unconditional (clamped): lands during this stage's MFMAs
+        const char * base = smem + (st & 1) * Q8s<TC>::STAGE;
+        const char * bb = base + Q8s<TC>::A_BYTES;
+        const float * db = (const float *)(bb + Q8s<TC>::B_BYTES);
+        // all of a block's MFMAs are issued before any result is folded, so they pipeline instead of
+        // each waiting out the previous one's latency
+#pragma unroll 2
+        for (int b = 0; b < 8; ++b) {
+            long av[2], bv[NT];
+            float dw[2][4], dx[NT];
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti) {
+                const int off = (wr + 16 * ti + l16) * 272 + b * 34 + 2 + 8 * kq;
+                const uint32_t * p = (const uint32_t *)(base + (off & ~3));
+                const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+                const uint32_t sh = (off & 3) * 8;
+                const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, sh), hi = __builtin_amdgcn_alignbit(d2, d1, sh);
+                av[ti] = (long)(((uint64_t)hi << 32) | lo);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    dw[ti][e] = dev_fp16_to_fp32(*(const uint16_t *)(base + (wr + 16 * ti + 4 * kq + e) * 272 + b * 34));
+            }
+#pragma unroll
+            for (int tj = 0; tj < NT; ++tj) {
+                const int c = wc + 16 * tj + l16;
+                const int q = 2 * b + (kq >> 1);
+                bv[tj] = *(const long *)(bb + (c * 16 + (q ^ (c & 15))) * 16 + 8 * (kq & 1));
+                dx[tj] = db[c * 8 + b];
+            }
+            i32x4_t sv[2][NT];
+#pragma unroll
+            for (int tj = 0; tj < NT; ++tj)
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti) {
+                    const i32x4_t z = {0, 0, 0, 0};
+                    sv[ti][tj] = __builtin_amdgcn_mfma_i32_16x16x32_i8(av[ti], bv[tj], z, 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);  // keep the scheduler from re-serializing them into one accumulator
+#pragma unroll
+            for (int tj = 0; tj < NT; ++tj)
+#pragma unroll
+                for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        acc[ti][tj][e] = __fadd_rn(acc[ti][tj][e], __fmul_rn((float)sv[ti][tj][e], __fmul_rn(dw[ti][e], dx[tj])));
+        }
+        // every wave is done with the other buffer (stage st - 1) since the last barrier
+        if (st + 1 < nst) stage_store((st + 1) & 1);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < NT; ++tj) {
+            const int64_t col = col0 + wc + 16 * tj + l16;
+            if (col >= j.M) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int64_t row = row0 + wr + 16 * ti + 4 * kq + e;
+                if (row < j.N) gemv_store<1>(j, mat, row, (int)col, acc[ti][tj][e]);
+            }
+        }
+}
+
+static bool gemm_q8s_ok(const tts_hip_backend * be, const GemvJob & j) {
+    if (be->gemm_q8_staged <= 0 || j.K % QK_K || j.w_row_bytes % 16 || ((uintptr_t)j.aq.qs & 15) || ((uintptr_t)j.aq.d & 15)) return false;
+    for (int m = 0; m < j.nmat; ++m)
+        if ((uintptr_t)j.W[m] & 15) return false;
+    return true;
+}
+
 static void launch_gemm_q8_0(tts_hip_backend * be, const GemvJob & j) {
+    if (gemm_q8s_ok(be, j)) {
+        static std::atomic<uint32_t> attr_done[2];
+        if (be->gemm_q8_staged == 1) {
+            set_lds_attr_once(attr_done[0], be->device, (const void *)k_gemm_q8_0s<64>);
+            const dim3 grid((unsigned)((j.N + 63) / 64), (unsigned)((j.M + 63) / 64), (unsigned)j.nmat);
+            hipLaunchKernelGGL(k_gemm_q8_0s<64>, grid, dim3(256), 2 * Q8s<64>::STAGE, be->stream, j);
+        } else {
+            set_lds_attr_once(attr_done[1], be->device, (const void *)k_gemm_q8_0s<128>);
+            const dim3 grid((unsigned)((j.N + 63) / 64), (unsigned)((j.M + 127) / 128), (unsigned)j.nmat);
+            hipLaunchKernelGGL(k_gemm_q8_0s<128>, grid, dim3(256), 2 * Q8s<128>::STAGE, be->stream, j);
+        }
+        return;
+    }
     const dim3 grid((unsigned)((j.N + 63) / 64), (unsigned)((j.M + 63) / 64), (unsigned)j.nmat);
     hipLaunchKernelGGL(k_gemm_q8_0, grid, dim3(256), 0, be->stream, j);
 }
@@ -2591,9 +2760,17 @@ static void launch_q80s(tts_hip_backend * be, const GemvJob & j) {
     while (RW > 1 && q80s_lds(MC, j.K, RW) > (be->gemv_q80_rw > 0 ? 160 : 80) * 1024) RW /= 2;  // auto: 2+ workgroups per CU
     const size_t lds = q80s_lds(MC, j.K, RW);
     const dim3 grid((unsigned)((j.N + RW - 1) / RW), (unsigned)j.nmat);
-    if (j.pro == PRO_LN) hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_LN>), grid, dim3(256), lds, be->stream, j, RW);
-    else if (j.pro == PRO_QUANT) hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_QUANT>), grid, dim3(256), lds, be->stream, j, RW);
-    else hipLaunchKernelGGL(k_gemv_q8_0s<MC>, grid, dim3(256), lds, be->stream, j, RW);
+    static std::atomic<uint32_t> attr_done[3];
+    if (j.pro == PRO_LN) {
+        set_lds_attr_once(attr_done[2], be->device, (const void *)k_gemv_q8_0s<MC, PRO_LN>);
+        hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_LN>), grid, dim3(256), lds, be->stream, j, RW);
+    } else if (j.pro == PRO_QUANT) {
+        set_lds_attr_once(attr_done[1], be->device, (const void *)k_gemv_q8_0s<MC, PRO_QUANT>);
+        hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_QUANT>), grid, dim3(256), lds, be->stream, j, RW);
+    } else {
+        set_lds_attr_once(attr_done[0], be->device, (const void *)k_gemv_q8_0s<MC>);
+        hipLaunchKernelGGL(k_gemv_q8_0s<MC>, grid, dim3(256), lds, be->stream, j, RW);
+    }
 }
 
 template <int MC>
