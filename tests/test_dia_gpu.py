@@ -100,7 +100,8 @@ def test_dia_full_depth_long_dialogue(hip):
 @pytest.mark.gpu
 def test_dia_q80_paths_bit_identical(hip):
     """Dia's decode GEMVs (Q8_0, 2 CFG columns) on every Q8_0 path: the (row, block)-per-thread kernel
-    after separate norm + quantize launches (the reference point), the slab kernel after them, and the
+    after separate norm + quantize launches with every graph fusion off (the reference point: one
+    launch per node), the slab kernel after them, and the
     slab kernel quantizing -- after the RMS norms, normalizing -- the activation inside every workgroup
     (TTS_HIP_OPT_GEMV_Q80_PRO / _SLAB, the defaults), with the MLP's SILU * up folded into the up
     product's epilogue (TTS_FUSE_EPI) or not.  Same arithmetic, so every logit is bit-identical.  The
@@ -109,7 +110,7 @@ def test_dia_q80_paths_bit_identical(hip):
     lib = ttship.lib()
     outs = []
     no_epi = ttship.FUSE_ALL & ~8  # TTS_FUSE_EPI off: the MLP's SILU and MUL run as their own launches
-    for pro, slab, fuse in ((0, 0, no_epi), (0, 1, no_epi), (1, 1, ttship.FUSE_ALL), (1, 0, ttship.FUSE_ALL), (0, 1, ttship.FUSE_ALL)):
+    for pro, slab, fuse in ((0, 0, 0), (0, 1, no_epi), (1, 1, ttship.FUSE_ALL), (1, 0, ttship.FUSE_ALL), (0, 1, ttship.FUSE_ALL)):
         assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_PRO"], pro) == 0
         assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_Q80_SLAB"], slab) == 0
         hip.set_option(0, fuse)

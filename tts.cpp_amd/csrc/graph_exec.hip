@@ -86,6 +86,8 @@ float opf(const tts_tensor * t, int i) {
 }
 
 // MUL_MAT with a 2-D weight matrix and evenly strided f32 columns: the decode GEMV.
+static int64_t nel(const tts_tensor * t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+
 bool is_gemv(const tts_tensor * n) {
     const tts_tensor * a = n->src[0];
     const tts_tensor * b = n->src[1];
@@ -141,6 +143,7 @@ struct Item {
     float lneps = 0.f;
     bool lnrms = false;
     bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
+    const tts_tensor * xsrc = nullptr;  // src1 is a skipped CONT of this contiguous tensor (same bytes): read its data
     bool shadow = false;    // ATTN: also write the private copy (be->shadow)
     int xattn = -1;         // GEMV: index of the short-context ATTN item whose query it produces (one launch)
     bool fused = false;     // ATTN: launched by the GEMV item that produces its query
@@ -170,7 +173,8 @@ struct Item {
     // ADAIN: per-channel norm + affine (+ snake)
     AdainArgs adain{};
     // MCPY: src (x) copied into every view in `terms`
-    // RINT: dst = repeat_interleave of x along dim 1 by `rint`
+    // RINT: dst = repeat_interleave of x along dim 1 by `rint` (rint_cpy: into the stand-in `node`)
+    bool rint_cpy = false;
     int rint = 1;
 };
 
@@ -670,6 +674,16 @@ struct Planner {
         if ((mask & TTS_FUSE_EPI) && try_silu_mul(i)) return;
         Item it;
         it.kind = Item::GEMV;
+        // src1 = a CONT made right before this product from a contiguous tensor of the same columns
+        // (Dia's cont_3d of the attention output): read that tensor and skip the copy
+        if ((mask & TTS_FUSE_CONTREAD) && x->op == TTS_OP_CONT && index.count(x) && act[index[x]] == 0 && uses[x] == 1 &&
+            next_real(index[x]) == i && x->src[0] && !(x->flags & (TTS_FLAG_OUTPUT | TTS_FLAG_PERSIST))) {
+            const tts_tensor * s0 = x->src[0];
+            if (s0->type == TTS_TYPE_F32 && contiguous(s0) && contiguous(x) && nel(s0) == nel(x)) {  // the same bytes
+                it.xsrc = s0;
+                act[index[x]] = -1;
+            }
+        }
         std::vector<int> skips;
         // Group MUL_MATs sharing src1 and weight type / shape into one launch at the first one's
         // position.  The reference's node order separates them (parler_build_kv_store and
@@ -781,9 +795,20 @@ struct Planner {
             ++j;
         }
         if (it.mms.size() == 1 && (mask & TTS_FUSE_EPI)) {
-            // epilogue: adjacent GELU or ADD(residual) consuming the single product
+            // epilogue: adjacent GELU or ADD(residual) consuming the single product -- directly, or
+            // through a CONT of the contiguous product into another shape of the same columns (Dia's
+            // cont_2d before the residual ADD, model.cpp:336-337 here), which is then never made
             const tts_tensor * E = sole_consumer(mm0);
-            if (E && next_real(i) == index[E] && E->src[0] == mm0 && E->type == TTS_TYPE_F32 && contiguous(E) && contiguous(mm0)) {
+            const tts_tensor * P = mm0;  // the node E reads
+            int iP = i;
+            if (E && E->op == TTS_OP_CONT && E->src[0] == mm0 && next_real(i) == index[E] && contiguous(E) && contiguous(mm0) &&
+                E->type == TTS_TYPE_F32 && E->ne[0] == mm0->ne[0] && nel(E) == nel(mm0) && act[index[E]] == 0) {
+                P = E;
+                iP = index[E];
+                E = sole_consumer(P);
+            }
+            if (E && next_real(iP) == index[E] && E->src[0] == P && E->type == TTS_TYPE_F32 && contiguous(E) && contiguous(mm0) &&
+                E->ne[0] == mm0->ne[0] && nel(E) == nel(mm0) && act[index[E]] == 0) {
                 if (E->op == TTS_OP_UNARY && E->op_params[0] == TTS_UNARY_GELU) {
                     it.epi = EPI_GELU;
                 } else if (E->op == TTS_OP_ADD && E->src[1]->type == TTS_TYPE_F32 && contiguous(E->src[1]) &&
@@ -793,8 +818,9 @@ struct Planner {
                     it.res = E->src[1];
                 }
                 if (it.epi != EPI_NONE && (a0->type != TTS_TYPE_F32 || !overlap(E, x))) {
-                    it.tgt[0] = GemvTarget{(float *)E->data, (int64_t)(E->nb[1] / 4), 1};
+                    it.tgt[0] = GemvTarget{(float *)E->data, (int64_t)(E->ne[0]), 1};  // contiguous: column stride ne0
                     act[index[E]] = -1;
+                    if (P != mm0) act[iP] = -1;
                 } else {
                     it.epi = EPI_NONE;
                     it.res = nullptr;
@@ -1529,7 +1555,65 @@ struct Planner {
         it.dst = R;
         it.rint = (int)r;
         for (int m : members) act[m] = -1;
+        // input: a = CONT of a same-shape tensor (Dia's cont(reshape_4d(k / v))) whose every reader is
+        // one of the leaves' views: read that tensor in place (TD strides) and skip the copy
+        if (a->op == TTS_OP_CONT && a->src[0] && index.count(a) && act[index[a]] == 0) {
+            const tts_tensor * s0 = a->src[0];
+            bool ok = s0->type == TTS_TYPE_F32 && !overlap(R, s0);
+            for (int d = 0; d < 4; ++d) ok &= s0->ne[d] == a->ne[d];
+            auto ca = consumers.find(a);
+            ok &= ca != consumers.end();
+            if (ok)
+                for (int k : ca->second) {
+                    const tts_tensor * v = nodes[k];
+                    const tts_tensor * u = sole_consumer(v);
+                    ok &= v->op == TTS_OP_VIEW && u && std::find(members.begin(), members.end(), index[u]) != members.end();
+                }
+            const int ia = ok ? index[a] : 0;
+            for (int j = ia + 1; ok && j < i; ++j) {
+                if (is_view(nodes[j]->op) || std::find(members.begin(), members.end(), j) != members.end()) continue;
+                if (overlap(nodes[j], s0)) ok = false;
+            }
+            if (ok) {
+                it.x = s0;
+                act[ia] = -1;
+            }
+        }
+        // output: R only feeds a CPY into a cache view, directly or through a CONT of a reshape (Dia's
+        // self K / V store, model.cpp:317-322 here): write the cache view in R's shape and skip both
+        rint_to_cpy(i, R, it);
         act[i] = add_item(std::move(it));
+    }
+
+    // R [n0, n1, n2, n3] contiguous -> [RESHAPE ->] [CONT ->] CPY into D with D->ne[0] == n0 n1 n2 and
+    // D->ne[1] == n3 (flat order: D(j0, j1) = R(i0, i1, i2, i3), j0 = i0 + n0 i1 + n0 n1 i2, j1 = i3):
+    // the RINT writes D through a stand-in tensor with R's shape and D's strides (it.node)
+    void rint_to_cpy(int i, const tts_tensor * R, Item & it) {
+        const tts_tensor * X = sole_consumer(R);
+        std::vector<int> skip;
+        while (X && X->op == TTS_OP_RESHAPE && X->src[0] && contiguous(X)) X = sole_consumer(X);
+        if (X && X->op == TTS_OP_CONT && contiguous(X) && index.count(X) && act[index[X]] == 0) {
+            skip.push_back(index[X]);
+            X = sole_consumer(X);
+        }
+        if (!X || X->op != TTS_OP_CPY || !index.count(X) || act[index[X]] != 0) return;
+        const int iP = index[X];
+        skip.push_back(iP);
+        const tts_tensor * D = X;  // the CPY's result is its destination view
+        if (D->type != TTS_TYPE_F32 || D->nb[0] != 4 || D->ne[0] != R->ne[0] * R->ne[1] * R->ne[2] || D->ne[1] != R->ne[3] ||
+            D->ne[2] != 1 || D->ne[3] != 1 || overlap(D, it.x))
+            return;
+        for (int j = i + 1; j < iP; ++j)
+            if (!is_view(nodes[j]->op) && std::find(skip.begin(), skip.end(), j) == skip.end()) return;
+        tts_tensor t = *R;
+        t.data = D->data;
+        t.nb[0] = 4;
+        t.nb[1] = 4 * R->ne[0];
+        t.nb[2] = t.nb[1] * R->ne[1];
+        t.nb[3] = D->nb[1];
+        it.node = t;
+        it.rint_cpy = true;
+        for (int k : skip) act[k] = -1;
     }
 
     void try_embed(int i) {
@@ -1810,12 +1894,18 @@ static int run_attn_item(tts_hip_backend * be, const Item & it) {
 static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xattn = nullptr) {
     const tts_tensor * mm0 = it.mms[0];
     const tts_tensor * a0 = mm0->src[0];
-    const tts_tensor * b = mm0->src[1];
+    // a skipped CONT (it.xsrc): its contiguous source holds the same bytes; read them in src1's shape
+    tts_tensor bx;
+    if (it.xsrc) {
+        bx = *mm0->src[1];
+        bx.data = it.xsrc->data;
+    }
+    const tts_tensor * b = it.xsrc ? &bx : mm0->src[1];
     GemvJob j;
     j.wtype = a0->type;
     j.K = a0->ne[0];
     j.N = a0->ne[1];
-    j.M = b->ne[1] * b->ne[2] * b->ne[3];
+    j.M = nel(b) / b->ne[0];
     j.w_row_bytes = (int64_t)a0->nb[1];
     j.x = (const float *)b->data;
     j.xcs = (int64_t)(b->nb[1] / 4);
@@ -2008,7 +2098,7 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             else launch_cpy_multi(be, it.x, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::RINT:
-            launch_repeat_interleave1(be, it.dst, it.x, it.rint);
+            launch_repeat_interleave1(be, it.rint_cpy ? &it.node : it.dst, it.x, it.rint);
             return 0;
         case Item::NODE:
             return run_node(be, &it.node);
@@ -2191,8 +2281,26 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
             if ((int32_t)it.mms.size() > counts[13]) counts[13] = (int32_t)it.mms.size();
         }
     }
+    static const bool dump = getenv("TTS_PLAN_DUMP") != nullptr;  // list the nodes launched one by one
+    if (dump)
+        for (int i = 0; i < n_nodes; ++i)
+            if (pl.act[i] > 0) {
+                const Item & it = pl.items[pl.act[i] - 1];
+                fprintf(stderr, "item %d kind %d", i, (int)it.kind);
+                if (it.kind == Item::GEMV)
+                    fprintf(stderr, " mms %d K %lld N %lld M %lld epi %d ln %d", (int)it.mms.size(), (long long)it.mms[0]->src[0]->ne[0],
+                            (long long)it.mms[0]->src[0]->ne[1], (long long)(nel(it.mms[0]->src[1]) / it.mms[0]->src[1]->ne[0]), it.epi, (int)it.ln);
+                if (it.kind == Item::COPY) fprintf(stderr, " bytes %zu", it.cp_bytes);
+                fprintf(stderr, "\n");
+            }
     for (int i = 0; i < n_nodes; ++i)
-        if (pl.act[i] == 0 && !is_view(nodes[i]->op)) counts[15]++;
+        if (pl.act[i] == 0 && !is_view(nodes[i]->op)) {
+            counts[15]++;
+            if (dump)
+                fprintf(stderr, "unfused %d op %d [%lld %lld %lld %lld] %s <- %s\n", i, (int)nodes[i]->op, (long long)nodes[i]->ne[0],
+                        (long long)nodes[i]->ne[1], (long long)nodes[i]->ne[2], (long long)nodes[i]->ne[3], nodes[i]->name,
+                        nodes[i]->src[0] ? nodes[i]->src[0]->name : "");
+        }
     return (int)pl.items.size();
 }
 
