@@ -721,7 +721,7 @@ struct Planner {
         };
         std::vector<const tts_tensor *> passed;  // nodes the later members are hoisted over
         const int max_mats = (mask & TTS_FUSE_GROUP) ? GEMV_MAX_MATS : 1;
-        const int jend = std::min(n, i + 96);
+        const int jend = std::min(n, i + 160);
         int j = i;
         while (j < jend && (int)it.mms.size() < max_mats) {
             const tts_tensor * mm = nodes[j];
@@ -788,7 +788,9 @@ struct Planner {
                 ++j;
                 continue;
             }
-            if (act[j] != 0 || overlap(mm, x) || (int)passed.size() > 64) break;
+            // a node already claimed by another item is passed over like any other: every item writes
+            // only tensors of its nodes (or backend scratch) and reads their sources, all listed here
+            if (overlap(mm, x) || (int)passed.size() > 256) break;
             passed.push_back(mm);
             for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
                 if (mm->src[s2]) passed.push_back(mm->src[s2]);
