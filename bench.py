@@ -426,6 +426,7 @@ def main():
     ap.add_argument("--gemv-q80-slab", type=int, default=None, help="TTS_HIP_OPT_GEMV_Q80_SLAB: slab-form Q8_0 GEMV (1) or the row-block kernel (0)")
     ap.add_argument("--gemv-q80-rw", type=int, default=None, help="TTS_HIP_OPT_GEMV_Q80_RW: rows per slab Q8_0 GEMV workgroup (0 = auto)")
     ap.add_argument("--gemm-q8-staged", type=int, default=None, help="TTS_HIP_OPT_GEMM_Q8_STAGED: many-column Q8_0 GEMM kernel (2 = 64x128 staged, 1 = 64x64 staged, 0 = direct)")
+    ap.add_argument("--gemv-kr-inkernel", type=int, default=None, help="TTS_HIP_OPT_GEMV_KR_INKERNEL: max K of K-relay GEMVs quantizing in-kernel (0 = operand pass)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
@@ -481,6 +482,8 @@ def main():
             rb.set_option(ttship.OPT["GEMV_Q80_RW"], args.gemv_q80_rw)
         if args.gemm_q8_staged is not None:
             rb.set_option(ttship.OPT["GEMM_Q8_STAGED"], args.gemm_q8_staged)
+        if args.gemv_kr_inkernel is not None:
+            rb.set_option(ttship.OPT["GEMV_KR_INKERNEL"], args.gemv_kr_inkernel)
         if args.attn_ks is not None:
             rb.set_option(ttship.OPT["ATTN_KS"], args.attn_ks)
         if args.attn_pv8 is not None:

@@ -306,6 +306,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_Q80_RW = 29,  /* slab Q8_0 GEMV rows per workgroup (0 = auto: the most that still fills every CU) */
     TTS_HIP_OPT_GEMM_Q8_STAGED = 30, /* many-column Q8_0 GEMM with K % 256 == 0: 2 (default) = staged LDS-DMA kernel over
                                      64 x 128 output tiles, 1 = over 64 x 64 tiles, 0 = the direct-load kernel */
+    TTS_HIP_OPT_GEMV_KR_INKERNEL = 31, /* K-relay Q4_K GEMVs with K <= value (<= 4096) norm / quantize the activation in every
+                                     workgroup instead of after the operand pass (0 = always the operand pass) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
 };

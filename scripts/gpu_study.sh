@@ -72,6 +72,10 @@ case "$1" in
       timeout -k 10 300 python3 bench.py --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --orpheus-steps 0 --no-cpu-baseline --b1-replicas 0 --dia-steps 100 $cfg > "$O/dia_$n.log" 2>&1 &&
       python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['dia'];print(sys.argv[2], d['ms_per_step'], d['encoder_step_ms'])" "$O/dia_$n.log" "$cfg" || exit 1
     done ;;
+  dac20_trace)  # kernel trace of the driver's short line (AR + DAC of 20 frames), AR/DAC legs only
+    shift
+    (cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/profd20" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 5 --kokoro-prompts 0 --orpheus-steps 0 --no-cpu-baseline --b1-replicas 0 --dia-steps 0 "$@" > "$O/dac20_trace.log" 2>&1) &&
+    tail -1 "$O/dac20_trace.log" | cut -c1-300 ;;
   dia_trace)   # kernel trace of the Dia leg + per-step breakdown (markers: the greedy step)
     shift
     (cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/profdia" -o run --output-format csv -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-dac --kokoro-prompts 0 --orpheus-steps 0 --no-cpu-baseline --b1-replicas 0 --dia-steps 40 "$@" > "$O/dia_trace.log" 2>&1) &&
@@ -84,5 +88,5 @@ case "$1" in
   mfma_f64)    # the f64 MFMA ceiling
     hipcc --offload-arch=gfx950 -O3 scripts/mfma_f64_peak.hip -o build/mfma_f64_peak && timeout -k 10 120 build/mfma_f64_peak > "$O/mfma_f64.log" 2>&1 && cat "$O/mfma_f64.log" ;;
   *)
-    echo "usage: $0 {ar|ar_trace|orph_trace|dia|dia_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
+    echo "usage: $0 {ar|ar_trace|orph_trace|dia|dia_trace|dac20_trace|replicas|cu_partition|kernarg|gemv_phase|attn|dac|dac_short|tests|sync|mfma_f64} [args]"; exit 2 ;;
 esac

@@ -177,9 +177,9 @@ def run_gpu_tiled(hip, w, x, N):
 KS_DEFAULT = 256  # backend default of TTS_HIP_OPT_GEMV_KS
 
 
-# (GEMV_KS tile cap, GEMV_KRELAY, GEMV_PREQUANT)
-MF_PATHS = {"mf": (0, 0, 1), "ks": (KS_DEFAULT, 0, 1), "ks_loop": (1 << 20, 0, 1), "kr": (KS_DEFAULT, 1, 1),
-            "mf_inkernel": (0, 0, 0), "ks_inkernel": (KS_DEFAULT, 0, 0)}
+# (GEMV_KS tile cap, GEMV_KRELAY, GEMV_PREQUANT, GEMV_KR_INKERNEL)
+MF_PATHS = {"mf": (0, 0, 1, 0), "ks": (KS_DEFAULT, 0, 1, 0), "ks_loop": (1 << 20, 0, 1, 0), "kr": (KS_DEFAULT, 1, 1, 0),
+            "kr_inkernel": (KS_DEFAULT, 1, 1, 4096), "mf_inkernel": (0, 0, 0, 0), "ks_inkernel": (KS_DEFAULT, 0, 0, 0)}
 
 
 @pytest.fixture(params=list(MF_PATHS), ids=list(MF_PATHS))
@@ -188,16 +188,18 @@ def ks_tiles(request, hip):
     (M <= 8, K <= 4096, N % 16 == 0) with the default tile cap and for every tile count (grids of more
     than 2048 tiles loop over tiles), on the K-relay kernel k_gemv_q4K_kr (M <= 8, K = 1024 * {1, 2,
     3, 4, 8}, N % 16 == 0; the default), each after the quantize pass (k_quant_mf, default) or with
-    the operands quantized inside every workgroup."""
+    the operands quantized inside every workgroup (for the K relay: K <= 4096)."""
     lib = ttship.lib()
-    ks, kr, pre = MF_PATHS[request.param]
+    ks, kr, pre, ink = MF_PATHS[request.param]
     assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], ks) == 0
     assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KRELAY"], kr) == 0
     assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_PREQUANT"], pre) == 0
+    assert lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KR_INKERNEL"], ink) == 0
     yield request.param
     lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KS"], KS_DEFAULT)
     lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KRELAY"], 1)
     lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_PREQUANT"], 1)
+    lib.tts_hip_set_option(hip.ptr, ttship.OPT["GEMV_KR_INKERNEL"], 0)
 
 
 @pytest.mark.gpu

@@ -83,11 +83,18 @@ def test_orpheus_wide_batch8(hip):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["mf", "inkernel"])
+@pytest.mark.parametrize("path", ["mf", "inkernel", "kr_inkernel"])
 def test_orpheus_wide_batch8_gemv_paths(hip, path):
     """The bench shape on the older matrix-core paths: k_gemv_q4K_mf after the quantize pass (K relay
     off), and every workgroup quantizing its own operands (quantize pass off); tokens bit-exact either way
     (the default, K relay after the pass, is test_orpheus_wide_batch8)."""
+    if path == "kr_inkernel":  # the K relay with the prologue in every workgroup (K <= 4096)
+        hip.set_option(ttship.OPT["GEMV_KR_INKERNEL"], 4096)
+        try:
+            run_pair(hip, WIDE, 8, 2, 2)
+        finally:
+            hip.set_option(ttship.OPT["GEMV_KR_INKERNEL"], 0)
+        return
     opt = "GEMV_KRELAY" if path == "mf" else "GEMV_PREQUANT"
     hip.set_option(ttship.OPT[opt], 0)
     try:

@@ -501,6 +501,10 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_GEMV_KRELAY_LOOP: be->gemv_kr_loop = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_Q80_PRO: be->gemv_q80_pro = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_Q80_SLAB: be->gemv_q80_slab = value != 0; return 0;
+        case TTS_HIP_OPT_GEMV_KR_INKERNEL:
+            if (value < 0) return TTS_STATUS_BAD_ARG;
+            be->gemv_kr_ink = value;
+            return 0;
         case TTS_HIP_OPT_GEMM_Q8_STAGED:
             if (value < 0 || value > 2) return TTS_STATUS_BAD_ARG;
             be->gemm_q8_staged = value;

@@ -1127,7 +1127,10 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 // the next tile's weights are requested before the current tile's relay); otherwise one tile per
 // workgroup.  Terms and running sums are kept as row pairs (packed f32 ops, each element still one
 // rounded multiply / add).
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false>
+// PRO (PRO_QUANT / PRO_LN, K <= 4096): no operand pass -- the workgroup norms / quantizes the
+// activation itself (q4k_prologue, the MFMA operand layout k_quant_mf writes), its first weight loads
+// issued between the prologue's activation loads and their use.
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY>
 __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
     constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
     typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1160,14 +1163,6 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     auto tile_row0 = [&](int64_t t, int mat) { return SW ? t * 16 : t * 16 - job_roff(j, mat); };
 
     TTS_TS(j, 0);
-    // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
-    {
-        const int nck = (int)(bqb >> 10);
-        for (int i = wave; i < nck; i += nw)
-            __builtin_amdgcn_global_load_lds(gptr(bqt + (size_t)i * 1024 + lane * 16),
-                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
-    }
-    TTS_PIN_LOADS();
     u32x4 hd[LOOP ? 2 : 1][BPW], qa[LOOP ? 2 : 1][BPW], qb[LOOP ? 2 : 1][BPW];
     auto load_w = [&](auto BUF, int64_t t) __attribute__((always_inline)) {
         constexpr int bf = decltype(BUF)::value;
@@ -1204,7 +1199,18 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, LOOP ? 1 : 0>;
     int64_t t = blockIdx.x;
-    load_w(B0{}, t);
+    if constexpr (PRO == PRO_COPY) {
+        // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
+        const int nck = (int)(bqb >> 10);
+        for (int i = wave; i < nck; i += nw)
+            __builtin_amdgcn_global_load_lds(gptr(bqt + (size_t)i * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
+        TTS_PIN_LOADS();
+        load_w(B0{}, t);
+    } else {
+        auto first = [&]() __attribute__((always_inline)) { load_w(B0{}, t); };
+        q4k_prologue<PRO, 16, true, decltype(first)>(j, nb, nullptr, xd_s, nullptr, b16, sbs, first);
+    }
     TTS_TS(j, 1);
     __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
     TTS_TS(j, 2);
@@ -2302,6 +2308,12 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
         }
         const int64_t nb = j.K / QK_K;
         const int64_t bq = (((j.M * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+        if (j.K <= be->gemv_kr_ink && !j.dbg) {  // K relay with the prologue in every workgroup
+            GemvJob ji = j;
+            ji.bq = nullptr;
+            ji.bq_bytes = bq;
+            if (launch_q4k_kr(be, ji)) continue;
+        }
         if (be->gemv_mf_prequant && !j.dbg && (size_t)(bq + 4 * j.K * j.M) <= be->scratch_size) {
             // operands to the top of scratch (its bottom may hold this GEMV's staged input columns)
             j.bq = be->scratch + be->scratch_size - bq;
@@ -2322,28 +2334,32 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 
 // ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false>
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY>
 static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
+    if constexpr (!LANE && PRO == PRO_COPY) {  // in-kernel prologue (launch_q4k_kr decides)
+        if (j.pro == PRO_LN) return launch_q4k_kr_t<BPW, SW, NWT, false, LOOP, PRO_LN>(be, j, gx, gy);
+        if (j.pro == PRO_QUANT) return launch_q4k_kr_t<BPW, SW, NWT, false, LOOP, PRO_QUANT>(be, j, gx, gy);
+    }
     if constexpr (SW && !LOOP && BPW <= 3) {  // (BPW 4: the prefetch registers would spill)
         // SwiGLU pairs (8 waves, ~170 VGPRs: one workgroup per CU): more pairs than CUs run as one
         // workgroup per CU walking its pairs, operands copied once, the next pair's weights prefetched
         if (be->gemv_kr_loop && gx > (unsigned)be->cus && gy == 1) {
-            launch_q4k_kr_t<BPW, SW, NWT, LANE, true>(be, j, (unsigned)be->cus, gy);
+            launch_q4k_kr_t<BPW, SW, NWT, LANE, true, PRO>(be, j, (unsigned)be->cus, gy);
             return;
         }
     }
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>);
     const size_t lds = q4k_kr_lds(j.bq_tile ? j.bq_tile : j.bq_bytes, SW);
     const dim3 blk(64 * NWT * (SW ? 2 : 1));
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP>), dim3(gx, gy), blk, lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>), dim3(gx, gy), blk, lds, be->stream, j);
 }
 
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
@@ -2387,9 +2403,11 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job) {
     TTS_HIP_CHECK(hipGetLastError());
     return true;
 }
-// PRO_COPY jobs (operands in j.bq) whose row length has an instantiation; false otherwise
+// PRO_COPY jobs (operands in j.bq) whose row length has an instantiation; false otherwise.
+// PRO_QUANT / PRO_LN jobs (K <= 4096, j.bq_bytes = the operands' LDS size): the in-kernel prologue.
 static bool launch_q4k_kr(tts_hip_backend * be, const GemvJob & j) {
-    if (!be->gemv_kr || j.pro != PRO_COPY || j.M > 8) return false;
+    if (!be->gemv_kr || j.M > 8) return false;
+    if (j.pro != PRO_COPY && !((j.pro == PRO_QUANT || j.pro == PRO_LN) && j.K <= 4 * 1024 && !j.bq_tile)) return false;
     const bool sw = j.epi == EPI_SWIGLU;
     if (!sw) {
         for (int m = 0; m <= j.nmat; ++m)
@@ -2446,6 +2464,12 @@ static void launch_q4k_ks(tts_hip_backend * be, const GemvJob & j) {
     const unsigned gx = (unsigned)(T < 2048 ? T : 2048);
     const size_t lds = q4k_ks_lds(j.M, nb);
     const int64_t bq = (((j.M * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+    if (j.K <= be->gemv_kr_ink && !j.dbg) {  // K relay with the prologue in every workgroup
+        GemvJob ji = j;
+        ji.bq = nullptr;
+        ji.bq_bytes = bq;
+        if (launch_q4k_kr(be, ji)) return;
+    }
     if (be->gemv_mf_prequant && !j.dbg && (size_t)(bq + 4 * j.K * j.M) <= be->scratch_size &&
         (size_t)bq <= lds) {
         // the prologue as a pass of its own (k_quant_mf), the GEMV copying its operands (k_gemv_q4K_mf);
