@@ -143,6 +143,7 @@ struct Item {
     float lneps = 0.f;
     bool lnrms = false;
     bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
+    const tts_tensor * snake_one = nullptr;  // SNAKE: b == nullptr, recip = snake_one[0] / alpha in the kernel
     const tts_tensor * xsrc = nullptr;  // src1 is a skipped CONT of this contiguous tensor (same bytes): read its data
     bool shadow = false;    // ATTN: also write the private copy (be->shadow)
     int xattn = -1;         // GEMV: index of the short-context ATTN item whose query it produces (one launch)
@@ -1197,6 +1198,15 @@ struct Planner {
         it.kind = Item::SNAKE;
         it.x = x, it.w = alpha, it.b = R, it.dst = A;
         act[index[M1]] = act[index[S]] = act[index[Q]] = act[index[M2]] = -1;
+        // reciprocal() = DIV(broadcast view of a scalar, alpha) feeding only this snake (DAC, SNAC):
+        // the kernel divides itself (the same correctly rounded division) and the node is skipped
+        const tts_tensor * O = R->src[0];
+        if (R->op == TTS_OP_DIV && O && R->src[1] == alpha && sole_consumer(R) == M2 && index.count(R) && act[index[R]] == 0 &&
+            O->type == TTS_TYPE_F32 && O->ne[0] == 1 && O->nb[1] == 0 && O->ne[2] * O->ne[3] == 1 && !overlap(A, O)) {
+            it.b = nullptr;
+            it.snake_one = O;
+            act[index[R]] = -1;
+        }
         act[i] = add_item(std::move(it));
     }
 
@@ -2087,7 +2097,7 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::SNAKE:
-            launch_snake(be, it.dst, it.x, it.w, it.b);
+            launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one);
             return 0;
         case Item::CONV:
             launch_conv1d_fused(be, it.conv);

@@ -427,7 +427,9 @@ int launch_sample_step(tts_hip_backend * be, const float * logits, int B, int NH
                        int32_t * rep_state, int step, int bos, int eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
 constexpr int EMBED_MAX_TERMS = 16;
 void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n);
-void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip);
+// recip == nullptr: the kernel evaluates reciprocal() = one[0] / alpha[c] itself (`one` a broadcast scalar)
+void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
+                  const tts_tensor * one = nullptr);
 void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);
 int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);

@@ -142,12 +142,13 @@ void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * out, const floa
 // ADD(x, MUL(SQR(SIN(MUL(x, alpha))), recip)) in one pass instead of five, keeping each node's f32
 // rounding: m = x*a, s = sin(m) (correctly rounded), q = s*s, r = q*recip, y = x + r.  alpha and
 // recip are per-channel ([1, C]: one value per row of the [T, C] activation).
+// recip == nullptr: r = one / alpha[c], the DIV node of reciprocal() (util.cpp:86-94) evaluated here.
 template <int V>
 __global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, const float * __restrict__ alpha,
-                        const float * __restrict__ recip, int64_t n, int64_t ne0, int64_t nc) {
+                        const float * __restrict__ recip, const float * __restrict__ one, int64_t n, int64_t ne0, int64_t nc) {
     for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V; k < n; k += (int64_t)gridDim.x * blockDim.x * V) {
         const int64_t c = (k / ne0) % nc;
-        const float a = alpha[c], r = recip[c];
+        const float a = alpha[c], r = recip ? recip[c] : cr_divf(*one, a);
         float xv[V], y[V];
         if (V == 4) {
             const float4 t = *(const float4 *)(x + k);
@@ -165,7 +166,10 @@ __global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, 
     }
 }
 
-void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip) {
+void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
+                  const tts_tensor * one) {
+    const float * rp = recip ? (const float *)recip->data : nullptr;
+    const float * op = one ? (const float *)one->data : nullptr;
     const int64_t n = dst->ne[0] * dst->ne[1] * dst->ne[2] * dst->ne[3];
     const int64_t ne0 = x->ne[0], nc = alpha->ne[1];
     const bool v4 = ne0 % 4 == 0 && ((uintptr_t)dst->data % 16) == 0 && ((uintptr_t)x->data % 16) == 0;
@@ -173,10 +177,10 @@ void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor
     if (g > 65536) g = 65536;
     if (v4)
         hipLaunchKernelGGL(k_snake<4>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
-                           (const float *)alpha->data, (const float *)recip->data, n, ne0, nc);
+                           (const float *)alpha->data, rp, op, n, ne0, nc);
     else
         hipLaunchKernelGGL(k_snake<1>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
-                           (const float *)alpha->data, (const float *)recip->data, n, ne0, nc);
+                           (const float *)alpha->data, rp, op, n, ne0, nc);
     TTS_HIP_CHECK(hipGetLastError());
 }
 
