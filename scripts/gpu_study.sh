@@ -54,7 +54,7 @@ case "$1" in
     done; done ;;
   ar_trace)    # kernel trace of the AR-only bench (one replica of 8 prompts unless options say otherwise) + per-step breakdown
     shift
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/proft" -o run --output-format csv -- python3 "$R/bench.py" $AR --steps 60 "$@" > "$O/ar_trace.log" 2>&1) &&
+    (cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/proft" -o run --output-format csv -- python3 "$R/bench.py" $AR --steps 60 "$@" > "$O/ar_trace.log" 2>&1) &&
     f=$(find "$O/proft" -name "*kernel_trace.csv" | sort | tail -1) && python3 scripts/step_breakdown.py "$f" 5 30 > "$O/ar_breakdown.txt" && cat "$O/ar_breakdown.txt" | cut -c1-150 ;;
   orph_trace)  # kernel trace of the Orpheus leg + per-step breakdown (markers: the wide-vocabulary greedy step)
     shift
