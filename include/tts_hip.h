@@ -261,7 +261,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_DEBUG = 10, /* matrix-core GEMV phase study: 1 = skip the row phase, 2 = skip the prologue
                                      (results invalid; micro-benchmarks only) */
     TTS_HIP_OPT_CONV_SPLIT = 12, /* 1 (default) = codec convolutions over short sequences split their input channels
-                                     over extra workgroups (f64 partial sums, reduced in split order); 0 = never */
+                                     over extra workgroups (f64 partial sums, reduced in split order) until a launch
+                                     has ~512 workgroups; N > 1 = until ~N workgroups; 0 = never */
     TTS_HIP_OPT_GEMV_UNIQUE = 11, /* 1 (default) = lane-layout Q4_K GEMVs run the unique-load kernel (an octet per
                                      (row, block), every weight byte loaded once, all columns per lane, ggml's chain
                                      finished from LDS: bit-identical); 0 = the octet-per-(row, column) kernel */

@@ -8,6 +8,7 @@ import ttship  # noqa: E402
 import torch  # noqa: E402
 
 T = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+SPLITS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else []  # CONV_SPLIT targets to compare
 be = ttship.HipBackend(0)
 cfg = ttship.dac_config(max_frames=T)
 dac = ttship.Dac(be.iface(), cfg)
@@ -20,4 +21,14 @@ for graphs in (1, 0, 1):
     for _ in range(10):
         t0 = time.perf_counter(); dac.decode(codes); ts.append(time.perf_counter() - t0)
     print(json.dumps({"frames": T, "graphs": graphs, "ms_min": round(1e3 * min(ts), 3), "ms_med": round(1e3 * float(np.median(ts)), 3)}), flush=True)
+ref = dac.decode(codes).copy()
+for sp in SPLITS:
+    be.set_option(ttship.OPT["CONV_SPLIT"], sp)
+    for _ in range(3):
+        pcm = dac.decode(codes)
+    ts = []
+    for _ in range(10):
+        t0 = time.perf_counter(); pcm = dac.decode(codes); ts.append(time.perf_counter() - t0)
+    print(json.dumps({"frames": T, "conv_split": sp, "ms_min": round(1e3 * min(ts), 3), "ms_med": round(1e3 * float(np.median(ts)), 3),
+                      "max_abs_vs_default": float(np.max(np.abs(pcm - ref)))}), flush=True)
 dac.close()

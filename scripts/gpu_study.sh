@@ -52,6 +52,13 @@ case "$1" in
           --dac-workers $w --dac-conv-split $sp > "$O/ds_${w}_$sp.log" 2>&1 &&
       python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('workers $w split $sp', d['value'], d['ar_ms_per_step'], d['dac_audio_sec_per_s'])" "$O/ds_${w}_$sp.log" || exit 1
     done; done ;;
+  conv_split)  # split-conv workgroup target: one 20-frame DAC decode, then the driver's short line
+    timeout -k 10 200 python3 scripts/dac_host_probe.py 20 1,768,1024,1536,2048 > "$O/conv_split_dac1.jsonl" 2>&1 && cat "$O/conv_split_dac1.jsonl" &&
+    for sp in ${@:2}; do
+      timeout -k 10 200 python3 bench.py --steps 20 --no-cpu-baseline --kokoro-prompts 0 --orpheus-steps 0 --dia-steps 0 --b1-replicas 0 \
+          --dac-conv-split $sp > "$O/cs_$sp.log" 2>&1 &&
+      python3 -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);print('split $sp', d['value'], d['ar_ms_per_step'], d['dac_audio_sec_per_s'])" "$O/cs_$sp.log" || exit 1
+    done ;;
   ar_trace)    # kernel trace of the AR-only bench (one replica of 8 prompts unless options say otherwise) + per-step breakdown
     shift
     (cd /tmp && export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 && timeout -k 10 300 rocprofv3 --kernel-trace -d "$O/proft" -o run --output-format csv -- python3 "$R/bench.py" $AR --steps 60 "$@" > "$O/ar_trace.log" 2>&1) &&

@@ -482,7 +482,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
     switch (option) {
         case TTS_HIP_OPT_FUSION: be->fusion = value; return 0;
         case TTS_HIP_OPT_CONVT_LDS: be->convt_lds = value != 0; return 0;
-        case TTS_HIP_OPT_CONV_SPLIT: be->conv_split = value != 0; return 0;
+        case TTS_HIP_OPT_CONV_SPLIT: be->conv_split = value < 0 ? 1 : value; return 0;
         case TTS_HIP_OPT_PROFILE_GEMV: be->profile_gemv = value != 0; return 0;
         case TTS_HIP_OPT_GRAPHS: be->use_graphs = value != 0; return 0;
         case TTS_HIP_OPT_CONV_F32ACC:

@@ -353,7 +353,7 @@ struct tts_hip_backend {
     // tiles alone would leave most CUs idle), summed in split order by a second pass
     double * conv_part = nullptr;
     size_t conv_part_doubles = 0;
-    int conv_split = 1;  // TTS_HIP_OPT_CONV_SPLIT: 1 = split short convolutions, 0 = never
+    int conv_split = 1;  // TTS_HIP_OPT_CONV_SPLIT: 1 = split short convolutions to ~512 workgroups, N > 1 = to ~N, 0 = never
     int fusion = 0x3FFF;  // bitmask of TTS_FUSE_* patterns (all on)
     bool profile_gemv = false;
     double gemv_ms[TTS_TYPE_COUNT] = {0};

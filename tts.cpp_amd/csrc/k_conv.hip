@@ -223,8 +223,10 @@ __global__ __launch_bounds__(256) void k_split_reduce(const double * __restrict_
 // workgroups to fill the chip (~2 per CU) while each split keeps >= `minlen` of the reduction and
 // the partials fit the scratch.  Returns 1 (no split) for grids that already fill the chip.
 static int split_count(const tts_hip_backend * be, int64_t tiles, int64_t K, int64_t minlen, int64_t outs) {
-    if (!be->conv_split || tiles >= 256) return 1;
-    int64_t z = (512 + tiles - 1) / tiles;
+    // aim for `target` workgroups (2 per CU by default; TTS_HIP_OPT_CONV_SPLIT > 1 sets it)
+    const int64_t target = be->conv_split > 1 ? be->conv_split : 512;
+    if (!be->conv_split || 2 * tiles >= target) return 1;
+    int64_t z = (target + tiles - 1) / tiles;
     const int64_t zk = K / minlen;
     if (z > zk) z = zk;
     const int64_t zm = outs > 0 ? (int64_t)(be->conv_part_doubles / (size_t)outs) : 1;
