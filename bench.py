@@ -312,7 +312,9 @@ def parler_b1_leg(args, rank, local, new_backend):
     `b1_replicas` runners, each on its own backend (HIP stream) driven by its own host thread, all
     prefilled to the same KV length; beside the headline's lock-step batches."""
     R, steps = args.b1_replicas, args.b1_steps
-    cfg = ttship.parler_config(batch=1, max_ctx=args.ctx + steps + args.warmup + 64)
+    # the same KV capacity rule as the lock-step leg: a multiple of 4 positions keeps every V row
+    # 16-B aligned, so P.V takes its vector-load kernel (k_attn_pv<true, ...>)
+    cfg = ttship.parler_config(batch=1, max_ctx=max(4096, args.ctx + steps + args.warmup + 64))
     bes = [new_backend() for _ in range(R)]
     runs = [ttship.Parler(b.iface(), cfg) for b in bes]
     try:
