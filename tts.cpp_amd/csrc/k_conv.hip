@@ -321,6 +321,7 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
     if (threadIdx.x == 0) xs[zslot] = 0.f;
     __syncthreads();
     const int wr0 = (wave >> 1) * 32, wc0 = (wave & 1) * 32;  // wave's oc / ol offsets in the tile
+    const bool wave_live = oc0 + wr0 < a.OC && ol0 + wc0 < a.OL;  // wave-uniform
     f64x4_t acc[2][2] = {};
     const int64_t base = ol0 * s - a.p;
     // Staging: thread t owns x-window elements e = t + 256u (u < CONV1D_XN) and kernel-slice
@@ -388,6 +389,12 @@ __global__ __launch_bounds__(256) void k_conv1d_f64(Conv1dArgs a) {
             }
         __syncthreads();
         if (ic0 + icc < ic_hi) fetch(ic0 + icc);
+        // a wave whose 32 x 32 sub-tile lies wholly past the last output channel or position (OC = 96
+        // or OC = 1 tiles, short sequences) only stages operands: its MFMAs would feed no store
+        if (!wave_live) {
+            __syncthreads();
+            continue;
+        }
         // batches of 8 reduction quads: every operand of the batch is read from LDS first (the
         // offset-table reads, then the dependent operand reads, all independent of each other),
         // then 32 MFMAs issue back to back
