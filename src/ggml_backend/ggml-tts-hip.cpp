@@ -149,10 +149,16 @@ void buf_set(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t
     // a whole Q4_K tensor is a weight (nothing else in TTS.cpp is Q4_K): the backend's own layouts
     if (t->type == GGML_TYPE_Q4_K && offset == 0 && size == ggml_nbytes(t) && !t->view_src) {
         tts_tensor w = weight_view(t);
-        if (tts_hip_weight_set(c->be, &w, data) == 0) {
-            std::lock_guard<std::mutex> lk(c->mu);
+        const int st = tts_hip_weight_set(c->be, &w, data);
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (st == 0) {
             c->layout[t->data] = w.flags & (TTS_FLAG_REPACKED | TTS_FLAG_TILED | TTS_FLAG_TILED_COPY);
+            return;
         }
+        // no backend layout (e.g. the tiled copy could not be allocated): the native bytes, no flags,
+        // so the weight is never left as uninitialised device memory (set_tensor cannot report failure)
+        c->layout.erase(t->data);
+        if (tts_hip_tensor_set(c->be, t->data, data, size) != 0) GGML_ABORT("tts-hip: set_tensor of the weight %s failed", t->name);
         return;
     }
     if (c->flags_of(t->data) && !(offset == 0 && size == ggml_nbytes(t))) {
@@ -181,8 +187,11 @@ void buf_get(ggml_backend_buffer_t b, const ggml_tensor * t, void * data, size_t
 
 bool buf_cpy(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tensor * dst) {
     if (!src->buffer || src->buffer->buft->iface.get_name != b->buft->iface.get_name) return false;
-    auto * c = (BufCtx *)b->context;
-    if (c->flags_of(src->data) || c->flags_of(dst->data)) return false;  // layouts: let ggml go through the host
+    auto * c = (BufCtx *)b->context;  // the destination's buffer
+    // each tensor's layout flags live in its own buffer's map (the source may be another TTS-HIP
+    // buffer); a weight in a backend layout goes through the host (ggml's get + set fallback)
+    const int32_t fs = ((BufCtx *)src->buffer->context)->flags_of(src->data);
+    if (fs || c->flags_of(dst->data)) return false;
     tts_hip_tensor_copy(c->be, dst->data, src->data, ggml_nbytes(src));
     tts_hip_synchronize(c->be);
     return true;

@@ -123,6 +123,18 @@ def test_malformed_files_are_rejected(tmp_path):
     raw = good.read_bytes()
     cases = {"magic": b"GGUX" + raw[4:], "version": raw[:4] + struct.pack("<I", 9) + raw[8:],
              "truncated_kv": raw[:30], "truncated_data": raw[:-8], "empty": b""}
+    # tensor info of "t": name (u64 length + bytes), n_dims u32, ne[0] i64, type u32, offset u64
+    ti = raw.index(struct.pack("<Q", 1) + b"t") + 9
+    ne_at, off_at = ti + 4, ti + 4 + 8 + 4
+
+    def patch(at, fmt, v):
+        return raw[:at] + struct.pack(fmt, v) + raw[at + struct.calcsize(fmt):]
+    # an aligned offset near 2^64: data_offset + offset + size wraps past the mapping check
+    cases["huge_offset"] = patch(off_at, "<Q", (1 << 64) - 32)
+    cases["offset_past_end"] = patch(off_at, "<Q", 1 << 20)
+    # 2^62 F32 elements: the byte size overflows 64 bits
+    cases["huge_ne"] = patch(ne_at, "<q", 1 << 62)
+    cases["huge_ne_2"] = patch(ne_at, "<q", (1 << 63) - 1)
     for name, data in cases.items():
         p = tmp_path / f"{name}.gguf"
         p.write_bytes(data)

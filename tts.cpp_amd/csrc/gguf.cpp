@@ -170,11 +170,31 @@ int64_t tts_gguf_blck_size(int32_t type) {
     }
 }
 
+// Element count of ne[0..3] (each >= 0), or -1 when the product would not fit int64 (ggml's gguf
+// reader rejects such files the same way: INT64_MAX / ne[1] / ne[2] / ne[3] bounds).
+static int64_t checked_nelements(const int64_t * ne) {
+    int64_t n = 1;
+    for (int d = 0; d < 4; ++d) {
+        if (ne[d] < 0) return -1;
+        if (ne[d] == 0) return 0;
+        if (n > INT64_MAX / ne[d]) return -1;
+        n *= ne[d];
+    }
+    return n;
+}
+
+// bytes of a tensor, or 0 for an unknown type / ragged blocks / a size that overflows 64 bits
 static uint64_t tensor_bytes(int32_t type, const int64_t * ne) {
     const size_t ts = tts_gguf_type_size(type);
     const int64_t bs = tts_gguf_blck_size(type);
-    if (!ts || !bs || ne[0] % bs) return 0;
-    return (uint64_t)(ne[0] / bs) * ts * (uint64_t)ne[1] * (uint64_t)ne[2] * (uint64_t)ne[3];
+    if (!ts || !bs || ne[0] % bs || checked_nelements(ne) < 0) return 0;
+    uint64_t b = (uint64_t)(ne[0] / bs);
+    const uint64_t f[4] = {(uint64_t)ts, (uint64_t)ne[1], (uint64_t)ne[2], (uint64_t)ne[3]};
+    for (uint64_t v : f) {
+        if (v && b > UINT64_MAX / v) return 0;
+        b *= v;
+    }
+    return b;
 }
 
 tts_gguf * tts_gguf_open(const char * path) {
@@ -264,8 +284,10 @@ tts_gguf * tts_gguf_open(const char * path) {
         if (!c.ok) return fail("truncated tensor info");
         for (int d = 0; d < 4; ++d)
             if (t.ne[d] < 0) return fail("negative dimension");
+        const int64_t nel = checked_nelements(t.ne);
+        if (nel < 0) return fail("element count overflows int64");
         t.size = tensor_bytes(t.type, t.ne);
-        if (t.size == 0 && t.ne[0] * t.ne[1] * t.ne[2] * t.ne[3] != 0) return fail("unknown tensor type or ragged blocks");
+        if (t.size == 0 && nel != 0) return fail("unknown tensor type, ragged blocks or size overflow");
         if (t.offset % g->alignment) return fail("unaligned tensor offset");
         if (g->tensor_index.count(t.name)) return fail("duplicate tensor name");
         g->tensor_index[t.name] = (int64_t)g->tensors.size();
@@ -273,8 +295,11 @@ tts_gguf * tts_gguf_open(const char * path) {
     }
     const uint64_t hdr = (uint64_t)(c.p - (const uint8_t *)map);
     g->data_offset = (hdr + g->alignment - 1) / g->alignment * g->alignment;
+    // overflow-safe: each term is compared with what is left of the mapping, never summed first
+    if (!g->tensors.empty() && g->data_offset > g->map_size) return fail("tensor data past the end of the file");
+    const uint64_t avail = g->data_offset > g->map_size ? 0 : g->map_size - g->data_offset;
     for (auto & t : g->tensors)
-        if (g->data_offset + t.offset + t.size > g->map_size) return fail("tensor data past the end of the file");
+        if (t.offset > avail || t.size > avail - t.offset) return fail("tensor data past the end of the file");
     return g;
 }
 
@@ -633,6 +658,11 @@ int tts_gguf_quantize(const char * in_path, const char * out_path, const tts_qua
         uint64_t size = tts_gguf_tensor_size(g, i);
         if (rule > 0 && type != TTS_TYPE_F32) {  // :248-253 / :266-271
             fprintf(stderr, "gguf quantize: tensor '%s' must be F32 to be converted (type %d)\n", name.c_str(), type);
+            st = TTS_STATUS_BAD_ARG;
+            break;
+        }
+        if (rule > 0 && n == 0) {  // the reader bounds n (int64, inside the mapping); an empty row cannot be converted
+            fprintf(stderr, "gguf quantize: tensor '%s' to be converted is empty\n", name.c_str());
             st = TTS_STATUS_BAD_ARG;
             break;
         }

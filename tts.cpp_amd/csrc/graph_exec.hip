@@ -649,6 +649,10 @@ struct Planner {
         if (iS <= i || iU <= i || iE <= iS || iE <= iU || act[iS] || act[iU] || act[iE]) return false;
         for (int k = iU + 1; k < iE; ++k)
             if (k != iS && !(is_view(nodes[k]->op) && act[k] == 0)) return false;
+        // G is read back by U's epilogue: nothing between G and U (the SILU aside) may write over it
+        // (the allocator frees G's memory after the SILU, so a later node could be placed there)
+        for (int k = i + 1; k < iU; ++k)
+            if (k != iS && !is_view(nodes[k]->op) && overlap(nodes[k], G)) return false;
         Item g;
         g.kind = Item::GEMV;
         g.mms = {G};

@@ -653,11 +653,22 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
     int32_t * d_next = (int32_t *)be.alloc(be.ctx, rowi);
     int32_t * d_hist = (int32_t *)be.alloc(be.ctx, rowi * (size_t)n_steps);
     int32_t * d_rep = p->sampling ? (int32_t *)be.alloc(be.ctx, 2 * rowi) : nullptr;
-    if (!d_seen || !d_next || !d_hist || (p->sampling && !d_rep)) return TTS_STATUS_ALLOC_FAILED;
+    // every exit frees whatever was allocated
+    auto release = [&] {
+        for (int32_t * q : {d_rep, d_seen, d_next, d_hist})
+            if (q) be.free(be.ctx, q);
+    };
+    if (!d_seen || !d_next || !d_hist || (p->sampling && !d_rep)) {
+        release();
+        return TTS_STATUS_ALLOC_FAILED;
+    }
     std::vector<int32_t> rep(2 * (size_t)B * NH);
     if (p->sampling) {
         for (size_t r = 0; r < (size_t)B * NH; ++r) rep[2 * r] = p->rep_last[r], rep[2 * r + 1] = p->rep_count[r];
-        if (be.set(be.ctx, d_rep, rep.data(), 2 * rowi) != 0) return TTS_STATUS_FAILED;
+        if (be.set(be.ctx, d_rep, rep.data(), 2 * rowi) != 0) {
+            release();
+            return TTS_STATUS_FAILED;
+        }
     }
     std::vector<int32_t> seen((size_t)B * NH), next((size_t)B * NH);
     for (int b = 0; b < B; ++b)
@@ -690,10 +701,7 @@ static int generate_device(tts_parler * p, int32_t n_steps, int32_t * tokens_out
         st = be.get(be.ctx, rep.data(), d_rep, 2 * rowi);
         for (size_t r = 0; r < (size_t)B * NH; ++r) p->rep_last[r] = rep[2 * r], p->rep_count[r] = rep[2 * r + 1];
     }
-    if (d_rep) be.free(be.ctx, d_rep);
-    be.free(be.ctx, d_seen);
-    be.free(be.ctx, d_next);
-    be.free(be.ctx, d_hist);
+    release();
     if (st != 0) return st;
     for (int s = 0; s < n_steps; ++s)
         for (int b = 0; b < B; ++b)
