@@ -20,7 +20,9 @@ CPP_SRCS := $(wildcard $(SRC)/*.cpp)
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJ)/%.hip.o,$(HIP_SRCS))
 CPP_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJ)/%.cpp.o,$(CPP_SRCS))
 
-all: $(OUT)/libtts_hip.so oracle/_build/liboracle.so
+HARNESS := tests/ggml_stub/_build/libtts_ggml_harness.so
+
+all: $(OUT)/libtts_hip.so oracle/_build/liboracle.so $(HARNESS)
 
 # k_gemv: MFMA results straight into VGPRs (the Q8_0 GEMM issues a block's MFMAs back to back instead of
 # funnelling each through one AGPR quad)
@@ -70,4 +72,13 @@ endif
 adapter-check:
 	g++ -std=c++17 -fsyntax-only -Wall -Wextra -Itests/ggml_stub -Iinclude -Isrc/ggml_backend src/ggml_backend/ggml-tts-hip.cpp
 
-.PHONY: ggml-adapter adapter-check
+# the adapter built against the runtime stand-in (tests/ggml_stub) + a tts_backend_iface that drives its
+# vtables: test infrastructure for tests/test_adapter_gpu.py (the runners run on top of the adapter)
+$(HARNESS): src/ggml_backend/ggml-tts-hip.cpp src/ggml_backend/ggml-tts-hip.h $(wildcard tests/ggml_stub/*.h) \
+            tests/ggml_stub/ggml_runtime.cpp tests/ggml_stub/adapter_harness.cpp include/tts_hip.h $(OUT)/libtts_hip.so
+	@mkdir -p $(dir $@)
+	g++ -std=c++17 -O2 -fPIC -shared -Wall -Wno-stringop-truncation -Itests/ggml_stub -Iinclude -Isrc/ggml_backend src/ggml_backend/ggml-tts-hip.cpp \
+	    tests/ggml_stub/ggml_runtime.cpp tests/ggml_stub/adapter_harness.cpp -L$(OUT) -ltts_hip -Wl,-rpath,'$$ORIGIN/../../../$(OUT)' -o $@
+adapter-harness: $(HARNESS)
+
+.PHONY: ggml-adapter adapter-check adapter-harness

@@ -22,6 +22,7 @@ struct ggml_backend_dev_props {
     struct ggml_backend_dev_caps caps;
 };
 enum ggml_backend_buffer_usage ggml_backend_buffer_get_usage(ggml_backend_buffer_t buffer);
+void ggml_backend_buffer_free(ggml_backend_buffer_t buffer);
 bool ggml_backend_buffer_is_host(ggml_backend_buffer_t buffer);
 #ifdef __cplusplus
 }

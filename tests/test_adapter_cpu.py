@@ -17,6 +17,23 @@ def test_adapter_compiles_against_ggml_declarations():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_adapter_harness_builds_and_exports():
+    """The adapter linked with the runtime stand-in (tests/ggml_stub) for tests/test_adapter_gpu.py."""
+    import ctypes
+    r = subprocess.run(["make", "-s", "-C", str(ROOT), "adapter-harness"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ttship.lib()
+    h = ctypes.CDLL(str(ROOT / "tests" / "ggml_stub" / "_build" / "libtts_ggml_harness.so"))
+    for name in ["tts_ggml_harness_create", "tts_ggml_harness_iface", "tts_ggml_harness_free", "tts_ggml_harness_stats",
+                 "tts_ggml_harness_hostleaf_supported", "ggml_backend_tts_hip_reg", "ggml_backend_tts_hip_init",
+                 "ggml_backend_tts_hip_buffer_type", "ggml_backend_is_tts_hip", "ggml_backend_tts_hip_register_custom"]:
+        assert hasattr(h, name), name
+    # no device here: the registry reports zero devices and the harness refuses to start
+    h.tts_ggml_harness_create.restype = ctypes.c_void_p
+    if ttship.lib().tts_hip_device_count() == 0:
+        assert not h.tts_ggml_harness_create(0, 1)
+
+
 def test_adapter_uses_exported_abi_only():
     import ctypes
     lib = ctypes.CDLL(str(ttship.LIB_PATH))

@@ -2,7 +2,9 @@
 // (one per runner, as TTS.cpp's server runs one runner per worker thread:
 // /root/reference/examples/server/server.cpp:316-321).
 #include <cmath>
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "hip_internal.h"
@@ -29,6 +31,25 @@ static const size_t kLstmFloats = 4u << 20;
 static const size_t kAttnFloats = 4u << 20;  // split attention scores: e.g. B 8 x H 16 x P 4096 = 512K floats
 static const size_t kVecScratchFloats = 1u << 18;  // per-channel vectors staged by fused items (AdaIN)
 static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tensor_async   // 16 MB: e.g. 2 chains of Hd 256 x T 8191
+
+// Process-wide registries: the live tts_hip_buffer_alloc ranges and the tile-layout copies of
+// medium lane-layout Q4_K weights, keyed by device address.  A weight buffer may be allocated and
+// written through one backend and read by the graphs of another (the ggml adapter allocates through
+// a utility backend, every ggml_backend computes on its own stream), so neither is per backend.
+namespace {
+std::mutex g_reg_mu;
+std::unordered_map<const void *, size_t> g_buffers;      // base -> bytes
+std::unordered_map<const void *, uint8_t *> g_tiled;     // weight -> its tile-layout copy
+std::atomic<size_t> g_tiled_n{0};
+}  // namespace
+
+namespace tts {
+const uint8_t * tiled_copy_find(const void * w) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_tiled.find(w);
+    return it == g_tiled.end() ? nullptr : it->second;
+}
+}  // namespace tts
 
 extern "C" {
 
@@ -96,8 +117,6 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     for (auto e : be->pin_events) hipEventDestroy(e);
     for (auto e : be->plan_ev) hipEventDestroy(e);
     hipHostFree(be->pin);
-    for (auto & kv : be->tiled_copy) hipFree(kv.second);  // tile-layout copies of medium Q4_K weights
-    be->tiled_copy.clear();
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->argmax_keys);
@@ -180,44 +199,58 @@ void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {
     hipSetDevice(be->device);
     void * p = nullptr;
     if (hipMalloc(&p, size ? size : 256) != hipSuccess) return nullptr;
-    be->buffers[p] = size ? size : 256;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_buffers[p] = size ? size : 256;
     return p;
 }
 
 // Tile-layout copies of weights inside [p, p + n): freed when their weight buffer goes away or its
 // bytes are overwritten by a plain tensor_set (a stale copy must never be read: run_gemv_item aborts
-// on a TILED_COPY weight whose copy is gone instead).
-static void drop_tiled_copies(tts_hip_backend_t be, const void * p, size_t n) {
+// on a TILED_COPY weight whose copy is gone instead).  The device is synchronised first: a graph on
+// any stream may still read a copy.
+static void drop_tiled_copies(const void * p, size_t n) {
+    if (g_tiled_n.load(std::memory_order_acquire) == 0) return;
     const char * a = (const char *)p;
-    bool synced = false;
-    for (auto it = be->tiled_copy.begin(); it != be->tiled_copy.end();) {
-        const char * k = (const char *)it->first;
-        if (k >= a && k < a + n) {
-            if (!synced) hipStreamSynchronize(be->stream), synced = true;
-            hipFree(it->second);
-            it = be->tiled_copy.erase(it);
-        } else {
-            ++it;
+    std::vector<uint8_t *> dead;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        for (auto it = g_tiled.begin(); it != g_tiled.end();) {
+            const char * k = (const char *)it->first;
+            if (k >= a && k < a + n) {
+                dead.push_back(it->second);
+                it = g_tiled.erase(it);
+            } else {
+                ++it;
+            }
         }
+        g_tiled_n.store(g_tiled.size(), std::memory_order_release);
     }
+    if (dead.empty()) return;
+    hipDeviceSynchronize();
+    for (uint8_t * c : dead) hipFree(c);
 }
 
 void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
     if (!be || !ptr) return;
     hipSetDevice(be->device);
     hipStreamSynchronize(be->stream);
-    auto b = be->buffers.find(ptr);
-    if (b != be->buffers.end()) {
-        drop_tiled_copies(be, ptr, b->second);
-        be->buffers.erase(b);
+    size_t n = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_reg_mu);
+        auto b = g_buffers.find(ptr);
+        if (b != g_buffers.end()) {
+            n = b->second;
+            g_buffers.erase(b);
+        }
     }
+    if (n) drop_tiled_copies(ptr, n);
     hipFree(ptr);
 }
 
 int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
-    if (!be->tiled_copy.empty()) drop_tiled_copies(be, dst, size);
+    drop_tiled_copies(dst, size);
     // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
     if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
     if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
@@ -375,6 +408,11 @@ static size_t tensor_bytes(const tts_tensor * t) {
 int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
     if (!be || !t) return TTS_STATUS_BAD_ARG;
     const size_t n = tensor_bytes(t);
+    // fault injection for the callers' failure paths (tests/test_adapter_gpu.py): no layout is written
+    if (t->type == TTS_TYPE_Q4_K) {
+        const char * f = getenv("TTS_HIP_FAULT_WEIGHT_SET");
+        if (f && f[0] == '1') return TTS_STATUS_ALLOC_FAILED;
+    }
     if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0 && t->ne[1] % 4 == 0 && t->ne[2] == 1 && t->ne[3] == 1 &&
         be->q4k_tile_bytes > 0 && (int64_t)n >= be->q4k_tile_bytes) {
         // large matrix: the matrix-core GEMV's tile layout
@@ -397,8 +435,15 @@ int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
             tts_repack_q4_K_tiled(src, tmp.data(), t->ne[1], t->ne[0] / 256, 0);
             uint8_t * cp = nullptr;
             if (hipMalloc((void **)&cp, n) != hipSuccess) return TTS_STATUS_ALLOC_FAILED;
-            if (hipMemcpy(cp, tmp.data(), n, hipMemcpyHostToDevice) != hipSuccess) return TTS_STATUS_FAILED;
-            be->tiled_copy[t->data] = cp;
+            if (hipMemcpy(cp, tmp.data(), n, hipMemcpyHostToDevice) != hipSuccess) {
+                hipFree(cp);
+                return TTS_STATUS_FAILED;
+            }
+            {
+                std::lock_guard<std::mutex> lk(g_reg_mu);
+                g_tiled[t->data] = cp;
+                g_tiled_n.store(g_tiled.size(), std::memory_order_release);
+            }
             t->flags |= TTS_FLAG_TILED_COPY;
         }
         return st;

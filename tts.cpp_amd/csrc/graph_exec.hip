@@ -1877,12 +1877,12 @@ static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, in
 
 static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a, bool tiled_copy = false) {
     if (tiled_copy) {
-        auto c = be->tiled_copy.find(a->data);
-        if (c == be->tiled_copy.end()) {
+        const uint8_t * c = tiled_copy_find(a->data);
+        if (!c) {
             fprintf(stderr, "tts_hip: missing tile-layout copy of %s\n", a->name);
             abort();
         }
-        return c->second;
+        return c;
     }
     if (a->type != TTS_TYPE_Q4_K || (a->flags & TTS_FLAG_REPACKED)) return a->data;
     // Q4_K matrix written with plain tensor_set (native ggml layout): repack into a temp

@@ -317,10 +317,12 @@ struct tts_hip_backend {
     // weight_set: lane-layout Q4_K matrices of >= this size (and below q4k_tile_bytes) also keep a
     // tile-layout copy (TTS_FLAG_TILED_COPY); GEMVs of >= 8 columns read it (0 = never)
     int64_t q4k_dual_bytes = 1 << 20;
-    std::unordered_map<const void *, uint8_t *> tiled_copy;
+    // (the tile-layout copies and the live buffer ranges are process-wide, tiled_copy_find: a weight
+    // buffer is allocated and written through one backend and read by the graphs of others -- the
+    // ggml adapter's buffer type allocates through a utility backend, each ggml_backend computes on
+    // its own stream)
     void * sample_cand = nullptr;  // wide-vocabulary sampling candidates (k_sample.hip)
     size_t sample_cand_size = 0;
-    std::unordered_map<const void *, size_t> buffers;  // live tts_hip_buffer_alloc ranges (base -> bytes)
     // KV prefetch of the next attention into MALL on a side stream (0 = off; else min KV length)
     int kv_prefetch_minp = 0;  // measured slower (Parler B = 8: 2.04 -> 2.53..3.16 ms/step), off by default
     int kv_prefetch_blocks = 128;
@@ -389,6 +391,10 @@ struct tts_hip_backend {
 };
 
 namespace tts {
+
+// ---- process-wide weight registry (backend.hip) ----
+// The tile-layout copy of a lane-layout Q4_K weight (TTS_FLAG_TILED_COPY), or null.
+const uint8_t * tiled_copy_find(const void * weight);
 
 // ---- launchers (k_gemv.hip) ----
 // Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
