@@ -449,8 +449,9 @@ def main():
     if R < 1 or args.batch % R:
         raise SystemExit(f"--replicas {R} must divide --batch {args.batch}")
     bl = args.batch // R  # prompts per replica
+    # the compute arena holds the prompt pass too (attention scores [ctx, ctx, H, prompts]): 4 GiB per 8 prompts
     cfg = ttship.parler_config(batch=bl, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
-                               arena_bytes=4 << 30)
+                               arena_bytes=max(4, (bl + 7) // 8 * 4) << 30)
     def new_backend():
         rb = ttship.HipBackend(local)
         if args.no_fusion:

@@ -309,6 +309,9 @@ enum tts_hip_option {
                                      64 x 128 output tiles, 1 = over 64 x 64 tiles, 0 = the direct-load kernel */
     TTS_HIP_OPT_GEMV_KR_INKERNEL = 31, /* K-relay Q4_K GEMVs with K <= value (<= 4096) norm / quantize the activation in every
                                      workgroup instead of after the operand pass (0 = always the operand pass) */
+    TTS_HIP_OPT_GEMV_F32_WIDE = 32, /* 1 (default): F32 MUL_MATs of >= 2048 rows x 9..64 columns (the output heads of a
+                                       many-prompt step) run the wide GEMV (one sequential f64 chain per output, each
+                                       weight read once) instead of the tiled GEMM; 0 = tiled GEMM */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
 };

@@ -76,6 +76,19 @@ def test_q4_K_prefill_gemm(hip, tiled, K, N, M):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N,M", [(1024, 64, 12000), (4096, 32, 3000)])
+def test_q4_K_prefill_gemm_column_chunks(hip, K, N, M):
+    """A prompt pass over many prompts (64 prompts x 448 tokens) has more columns than the 64 MiB operand
+    area holds: the GEMM runs in passes over column chunks of whole 16-column tiles, bit-identical."""
+    rng = np.random.default_rng(K + N + M)
+    w = helpers.rand_q4_K(rng, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+    got = run_gpu(hip, ttship.Q4_K, w, x, N)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+
+
 Q80_PATHS = {"slab_pro": (1, 1, 0), "slab": (1, 0, 0), "rows_pro": (0, 1, 0), "rows": (0, 0, 0), "slab_rw1": (1, 1, 1),
              "slab_rw32": (1, 0, 32)}
 

@@ -148,6 +148,28 @@ def test_mul_mat_f32_gemm(hip, K, N, M, epi):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,N,M", [(1024, 9792, 32), (1024, 2176, 9), (1000, 4100, 16), (1024, 3000, 17), (512, 2048, 33),
+                                   (1024, 2304, 64), (130, 5000, 24)])
+@pytest.mark.parametrize("epi", [None, "GELU", "ADD"])
+def test_mul_mat_f32_wide(hip, K, N, M, epi):
+    """Many-row float MUL_MATs with 9..64 columns (the output heads of a 32-prompt step) run the wide
+    GEMV (k_gemv_f32_wide: one ascending-k f64 chain per output, ggml_vec_dot_f32's order), K tails and
+    row remainders included: bit-identical to the oracle."""
+    a = rnd(31, N, K, scale=0.2)
+    b = rnd(32, M, K)
+    r = rnd(33, M, N)
+
+    def build(g):
+        mm = g.node("MUL_MAT", F32, [N, M], [g.leaf(a), g.leaf(b)])
+        if epi == "GELU":
+            return [g.node("UNARY", F32, [N, M], [mm], params=[5])]
+        if epi == "ADD":
+            return [g.node("ADD", F32, [N, M], [mm, g.leaf(r)])]
+        return [mm]
+    assert_bits(run_both(hip, build), f"wide gemv {epi}")
+
+
+@pytest.mark.gpu
 def test_custom_maps(hip):
     """The reference's CPU callbacks restated on the device: cfg_scale (MAP_CUSTOM2, Dia) and
     uv_noise_compute (MAP_CUSTOM3, Kokoro, host draws and device-hashed draws)."""

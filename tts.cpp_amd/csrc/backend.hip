@@ -592,6 +592,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
             return 0;
         }
         case TTS_HIP_OPT_BGEMM_F32: be->bgemm_f32 = value != 0; return 0;
+        case TTS_HIP_OPT_GEMV_F32_WIDE: be->gemv_f32_wide = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;

@@ -1854,6 +1854,33 @@ struct Planner {
 
 }  // namespace
 
+// Backend scratch of at least `bytes` (eager launches only).  Prompt passes over many prompts stage
+// column copies larger than the default 64 MiB (Parler, 64 prompts x 448 tokens x 4096: 470 MB): the
+// buffer is re-allocated after the stream drains.  Recorded graphs hold the old address, so every
+// cached step graph is dropped (re-recorded on its next call); with a prepared plan outstanding, or
+// while recording, the buffer cannot move and the caller's fallback applies.
+static bool ensure_scratch(tts_hip_backend * be, size_t bytes) {
+    if (bytes <= be->scratch_size) return true;
+    if (be->stream == be->cap_stream || be->pexec[0] || be->pexec[1]) return false;
+    TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+    for (int k = 0; k < tts_hip_backend::N_GSIG; ++k) {
+        if (be->gsig_exec[k]) TTS_HIP_CHECK(hipGraphExecDestroy(be->gsig_exec[k]));
+        be->gsig_exec[k] = nullptr;
+        be->gsig[k] = 0;
+    }
+    const size_t n = (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    char * p = nullptr;
+    if (hipMalloc((void **)&p, n) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    TTS_HIP_CHECK(hipFree(be->scratch));
+    be->scratch = p;
+    be->scratch_size = n;
+    be->aq.src = nullptr;
+    return true;
+}
+
 // ---- activation preparation (cached per graph by src pointer) ----
 static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, int64_t K, int64_t M, ActQuant & out) {
     ActQuant & aq = be->aq;
@@ -1866,7 +1893,7 @@ static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, in
     const int vt = wtype == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : wtype;
     const bool hit = aq.src == b->data && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
     if (!hit) {
-        if (act_quant_bytes(wtype, K, M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+        if (!ensure_scratch(be, act_quant_bytes(wtype, K, M))) return TTS_STATUS_ALLOC_FAILED;
         launch_quantize_act(be, wtype, (const float *)b->data, xcs, K, M, aq);
         aq.src = b->data;
         aq.graph_epoch = be->graph_epoch;
@@ -1973,7 +2000,7 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         // the prologue reads 16-B vectors: x 16-B aligned, columns 16-B strided (contiguous for PRO_QUANT)
         x_hit |= ((uintptr_t)j.x & 15) != 0 || (j.xcs & 3) != 0 || (j.pro == PRO_QUANT && j.xcs != j.K);
         if (x_hit) {
-            if ((size_t)(4 * j.K * j.M) > be->scratch_size) return TTS_STATUS_ALLOC_FAILED;
+            if (!ensure_scratch(be, (size_t)(4 * j.K * j.M))) return TTS_STATUS_ALLOC_FAILED;
             launch_copy_cols(be, (float *)be->scratch, j.x, j.K, j.xcs, j.M);
             be->aq.src = nullptr;
             j.x = (const float *)be->scratch;

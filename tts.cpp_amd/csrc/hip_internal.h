@@ -301,6 +301,7 @@ struct tts_hip_backend {
     int64_t cus = 256;  // compute units this backend's stream may use (TTS_HIP_OPT_CU_PARTITION); grids are sized to it
     int cu_total = 256;
     int bgemm_f32 = 1;  // TTS_HIP_OPT_BGEMM_F32
+    int gemv_f32_wide = 1;  // TTS_HIP_OPT_GEMV_F32_WIDE
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;

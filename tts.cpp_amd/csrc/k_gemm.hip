@@ -115,6 +115,90 @@ __global__ __launch_bounds__(256) void k_gemm_f32_f64(GemvJob j, int ks, int64_t
     }
 }
 
+// Many rows x a few dozen columns (the 9 output heads at 32 lock-step prompts: 9 792 rows x 1 024 x 32):
+// the 64 x 64 tiles above pad the columns and split K into partial sums; here every (row, column)
+// output is ONE sequential f64 chain in ascending k -- exactly ggml_vec_dot_f32's generic order -- and
+// every weight byte is read once.  A workgroup owns R = P * RW consecutive flat (matrix, row) rows; lane
+// (slot s, column c) of wave w accumulates rows s + RPS * w + RW * p (p < P) in registers.  K runs in
+// chunks of KC staged through LDS: the columns k-major, padded (lanes of one k read consecutive words), the
+// rows padded by one word (the RPS row slots of a wave read different banks; a row's lanes share one
+// broadcast word).  The next chunk is fetched into registers while the current one is summed.
+constexpr int WKC = 64;
+template <int MC, int P>
+__global__ __launch_bounds__(256) void k_gemv_f32_wide(GemvJob j, int64_t rows_total) {
+    constexpr int RPS = 64 / MC, RW = 4 * RPS, R = RW * P;
+    constexpr int XN = WKC * MC, WN = R * WKC;                  // floats staged per chunk
+    constexpr int XL = (XN + 255) / 256, WL = (WN + 255) / 256;  // per thread
+    __shared__ float xs[WKC * (MC + 1)];
+    __shared__ float ws[R * (WKC + 1)];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane % MC, s = lane / MC;
+    const int64_t r0 = (int64_t)blockIdx.x * R;
+    const int64_t K = j.K, M = j.M, N = j.N, wrs = j.w_row_bytes / 4;
+    double acc[P];
+#pragma unroll
+    for (int p = 0; p < P; ++p) acc[p] = 0.0;
+    float xr[XL], wr[WL];
+    auto fetch = [&](int64_t k0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < XL; ++i) {  // x: element e = col * WKC + kk (coalesced along k)
+            const int e = i * 256 + tid, col = e / WKC, kk = e % WKC;
+            const int64_t k = k0 + kk;
+            xr[i] = (e < XN && col < M && k < K) ? j.x[(int64_t)col * j.xcs + k] : 0.0f;
+        }
+#pragma unroll
+        for (int i = 0; i < WL; ++i) {  // w: element e = row * WKC + kk (a row's chunk is contiguous)
+            const int e = i * 256 + tid, rr = e / WKC, kk = e % WKC;
+            const int64_t fr = r0 + rr, k = k0 + kk;
+            float v = 0.0f;
+            if (e < WN && fr < rows_total && k < K) {
+                const int mat = (int)(fr / N);
+                v = ((const float *)j.W[mat])[(fr - (int64_t)mat * N) * wrs + k];
+            }
+            wr[i] = v;
+        }
+    };
+    fetch(0);
+    for (int64_t k0 = 0; k0 < K; k0 += WKC) {
+        __syncthreads();  // every lane is done with the previous chunk
+#pragma unroll
+        for (int i = 0; i < XL; ++i) {
+            const int e = i * 256 + tid;
+            if (e < XN) xs[(e % WKC) * (MC + 1) + e / WKC] = xr[i];
+        }
+#pragma unroll
+        for (int i = 0; i < WL; ++i) {
+            const int e = i * 256 + tid;
+            if (e < WN) ws[(e / WKC) * (WKC + 1) + e % WKC] = wr[i];
+        }
+        __syncthreads();
+        if (k0 + WKC < K) fetch(k0 + WKC);
+        const int kn = K - k0 < WKC ? (int)(K - k0) : WKC;  // zero-filled tail: the padded terms are never added
+        if (kn == WKC) {
+#pragma unroll 8
+            for (int kk = 0; kk < WKC; ++kk) {
+                const float xv = xs[kk * (MC + 1) + c];
+#pragma unroll
+                for (int p = 0; p < P; ++p) acc[p] += (double)__fmul_rn(ws[(s + RPS * wave + RW * p) * (WKC + 1) + kk], xv);
+            }
+        } else {
+            for (int kk = 0; kk < kn; ++kk) {
+                const float xv = xs[kk * (MC + 1) + c];
+#pragma unroll
+                for (int p = 0; p < P; ++p) acc[p] += (double)__fmul_rn(ws[(s + RPS * wave + RW * p) * (WKC + 1) + kk], xv);
+            }
+        }
+    }
+    if (c >= M) return;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+        const int64_t fr = r0 + s + RPS * wave + RW * p;
+        if (fr >= rows_total) continue;
+        const int mat = (int)(fr / N);
+        gemm_store(j, mat, fr - (int64_t)mat * N, c, acc[p]);
+    }
+}
+
 // the splits' partials of each output summed in split order, then the f32 rounding and epilogue
 __global__ __launch_bounds__(256) void k_gemm_reduce(GemvJob j, int ks, const double * __restrict__ part) {
     const int64_t per = j.M * j.N, n = per * j.nmat;
@@ -234,7 +318,38 @@ bool gemm_f32_ok(const GemvJob & j) {
            (j.M + GT - 1) / GT <= 65535 && (j.w_row_bytes % 4) == 0 && (j.xcs >= j.K);
 }
 
+template <int MC>
+static void launch_wide(tts_hip_backend * be, const GemvJob & j, int64_t rows) {
+    constexpr int RW = 4 * (64 / MC);
+    // rows per lane: as few as keep >= 4 workgroups (16 waves) per CU -- each lane's f64 chains are
+    // serial, so the SIMDs need several waves to overlap their latencies
+    int64_t p = (rows + 4 * be->cus * RW - 1) / (4 * be->cus * RW);
+    const int P = p <= 1 ? 1 : p <= 2 ? 2 : p <= 4 ? 4 : 8;
+    const unsigned g = (unsigned)((rows + (int64_t)P * RW - 1) / ((int64_t)P * RW));
+    switch (P) {
+        case 1: hipLaunchKernelGGL((k_gemv_f32_wide<MC, 1>), dim3(g), dim3(256), 0, be->stream, j, rows); break;
+        case 2: hipLaunchKernelGGL((k_gemv_f32_wide<MC, 2>), dim3(g), dim3(256), 0, be->stream, j, rows); break;
+        case 4: hipLaunchKernelGGL((k_gemv_f32_wide<MC, 4>), dim3(g), dim3(256), 0, be->stream, j, rows); break;
+        default: hipLaunchKernelGGL((k_gemv_f32_wide<MC, 8>), dim3(g), dim3(256), 0, be->stream, j, rows); break;
+    }
+}
+
+// many rows (>= 2048 flat) x 9..64 columns: the wide GEMV (one sequential f64 chain per output)
+static bool wide_ok(const tts_hip_backend * be, const GemvJob & j) {
+    const int64_t rows = j.N * j.nmat;
+    return be->gemv_f32_wide && j.M > 8 && j.M <= 64 && rows >= 2048 &&
+           (j.epi == EPI_NONE || j.epi == EPI_GELU || j.epi == EPI_ADD);
+}
+
 void launch_gemm_f32(tts_hip_backend * be, const GemvJob & j) {
+    if (wide_ok(be, j)) {
+        const int64_t rows = j.N * j.nmat;
+        if (j.M <= 16) launch_wide<16>(be, j, rows);
+        else if (j.M <= 32) launch_wide<32>(be, j, rows);
+        else launch_wide<64>(be, j, rows);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     bool vec = (j.K % 4) == 0 && (j.w_row_bytes % 16) == 0 && (j.xcs % 4) == 0 && ((uintptr_t)j.x % 16) == 0;
     for (int i = 0; i < j.nmat; ++i) vec = vec && ((uintptr_t)j.W[i] % 16) == 0;
     const int64_t tiles = ((j.N + GT - 1) / GT) * ((j.M + GT - 1) / GT) * j.nmat;

@@ -2366,7 +2366,7 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
 // (16-column tiles), then the K-relay kernel over (row tile, column tile) -- the same per-(row,
 // column) arithmetic as the GEMV, so bit-identical to ggml's order, in two launches instead of one
 // 8-column GEMV launch per 8 columns.  Lane-layout or tile-layout weights, K = 1024 x {1, 2, 3, 4}.
-static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job) {
+static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t lo_res = SIZE_MAX) {
     if (!be->gemv_kr || !be->gemv_mf_prequant || job.wtype != TTS_TYPE_Q4_K || job.M <= 8 || job.epi == EPI_SWIGLU || job.dbg) return false;
     if (job.pro != PRO_QUANT && job.pro != PRO_LN) return false;
     if (job.pro == PRO_LN && job.K > 4 * 1024) return false;
@@ -2377,7 +2377,29 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job) {
     const int64_t tile = (((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
     const int64_t nct = (job.M + 15) / 16;
     if (q4k_kr_lds(tile, false) > 160 * 1024) return false;
-    if ((size_t)(tile * nct + 4 * job.K * job.M) > be->scratch_size || nct > 65535) return false;
+    // the operands go to the top of scratch; its bottom may hold this job's staged input columns
+    const char * xs0 = (const char *)job.x;
+    const char * xs1 = xs0 + 4 * (size_t)((job.M - 1) * job.xcs + job.K);
+    // (a chunk pass keeps the whole job's reservation: later chunks' columns lie above its own)
+    const size_t lo = lo_res != SIZE_MAX ? lo_res
+                      : (xs0 >= be->scratch && xs0 < be->scratch + be->scratch_size) ? (size_t)(xs1 - be->scratch) : 0;
+    const int64_t avail = lo < be->scratch_size ? (int64_t)(be->scratch_size - lo) : 0;
+    if (tile * nct > avail || (lo == 0 && (size_t)(tile * nct + 4 * job.K * job.M) > be->scratch_size) || nct > 65535) {
+        // more columns than the operand area holds (a many-prompt prefill): passes over column chunks
+        // of whole 16-column tiles, each the same per-(row, column) arithmetic
+        const int64_t per = (lo ? avail / tile : (int64_t)be->scratch_size / (tile + 16 * 4 * job.K)) * 16;
+        if (per < 16 || job.rep_mat >= 0) return false;  // (epilogues are per output element: column offsets carry them)
+        for (int64_t m0 = 0; m0 < job.M; m0 += per) {
+            GemvJob j = job;
+            j.M = job.M - m0 < per ? job.M - m0 : per;
+            if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
+            j.x = job.x + m0 * job.xcs;
+            for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+            if (job.res) j.res = job.res + m0 * job.rcs;
+            if (!launch_gemm_q4k_kr(be, j, lo)) return false;  // (the first chunk is checked before any launch below)
+        }
+        return true;
+    }
     GemvJob j = job;
     j.bq_tile = tile;
     j.bq_bytes = tile * nct;
