@@ -73,6 +73,14 @@ def test_orpheus_wide_two_layers(hip):
 
 
 @pytest.mark.gpu
+def test_orpheus_3b_full_depth(hip):
+    """BASELINE configs[4] at full depth: Orpheus-3B's 28 layers and the 156 940-row Q4_K head
+    (src/models/orpheus/model.h:31-46, model.cpp:230-311), 2 prompts, 16 greedy steps: tokens bit-exact,
+    logits within 1e-4 -- the K-relay chains, tile-layout head and GQA cache copies over every layer."""
+    run_pair(hip, dict(max_ctx=40), 2, 4, 16)
+
+
+@pytest.mark.gpu
 def test_orpheus_wide_batch8(hip):
     """The bench's shape (8 prompts = 8 GEMV columns): q / k / v as one launch over the stored-tiled q
     and the tile-layout copies of k / v, the SwiGLU launch, residue-split tiles; one GEMV item per
