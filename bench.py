@@ -153,15 +153,13 @@ def gather_audio(dist, rank, world, local, pcms):
     return out
 
 
-def cpu_baseline(args, n_threads):
+def cpu_baseline(args, n_threads, B):
     """Oracle (C restatement of ggml-cpu) on the GPU leg's workload shape, on host cores: the same
-    Parler step graph at the same batch (all of this GPU's prompts in one runner) and the same KV
-    length when timing starts (tts_parler_set_position: the prefill is skipped, the step's work is
-    the same), then the same DAC graph over a few frames per prompt; rates per audio-second,
-    end to end = 1 / (1/AR + 1/DAC)."""
+    Parler step graph at the same lock-step batch as one GPU replica and the same KV length when timing
+    starts (tts_parler_set_position: the prefill is skipped, the step's work is the same), then the
+    same DAC graph over a few frames per prompt; rates per audio-second, end to end = 1 / (1/AR + 1/DAC)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import py_oracle
-    B = args.batch
     cfg = ttship.parler_config(batch=B, max_ctx=args.ctx + 64)
     p = ttship.Parler(py_oracle.iface(n_threads), cfg)
     try:
@@ -176,45 +174,57 @@ def cpu_baseline(args, n_threads):
         toks = p.generate(2)
     finally:
         p.close()
-    frames = 2
+    frames, nd = 2, min(B, 8)
     dcfg = ttship.dac_config(max_frames=frames)
     dac = ttship.Dac(py_oracle.iface(n_threads), dcfg)
     try:
         t0 = time.perf_counter()
-        for b in range(B):
+        for b in range(nd):
             dac.decode(dac_codes(toks[b], dcfg.codebook_size))
         dt_dac = time.perf_counter() - t0
     finally:
         dac.close()
     ar = B * steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt_ar
-    dac_rate = B * frames * SAMPLES_PER_STEP / SAMPLE_RATE / dt_dac
+    dac_rate = nd * frames * SAMPLES_PER_STEP / SAMPLE_RATE / dt_dac
     return {"value": 1.0 / (1.0 / ar + 1.0 / dac_rate), "unit": "audio-sec/wall-sec", "cores": n_threads, "kind": "port",
-            "sample": f"{steps} Parler-mini Q4_K decode steps of {B} prompts at KV length {args.ctx} (the GPU leg's batch and KV "
-                      f"length; prefill skipped) + DAC-44k decode of {frames} frames per prompt (oracle/ggml_ref.c, C restatement "
-                      f"of ggml-cpu scalar paths; reference ggml-cpu unbuildable offline)",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": f"{steps} Parler-mini Q4_K decode steps of {B} lock-step prompts (one GPU replica's batch) at KV length "
+                      f"{args.ctx} (prefill skipped) + DAC-44k decode of {frames} frames for {nd} prompts (oracle/ggml_ref.c, C "
+                      f"restatement of ggml-cpu scalar paths, {n_threads} threads = the box's CPU share; reference ggml-cpu "
+                      f"unbuildable offline)",
             "ar_audio_sec_per_s": round(ar, 5), "dac_audio_sec_per_s": round(dac_rate, 5),
             "codec_tokens_per_s": B * steps * HEADS / dt_ar}
 
 
 def gemv_roofline(be, runner, steps):
-    """Dominant kernel (Q4_K dequant-GEMV): algorithmic bytes per launch / its average duration,
-    HIP events on the backend stream around each launch during profiled decode steps."""
+    """Dominant kernels of the decode step, from HIP events carried in their dispatch packets over
+    profiled steps: the Q4_K dequant-GEMV / matrix-core GEMM launches (algorithmic bytes per launch =
+    every weight byte once + activations + outputs) and the decode attention's scores + P.V pair
+    (bytes = every K and V row read).  `traffic` is PMC HBM bytes per launch from a committed
+    rocprofv3 pass (source and mode named beside it), not taken in this run."""
     be.set_option(1, 1)
     be.gemv_stats(-1, reset=True)
     runner.generate(steps)
-    ms, launches, nbytes = be.gemv_stats(ttship.Q4_K, reset=True)
+    ms, launches, nbytes = be.gemv_stats(ttship.Q4_K, reset=False)
+    ams, alaunches, abytes = be.gemv_stats(ttship.PROF_ATTN, reset=True)
     be.set_option(1, 0)
     avg_us = 1000.0 * ms / max(launches, 1)
     bpl = nbytes / max(launches, 1)
     gbs = bpl / (avg_us * 1e-6) / 1e9 if launches else 0.0
-    traffic, src = None, None
+    traffic, src, mode = None, None, None
     if PMC_FILE.exists():
         pmc = json.loads(PMC_FILE.read_text())
-        traffic, src = pmc.get("hbm_bytes_per_launch"), str(PMC_FILE.relative_to(ROOT))
+        traffic, src, mode = pmc.get("hbm_bytes_per_launch"), str(PMC_FILE.relative_to(ROOT)), pmc.get("command")
+    a_us = 1000.0 * ams / max(alaunches, 1)
+    a_bpl = abytes / max(alaunches, 1)
+    a_gbs = a_bpl / (a_us * 1e-6) / 1e9 if alaunches else 0.0
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src,
-            "kernel": "k_gemv_q4_K", "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(bpl, 1),
-            "launches_sampled": launches}
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": src, "traffic_mode": mode,
+            "kernel": "k_gemv_q4K_kr (K-relay matrix-core GEMM, > 8 lock-step columns) / k_gemv_q4_K (<= 8)",
+            "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(bpl, 1), "launches_sampled": launches,
+            "attention": {"kernel": "k_attn_scores + k_attn_pv (one decode attention)", "achieved": round(a_gbs, 1),
+                          "frac": round(a_gbs / HBM_PEAK_GBS, 4), "avg_us": round(a_us, 3), "bytes_per_call": round(a_bpl, 1),
+                          "calls_sampled": alaunches}}
 
 
 def run_replicas(fn, n):
@@ -243,23 +253,52 @@ def run_replicas(fn, n):
 ORPHEUS_TOK_PER_AUDIO_S = 82.03  # 820 Orpheus tokens = 10.0 s of audio
 
 
+ORPHEUS_HEADS = (0, 1, 2, 2, 1, 2, 2)  # SNAC codebook of each token in a 7-token frame (orpheus model.h heads)
+
+
+def orpheus_snac_heads(toks):
+    """orpheus_runner::prepare_output_tokens (src/models/orpheus/model.cpp:370-386): whole 7-token
+    frames, token ii of a frame -> codebook heads[ii], code = token - 128266 - ii * 4096.  Synthetic
+    weights emit arbitrary ids, so codes are folded into [0, 4096) (a trained model emits in range)."""
+    n = len(toks) // 7 * 7
+    heads = [[], [], []]
+    for i in range(n):
+        ii = i % 7
+        heads[ORPHEUS_HEADS[ii]].append((int(toks[i]) - 128266 - ii * 4096) % 4096)
+    return [np.asarray(h, dtype=np.int32) for h in heads]
+
+
 def orpheus_leg(be, args, rank):
     """BASELINE configs[4] per-GPU shard: Orpheus-3B Q4_K (synthetic weights, every matrix incl. the
     156 940-row head in Q4_K), `orpheus_batch` prompts in lockstep, greedy decode with device
-    sampling; plus the dequant-GEMV roofline over profiled steps (the tile-layout matrix-core kernel
-    carries every matrix >= 4 MiB)."""
+    sampling, then every prompt's tokens through the SNAC-24k vocoder (orpheus model.cpp:389-405:
+    prepare_output_tokens + snac_runner::run) -- audio_sec_per_s counts produced PCM over decode + SNAC;
+    plus the dequant-GEMV roofline over profiled steps."""
     B, steps, n_prompt = args.orpheus_batch, args.orpheus_steps, 32
     cfg = ttship.orpheus_config(batch=B, max_ctx=n_prompt + steps + 64, arena_bytes=1 << 30)
     o = ttship.Orpheus(be.iface(), cfg)
+    scfg = ttship.snac_config(max_frames=4 * (steps // 7) + 8)
+    snac = ttship.Snac(be.iface(), scfg)
     try:
         prompt = (np.arange(B * n_prompt, dtype=np.int32).reshape(B, n_prompt) * 7919 + 128000 + rank) % cfg.vocab_size
         first = o.prefill(prompt).argmax(axis=1).astype(np.int32)
         toks = o.generate(first, 4)
+        heads0 = orpheus_snac_heads(toks[0].tolist() * 7)
+        snac.decode(heads0, np.zeros(snac.noise_per_frame * len(heads0[-1]), np.float32))  # warm
+        rng = np.random.default_rng(rank)
         be.sync()
         t0 = time.perf_counter()
         toks = o.generate(toks[:, -1], steps)
         be.sync()
-        dt = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        samples = 0
+        for b in range(B):
+            hs = orpheus_snac_heads(toks[b])
+            noise = rng.standard_normal(snac.noise_per_frame * len(hs[-1])).astype(np.float32)
+            samples += snac.decode(hs, noise).shape[0]
+        be.sync()
+        t2 = time.perf_counter()
+        dt = t1 - t0
         be.set_option(ttship.OPT["PROFILE_GEMV"], 1)
         be.gemv_stats(-1, reset=True)
         o.generate(toks[:, -1], 8)
@@ -267,43 +306,91 @@ def orpheus_leg(be, args, rank):
         be.set_option(ttship.OPT["PROFILE_GEMV"], 0)
         avg_us = 1000.0 * ms / max(launches, 1)
         gbs = nbytes / max(launches, 1) / (avg_us * 1e-6) / 1e9 if launches else 0.0
-        return {"workload": f"Orpheus-3B Q4_K greedy decode (BASELINE configs[4] per-GPU shard), {B} prompts, "
-                            f"prompt {n_prompt} + {steps} timed steps, synthetic weights",
-                "tokens_per_s": round(B * steps / dt, 1), "audio_sec_per_s": round(B * steps / dt / ORPHEUS_TOK_PER_AUDIO_S, 3),
-                "ms_per_step": round(1000 * dt / steps, 3), "graph_nodes": o.last_graph_nodes(),
-                "weight_bytes": o.weight_bytes(),
+        pmc = json.loads(PMC_FILE_ORPH.read_text()) if PMC_FILE_ORPH else {}
+        return {"workload": f"Orpheus-3B Q4_K greedy decode (BASELINE configs[4] per-GPU shard), {B} prompts, prompt {n_prompt} + "
+                            f"{steps} timed steps, then SNAC-24k of every prompt's {steps // 7} frames; synthetic weights",
+                "tokens_per_s": round(B * steps / dt, 1), "ms_per_step": round(1000 * dt / steps, 3),
+                "snac_ms": round(1000 * (t2 - t1), 3), "audio_sec_per_gpu": round(samples / 24000.0, 4), "wall_s": t2 - t0,
+                "audio_sec_per_s": round(samples / 24000.0 / (t2 - t0), 3),
+                "graph_nodes": o.last_graph_nodes(), "weight_bytes": o.weight_bytes(),
                 "roofline": {"bound": "hbm", "kernel": "k_gemv_q4K_kr (K relay, tile layout, >= 4 MiB; its operand pass k_quant_mf "
                                                       "not included) + k_gemv_q4_K (k / v lane layout)",
                              "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
                              "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(nbytes / max(launches, 1), 1),
-                             "launches_sampled": launches,
-                             "traffic_kr": (json.loads(PMC_FILE_ORPH.read_text()).get("hbm_bytes_per_launch") if PMC_FILE_ORPH else None),
-                             "traffic_source": str(PMC_FILE_ORPH.relative_to(ROOT)) if PMC_FILE_ORPH else None}}
+                             "launches_sampled": launches, "traffic_kr": pmc.get("hbm_bytes_per_launch"),
+                             "traffic_source": str(PMC_FILE_ORPH.relative_to(ROOT)) if PMC_FILE_ORPH else None,
+                             "traffic_mode": pmc.get("command")}}
     finally:
+        snac.close()
         o.close()
 
 
+DIA_DELAYS = (0, 8, 9, 10, 11, 12, 13, 14, 15)  # Dia's delay pattern (dia model.h), max_delay 15
+
+
+def dia_frames(toks):
+    """dia_runner::adjust_output_tokens (src/models/dia/model.cpp:825-846): frame i takes head ii's token
+    of step i + delay[ii]; synthetic weights' ids >= 1024 (BOS / EOS / pad) are folded into the codebook
+    range instead of dropping the frame, so every step yields audio."""
+    n = toks.shape[0] - DIA_DELAYS[-1]
+    return np.stack([toks[i + np.array(DIA_DELAYS), np.arange(9)] % 1024 for i in range(n)]).astype(np.int32)
+
+
+def dialogue(n_chars):
+    """A two-speaker dialogue (Dia's [S1] / [S2] speaker tags as the tokenizer's bytes 0x01 / 0x02) of
+    Harvard sentences, cut to n_chars bytes (tests/test_dia_gpu.py)."""
+    out, i = b"", 0
+    while len(out) < n_chars:
+        out += (b"\x01 " if i % 2 == 0 else b" \x02 ") + HARVARD[i % len(HARVARD)].encode()
+        i += 1
+    return np.frombuffer(out[:n_chars], dtype=np.uint8).astype(np.int32)
+
+
 def dia_leg(be, args):
-    """BASELINE configs[3]: Dia-1.6B Q8_0 (synthetic weights), encoder step over a Harvard-sentence
-    prompt, then timed CFG decoder steps (conditioned + unconditioned in one graph, greedy heads fed
-    back).  One step = one 9-codebook DAC frame = 512 samples at 44.1 kHz."""
-    d = ttship.Dia(be.iface(), ttship.dia_config(max_generation_size=args.dia_steps + 16))
+    """BASELINE configs[3]: Dia-1.6B Q8_0 (synthetic weights), the encoder step over a long-form
+    two-speaker dialogue (the whole 1024-position encoder context), timed CFG decoder steps (conditioned
+    + unconditioned in one graph, greedy heads fed back), then the delay pattern undone and the frames
+    through DAC-44k (dia model.cpp:849-870); audio_sec_per_s counts produced PCM over decode + DAC.
+    Plus the Q8_0 slab GEMV roofline over profiled steps."""
+    dcfg = ttship.dia_config(max_generation_size=args.dia_steps + 16)
+    d = ttship.Dia(be.iface(), dcfg)
+    dac = ttship.Dac(be.iface(), ttship.dac_config(max_frames=args.dia_steps))
     try:
-        text = np.frombuffer(("\x01 " + HARVARD[0] + " " + HARVARD[1]).encode(), dtype=np.uint8).astype(np.int32)
+        text = dialogue(dcfg.max_encoder_context_length)
         t0 = time.perf_counter()
         audio = d.prefill(text, np.full(9, 1026, dtype=np.int32)).argmax(axis=1).astype(np.int32)
         t_enc = time.perf_counter() - t0
         audio = d.generate(audio, 3)[-1]  # warm (plans, code objects)
+        dac.decode(np.zeros((8, 9), np.int32))
         be.sync()
         t0 = time.perf_counter()
-        d.generate(audio, args.dia_steps)  # device-resident greedy loop
+        toks = d.generate(audio, args.dia_steps)  # device-resident greedy loop
         be.sync()
-        dt = time.perf_counter() - t0
-        return {"workload": "Dia-1.6B Q8_0 CFG decode (BASELINE configs[3]), 1 prompt, synthetic weights",
-                "ms_per_step": round(1000 * dt / args.dia_steps, 3),
-                "audio_sec_per_s": round(args.dia_steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3),
-                "encoder_step_ms": round(1000 * t_enc, 1), "weight_bytes": d.weight_bytes()}
+        t1 = time.perf_counter()
+        pcm = dac.decode(dia_frames(toks))
+        be.sync()
+        t2 = time.perf_counter()
+        dt = t1 - t0
+        be.set_option(ttship.OPT["PROFILE_GEMV"], 1)
+        be.gemv_stats(-1, reset=True)
+        d.generate(toks[-1], 8)
+        ms, launches, nbytes = be.gemv_stats(ttship.Q8_0, reset=True)
+        be.set_option(ttship.OPT["PROFILE_GEMV"], 0)
+        avg_us = 1000.0 * ms / max(launches, 1)
+        gbs = nbytes / max(launches, 1) / (avg_us * 1e-6) / 1e9 if launches else 0.0
+        return {"workload": f"Dia-1.6B Q8_0 CFG decode (BASELINE configs[3]), 1 prompt = a {len(text)}-byte two-speaker dialogue, "
+                            f"{args.dia_steps} timed steps, then DAC-44k of the {args.dia_steps - DIA_DELAYS[-1]} undelayed frames; "
+                            "synthetic weights",
+                "ms_per_step": round(1000 * dt / args.dia_steps, 3), "dac_ms": round(1000 * (t2 - t1), 3),
+                "ar_audio_sec_per_s": round(args.dia_steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3),
+                "audio_sec_per_gpu": round(pcm.shape[0] / SAMPLE_RATE, 4), "wall_s": t2 - t0,
+                "audio_sec_per_s": round(pcm.shape[0] / SAMPLE_RATE / (t2 - t0), 3),
+                "encoder_step_ms": round(1000 * t_enc, 1), "weight_bytes": d.weight_bytes(),
+                "roofline": {"bound": "hbm", "kernel": "k_gemv_q8_0s (slab Q8_0 GEMV, <= 8 columns)", "achieved": round(gbs, 1),
+                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_us, 3),
+                             "bytes_per_launch": round(nbytes / max(launches, 1), 1), "launches_sampled": launches, "traffic": None}}
     finally:
+        dac.close()
         d.close()
 
 
@@ -395,12 +482,66 @@ def kokoro_leg(backends, args, rank, dist, local, world):
             k.close()
 
 
+def parler_replicas(args, per_gpu, R, rank, new_backend, dac_cfg=None):
+    """R replicas (each its own backend = HIP stream, driven by its own host thread) of per_gpu / R
+    lock-step prompts, prefilled to the KV start length and warmed; + per-replica prefill times."""
+    bl = per_gpu // R
+    # the compute arena holds the prompt pass too (attention scores [ctx, ctx, H, prompts]): 4 GiB per 8 prompts
+    cfg = ttship.parler_config(batch=bl, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
+                               arena_bytes=max(4, (bl + 7) // 8 * 4) << 30)
+    reps, prefill_ms = [], []
+    for r in range(R):
+        rb = new_backend()
+        if args.cu_partition and R > 1:
+            rb.set_option(ttship.OPT["CU_PARTITION"], (r << 8) | R | ((args.cu_partition - 1) << 16))
+        rr = ttship.Parler(rb.iface(), cfg)
+        rd = None if dac_cfg is None else new_dac_for(args, rb, dac_cfg)
+        reps.append((rb, rr, rd))
+    for r, (rb, rr, rd) in enumerate(reps):
+        rb.sync()
+        tp0 = time.perf_counter()
+        rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * per_gpu + r * bl))
+        rb.sync()
+        prefill_ms.append(1000.0 * (time.perf_counter() - tp0))
+        rr.generate(args.warmup)
+        rb.sync()
+    return reps, prefill_ms, cfg
+
+
+def new_dac_for(args, rb, dcfg):
+    if args.dac_conv_split is not None:  # concurrent decoders each sizing split convs for the whole chip
+        rb.set_option(ttship.OPT["CONV_SPLIT"], args.dac_conv_split)
+    rd = ttship.Dac(rb.iface(), dcfg)
+    rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+    return rd
+
+
+def close_replicas(reps):
+    for rb, rr, rd in reps:
+        if rd is not None:
+            rd.close()
+        rr.close()
+        rb.close()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=861, help="AR steps per prompt (861 = 10.0 s of audio, SURVEY §8d)")
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="prompts per GPU (64-prompt batch / 8 GPUs)")
+    ap.add_argument("--prompts", type=int, default=64, help="the fixed synthetic prompt set (north_star: a 64-prompt batch), "
+                    "split over the ranks: strong scaling")
+    ap.add_argument("--batch", type=int, default=None, help="prompts per GPU instead of --prompts / world (weak scaling)")
     ap.add_argument("--ctx", type=int, default=448, help="KV length when timing starts (prompt prefill)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -408,11 +549,13 @@ def main():
     ap.add_argument("--b1-replicas", type=int, default=8, help="the B=1 leg: this many runners of one prompt each, as "
                     "TTS.cpp's server workers run (0 = skip)")
     ap.add_argument("--b1-steps", type=int, default=100)
+    ap.add_argument("--p8", type=int, default=1, help="beside the headline, the AR line at 8 prompts per GPU (2 replicas x 4: "
+                    "the 64-prompt batch over 8 GPUs) when the headline runs more (0 = skip)")
     ap.add_argument("--no-fusion", action="store_true")
     ap.add_argument("--no-dac", action="store_true", help="AR decode only")
     ap.add_argument("--attn-split", type=int, default=None, help="TTS_HIP_OPT_ATTN_SPLIT: min KV length for split attention (0 = off)")
     ap.add_argument("--replicas", type=int, default=2, help="concurrent runner replicas per GPU, each on its own "
-                    "backend/stream with batch/replicas prompts (the server's worker model)")
+                    "backend/stream with prompts/replicas lock-step prompts (the server's worker model)")
     ap.add_argument("--kv-prefetch", type=int, default=None, help="TTS_HIP_OPT_KV_PREFETCH: min KV length (0 = off)")
     ap.add_argument("--kv-prefetch-blocks", type=int, default=None)
     ap.add_argument("--conv-acc", type=int, default=None, help="TTS_HIP_OPT_CONV_F32ACC for the codec / vocoder convs")
@@ -430,6 +573,7 @@ def main():
     ap.add_argument("--gemm-q8-staged", type=int, default=None, help="TTS_HIP_OPT_GEMM_Q8_STAGED: many-column Q8_0 GEMM kernel (2 = 64x128 staged, 1 = 64x64 staged, 0 = direct)")
     ap.add_argument("--gemv-kr-inkernel", type=int, default=None, help="TTS_HIP_OPT_GEMV_KR_INKERNEL: max K of K-relay GEMVs quantizing in-kernel (0 = operand pass)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
+    ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
                     "replica on all CUs, 1 = replica r on the r-th contiguous CU set, 2 = on CUs c with c %% R == r")
@@ -441,97 +585,45 @@ def main():
     ap.add_argument("--kokoro-prompts", type=int, default=8, help="Kokoro-82M prompts per GPU, end to end (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
-    ap.add_argument("--dia-steps", type=int, default=32, help="timed Dia-1.6B decoder steps per GPU (0 = skip)")
+    ap.add_argument("--dia-steps", type=int, default=64, help="timed Dia-1.6B decoder steps per GPU (0 = skip)")
     args = ap.parse_args()
 
     rank, world, local, dist = dist_init()
     R = args.replicas
-    if R < 1 or args.batch % R:
-        raise SystemExit(f"--replicas {R} must divide --batch {args.batch}")
-    bl = args.batch // R  # prompts per replica
-    # the compute arena holds the prompt pass too (attention scores [ctx, ctx, H, prompts]): 4 GiB per 8 prompts
-    cfg = ttship.parler_config(batch=bl, max_ctx=max(4096, args.ctx + args.steps + args.warmup + 64),
-                               arena_bytes=max(4, (bl + 7) // 8 * 4) << 30)
+    strong = args.batch is None
+    if strong and args.prompts % world:
+        raise SystemExit(f"--prompts {args.prompts} must split evenly over {world} GPUs")
+    per_gpu = args.prompts // world if strong else args.batch
+    if R < 1 or per_gpu % R:
+        raise SystemExit(f"--replicas {R} must divide the {per_gpu} prompts per GPU")
+    bl = per_gpu // R  # prompts per replica
+
     def new_backend():
         rb = ttship.HipBackend(local)
         if args.no_fusion:
             rb.set_option(0, 0)
         rb.set_option(2, args.graphs)
-        if args.conv_acc is not None:
-            rb.set_option(ttship.OPT["CONV_F32ACC"], args.conv_acc)
-        if args.attn_split is not None:
-            rb.set_option(ttship.OPT["ATTN_SPLIT"], args.attn_split)
-        if args.kv_prefetch is not None:
-            rb.set_option(ttship.OPT["KV_PREFETCH"], args.kv_prefetch)
-        if args.gemv_unique is not None:
-            rb.set_option(ttship.OPT["GEMV_UNIQUE"], args.gemv_unique)
-        if args.tile_bytes is not None:
-            rb.set_option(ttship.OPT["Q4K_TILE_BYTES"], args.tile_bytes)
-        if args.gemv_ks is not None:
-            rb.set_option(ttship.OPT["GEMV_KS"], args.gemv_ks)
-        if args.attn_fused is not None:
-            rb.set_option(ttship.OPT["ATTN_FUSED"], args.attn_fused)
-        if args.attn_pv16 is not None:
-            rb.set_option(ttship.OPT["ATTN_PV16"], args.attn_pv16)
-        if args.gemv_krelay is not None:
-            rb.set_option(ttship.OPT["GEMV_KRELAY"], args.gemv_krelay)
-        if args.gemv_nw_min is not None:
-            rb.set_option(ttship.OPT["GEMV_NW_MIN"], args.gemv_nw_min)
-        if args.gemv_q80_pro is not None:
-            rb.set_option(ttship.OPT["GEMV_Q80_PRO"], args.gemv_q80_pro)
-        if args.gemv_q80_slab is not None:
-            rb.set_option(ttship.OPT["GEMV_Q80_SLAB"], args.gemv_q80_slab)
-        if args.gemv_q80_rw is not None:
-            rb.set_option(ttship.OPT["GEMV_Q80_RW"], args.gemv_q80_rw)
-        if args.gemm_q8_staged is not None:
-            rb.set_option(ttship.OPT["GEMM_Q8_STAGED"], args.gemm_q8_staged)
-        if args.gemv_kr_inkernel is not None:
-            rb.set_option(ttship.OPT["GEMV_KR_INKERNEL"], args.gemv_kr_inkernel)
-        if args.attn_ks is not None:
-            rb.set_option(ttship.OPT["ATTN_KS"], args.attn_ks)
-        if args.attn_pv8 is not None:
-            rb.set_option(ttship.OPT["ATTN_PV8"], args.attn_pv8)
-        if args.kv_prefetch_blocks is not None:
-            rb.set_option(ttship.OPT["KV_PREFETCH_BLOCKS"], args.kv_prefetch_blocks)
+        for flag, opt in (("conv_acc", "CONV_F32ACC"), ("attn_split", "ATTN_SPLIT"), ("kv_prefetch", "KV_PREFETCH"),
+                          ("gemv_unique", "GEMV_UNIQUE"), ("tile_bytes", "Q4K_TILE_BYTES"), ("gemv_ks", "GEMV_KS"),
+                          ("attn_fused", "ATTN_FUSED"), ("attn_pv16", "ATTN_PV16"), ("gemv_krelay", "GEMV_KRELAY"),
+                          ("gemv_nw_min", "GEMV_NW_MIN"), ("gemv_q80_pro", "GEMV_Q80_PRO"), ("gemv_q80_slab", "GEMV_Q80_SLAB"),
+                          ("gemv_q80_rw", "GEMV_Q80_RW"), ("gemm_q8_staged", "GEMM_Q8_STAGED"),
+                          ("gemv_kr_inkernel", "GEMV_KR_INKERNEL"), ("attn_ks", "ATTN_KS"), ("attn_pv8", "ATTN_PV8"),
+                          ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE")):
+            v = getattr(args, flag)
+            if v is not None:
+                rb.set_option(ttship.OPT[opt], v)
         return rb
 
     dcfg = ttship.dac_config(max_frames=args.steps)
-
-    def new_dac(rb):
-        if args.dac_conv_split is not None:  # concurrent decoders each sizing split convs for the whole chip
-            rb.set_option(ttship.OPT["CONV_SPLIT"], args.dac_conv_split)
-        rd = ttship.Dac(rb.iface(), dcfg)
-        rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
-        return rd
-
-    reps = []
-    for r in range(R):
-        # a replica = one backend (its own HIP stream) + its own runners, as a server worker owns its
-        # runners (examples/server/server.cpp:316-321); replicas run concurrently from host threads
-        rb = new_backend()
-        if args.cu_partition and R > 1:
-            rb.set_option(ttship.OPT["CU_PARTITION"], (r << 8) | R | ((args.cu_partition - 1) << 16))
-        rr = ttship.Parler(rb.iface(), cfg)
-        rd = None if args.no_dac else new_dac(rb)
-        reps.append((rb, rr, rd))
+    reps, prefill_ms, cfg = parler_replicas(args, per_gpu, R, rank, new_backend, None if args.no_dac else dcfg)
     be, runner, dac = reps[0]
     # DAC workers: the replicas' decoders plus extra backends of their own
-    W = 0 if args.no_dac else max(1, min(args.dac_workers, args.batch))
+    W = 0 if args.no_dac else max(1, min(args.dac_workers, per_gpu))
     dac_workers = [(rb, rd) for rb, _, rd in reps[:W]]
     while len(dac_workers) < W:
         xb = new_backend()
-        dac_workers.append((xb, new_dac(xb)))
-    # text-prompt pass to reach the measured KV length (timed on its own: the prompt prefill, batch x ctx
-    # columns per Q4_K product, on the matrix-core GEMM; not part of the headline's timed region)
-    prefill_ms = []
-    for r, (rb, rr, rd) in enumerate(reps):
-        rb.sync()
-        tp0 = time.perf_counter()
-        rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * args.batch + r * bl))
-        rb.sync()
-        prefill_ms.append(1000.0 * (time.perf_counter() - tp0))
-        rr.generate(args.warmup)
-        rb.sync()
+        dac_workers.append((xb, new_dac_for(args, xb, dcfg)))
     barrier_sync(dist, be)
 
     runner.host_stats(reset=True)
@@ -543,12 +635,12 @@ def main():
         toks_r[r] = rr.generate(args.steps)
         rb.sync()
 
-    pcm = [None] * args.batch
+    pcm = [None] * per_gpu
 
     def dac_leg(w):
-        # worker w decodes every W-th prompt of the whole per-GPU batch
+        # worker w decodes every W-th prompt of this GPU's prompts
         xb, rd = dac_workers[w]
-        for g in range(w, args.batch, W):
+        for g in range(w, per_gpu, W):
             pcm[g] = rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
         xb.sync()
 
@@ -566,33 +658,6 @@ def main():
     # parts of compute_enqueue: waiting on the device for the plan slot, planner, launches under
     # capture (incl. planner), exec update
     host.update({k.replace("_ns", "_us"): round(v, 1) for k, v in cdelta.items()})
-    b1 = None
-    if args.b1_replicas > 0:
-        barrier_sync(dist, be)
-        b1 = parler_b1_leg(args, rank, local, new_backend)
-        t = max_over_ranks(dist, local, b1["ms_per_step"])
-        b1["ms_per_step"] = t
-        b1["ar_audio_sec_per_s"] = round(world * args.b1_replicas * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
-    kres = None
-    if args.kokoro_prompts > 0:
-        barrier_sync(dist, be)
-        kres = kokoro_leg([rb for rb, _, _ in reps], args, rank, dist, local, world)
-    ores = None
-    if args.orpheus_steps > 0:
-        barrier_sync(dist, be)
-        ores = orpheus_leg(be, args, rank)
-        # whole-job rate: every rank decoded its own shard; the slowest rank's step time sets it
-        t = max_over_ranks(dist, local, ores["ms_per_step"])
-        ores["ms_per_step"] = t
-        ores["tokens_per_s"] = round(world * args.orpheus_batch * 1000.0 / t, 1)
-        ores["audio_sec_per_s"] = round(ores["tokens_per_s"] / ORPHEUS_TOK_PER_AUDIO_S, 3)
-    dres = None
-    if args.dia_steps > 0:
-        barrier_sync(dist, be)
-        dres = dia_leg(be, args)
-        t = max_over_ranks(dist, local, dres["ms_per_step"])
-        dres["ms_per_step"] = t
-        dres["audio_sec_per_s"] = round(world * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
     dt = max_over_ranks(dist, local, t2 - t0)
     dt_ar = max_over_ranks(dist, local, t1 - t0)
     dt_dac = max_over_ranks(dist, local, t2 - t1)
@@ -603,16 +668,71 @@ def main():
         tg0 = time.perf_counter()
         gathered = gather_audio(dist, rank, world, local, pcm)
         t_gather = time.perf_counter() - tg0
-
-    total_prompts = args.batch * world
+    total_prompts = per_gpu * world
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
     roof = gemv_roofline(be, runner, max(5, min(40, args.steps // 5)))
+    graph_nodes = runner.last_graph_nodes()
+    dac_nodes = dac.last_graph_nodes() if dac is not None else None
+    for xb, rd in dac_workers[R:]:
+        rd.close()
+        xb.close()
+    close_replicas(reps)
+
+    p8 = None  # the 8-prompts-per-GPU line (the 64-prompt batch over 8 GPUs) beside a many-prompt headline
+    if args.p8 and per_gpu > 8 and strong:
+        barrier_sync(dist, None)
+        reps8, pf8, _ = parler_replicas(args, 8, 2, rank, new_backend)
+        barrier_sync(dist, reps8[0][0])
+        t80 = time.perf_counter()
+        run_replicas(lambda r: (reps8[r][1].generate(args.steps), reps8[r][0].sync()), 2)
+        d8 = max_over_ranks(dist, local, time.perf_counter() - t80)
+        close_replicas(reps8)
+        p8 = {"workload": "Parler-mini Q4_K AR decode, 8 prompts per GPU (2 lock-step replicas x 4)", "ar_ms_per_step": round(1000 * d8 / args.steps, 4),
+              "ar_audio_sec_per_s": round(world * 8 * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE / d8, 3)}
+    b1 = None
+    if args.b1_replicas > 0:
+        barrier_sync(dist, None)
+        b1 = parler_b1_leg(args, rank, local, new_backend)
+        t = max_over_ranks(dist, local, b1["ms_per_step"])
+        b1["ms_per_step"] = t
+        b1["ar_audio_sec_per_s"] = round(world * args.b1_replicas * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
+    kres = None
+    if args.kokoro_prompts > 0:
+        kb = [new_backend() for _ in range(2)]
+        barrier_sync(dist, kb[0])
+        kres = kokoro_leg(kb, args, rank, dist, local, world)
+        for b in kb:
+            b.close()
+    ores = None
+    if args.orpheus_steps > 0:
+        ob = new_backend()
+        barrier_sync(dist, ob)
+        ores = orpheus_leg(ob, args, rank)
+        ob.close()
+        # whole-job rate: every rank decoded its own shard; the slowest rank's time sets it
+        t = max_over_ranks(dist, local, ores["ms_per_step"])
+        ores["ms_per_step"] = t
+        ores["tokens_per_s"] = round(world * args.orpheus_batch * 1000.0 / t, 1)
+        ores["ar_audio_sec_per_s"] = round(ores["tokens_per_s"] / ORPHEUS_TOK_PER_AUDIO_S, 3)
+        ts = max_over_ranks(dist, local, ores["wall_s"])
+        ores["audio_sec_per_s"] = round(world * ores["audio_sec_per_gpu"] / ts, 3)
+    dres = None
+    if args.dia_steps > 0:
+        db = new_backend()
+        barrier_sync(dist, db)
+        dres = dia_leg(db, args)
+        db.close()
+        t = max_over_ranks(dist, local, dres["ms_per_step"])
+        dres["ms_per_step"] = t
+        ts = max_over_ranks(dist, local, dres["wall_s"])
+        dres["audio_sec_per_s"] = round(world * dres["audio_sec_per_gpu"] / ts, 3)
 
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            ncpu = min(16, len(os.sched_getaffinity(0)))
-            cpu = cpu_baseline(args, ncpu)
+            # the box's CPU share: OMP_NUM_THREADS is set to it on the GPU box (16 per GPU); else every core we may use
+            ncpu = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+            cpu = cpu_baseline(args, ncpu, bl)
         what = "AR decode + DAC decode" if dac is not None else "AR decode"
         result = {
             "metric": f"audio-sec/wall-sec (RTF^-1), Parler-TTS-mini v1 Q4_K {what}",
@@ -623,16 +743,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * dt / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "q4_K weights x q8_K activations (int dot, f32 combine); DAC f16 im2col x f32 weights, f64 accumulate",
             "data": "synthetic (deterministic weights in Parler-mini v1 Q4_K and DAC-44k shapes; token ids from Harvard sentences)",
-            "config": {"workload": f"Parler-TTS-mini-v1 Q4_K, greedy AR decode + DAC-44k (BASELINE configs[2])",
-                       "model": "parler-tts-mini-v1", "prompts_per_gpu": args.batch, "global_batch": total_prompts,
-                       "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
-                       "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} prompts per GPU, {W} concurrent DAC decoders",
-                       "graph_nodes_per_step": runner.last_graph_nodes(),
-                       "dac_graph_nodes": dac.last_graph_nodes() if dac is not None else None},
+            "config": {"workload": f"Parler-TTS-mini-v1 Q4_K, greedy AR decode + DAC-44k (BASELINE configs[2]) over the fixed "
+                                   f"{total_prompts}-prompt set", "model": "parler-tts-mini-v1", "prompts_per_gpu": per_gpu,
+                       "global_batch": total_prompts, "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
+                       "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} lock-step prompts per GPU, "
+                                      f"{W} concurrent DAC decoders",
+                       "graph_nodes_per_step": graph_nodes, "dac_graph_nodes": dac_nodes},
             "ar_audio_sec_per_s": round(audio_s / dt_ar, 3),
             "ar_ms_per_step": round(1000.0 * dt_ar / args.steps, 4),
             "dac_audio_sec_per_s": round(audio_s / dt_dac, 3) if dac is not None else None,
@@ -643,6 +763,7 @@ def main():
             "audio_gather": None if gathered is None else {
                 "prompts": len(gathered), "audio_sec": round(sum(len(p) for p in gathered) / SAMPLE_RATE, 3),
                 "ms": round(1000.0 * t_gather, 3), "transport": "RCCL send/recv (gatherv) to rank 0" if world > 1 else "local"},
+            "parler_8_prompts_per_gpu": p8,
             "parler_b1": b1,
             "kokoro": kres,
             "orpheus": ores,
@@ -651,14 +772,6 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
-    for xb, rd in dac_workers[R:]:
-        rd.close()
-        xb.close()
-    for rb, rr, rd in reps:
-        if rd is not None:
-            rd.close()
-        rr.close()
-        rb.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

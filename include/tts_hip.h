@@ -145,6 +145,10 @@ enum tts_status {
 };
 
 /* tts_tensor.flags bits */
+/* tts_hip_gemv_stats type slot of the decode attention launches (the split scores + P.V pair, timed
+ * from the first kernel's start to the second's end; bytes = the K and V rows read + q + output) */
+#define TTS_PROF_ATTN 39
+
 #define TTS_FLAG_INPUT 1
 #define TTS_FLAG_HOSTDATA 2 /* data is host memory without a buffer (util.cpp:86-94 trick) */
 #define TTS_FLAG_OUTPUT 4

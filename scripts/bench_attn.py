@@ -24,8 +24,8 @@ def run(hip, P, hd, H, Hk, B, reps, split):
     rng = np.random.default_rng(P)
     max_ctx = 4096
     q = rng.standard_normal((B, H, hd)).astype(np.float32)
-    kc = rng.standard_normal((B, max_ctx, Hk * hd)).astype(np.float32)
-    vc = rng.standard_normal((B, Hk * hd, max_ctx)).astype(np.float32)
+    kc = rng.standard_normal((B, max_ctx, Hk * hd), dtype=np.float32)
+    vc = rng.standard_normal((B, Hk * hd, max_ctx), dtype=np.float32)
     mask = np.zeros(P, np.float32)
     g = nd.Graph()
     build(g, q, kc, vc, mask, P, hd, H, Hk, B, max_ctx)
@@ -68,8 +68,12 @@ def run(hip, P, hd, H, Hk, B, reps, split):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
     hip = ttship.HipBackend(0)
-    for (hd, H, Hk, B) in [(64, 16, 16, 8), (128, 24, 24, 1)]:
-        for P in (448, 900, 1309, 2048):
+    shapes = [(64, 16, 16, 8), (128, 24, 24, 1)]
+    Ps = (448, 900, 1309, 2048)
+    if "--many" in sys.argv:  # the many-prompt decode step: Parler at 32 / 64 lock-step prompts
+        shapes, Ps = [(64, 16, 16, 32), (64, 16, 16, 64)], (460,)
+    for (hd, H, Hk, B) in shapes:
+        for P in Ps:
             for split in ("rows", "split", "fused"):
                 print(json.dumps(run(hip, P, hd, H, Hk, B, reps, split)), flush=True)
     hip.close()

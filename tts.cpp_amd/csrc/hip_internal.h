@@ -397,6 +397,11 @@ namespace tts {
 // The tile-layout copy of a lane-layout Q4_K weight (TTS_FLAG_TILED_COPY), or null.
 const uint8_t * tiled_copy_find(const void * weight);
 
+// ---- profiled launches (k_gemv.hip): a start / stop event pair carried in the dispatch packets
+// (hipExtLaunchKernelGGL), folded into tts_hip_gemv_stats under `type` with `bytes` algorithmic bytes
+void profile_pair(tts_hip_backend * be, hipEvent_t & e0, hipEvent_t & e1);
+void profile_push(tts_hip_backend * be, hipEvent_t e0, hipEvent_t e1, double bytes, int type);
+
 // ---- launchers (k_gemv.hip) ----
 // Quantize M columns (column stride xcs floats) of x to the vec_dot type of `wtype`.
 void launch_quantize_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & aq);

@@ -6,6 +6,7 @@
 // accumulated in f64 (ggml_vec_dot_f32), ggml's soft_max (scale, mask, max, expf, f64 sum, 1/sum),
 // with expf correctly rounded (transcendental policy, hip_internal.h).
 #include "hip_internal.h"
+#include <hip/hip_ext.h>
 
 namespace tts {
 
@@ -898,9 +899,13 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             float * sbuf = be->attn_buf;
             float * mxbuf = be->attn_buf + rows * pstride;
             const dim3 g1((unsigned)nch, (unsigned)H, (unsigned)(n * B));
+            // profiled (TTS_HIP_OPT_PROFILE_GEMV): the pair's start / stop events ride in the two dispatch
+            // packets, bytes = every K and V row read + q + the output
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (be->profile_gemv) profile_pair(be, e0, e1);
             auto scores = [&](auto DPR, auto KSc) {
-                hipLaunchKernelGGL((k_attn_scores<decltype(DPR)::value, decltype(KSc)::value>), g1, dim3(ATTN_THREADS), 0, be->stream, a, sbuf, pstride,
-                                   mxbuf, nch);
+                hipExtLaunchKernelGGL((k_attn_scores<decltype(DPR)::value, decltype(KSc)::value>), g1, dim3(ATTN_THREADS), 0, be->stream, e0,
+                                      nullptr, 0u, a, sbuf, pstride, mxbuf, nch);
             };
             using C1 = std::integral_constant<int, 1>;
             using C2 = std::integral_constant<int, 2>;
@@ -913,11 +918,15 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const dim3 g2((unsigned)(hd / 16), (unsigned)H, (unsigned)(n * B));
             const dim3 g2h((unsigned)(hd / 8), (unsigned)H, (unsigned)(n * B));  // 8 dims per workgroup
             // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
-            if (vvec && P <= 1024 && be->attn_pv_uv16) hipLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
-            else if (vvec && be->attn_pv8) hipLaunchKernelGGL((k_attn_pv<true, 8, 2>), g2h, dim3(128), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
-            else if (vvec) hipLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
-            else hipLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, a, sbuf, pstride, mxbuf, nch);
+            if (vvec && P <= 1024 && be->attn_pv_uv16)
+                hipExtLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            else if (vvec && be->attn_pv8)
+                hipExtLaunchKernelGGL((k_attn_pv<true, 8, 2>), g2h, dim3(128), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            else if (vvec) hipExtLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            else hipExtLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
             TTS_HIP_CHECK(hipGetLastError());
+            if (be->profile_gemv)
+                profile_push(be, e0, e1, (double)rows * (2.0 * P * hd + 2.0 * hd) * 4.0, TTS_PROF_ATTN);
             return;
         }
     }

@@ -154,6 +154,16 @@ __device__ __forceinline__ void q4k_scale_min(const uint8_t * q, int j, int & sc
 
 __device__ __forceinline__ size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
 
+// XCD-contiguous workgroup order: the dispatcher hands workgroup b to XCD b % 8, so consecutive
+// workgroups -- and the rows they own -- land on different XCDs and every XCD's L2 fetches the 128-B
+// lines two neighbouring 576-B Q4_K rows share.  Renumbering b so that XCD x's workgroups take one
+// contiguous span (prefix(x) + b / 8, a bijection on [0, n)) leaves one shared line per XCD boundary.
+// The arithmetic per (row, column) is untouched.
+__device__ __forceinline__ int xcd_contiguous(int b, int n) {
+    const int x = b & 7, q = n >> 3, r = n & 7;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // A kernel argument indexed by a matrix index the compiler cannot prove wave-uniform compiles to a
 // VECTOR load of the kernarg segment, and the s_waitcnt vmcnt(0) that guards its use also waits for
 // every weight and activation load already in flight (it serialised a GEMV's first weight loads
@@ -548,7 +558,7 @@ __global__ __launch_bounds__(NBMAX <= 4 ? 1024 : 512) void k_gemv_q4_K(GemvJob j
     const int l = lane & 7, m = (lane >> 3) % MC, s = lane / (8 * MC);
     const int64_t G = ((int64_t)j.nmat * j.N + S - 1) / S;
     const int64_t gstride = (int64_t)gridDim.x * nw;
-    int64_t g = (int64_t)blockIdx.x * nw + wave;
+    int64_t g = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * nw + wave;
     auto mat_of = [&](int64_t flat) {  // wave-uniform; nmat <= 16, so no 64-bit division
         int mt = 0;
         while (mt + 1 < j.nmat && flat >= (int64_t)(mt + 1) * j.N) ++mt;
@@ -692,7 +702,7 @@ __global__ __launch_bounds__(512) void k_gemv_q4_K_u(GemvJob j, int R, int NCG) 
     const int CPL = (M + NCG - 1) / NCG;
     const int m0 = cg * CPL;
     const int64_t NR = (int64_t)j.nmat * j.N;
-    const int64_t row0 = (int64_t)blockIdx.x * R;
+    const int64_t row0 = (int64_t)xcd_contiguous(blockIdx.x, gridDim.x) * R;
     const bool own = cg < NCG && m0 < M && row0 + r < NR;  // this octet has (row, block, columns) work
     u32x4 hdr, qw;
     TTS_TS(j, 0);
@@ -1994,7 +2004,7 @@ static int64_t q4k_max_cols(int64_t K) {
     return c >= 8 ? 8 : c >= 4 ? 4 : c >= 2 ? 2 : 1;
 }
 
-static void profile_pair(tts_hip_backend * be, hipEvent_t & e0, hipEvent_t & e1) {
+void profile_pair(tts_hip_backend * be, hipEvent_t & e0, hipEvent_t & e1) {
     if (be->ev_free.size() < 2) {
         hipEvent_t a, b;
         TTS_HIP_CHECK(hipEventCreate(&a));
@@ -2008,7 +2018,7 @@ static void profile_pair(tts_hip_backend * be, hipEvent_t & e0, hipEvent_t & e1)
     be->ev_free.pop_back();
 }
 
-static void profile_push(tts_hip_backend * be, hipEvent_t e0, hipEvent_t e1, double bytes, int type) {
+void profile_push(tts_hip_backend * be, hipEvent_t e0, hipEvent_t e1, double bytes, int type) {
     be->ev_pending.push_back({e0, e1});
     be->ev_bytes.push_back(bytes);
     be->ev_type.push_back(type);
@@ -2807,16 +2817,20 @@ static void launch_q80s(tts_hip_backend * be, const GemvJob & j) {
     const size_t lds = q80s_lds(MC, j.K, RW);
     const dim3 grid((unsigned)((j.N + RW - 1) / RW), (unsigned)j.nmat);
     static std::atomic<uint32_t> attr_done[3];
+    // profiled: in-packet events (the Dia leg's roofline; launch_gemv_job leaves Q8_0 slab jobs to this)
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (be->profile_gemv) profile_pair(be, e0, e1);
     if (j.pro == PRO_LN) {
         set_lds_attr_once(attr_done[2], be->device, (const void *)k_gemv_q8_0s<MC, PRO_LN>);
-        hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_LN>), grid, dim3(256), lds, be->stream, j, RW);
+        hipExtLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_LN>), grid, dim3(256), (uint32_t)lds, be->stream, e0, e1, 0u, j, RW);
     } else if (j.pro == PRO_QUANT) {
         set_lds_attr_once(attr_done[1], be->device, (const void *)k_gemv_q8_0s<MC, PRO_QUANT>);
-        hipLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_QUANT>), grid, dim3(256), lds, be->stream, j, RW);
+        hipExtLaunchKernelGGL((k_gemv_q8_0s<MC, PRO_QUANT>), grid, dim3(256), (uint32_t)lds, be->stream, e0, e1, 0u, j, RW);
     } else {
         set_lds_attr_once(attr_done[0], be->device, (const void *)k_gemv_q8_0s<MC>);
-        hipLaunchKernelGGL(k_gemv_q8_0s<MC>, grid, dim3(256), lds, be->stream, j, RW);
+        hipExtLaunchKernelGGL(k_gemv_q8_0s<MC>, grid, dim3(256), (uint32_t)lds, be->stream, e0, e1, 0u, j, RW);
     }
+    if (be->profile_gemv) profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q8_0);
 }
 
 template <int MC>
@@ -2863,8 +2877,8 @@ void launch_profile_spin(tts_hip_backend * be, double us) {
 }
 
 void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
-    // Q4_K launches profile themselves (launch_q4k); other weight types time the whole job
-    const bool prof = be->profile_gemv && job.wtype != TTS_TYPE_Q4_K;
+    // Q4_K launches and Q8_0 slab GEMVs profile themselves (in-packet events); other jobs are timed whole
+    const bool prof = be->profile_gemv && job.wtype != TTS_TYPE_Q4_K && !(job.wtype == TTS_TYPE_Q8_0 && job.M <= 8 && q80s_ok(be, job));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (prof) {
         profile_pair(be, e0, e1);

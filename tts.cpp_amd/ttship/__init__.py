@@ -14,6 +14,7 @@ LIB_PATH = PKG_ROOT / "lib" / "libtts_hip.so"
 
 # ggml type ids (include/tts_hip.h)
 F32, F16, Q4_0, Q8_0, Q4_K, Q8_K, I32 = 0, 1, 2, 8, 12, 15, 26
+PROF_ATTN = 39  # tts_hip_gemv_stats slot of the decode attention pair (TTS_PROF_ATTN)
 
 OPS = ["NONE", "DUP", "ADD", "SUB", "MUL", "DIV", "SQR", "SQRT", "SIN", "COS", "SUM_ROWS", "REPEAT",
        "CONCAT", "NORM", "RMS_NORM", "MUL_MAT", "SCALE", "CPY", "CONT", "RESHAPE", "VIEW", "PERMUTE",
