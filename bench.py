@@ -552,6 +552,7 @@ def main():
     ap.add_argument("--p8", type=int, default=1, help="beside the headline, the AR line at 8 prompts per GPU (2 replicas x 4: "
                     "the 64-prompt batch over 8 GPUs) when the headline runs more (0 = skip)")
     ap.add_argument("--no-fusion", action="store_true")
+    ap.add_argument("--fusion-mask", type=int, default=None, help="TTS_HIP_OPT_FUSION: TTS_FUSE_* bitmask (default: all)")
     ap.add_argument("--no-dac", action="store_true", help="AR decode only")
     ap.add_argument("--attn-split", type=int, default=None, help="TTS_HIP_OPT_ATTN_SPLIT: min KV length for split attention (0 = off)")
     ap.add_argument("--replicas", type=int, default=2, help="concurrent runner replicas per GPU, each on its own "
@@ -573,6 +574,7 @@ def main():
     ap.add_argument("--gemm-q8-staged", type=int, default=None, help="TTS_HIP_OPT_GEMM_Q8_STAGED: many-column Q8_0 GEMM kernel (2 = 64x128 staged, 1 = 64x64 staged, 0 = direct)")
     ap.add_argument("--gemv-kr-inkernel", type=int, default=None, help="TTS_HIP_OPT_GEMV_KR_INKERNEL: max K of K-relay GEMVs quantizing in-kernel (0 = operand pass)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
+    ap.add_argument("--attn-pv-mp", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV_MP: all dims of a head per P.V workgroup (1) or 16 (0)")
     ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
     ap.add_argument("--cu-partition", type=int, default=0, help="TTS_HIP_OPT_CU_PARTITION for the AR replicas: 0 = every "
@@ -602,6 +604,8 @@ def main():
         rb = ttship.HipBackend(local)
         if args.no_fusion:
             rb.set_option(0, 0)
+        elif args.fusion_mask is not None:
+            rb.set_option(0, args.fusion_mask)
         rb.set_option(2, args.graphs)
         for flag, opt in (("conv_acc", "CONV_F32ACC"), ("attn_split", "ATTN_SPLIT"), ("kv_prefetch", "KV_PREFETCH"),
                           ("gemv_unique", "GEMV_UNIQUE"), ("tile_bytes", "Q4K_TILE_BYTES"), ("gemv_ks", "GEMV_KS"),
@@ -609,7 +613,8 @@ def main():
                           ("gemv_nw_min", "GEMV_NW_MIN"), ("gemv_q80_pro", "GEMV_Q80_PRO"), ("gemv_q80_slab", "GEMV_Q80_SLAB"),
                           ("gemv_q80_rw", "GEMV_Q80_RW"), ("gemm_q8_staged", "GEMM_Q8_STAGED"),
                           ("gemv_kr_inkernel", "GEMV_KR_INKERNEL"), ("attn_ks", "ATTN_KS"), ("attn_pv8", "ATTN_PV8"),
-                          ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE")):
+                          ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE"),
+                          ("attn_pv_mp", "ATTN_PV_MP")):
             v = getattr(args, flag)
             if v is not None:
                 rb.set_option(ttship.OPT[opt], v)

@@ -316,6 +316,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMV_F32_WIDE = 32, /* 1 (default): F32 MUL_MATs of >= 2048 rows x 9..64 columns (the output heads of a
                                        many-prompt step) run the wide GEMV (one sequential f64 chain per output, each
                                        weight read once) instead of the tiled GEMM; 0 = tiled GEMM */
+    TTS_HIP_OPT_ATTN_PV_MP = 33, /* 1 (default): the split P.V runs every output dim of a (head, query, sequence) in one
+                                    workgroup (NPASS = hd / 16 passes, P <= 512): the softmax once instead of hd / 16 times */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
 };

@@ -77,6 +77,31 @@ def set_mode(hip, mode):
     hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
     hip.set_option(ttship.OPT["ATTN_KS"], 1 if mode == "split_ks1" else 4 if mode == "split_ks4_pv8" else 2)
     hip.set_option(ttship.OPT["ATTN_PV8"], 1 if mode == "split_ks4_pv8" else 0)
+    hip.set_option(ttship.OPT["ATTN_PV_MP"], 0 if mode in ("split_ks4_pv8", "split_pv16") else 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,hd,B", [(129, 64, 3), (460, 64, 5), (512, 64, 2), (513, 64, 2), (300, 128, 2)])
+def test_pv_all_dims_bit_identical(hip, P, hd, B):
+    """The split P.V with every dim of a (head, query, sequence) in one workgroup (k_attn_pv_mp, P <= 512;
+    the softmax once per head) against 16 dims per workgroup (k_attn_pv): the same sums, identical bits."""
+    H = 16
+    rng = np.random.default_rng(P * 3 + hd + B)
+    max_ctx = (P + 8 + 3) // 4 * 4  # 16-B V rows: the vector-load P.V kernels
+    q = rng.standard_normal((B, H, hd)).astype(np.float32)
+    kc = rng.standard_normal((B, max_ctx, H * hd)).astype(np.float32)
+    vc = rng.standard_normal((B, H * hd, max_ctx)).astype(np.float32)
+    mask = np.zeros(P, np.float32)
+    mask[P // 2] = -np.inf
+    outs = []
+    for mode in ("split", "split_pv16"):
+        set_mode(hip, mode)
+        g = nd.Graph()
+        o = build(g, q, kc, vc, mask, P, hd, H, H, B, max_ctx)
+        g.run_hip(hip)
+        outs.append(g.node_array(o))
+    set_mode(hip, "default")
+    assert np.array_equal(outs[0], outs[1])
 
 
 @pytest.mark.gpu

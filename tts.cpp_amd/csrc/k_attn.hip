@@ -199,7 +199,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
 // ATTN_UV: V chunks (per lane, per dim pass) in flight.
 template <int DPR, bool VVEC, bool PF, int ATTN_UV>
 __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    extern __shared__ __attribute__((aligned(16))) float s_p[];  // (P rounded to 64) + 64 floats (launcher)
     __shared__ float s_wf[ATTN_THREADS / 64];
     __shared__ double s_wd[ATTN_THREADS / 64];
     constexpr int NW = ATTN_THREADS / 64;
@@ -375,8 +375,9 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
 template <int DPR, bool PF, int UV = 8>
 static void launch_attn_rows(tts_hip_backend * be, const AttnArgs & a, bool vvec) {
     const dim3 grid((unsigned)a.H, (unsigned)a.n, (unsigned)a.B);
-    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true, PF, UV>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
-    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false, PF, UV>), grid, dim3(ATTN_THREADS), 0, be->stream, a);
+    const size_t pl = (size_t)(((a.P + 63) & ~63) + 64) * sizeof(float);  // s_p: the context, not ATTN_MAXP
+    if (vvec) hipLaunchKernelGGL((k_attn_decode_rows<DPR, true, PF, UV>), grid, dim3(ATTN_THREADS), pl, be->stream, a);
+    else hipLaunchKernelGGL((k_attn_decode_rows<DPR, false, PF, UV>), grid, dim3(ATTN_THREADS), pl, be->stream, a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -465,7 +466,9 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
                                                     const float * __restrict__ mxbuf, int nch) {
     // NW waves x 4 output dims each (4 NW dims per workgroup)
     constexpr int NTH = 64 * NW;
-    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    // the probabilities in dynamic LDS sized to the context (launcher: (P rounded to 64) + 64 floats): a
+    // fixed ATTN_MAXP array (33 KB) held the P.V grid to 4 workgroups per CU
+    extern __shared__ __attribute__((aligned(16))) float s_p[];
     __shared__ double s_wd[NW];
     const int h = blockIdx.y, z = blockIdx.z;
     const int b = z / a.n, tq = z - b * a.n;
@@ -544,6 +547,94 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
     }
 }
 
+// The same P.V with NPASS passes of 4 * NW output dims per workgroup (all hd dims of a (head, query,
+// sequence) at NPASS = hd / 16): the softmax (P correctly rounded expf and an f64 sum) runs once per
+// workgroup instead of once per 16 dims -- at 64 lock-step prompts the P.V grid otherwise evaluates
+// every exponential hd / 16 = 4 times.  A lane's whole V slice of one pass (P <= 64 UV positions,
+// launcher-checked) is one batch of UV 16-B loads; the next pass's batch is requested before the
+// current pass is summed.  Each output dim is the same f64 sum in the same lane order as k_attn_pv:
+// bit-identical.
+template <int UV, int NW, int NPASS>
+__global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float * __restrict__ sbuf, int pstride,
+                                                       const float * __restrict__ mxbuf, int nch) {
+    constexpr int NTH = 64 * NW;
+    extern __shared__ __attribute__((aligned(16))) float s_p[];
+    __shared__ double s_wd[NW];
+    const int h = blockIdx.y, z = blockIdx.z;
+    const int b = z / a.n, tq = z - b * a.n;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int r = lane >> 4, t = lane & 15;
+    const int P = a.P;
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const int64_t vnb1 = a.v.nb[1];
+    const int ilast = ((P - 1) >> 2) << 2;
+    const int d0 = blockIdx.x * 4 * NW * NPASS + wave * 4 + r;
+    float4 w4[2][UV];
+    auto load_v = [&](auto BUF, int pass) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
+        const char * vrow = vbase + (int64_t)min(d0 + pass * 4 * NW, a.hd - 1) * vnb1;
+#pragma unroll
+        for (int u = 0; u < UV; ++u) w4[bf][u] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(64 * u + 4 * t, ilast)));
+    };
+    load_v(std::integral_constant<int, 0>{}, 0);  // in flight during the softmax
+    const float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
+    const float * mrow = mxbuf + ((int64_t)z * a.H + h) * nch;
+    float mx = -INFINITY;
+    for (int k = 0; k < nch; ++k) mx = fmaxf(mx, mrow[k]);
+    double sum = 0.0;
+    for (int i = tid; i < P; i += NTH) {
+        const float e = cr_expf(__fsub_rn(srow[i], mx));
+        s_p[i] = e;
+        sum += (double)e;
+    }
+    sum = wave_sum_f64(sum);
+    if (lane == 0) s_wd[wave] = sum;
+    __syncthreads();
+    sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) sum += s_wd[w];
+    const float inv = (float)(1.0 / sum);
+    const int P64 = (P + 63) & ~63;
+    for (int i = tid; i < P64; i += NTH) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
+    __syncthreads();
+    auto pass_sum = [&](auto BUF, int pass) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+            const int i = 64 * u + 4 * t;
+            const float4 pp = *(const float4 *)(s_p + min(i, P64 - 4));
+            const float4 vq = w4[bf][u];
+            acc += i + 0 < P ? (double)__fmul_rn(pp.x, vq.x) : 0.0;
+            acc += i + 1 < P ? (double)__fmul_rn(pp.y, vq.y) : 0.0;
+            acc += i + 2 < P ? (double)__fmul_rn(pp.z, vq.z) : 0.0;
+            acc += i + 3 < P ? (double)__fmul_rn(pp.w, vq.w) : 0.0;
+        }
+        acc += dpp_f64<DPP_XOR1>(acc);
+        acc += dpp_f64<DPP_XOR2>(acc);
+        acc += dpp_f64<DPP_HALF_MIRROR>(acc);
+        acc += dpp_f64<DPP_MIRROR>(acc);
+        const int d = d0 + pass * 4 * NW;
+        if (t == 0 && d < a.hd) {
+            const int64_t o = (((int64_t)b * a.n + tq) * a.H + h) * a.hd + d;
+            a.out[o] = (float)acc;
+            if (a.out2) a.out2[o] = (float)acc;
+        }
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+#pragma unroll
+    for (int pass = 0; pass < NPASS; pass += 2) {
+        if (pass + 1 < NPASS) load_v(B1{}, pass + 1);
+        pass_sum(B0{}, pass);
+        if (pass + 1 >= NPASS) break;
+        if (pass + 2 < NPASS) load_v(B0{}, pass + 2);
+        pass_sum(B1{}, pass + 1);
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // Fused decode attention for long contexts: ONE launch per attention, one 1024-thread workgroup per
 // (head, query, sequence).  The split pair above pays two launch ramps and an L2 round trip of the
@@ -559,7 +650,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
 constexpr int FUSED_THREADS = 1024;
 template <int DPR, int UVC>
 __global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_p[ATTN_MAXP + 64];
+    extern __shared__ __attribute__((aligned(16))) float s_p[];  // (P rounded to 64) + 64 floats (launcher)
     __shared__ float s_wf[FUSED_THREADS / 64];
     __shared__ double s_wd[FUSED_THREADS / 64];
     constexpr int NW = FUSED_THREADS / 64;
@@ -885,8 +976,9 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
                           (((uintptr_t)v.data) % 16) == 0 && v.nb[1] >= (size_t)16 * ((P + 3) / 4);
     if (krows && vvec_all && be->attn_fused_minp > 0 && P >= be->attn_fused_minp && P <= ATTN_MAXP) {
         const dim3 grid((unsigned)H, (unsigned)n, (unsigned)B);
-        if (hd == 64) hipLaunchKernelGGL((k_attn_fused<1, 8>), grid, dim3(FUSED_THREADS), 0, be->stream, a);
-        else hipLaunchKernelGGL((k_attn_fused<2, 8>), grid, dim3(FUSED_THREADS), 0, be->stream, a);
+        const size_t pl = (size_t)(((P + 63) & ~63) + 64) * sizeof(float);
+        if (hd == 64) hipLaunchKernelGGL((k_attn_fused<1, 8>), grid, dim3(FUSED_THREADS), pl, be->stream, a);
+        else hipLaunchKernelGGL((k_attn_fused<2, 8>), grid, dim3(FUSED_THREADS), pl, be->stream, a);
         TTS_HIP_CHECK(hipGetLastError());
         return;
     }
@@ -918,12 +1010,17 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const dim3 g2((unsigned)(hd / 16), (unsigned)H, (unsigned)(n * B));
             const dim3 g2h((unsigned)(hd / 8), (unsigned)H, (unsigned)(n * B));  // 8 dims per workgroup
             // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
-            if (vvec && P <= 1024 && be->attn_pv_uv16)
-                hipExtLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            const uint32_t pl = (uint32_t)((((P + 63) & ~63) + 64) * sizeof(float));  // s_p
+            if (vvec && P <= 512 && be->attn_pv_mp && (hd == 64 || hd == 128)) {  // all dims of a (head, query, seq) per workgroup
+                const dim3 g3(1u, (unsigned)H, (unsigned)(n * B));
+                if (hd == 64) hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 4>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                else hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 8>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            } else if (vvec && P <= 1024 && be->attn_pv_uv16)
+                hipExtLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
             else if (vvec && be->attn_pv8)
-                hipExtLaunchKernelGGL((k_attn_pv<true, 8, 2>), g2h, dim3(128), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
-            else if (vvec) hipExtLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
-            else hipExtLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), 0, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                hipExtLaunchKernelGGL((k_attn_pv<true, 8, 2>), g2h, dim3(128), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            else if (vvec) hipExtLaunchKernelGGL((k_attn_pv<true, 8>), g2, dim3(PV_THREADS), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+            else hipExtLaunchKernelGGL((k_attn_pv<false, 8>), g2, dim3(PV_THREADS), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
             TTS_HIP_CHECK(hipGetLastError());
             if (be->profile_gemv)
                 profile_push(be, e0, e1, (double)rows * (2.0 * P * hd + 2.0 * hd) * 4.0, TTS_PROF_ATTN);

@@ -652,8 +652,19 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, 
     constexpr int QT = 64, OCT = 32, ICC = 16, XW = QT + JM - 1;
     constexpr int NX = ICC * XW, NW4 = ICC * K * OCT / 4;
     constexpr int XR = (NX + 255) / 256, WR = (NW4 + 255) / 256;
-    __shared__ float xs[ICC][XW];
-    __shared__ float ws[ICC * K * OCT];  // [ic][k][oc]
+    // Padded LDS strides (ds_read_b32 / ds_write_b32 bank = dword index mod 32, per 32-lane half):
+    //  - reads of one MFMA step: lanes (kq, c16) of a half take two consecutive input channels, so the
+    //    x row stride XWP and the weight channel stride WIC are = 16 mod 32 (the two 16-lane groups on
+    //    opposite bank halves);
+    //  - the weight stage: a half's 32 lanes hold 4 taps of (channel oc, tap group kg); with a tap
+    //    stride WK, 4 * WK = 32 / (K / 4) mod 32 spreads the tap groups over disjoint bank ranges
+    //    (S = 8: 34, S = 4: 36; S = 2 has one group).  Unpadded, these were 2- to 4-way conflicts
+    //    (5.3 per LDS instruction measured on S = 8).  Same values, same MFMA order: bit-identical.
+    constexpr int XWP = 80;
+    constexpr int WK = S == 8 ? 34 : S == 4 ? 36 : OCT + 1;
+    constexpr int WIC0 = K * WK, WIC = WIC0 + ((16 - WIC0 % 32) + 32) % 32;
+    __shared__ float xs[ICC][XWP];
+    __shared__ float ws[ICC * WIC];  // [ic][k][oc] at ic * WIC + k * WK + oc
     const int lane = threadIdx.x & 63, qw = threadIdx.x >> 6;
     const int c16 = lane & 15, kq = lane >> 4;
     const int OC = (int)w.ne[1], IC = (int)w.ne[2];
@@ -704,8 +715,8 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, 
             if (t >= NW4) continue;
             const int ic = t / (K * OCT / 4), rem = (t - ic * (K * OCT / 4)) * 4;
             const int oc = rem / K, k = rem - oc * K;  // 4 consecutive taps k..k+3 of channel oc
-            float * o = ws + (ic * K + k) * OCT + oc;
-            o[0] = wr[u].x, o[OCT] = wr[u].y, o[2 * OCT] = wr[u].z, o[3 * OCT] = wr[u].w;
+            float * o = ws + ic * WIC + k * WK + oc;
+            o[0] = wr[u].x, o[WK] = wr[u].y, o[2 * WK] = wr[u].z, o[3 * WK] = wr[u].w;
         }
     };
     // split launch: input channels [ic_lo, ic_hi) (whole chunks), f64 partials to part[z][oc][o]
@@ -727,7 +738,7 @@ __global__ __launch_bounds__(256) void k_convt_f64_lds(TD y, TD x, TD w, int p, 
 #pragma unroll
                 for (int r = 0; r < S; ++r)
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) aw[j][r][h] = ws[(icl * K + r + S * j) * OCT + h * 16 + c16];
+                    for (int h = 0; h < 2; ++h) aw[j][r][h] = ws[icl * WIC + (r + S * j) * WK + h * 16 + c16];
             }
 #pragma unroll
             for (int j = 0; j < JM; ++j) {
