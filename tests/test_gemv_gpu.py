@@ -77,6 +77,24 @@ def test_q4_K_prefill_gemm(hip, tiled, K, N, M):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("K,N,M", [(4096, 1024, 32), (2048, 160, 17), (4096, 512, 64)])
+def test_q4_K_prefill_gemm_eight_waves(hip, tiled, K, N, M):
+    """The many-column K-relay GEMM with a tile's blocks over eight waves (TTS_HIP_OPT_GEMM_KR_NW = 8,
+    K >= 2048): the relay hands ggml's chain through eight waves in block order, bit-identical."""
+    hip.set_option(ttship.OPT["GEMM_KR_NW"], 8)
+    try:
+        rng = np.random.default_rng(K * 5 + N + M + tiled)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        hip.set_option(ttship.OPT["GEMM_KR_NW"], 4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,N,M", [(1024, 64, 12000), (4096, 32, 3000)])
 def test_q4_K_prefill_gemm_column_chunks(hip, K, N, M):
     """A prompt pass over many prompts (64 prompts x 448 tokens) has more columns than the 64 MiB operand

@@ -303,6 +303,7 @@ struct tts_hip_backend {
     int cu_total = 256;
     int bgemm_f32 = 1;  // TTS_HIP_OPT_BGEMM_F32
     int gemv_f32_wide = 1;  // TTS_HIP_OPT_GEMV_F32_WIDE
+    int gemm_kr_nw = 4;     // TTS_HIP_OPT_GEMM_KR_NW: waves per tile of the many-column K-relay GEMM (4 or 8)
     // tile-layout Q4_K GEMVs of at most this many 16-row tiles (M <= 8, K <= 4096) run the K-split
     // matrix-core kernel k_gemv_q4K_ks (0 = never)
     int64_t gemv_ks_tiles = 256;

@@ -2423,11 +2423,14 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     const unsigned gx = (unsigned)(job_rows(j) / 16), gy = (unsigned)nct;
     auto go = [&](auto LANE) {
         constexpr bool L = decltype(LANE)::value;
+        // TTS_HIP_OPT_GEMM_KR_NW = 8: a tile's blocks over eight waves (K >= 2048; a longer relay, half the
+        // blocks per wave)
+        const bool nw8 = be->gemm_kr_nw == 8;
         switch (nb) {
             case 4: launch_q4k_kr_t<1, false, 4, L>(be, j, gx, gy); break;
-            case 8: launch_q4k_kr_t<2, false, 4, L>(be, j, gx, gy); break;
+            case 8: nw8 ? launch_q4k_kr_t<1, false, 8, L>(be, j, gx, gy) : launch_q4k_kr_t<2, false, 4, L>(be, j, gx, gy); break;
             case 12: launch_q4k_kr_t<3, false, 4, L>(be, j, gx, gy); break;
-            default: launch_q4k_kr_t<4, false, 4, L>(be, j, gx, gy); break;
+            default: nw8 ? launch_q4k_kr_t<2, false, 8, L>(be, j, gx, gy) : launch_q4k_kr_t<4, false, 4, L>(be, j, gx, gy); break;
         }
     };
     if (j.tiled) go(std::false_type{});
