@@ -283,7 +283,7 @@ def orpheus_leg(be, args, rank):
         prompt = (np.arange(B * n_prompt, dtype=np.int32).reshape(B, n_prompt) * 7919 + 128000 + rank) % cfg.vocab_size
         first = o.prefill(prompt).argmax(axis=1).astype(np.int32)
         toks = o.generate(first, 4)
-        heads0 = orpheus_snac_heads(toks[0].tolist() * 7)
+        heads0 = orpheus_snac_heads((toks[0].tolist() * 7)[:7])  # one 7-token frame
         snac.decode(heads0, np.zeros(snac.noise_per_frame * len(heads0[-1]), np.float32))  # warm
         rng = np.random.default_rng(rank)
         be.sync()
