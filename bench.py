@@ -512,8 +512,21 @@ def new_dac_for(args, rb, dcfg):
     if args.dac_conv_split is not None:  # concurrent decoders each sizing split convs for the whole chip
         rb.set_option(ttship.OPT["CONV_SPLIT"], args.dac_conv_split)
     rd = ttship.Dac(rb.iface(), dcfg)
-    rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
+    nbd = dac_batch(args)
+    if nbd > 1:  # warm the batched shape twice: the first sighting launches eagerly, the second records the graph
+        for _ in range(2):
+            rd.decode_batch(np.zeros((nbd, args.steps, dcfg.n_codebooks), dtype=np.int32))
+    else:
+        rd.decode(np.zeros((min(8, args.steps), dcfg.n_codebooks), dtype=np.int32))  # warm (code objects, arena)
     return rd
+
+
+def dac_batch(args):
+    """Prompts per batched DAC decode: short codec sequences fill few CUs, so up to 64 frames per prompt
+    eight prompts decode as one graph (tts_dac_decode_batch); longer ones one by one."""
+    if args.dac_batch is not None:
+        return max(1, args.dac_batch)
+    return 8 if args.steps <= 64 else 1
 
 
 def close_replicas(reps):
@@ -585,6 +598,8 @@ def main():
     ap.add_argument("--dac-workers", type=int, default=8, help="concurrent DAC decoders per GPU (each its own backend / "
                     "stream; the AR replicas' backends first): short codec sequences fill few CUs, so several "
                     "prompts decode side by side")
+    ap.add_argument("--dac-batch", type=int, default=None, help="prompts per batched DAC decode (tts_dac_decode_batch: one "
+                    "graph, zeroed gaps, PCM bit-identical to one decode per prompt); default: 8 up to 64 frames, else 1")
     ap.add_argument("--kokoro-prompts", type=int, default=8, help="Kokoro-82M prompts per GPU, end to end (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
@@ -621,11 +636,14 @@ def main():
                 rb.set_option(ttship.OPT[opt], v)
         return rb
 
-    dcfg = ttship.dac_config(max_frames=args.steps)
+    # (batched decodes: nb prompts + the gaps between them, <= 8 frames each, in one graph)
+    dcfg = ttship.dac_config(max_frames=args.steps if dac_batch(args) == 1 else dac_batch(args) * (args.steps + 8))
     reps, prefill_ms, cfg = parler_replicas(args, per_gpu, R, rank, new_backend, None if args.no_dac else dcfg)
     be, runner, dac = reps[0]
     # DAC workers: the replicas' decoders plus extra backends of their own
-    W = 0 if args.no_dac else max(1, min(args.dac_workers, per_gpu))
+    NBD = min(dac_batch(args), per_gpu)
+    n_dac_batches = (per_gpu + NBD - 1) // NBD
+    W = 0 if args.no_dac else max(1, min(args.dac_workers, n_dac_batches))
     dac_workers = [(rb, rd) for rb, _, rd in reps[:W]]
     while len(dac_workers) < W:
         xb = new_backend()
@@ -644,10 +662,17 @@ def main():
     pcm = [None] * per_gpu
 
     def dac_leg(w):
-        # worker w decodes every W-th prompt of this GPU's prompts
+        # worker w decodes every W-th batch of NBD prompts of this GPU's prompts
         xb, rd = dac_workers[w]
-        for g in range(w, per_gpu, W):
-            pcm[g] = rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
+        for bt in range(w, n_dac_batches, W):
+            gs = list(range(bt * NBD, min(per_gpu, (bt + 1) * NBD)))
+            if len(gs) == 1 or NBD == 1:
+                for g in gs:
+                    pcm[g] = rd.decode(dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size))
+            else:
+                out = rd.decode_batch(np.stack([dac_codes(toks_r[g // bl][g % bl], dcfg.codebook_size) for g in gs]))
+                for i, g in enumerate(gs):
+                    pcm[g] = out[i]
         xb.sync()
 
     t0 = time.perf_counter()
@@ -757,7 +782,7 @@ def main():
                                    f"{total_prompts}-prompt set", "model": "parler-tts-mini-v1", "prompts_per_gpu": per_gpu,
                        "global_batch": total_prompts, "kv_len_start": args.ctx, "frames_per_prompt": args.steps,
                        "parallelism": f"dp{world} (prompt shards), {R} concurrent replicas x {bl} lock-step prompts per GPU, "
-                                      f"{W} concurrent DAC decoders",
+                                      f"{W} concurrent DAC decoders" + (f" of {NBD} prompts per batched decode" if NBD > 1 else ""),
                        "graph_nodes_per_step": graph_nodes, "dac_graph_nodes": dac_nodes},
             "ar_audio_sec_per_s": round(audio_s / dt_ar, 3),
             "ar_ms_per_step": round(1000.0 * dt_ar / args.steps, 4),

@@ -194,6 +194,15 @@ void tts_dac_free(tts_dac * d);
 int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, float * pcm);
 int64_t tts_dac_hop(const tts_dac * d);
 int32_t tts_dac_last_graph_nodes(const tts_dac * d);
+/* Batched decode of nb prompts of T frames each (a serving-side layout; TTS.cpp decodes one prompt per
+ * dac_runner::run): ONE graph over nb * T + (nb - 1) * gap frames, the gaps zeroed before every conv that
+ * reaches across them, so each prompt's PCM is bit-identical to tts_dac_decode of that prompt.
+ * codes: [nb][T][n_codebooks]; pcm: [nb][T * hop]; gap 0 = tts_dac_min_gap; nb * T + (nb - 1) * gap
+ * <= max_frames. */
+int tts_dac_decode_batch(tts_dac * d, const int32_t * codes, int32_t nb, int32_t T, int32_t gap, float * pcm);
+int64_t tts_dac_min_gap(const tts_dac * d);
+/* The last decode's node array (fusion statistics: tts_hip_plan_stats). */
+tts_tensor * const * tts_dac_graph(const tts_dac * d, int32_t * n_nodes);
 
 /* SNAC decoder (Orpheus' vocoder: three codebook streams -> 24 kHz PCM): snac_runner::run /
  * build_snac_graph, /root/reference/src/decoder/snac_model.cpp:86-208, with the shared codec layers

@@ -72,9 +72,13 @@ def main():
     Ps = (448, 900, 1309, 2048)
     if "--many" in sys.argv:  # the many-prompt decode step: Parler at 32 / 64 lock-step prompts
         shapes, Ps = [(64, 16, 16, 32), (64, 16, 16, 64)], (460,)
+    modes = ("rows", "split", "fused")
+    for a in sys.argv:
+        if a.startswith("--P="):  # e.g. --P=460,1200 (with --many: the split pair only)
+            Ps, modes = tuple(int(x) for x in a[4:].split(",")), ("split",)
     for (hd, H, Hk, B) in shapes:
         for P in Ps:
-            for split in ("rows", "split", "fused"):
+            for split in modes:
                 print(json.dumps(run(hip, P, hd, H, Hk, B, reps, split)), flush=True)
     hip.close()
 

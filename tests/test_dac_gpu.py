@@ -41,3 +41,26 @@ def test_dac_pcm_matches_oracle(hip, name, T, acc):
     # per-32-term f32 rounding flips downstream f16 re-roundings (measured 1.4e-3 on DAC-44k)
     assert err <= (1e-4 if acc == 0 else 5e-3), f"max |pcm_gpu - pcm_oracle| = {err:.3e}"
     assert float(np.std(ref)) > 0.05  # not a degenerate (saturated / silent) decoder
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,nb,T", [("dac44k", 8, 20), ("dac44k", 3, 7), ("dac44k_narrow", 4, 5)])
+def test_dac_batch_bit_identical(hip, name, nb, T):
+    """tts_dac_decode_batch on the GPU: nb prompts as one graph (zeroed gaps between them) against one
+    decode per prompt: identical PCM bits (the conv tiles / splits change with the longer sequence, the
+    per-output sums do not).  The narrow config is also held against the oracle's single decodes."""
+    kw = dict(CFGS[name])
+    kw["max_frames"] = nb * (T + 8)
+    cfg = ttship.dac_config(**kw)
+    codes = np.random.default_rng(nb * 100 + T).integers(0, cfg.codebook_size, size=(nb, T, cfg.n_codebooks))
+    d = ttship.Dac(hip.iface(), cfg)
+    try:
+        single = np.stack([d.decode(codes[z]) for z in range(nb)])
+        batched = d.decode_batch(codes)
+        again = d.decode_batch(codes)  # the masks and the recorded graph are reused
+    finally:
+        d.close()
+    assert np.array_equal(batched, single) and np.array_equal(again, single)
+    if name == "dac44k_narrow":
+        ref = np.stack([decode(py_oracle.iface(8), cfg, codes[z]) for z in range(nb)])
+        assert float(np.max(np.abs(batched.astype(np.float64) - ref))) <= 1e-4

@@ -4,6 +4,7 @@
 // (general_neural_audio_codec.cpp:133-172) and snake_1d / reciprocal (util.cpp:86-101).
 // Runs on any tts_backend_iface (HIP backend, or the oracle in tests).  Weights are deterministic
 // synthetic tensors in DAC-44k shapes (no checkpoints offline).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -58,6 +59,11 @@ struct tts_dac {
     uint64_t tensor_index = 0;
     std::vector<wspec> specs;
     const tts_gguf * gguf = nullptr;  // weight source while creating from a file (else synthetic)
+    // batched decode (tts_dac_decode_batch): the prompt masks of the last (nb, T, gap), one per rate
+    void * mask_buf = nullptr;
+    size_t mask_bytes = 0;
+    int32_t mask_key[3] = {0, 0, 0};
+    std::vector<size_t> mask_off;  // float offset of rate level l's mask
 };
 
 extern "C" void tts_dac_default_config(tts_dac_config * c) {
@@ -214,6 +220,7 @@ extern "C" tts_dac * tts_dac_create(const tts_backend_iface * be, const tts_dac_
 extern "C" void tts_dac_free(tts_dac * d) {
     if (!d) return;
     if (d->arena) d->be.free(d->be.ctx, d->arena);
+    if (d->mask_buf) d->be.free(d->be.ctx, d->mask_buf);
     if (d->wbuf) d->be.free(d->be.ctx, d->wbuf);
     delete d;
 }
@@ -231,10 +238,22 @@ static tts_tensor * snake(tts_dac * d, tg::context & c, tts_tensor * alpha, tts_
     return tg::add(c, x, tg::mul(c, tg::sqr(c, tg::sin(c, tg::mul(c, x, alpha))), recip));
 }
 
-static tts_tensor * build_graph(tts_dac * d, int64_t T) {
+// masks (batched decode): masks[l] = [T_l, 1] f32 of rate level l (0 = latent frames, l = after block
+// l), 1 inside a prompt's span and 0 in the gaps between prompts; `cur` is multiplied by the level's
+// mask wherever a conv with reach > 0 (or a transposed conv) reads it next, so every prompt's outputs
+// see zeros beyond its ends, exactly as the zero padding of a decode of its own
+static tts_tensor * build_graph(tts_dac * d, int64_t T, const std::vector<tts_tensor *> * masks = nullptr) {
     const auto & cf = d->cfg;
     tg::context & c = d->gctx;
     c.reset();
+    std::vector<tts_tensor *> mk;
+    if (masks)
+        for (size_t l = 0; l < masks->size(); ++l) {
+            tts_tensor * m = tg::new_tensor_2d(c, TTS_TYPE_F32, (*masks)[l]->ne[0], 1);
+            m->data = (*masks)[l]->data;  // the runner's mask buffer (not arena memory)
+            mk.push_back(m);
+        }
+    auto gate = [&](tts_tensor * x, size_t l) { return l < mk.size() ? tg::mul(c, x, mk[l]) : x; };
     // dac_build_audio_inputs (dac_model.cpp:100-123): codes [T * n_codebooks], time-major
     d->in_codes = tg::new_tensor_1d(c, TTS_TYPE_I32, T * cf.n_codebooks);
     tg::set_input(d->in_codes);
@@ -249,17 +268,18 @@ static tts_tensor * build_graph(tts_dac * d, int64_t T) {
         cur = tg::add(c, cur, d->quant[i].out_bias);
         embd = i == 0 ? cur : tg::add(c, embd, cur);
     }
-    tts_tensor * cur = tg::conv_1d(c, d->in_kernel, embd, 1, 3, 1);
+    tts_tensor * cur = tg::conv_1d(c, d->in_kernel, gate(embd, 0), 1, 3, 1);
     cur = tg::add(c, cur, d->in_bias);
+    size_t lvl = 0;
     for (auto & L : d->layers) {
         // build_layer (general_neural_audio_codec.cpp:151-163)
-        cur = snake(d, c, L.in_alpha, cur);
+        cur = snake(d, c, L.in_alpha, gate(cur, lvl++));
         cur = tg::conv_transpose_1d(c, L.kernel, cur, L.stride, L.padding, 1, 0, 1);
         cur = tg::add(c, cur, L.bias);
         for (auto & u : L.ru) {
             // build_residual_unit (general_neural_audio_codec.cpp:133-149), groups = 1
-            tts_tensor * residual = cur;
-            cur = snake(d, c, u.in_alpha, cur);
+            tts_tensor * residual = cur;  // (its gap values never reach a prompt: the next conv input is gated)
+            cur = snake(d, c, u.in_alpha, gate(cur, lvl));
             cur = tg::conv_1d(c, u.in_kernel, cur, 1, u.padding, u.dilation);
             cur = tg::add(c, cur, u.in_bias);
             cur = snake(d, c, u.out_alpha, cur);
@@ -268,7 +288,7 @@ static tts_tensor * build_graph(tts_dac * d, int64_t T) {
             cur = tg::add(c, cur, residual);
         }
     }
-    cur = snake(d, c, d->out_alpha, cur);
+    cur = snake(d, c, d->out_alpha, gate(cur, lvl));
     cur = tg::conv_1d(c, d->out_kernel, cur, 1, 3, 1);
     cur = tg::add(c, cur, d->out_bias);
     cur = tg::tanh(c, cur);
@@ -291,7 +311,90 @@ extern "C" int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, flo
     return st;
 }
 
+// Batched decode: nb prompts of T frames each as ONE graph over nb * T + (nb - 1) * gap frames, the
+// prompts laid out along time with `gap` frames between them and the rate-level masks zeroing the
+// gaps before every conv that reaches across (build_graph).  A prompt's PCM is the samples of its
+// span: each of its outputs is the same sum of the same products as in a decode of its own (the
+// terms a lone decode takes from zero padding come from the zeroed gap), so it is bit-identical to
+// tts_dac_decode of that prompt.  Every node keeps the reference op's semantics (a serving-side
+// layout, not a new op), so the oracle runs the same batched graph.  gap = 0: the smallest gap the
+// convs' reach allows.
+static int64_t dac_min_gap(const tts_dac * d) {
+    int64_t g = 3, rate = 1;  // the initial conv (k 7, pad 3) at the latent rate
+    for (const auto & L : d->layers) {
+        rate *= L.stride;
+        for (const auto & u : L.ru) g = std::max(g, (u.padding + rate - 1) / rate);
+        g = std::max<int64_t>(g, 1);  // a transposed conv's first output of the next prompt: (T + gap) * s - p >= T * s
+    }
+    return std::max<int64_t>(g, (3 + rate - 1) / rate);  // the final conv (k 7, pad 3)
+}
+
+extern "C" int tts_dac_decode_batch(tts_dac * d, const int32_t * codes, int32_t nb, int32_t T, int32_t gap, float * pcm) {
+    if (!d || nb <= 0 || T <= 0 || gap < 0) return TTS_STATUS_BAD_ARG;
+    if (nb == 1) return tts_dac_decode(d, codes, T, pcm);
+    const int64_t G = gap ? gap : dac_min_gap(d);
+    if (G < dac_min_gap(d)) return TTS_STATUS_BAD_ARG;
+    const int64_t span = T + G, Tt = (int64_t)nb * span - G;
+    if (Tt > d->cfg.max_frames) return TTS_STATUS_BAD_ARG;
+    const int ncb = d->cfg.n_codebooks;
+    // the masks of (nb, T, G), kept while the shape repeats
+    const int nl = (int)d->layers.size() + 1;
+    if (d->mask_key[0] != nb || d->mask_key[1] != T || d->mask_key[2] != (int32_t)G || !d->mask_buf) {
+        std::vector<float> host;
+        d->mask_off.assign(nl, 0);
+        int64_t rate = 1;
+        for (int l = 0; l < nl; ++l) {
+            if (l > 0) rate *= d->layers[l - 1].stride;
+            d->mask_off[l] = host.size();
+            const int64_t n = Tt * rate;
+            for (int64_t i = 0; i < n; ++i) host.push_back((i / rate) % span < T ? 1.0f : 0.0f);
+        }
+        const size_t bytes = host.size() * sizeof(float);
+        if (bytes > d->mask_bytes) {
+            if (d->mask_buf) d->be.free(d->be.ctx, d->mask_buf);
+            d->mask_buf = d->be.alloc(d->be.ctx, bytes);
+            d->mask_bytes = d->mask_buf ? bytes : 0;
+            if (!d->mask_buf) return TTS_STATUS_ALLOC_FAILED;
+        }
+        const int st = d->be.set(d->be.ctx, d->mask_buf, host.data(), bytes);
+        if (st != 0) return st;
+        d->mask_key[0] = nb, d->mask_key[1] = T, d->mask_key[2] = (int32_t)G;
+    }
+    tg::context mctx;  // the masks' descriptors (data in mask_buf)
+    std::vector<tts_tensor *> masks;
+    int64_t rate = 1;
+    for (int l = 0; l < nl; ++l) {
+        if (l > 0) rate *= d->layers[l - 1].stride;
+        tts_tensor * m = tg::new_tensor_2d(mctx, TTS_TYPE_F32, Tt * rate, 1);
+        m->data = (char *)d->mask_buf + d->mask_off[l] * sizeof(float);
+        masks.push_back(m);
+    }
+    tts_tensor * out = build_graph(d, Tt, &masks);
+    if (!tg::alloc_graph(d->gctx, d->arena, d->arena_size, true)) {
+        fprintf(stderr, "dac: compute arena too small (%zu needed)\n", d->gctx.arena_used);
+        return TTS_STATUS_ALLOC_FAILED;
+    }
+    // codes of the gaps: code 0 (their embeddings are masked before the first conv)
+    std::vector<int32_t> all((size_t)Tt * ncb, 0);
+    for (int z = 0; z < nb; ++z)
+        memcpy(all.data() + (size_t)z * span * ncb, codes + (size_t)z * T * ncb, sizeof(int32_t) * (size_t)T * ncb);
+    int st = d->be.set(d->be.ctx, d->in_codes->data, all.data(), sizeof(int32_t) * all.size());
+    if (st == 0) st = d->be.compute(d->be.ctx, d->gctx.nodes.data(), (int)d->gctx.nodes.size());
+    const int64_t hop = tts_dac_hop(d);
+    for (int z = 0; st == 0 && pcm && z < nb; ++z)
+        st = d->be.get(d->be.ctx, pcm + (size_t)z * T * hop, (const char *)out->data + sizeof(float) * (size_t)z * span * hop,
+                       sizeof(float) * (size_t)T * hop);
+    return st;
+}
+
+extern "C" int64_t tts_dac_min_gap(const tts_dac * d) { return d ? dac_min_gap(d) : 0; }
+
 extern "C" int32_t tts_dac_last_graph_nodes(const tts_dac * d) { return (int32_t)d->gctx.nodes.size(); }
+
+extern "C" tts_tensor * const * tts_dac_graph(const tts_dac * d, int32_t * n_nodes) {
+    if (n_nodes) *n_nodes = d ? (int32_t)d->gctx.nodes.size() : 0;
+    return d ? d->gctx.nodes.data() : nullptr;
+}
 
 // ---- GGUF loader path (dac_model::prep_constants / prep_layers / assign_weight) ----
 static bool key_u32(const tts_gguf * g, std::initializer_list<const char *> keys, uint32_t * out) {

@@ -144,6 +144,7 @@ struct Item {
     bool lnrms = false;
     bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
     const tts_tensor * snake_one = nullptr;  // SNAKE: b == nullptr, recip = snake_one[0] / alpha in the kernel
+    const tts_tensor * snake_mask = nullptr;  // SNAKE: x = x * mask[t] first (the MUL node of a batched DAC decode's gap mask)
     const tts_tensor * xsrc = nullptr;  // src1 is a skipped CONT of this contiguous tensor (same bytes): read its data
     bool shadow = false;    // ATTN: also write the private copy (be->shadow)
     int xattn = -1;         // GEMV: index of the short-context ATTN item whose query it produces (one launch)
@@ -1201,6 +1202,22 @@ struct Planner {
         Item it;
         it.kind = Item::SNAKE;
         it.x = x, it.w = alpha, it.b = R, it.dst = A;
+        // a time mask in front, read by this snake only (tts_dac_decode_batch zeroes the gaps between
+        // prompts): x = MUL(x0, m [ne0, 1]) -> the kernel multiplies (the same f32 product) and the node is skipped
+        if (x->op == TTS_OP_MUL && index.count(x) && act[index[x]] == 0 && uses[x] == 2) {
+            const tts_tensor *x0 = x->src[0], *m = x->src[1];
+            const auto ci = consumers.find(x);
+            bool only = ci != consumers.end() && ci->second.size() == 2;
+            if (only)
+                for (int c : ci->second) only &= nodes[c] == M1 || nodes[c] == A;
+            if (only && x0 && m && x0->type == TTS_TYPE_F32 && contiguous(x0) && x0->ne[0] == x->ne[0] && x0->ne[1] == x->ne[1] &&
+                x0->ne[2] == x->ne[2] && x0->ne[3] == x->ne[3] && m->type == TTS_TYPE_F32 && contiguous(m) && m->ne[0] == x->ne[0] &&
+                m->ne[1] * m->ne[2] * m->ne[3] == 1 && !overlap(A, m) && !(overlap(A, x0) && A->data != x0->data)) {
+                it.x = x0;
+                it.snake_mask = m;
+                act[index[x]] = -1;
+            }
+        }
         act[index[M1]] = act[index[S]] = act[index[Q]] = act[index[M2]] = -1;
         // reciprocal() = DIV(broadcast view of a scalar, alpha) feeding only this snake (DAC, SNAC):
         // the kernel divides itself (the same correctly rounded division) and the node is skipped
@@ -2128,7 +2145,7 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::SNAKE:
-            launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one);
+            launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one, it.snake_mask);
             return 0;
         case Item::CONV:
             launch_conv1d_fused(be, it.conv);

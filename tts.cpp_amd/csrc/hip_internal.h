@@ -285,7 +285,7 @@ struct tts_hip_backend {
     size_t attn_floats = 0;
     int attn_split_minp = 128;
     int attn_ks = 2;   // split scores: 128 * attn_ks positions per workgroup (TTS_HIP_OPT_ATTN_KS)
-    int attn_pv_mp = 1;  // split P.V: every dim of a (head, query, sequence) in one workgroup, P <= 512 (TTS_HIP_OPT_ATTN_PV_MP)
+    int attn_pv_mp = 1;  // split P.V: every dim of a (head, query, sequence) in one workgroup (TTS_HIP_OPT_ATTN_PV_MP)
     int attn_pv8 = 0;  // split P.V: 8 output dims per workgroup instead of 16 (TTS_HIP_OPT_ATTN_PV8)
     int attn_pv_uv16 = 0;  // split P.V: one 16-chunk V batch per lane for P <= 1024 (TTS_HIP_OPT_ATTN_PV16; measured equal, off)
     int attn_fused_minp = 0;  // the one-launch 1024-thread decode attention from this many keys (0 = off: measured no faster in the Parler step)
@@ -443,7 +443,7 @@ constexpr int EMBED_MAX_TERMS = 16;
 void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n);
 // recip == nullptr: the kernel evaluates reciprocal() = one[0] / alpha[c] itself (`one` a broadcast scalar)
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
-                  const tts_tensor * one = nullptr);
+                  const tts_tensor * one = nullptr, const tts_tensor * mask = nullptr);
 void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * final_out, const float * hist, int64_t Hd, int64_t T);
 bool audio_op_supported(const tts_tensor * n);
 int launch_audio_op(tts_hip_backend * be, const tts_tensor * n);

@@ -550,14 +550,16 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
 // The same P.V with NPASS passes of 4 * NW output dims per workgroup (all hd dims of a (head, query,
 // sequence) at NPASS = hd / 16): the softmax (P correctly rounded expf and an f64 sum) runs once per
 // workgroup instead of once per 16 dims -- at 64 lock-step prompts the P.V grid otherwise evaluates
-// every exponential hd / 16 = 4 times.  A lane's whole V slice of one pass (P <= 64 UV positions,
-// launcher-checked) is one batch of UV 16-B loads; the next pass's batch is requested before the
-// current pass is summed.  Each output dim is the same f64 sum in the same lane order as k_attn_pv:
-// bit-identical.
+// every exponential hd / 16 = 4 times.  The work is a sequence of items (pass, 64 * UV positions): a
+// lane's V slice of one item is one batch of UV 16-B loads, and the next item's batch is requested
+// before the current one is summed (two register buffers), so any context length streams.  Each output
+// dim is the same f64 sum in the same lane order as k_attn_pv (positions 4t + 64u, ascending u across
+// items, then the DPP row reduction): bit-identical.
 template <int UV, int NW, int NPASS>
 __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float * __restrict__ sbuf, int pstride,
                                                        const float * __restrict__ mxbuf, int nch) {
     constexpr int NTH = 64 * NW;
+    constexpr int KSTEP = 64 * UV;
     extern __shared__ __attribute__((aligned(16))) float s_p[];
     __shared__ double s_wd[NW];
     const int h = blockIdx.y, z = blockIdx.z;
@@ -571,12 +573,15 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
     const int64_t vnb1 = a.v.nb[1];
     const int ilast = ((P - 1) >> 2) << 2;
     const int d0 = blockIdx.x * 4 * NW * NPASS + wave * 4 + r;
+    const int nck = (P + KSTEP - 1) / KSTEP;  // items per pass
+    const int nit = NPASS * nck;
     float4 w4[2][UV];
-    auto load_v = [&](auto BUF, int pass) __attribute__((always_inline)) {
+    auto load_v = [&](auto BUF, int j) __attribute__((always_inline)) {
         constexpr int bf = decltype(BUF)::value;
+        const int pass = j / nck, k0 = (j - pass * nck) * KSTEP;
         const char * vrow = vbase + (int64_t)min(d0 + pass * 4 * NW, a.hd - 1) * vnb1;
 #pragma unroll
-        for (int u = 0; u < UV; ++u) w4[bf][u] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(64 * u + 4 * t, ilast)));
+        for (int u = 0; u < UV; ++u) w4[bf][u] = TTS_KVLOAD((const float4 *)(vrow + 4 * (int64_t)min(k0 + 64 * u + 4 * t, ilast)));
     };
     load_v(std::integral_constant<int, 0>{}, 0);  // in flight during the softmax
     const float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
@@ -599,12 +604,13 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
     const int P64 = (P + 63) & ~63;
     for (int i = tid; i < P64; i += NTH) s_p[i] = i < P ? __fmul_rn(s_p[i], inv) : 0.f;
     __syncthreads();
-    auto pass_sum = [&](auto BUF, int pass) __attribute__((always_inline)) {
+    double acc = 0.0;
+    auto item_sum = [&](auto BUF, int j) __attribute__((always_inline)) {
         constexpr int bf = decltype(BUF)::value;
-        double acc = 0.0;
+        const int pass = j / nck, k0 = (j - pass * nck) * KSTEP;
 #pragma unroll
         for (int u = 0; u < UV; ++u) {
-            const int i = 64 * u + 4 * t;
+            const int i = k0 + 64 * u + 4 * t;
             const float4 pp = *(const float4 *)(s_p + min(i, P64 - 4));
             const float4 vq = w4[bf][u];
             acc += i + 0 < P ? (double)__fmul_rn(pp.x, vq.x) : 0.0;
@@ -612,6 +618,7 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
             acc += i + 2 < P ? (double)__fmul_rn(pp.z, vq.z) : 0.0;
             acc += i + 3 < P ? (double)__fmul_rn(pp.w, vq.w) : 0.0;
         }
+        if (k0 + KSTEP < P) return;  // the pass continues in the next item (uniform)
         acc += dpp_f64<DPP_XOR1>(acc);
         acc += dpp_f64<DPP_XOR2>(acc);
         acc += dpp_f64<DPP_HALF_MIRROR>(acc);
@@ -622,16 +629,16 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
             a.out[o] = (float)acc;
             if (a.out2) a.out2[o] = (float)acc;
         }
+        acc = 0.0;
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
-#pragma unroll
-    for (int pass = 0; pass < NPASS; pass += 2) {
-        if (pass + 1 < NPASS) load_v(B1{}, pass + 1);
-        pass_sum(B0{}, pass);
-        if (pass + 1 >= NPASS) break;
-        if (pass + 2 < NPASS) load_v(B0{}, pass + 2);
-        pass_sum(B1{}, pass + 1);
+    for (int j = 0; j < nit; j += 2) {
+        if (j + 1 < nit) load_v(B1{}, j + 1);
+        item_sum(B0{}, j);
+        if (j + 1 >= nit) break;
+        if (j + 2 < nit) load_v(B0{}, j + 2);
+        item_sum(B1{}, j + 1);
     }
 }
 
@@ -1011,7 +1018,7 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const dim3 g2h((unsigned)(hd / 8), (unsigned)H, (unsigned)(n * B));  // 8 dims per workgroup
             // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
             const uint32_t pl = (uint32_t)((((P + 63) & ~63) + 64) * sizeof(float));  // s_p
-            if (vvec && P <= 512 && be->attn_pv_mp && (hd == 64 || hd == 128)) {  // all dims of a (head, query, seq) per workgroup
+            if (vvec && be->attn_pv_mp && (hd == 64 || hd == 128)) {  // all dims of a (head, query, seq) per workgroup
                 const dim3 g3(1u, (unsigned)H, (unsigned)(n * B));
                 if (hd == 64) hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 4>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
                 else hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 8>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);

@@ -143,9 +143,11 @@ void launch_lstm_finish(tts_hip_backend * be, const tts_tensor * out, const floa
 // rounding: m = x*a, s = sin(m) (correctly rounded), q = s*s, r = q*recip, y = x + r.  alpha and
 // recip are per-channel ([1, C]: one value per row of the [T, C] activation).
 // recip == nullptr: r = one / alpha[c], the DIV node of reciprocal() (util.cpp:86-94) evaluated here.
+// mask != nullptr: x = x * mask[t] first (t = the position along ne0; a MUL node's f32 product).
 template <int V>
 __global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, const float * __restrict__ alpha,
-                        const float * __restrict__ recip, const float * __restrict__ one, int64_t n, int64_t ne0, int64_t nc) {
+                        const float * __restrict__ recip, const float * __restrict__ one, const float * __restrict__ mask, int64_t n,
+                        int64_t ne0, int64_t nc) {
     for (int64_t k = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * V; k < n; k += (int64_t)gridDim.x * blockDim.x * V) {
         const int64_t c = (k / ne0) % nc;
         const float a = alpha[c], r = recip ? recip[c] : cr_divf(*one, a);
@@ -155,6 +157,11 @@ __global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, 
             xv[0] = t.x, xv[1] = t.y, xv[2] = t.z, xv[3] = t.w;
         } else {
             xv[0] = x[k];
+        }
+        if (mask) {
+            const int64_t t0 = k % ne0;  // V == 4: ne0 % 4 == 0, the 4 elements share a row
+#pragma unroll
+            for (int e = 0; e < V; ++e) xv[e] = __fmul_rn(xv[e], mask[t0 + e]);
         }
 #pragma unroll
         for (int e = 0; e < V; ++e) {
@@ -167,9 +174,10 @@ __global__ void k_snake(float * __restrict__ dst, const float * __restrict__ x, 
 }
 
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
-                  const tts_tensor * one) {
+                  const tts_tensor * one, const tts_tensor * mask) {
     const float * rp = recip ? (const float *)recip->data : nullptr;
     const float * op = one ? (const float *)one->data : nullptr;
+    const float * mp = mask ? (const float *)mask->data : nullptr;
     const int64_t n = dst->ne[0] * dst->ne[1] * dst->ne[2] * dst->ne[3];
     const int64_t ne0 = x->ne[0], nc = alpha->ne[1];
     const bool v4 = ne0 % 4 == 0 && ((uintptr_t)dst->data % 16) == 0 && ((uintptr_t)x->data % 16) == 0;
@@ -177,10 +185,10 @@ void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor
     if (g > 65536) g = 65536;
     if (v4)
         hipLaunchKernelGGL(k_snake<4>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
-                           (const float *)alpha->data, rp, op, n, ne0, nc);
+                           (const float *)alpha->data, rp, op, mp, n, ne0, nc);
     else
         hipLaunchKernelGGL(k_snake<1>, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const float *)x->data,
-                           (const float *)alpha->data, rp, op, n, ne0, nc);
+                           (const float *)alpha->data, rp, op, mp, n, ne0, nc);
     TTS_HIP_CHECK(hipGetLastError());
 }
 

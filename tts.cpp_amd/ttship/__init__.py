@@ -382,6 +382,9 @@ def lib():
         "tts_dac_decode": (ctypes.c_int, [vp, vp, i32, vp]),
         "tts_dac_hop": (i64, [vp]),
         "tts_dac_last_graph_nodes": (i32, [vp]),
+        "tts_dac_decode_batch": (ctypes.c_int, [vp, vp, i32, i32, i32, vp]),
+        "tts_dac_min_gap": (i64, [vp]),
+        "tts_dac_graph": (vp, [vp, ctypes.POINTER(i32)]),
         "tts_snac_default_config": (None, [ctypes.POINTER(SnacConfig)]),
         "tts_snac_create": (vp, [ctypes.POINTER(BackendIface), ctypes.POINTER(SnacConfig)]),
         "tts_snac_free": (None, [vp]),
@@ -879,6 +882,28 @@ class Dac:
         if st != 0:
             raise RuntimeError(f"tts_dac_decode failed {st}")
         return pcm
+
+    def decode_batch(self, codes, gap=0):
+        """codes: (nb, T, n_codebooks) int -> (nb, T * hop) float32 PCM, one graph for all nb prompts
+        (tts_dac_decode_batch: bit-identical to nb decode() calls)."""
+        import numpy as np
+        c = np.ascontiguousarray(codes, dtype=np.int32)
+        nb, T = c.shape[0], c.shape[1]
+        pcm = np.empty((nb, T * self.hop), dtype=np.float32)
+        st = self.L.tts_dac_decode_batch(self.ptr, c.ctypes.data, nb, T, gap, pcm.ctypes.data)
+        if st != 0:
+            raise RuntimeError(f"tts_dac_decode_batch failed {st}")
+        return pcm
+
+    @property
+    def min_gap(self):
+        return self.L.tts_dac_min_gap(self.ptr)
+
+    def plan_stats(self, mask=None):
+        """Fusion coverage of the last decode graph (no device needed)."""
+        n = ctypes.c_int32()
+        p = self.L.tts_dac_graph(self.ptr, ctypes.byref(n))
+        return plan_stats(p, n.value, FUSE_ALL if mask is None else mask)
 
     def last_graph_nodes(self):
         return self.L.tts_dac_last_graph_nodes(self.ptr)
