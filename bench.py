@@ -503,9 +503,18 @@ def parler_replicas(args, per_gpu, R, rank, new_backend, dac_cfg=None):
         rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * per_gpu + r * bl))
         rb.sync()
         prefill_ms.append(1000.0 * (time.perf_counter() - tp0))
-        rr.generate(args.warmup)
+        rr.generate(min(2, args.warmup))  # the step graph recorded (first sighting eager, then captured)
         rb.sync()
     return reps, prefill_ms, cfg
+
+
+def warm_concurrent(args, reps):
+    """The rest of the W warmup steps with every replica running at once, right before the timed
+    region: the device sees the timed shape (and its clocks) immediately before timing starts, whatever
+    ran before it (DAC workers' setup, another leg)."""
+    n = max(0, args.warmup - min(2, args.warmup))
+    if n:
+        run_replicas(lambda r: (reps[r][1].generate(n), reps[r][0].sync()), len(reps))
 
 
 def new_dac_for(args, rb, dcfg):
@@ -600,6 +609,7 @@ def main():
                     "prompts decode side by side")
     ap.add_argument("--dac-batch", type=int, default=None, help="prompts per batched DAC decode (tts_dac_decode_batch: one "
                     "graph, zeroed gaps, PCM bit-identical to one decode per prompt); default: 8 up to 64 frames, else 1")
+    ap.add_argument("--idle-ms", type=float, default=0.0, help="study: idle host sleep between the warmup and the timed region")
     ap.add_argument("--kokoro-prompts", type=int, default=8, help="Kokoro-82M prompts per GPU, end to end (0 = skip)")
     ap.add_argument("--orpheus-steps", type=int, default=64, help="timed Orpheus-3B decode steps per GPU (0 = skip)")
     ap.add_argument("--orpheus-batch", type=int, default=8, help="Orpheus prompts per GPU (64-prompt batch / 8 GPUs)")
@@ -648,6 +658,9 @@ def main():
     while len(dac_workers) < W:
         xb = new_backend()
         dac_workers.append((xb, new_dac_for(args, xb, dcfg)))
+    warm_concurrent(args, reps)
+    if args.idle_ms:  # study: an idle gap between the warmup and the timed region
+        time.sleep(args.idle_ms / 1e3)
     barrier_sync(dist, be)
 
     runner.host_stats(reset=True)
@@ -713,6 +726,7 @@ def main():
     if args.p8 and per_gpu > 8 and strong:
         barrier_sync(dist, None)
         reps8, pf8, _ = parler_replicas(args, 8, 2, rank, new_backend)
+        warm_concurrent(args, reps8)
         barrier_sync(dist, reps8[0][0])
         t80 = time.perf_counter()
         run_replicas(lambda r: (reps8[r][1].generate(args.steps), reps8[r][0].sync()), 2)

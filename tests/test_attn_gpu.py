@@ -77,7 +77,7 @@ def set_mode(hip, mode):
     hip.set_option(ttship.OPT["ATTN_SPLIT"], ttship.ATTN_SPLIT_DEFAULT if split else 0)
     hip.set_option(ttship.OPT["ATTN_KS"], 1 if mode == "split_ks1" else 4 if mode == "split_ks4_pv8" else 2)
     hip.set_option(ttship.OPT["ATTN_PV8"], 1 if mode == "split_ks4_pv8" else 0)
-    hip.set_option(ttship.OPT["ATTN_PV_MP"], 0 if mode in ("split_ks4_pv8", "split_pv16") else 1)
+    hip.set_option(ttship.OPT["ATTN_PV_MP"], 0 if mode in ("split_ks4_pv8", "split_pv16") else 2 if mode == "split_mp8" else 1)
 
 
 @pytest.mark.gpu
@@ -95,14 +95,14 @@ def test_pv_all_dims_bit_identical(hip, P, hd, B):
     mask = np.zeros(P, np.float32)
     mask[P // 2] = -np.inf
     outs = []
-    for mode in ("split", "split_pv16"):
+    for mode in ("split", "split_pv16", "split_mp8"):
         set_mode(hip, mode)
         g = nd.Graph()
         o = build(g, q, kc, vc, mask, P, hd, H, H, B, max_ctx)
         g.run_hip(hip)
         outs.append(g.node_array(o))
     set_mode(hip, "default")
-    assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
 
 
 @pytest.mark.gpu

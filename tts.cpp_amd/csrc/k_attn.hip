@@ -1020,8 +1020,15 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const uint32_t pl = (uint32_t)((((P + 63) & ~63) + 64) * sizeof(float));  // s_p
             if (vvec && be->attn_pv_mp && (hd == 64 || hd == 128)) {  // all dims of a (head, query, seq) per workgroup
                 const dim3 g3(1u, (unsigned)H, (unsigned)(n * B));
-                if (hd == 64) hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 4>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
-                else hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 8>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                // TTS_HIP_OPT_ATTN_PV_MP = 2: eight waves per workgroup (half the passes; same sums)
+                if (be->attn_pv_mp == 2) {
+                    if (hd == 64) hipExtLaunchKernelGGL((k_attn_pv_mp<8, 8, 2>), g3, dim3(512), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                    else hipExtLaunchKernelGGL((k_attn_pv_mp<8, 8, 4>), g3, dim3(512), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                } else if (hd == 64) {
+                    hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 4>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                } else {
+                    hipExtLaunchKernelGGL((k_attn_pv_mp<8, 4, 8>), g3, dim3(256), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
+                }
             } else if (vvec && P <= 1024 && be->attn_pv_uv16)
                 hipExtLaunchKernelGGL((k_attn_pv<true, 16>), g2, dim3(PV_THREADS), pl, be->stream, nullptr, e1, 0u, a, sbuf, pstride, mxbuf, nch);
             else if (vvec && be->attn_pv8)
