@@ -129,3 +129,59 @@ def test_device_sampling_eos_rule(hip):
     finally:
         g.close()
         c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 4])
+def test_graph_replay_across_kernel_switches(hip, batch):
+    """The step graph is recorded once and then updated in place (hipGraphExecUpdate) every step; here the
+    KV length crosses the attention kernel boundaries (k_attn_small up to 64 keys, the row kernel, the
+    split pair from 128 keys, its chunk count growing), so the update sees new grids and new kernels.
+    Tokens bit-exact vs the oracle over 75 steps, and the replayed runner's logits bit-identical to a
+    runner on a backend that launches every step eagerly (graphs off)."""
+    kw = dict(TINY, max_ctx=192, max_positions=256)
+    g, c = make_pair(hip, batch=batch, **kw)
+    eager_be = ttship.HipBackend(0)
+    eager_be.set_option(ttship.OPT["GRAPHS"], 0)
+    e = ttship.Parler(eager_be.iface(), ttship.parler_config(batch=batch, **kw))
+    try:
+        prompt = (np.arange(60 * batch, dtype=np.int32).reshape(batch, 60) * 53 + 11) % 512
+        for r in (g, c, e):
+            r.prefill(prompt)
+        tg, tc, te = g.generate(75), c.generate(75), e.generate(75)
+        assert np.array_equal(tg, tc), f"token mismatch vs oracle\n{tg}\n{tc}"
+        assert np.array_equal(tg, te)
+        toks = np.full((batch, 9), 5, dtype=np.int32)
+        lg, le = g.decode(toks), e.decode(toks)
+        assert np.array_equal(lg, le)
+    finally:
+        e.close()
+        eager_be.close()
+        g.close()
+        c.close()
+
+
+@pytest.mark.gpu
+def test_many_prompt_step_in_kernel_operands(hip):
+    """Parler-mini Q4_K at 16 lock-step prompts (every decode product has M = 16 > 8 columns: the K-relay
+    GEMM) with the LN / quantize prologues inside the GEMM workgroups (TTS_HIP_OPT_GEMM_KR_INKERNEL)
+    against the operand pass: tokens and logits bit-identical, tokens equal to the oracle's."""
+    B = 16
+    prompt = (np.arange(7 * B, dtype=np.int32).reshape(B, 7) * 41 + 3) % 1000
+    ink_be = ttship.HipBackend(0)
+    ink_be.set_option(ttship.OPT["GEMM_KR_INKERNEL"], 64)
+    g, c = make_pair(hip, batch=B)
+    k = ttship.Parler(ink_be.iface(), ttship.parler_config(batch=B))
+    try:
+        for r in (g, c, k):
+            r.prefill(prompt)
+        tg, tc, tk = g.generate(4), c.generate(4), k.generate(4)
+        assert np.array_equal(tg, tc), f"token mismatch vs oracle\n{tg}\n{tc}"
+        assert np.array_equal(tk, tg)
+        toks = np.full((B, 9), 5, dtype=np.int32)
+        assert np.array_equal(g.decode(toks), k.decode(toks))
+    finally:
+        k.close()
+        ink_be.close()
+        g.close()
+        c.close()

@@ -316,6 +316,8 @@ struct ProOv {
     float * lncol = nullptr;      // ... and write its LN output here (or nowhere)
     int slot0 = 0;                // first output slot
     int trash = -1;               // slot absorbing padding writes (-1: M * nb)
+    int col0 = 0;                 // a column tile: j.x's columns col0 .. col0 + mcols - 1 (LN output likewise)
+    int mcols = 0;                // (0: j.M columns from col0)
 };
 template <int PRO, int NCH, bool MF = false, typename Mid = NoMid, bool Q80 = false>
 __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t * xq_s, float * xd_s, int16_t * xs_s,
@@ -330,8 +332,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
     float * const lncol = ov.lncol;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nwaves ? nwaves : blockDim.x >> 6;
     const int r = lane >> 4, t = lane & 15;
-    const int M = xcol ? 1 : (int)j.M;
-    const float * const X = xcol ? xcol : j.x;
+    const int M = xcol ? 1 : ov.mcols > 0 ? ov.mcols : (int)j.M;
+    const float * const X = xcol ? xcol : j.x + (int64_t)ov.col0 * j.xcs;  // (PRO_QUANT: xcs == K, launcher-checked)
     const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
     auto put = [&](const float (&v)[16], int lane, int slot) {
         slot = slot == trash ? (ov.trash >= 0 ? ov.trash : slot) : ov.slot0 + slot;
@@ -372,7 +374,7 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         constexpr int NP = (NCH + 3) / 4;
         constexpr bool PRE = NCH <= 4;
         const double Kd = (double)j.K;
-        float * const lno = xcol ? lncol : j.lnout;
+        float * const lno = xcol ? lncol : j.lnout ? j.lnout + (int64_t)ov.col0 * j.locs : nullptr;
         const bool write = lno && (xcol || blockIdx.x == 0);
         const float * lnb = j.lnb ? j.lnb : j.lnw;
         float wp[PRE ? NP : 1][16], bp[PRE ? NP : 1][16];
@@ -1219,7 +1221,10 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
         load_w(B0{}, t);
     } else {
         auto first = [&]() __attribute__((always_inline)) { load_w(B0{}, t); };
-        q4k_prologue<PRO, 16, true, decltype(first)>(j, nb, nullptr, xd_s, nullptr, b16, sbs, first);
+        ProOv ov;  // a column tile (j.bq_tile: the many-column GEMM at decode sizes) quantizes its own columns
+        ov.col0 = c0;
+        ov.mcols = M;
+        q4k_prologue<PRO, 16, true, decltype(first)>(j, nb, nullptr, xd_s, nullptr, b16, sbs, first, ov);
     }
     TTS_TS(j, 1);
     __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
@@ -2346,9 +2351,9 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
 template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY>
 static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
-    if constexpr (!LANE && PRO == PRO_COPY) {  // in-kernel prologue (launch_q4k_kr decides)
-        if (j.pro == PRO_LN) return launch_q4k_kr_t<BPW, SW, NWT, false, LOOP, PRO_LN>(be, j, gx, gy);
-        if (j.pro == PRO_QUANT) return launch_q4k_kr_t<BPW, SW, NWT, false, LOOP, PRO_QUANT>(be, j, gx, gy);
+    if constexpr (PRO == PRO_COPY) {  // in-kernel prologue (launch_q4k_kr / launch_gemm_q4k_kr decide)
+        if (j.pro == PRO_LN) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_LN>(be, j, gx, gy);
+        if (j.pro == PRO_QUANT) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_QUANT>(be, j, gx, gy);
     }
     if constexpr (SW && !LOOP && BPW <= 3) {  // (BPW 4: the prefetch registers would spill)
         // SwiGLU pairs (8 waves, ~170 VGPRs: one workgroup per CU): more pairs than CUs run as one
@@ -2413,13 +2418,22 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     GemvJob j = job;
     j.bq_tile = tile;
     j.bq_bytes = tile * nct;
-    j.bq = be->scratch + be->scratch_size - j.bq_bytes;
-    const dim3 qg((unsigned)((nb + 3) / 4), (unsigned)j.M);
-    if (j.pro == PRO_LN) hipLaunchKernelGGL(k_quant_mf<PRO_LN>, qg, dim3(64), 0, be->stream, j);
-    else hipLaunchKernelGGL(k_quant_mf<PRO_QUANT>, qg, dim3(64), 0, be->stream, j);
-    TTS_HIP_CHECK(hipGetLastError());
-    j.pro = PRO_COPY;
-    j.lnout = nullptr;
+    // TTS_HIP_OPT_GEMM_KR_INKERNEL = max M: decode-sized products skip the operand pass, every (row tile,
+    // column tile) workgroup norms / quantizes its 16 columns itself (q4k_prologue, its first weight
+    // loads issued between the activation loads and their use); the same operand values, bit-identical
+    const bool ink = be->gemm_kr_ink > 0 && job.M <= be->gemm_kr_ink && job.K <= 4 * 1024 && !job.dbg &&
+                     (job.pro == PRO_LN || job.xcs == job.K);
+    if (ink) {
+        j.bq = nullptr;
+    } else {
+        j.bq = be->scratch + be->scratch_size - j.bq_bytes;
+        const dim3 qg((unsigned)((nb + 3) / 4), (unsigned)j.M);
+        if (j.pro == PRO_LN) hipLaunchKernelGGL(k_quant_mf<PRO_LN>, qg, dim3(64), 0, be->stream, j);
+        else hipLaunchKernelGGL(k_quant_mf<PRO_QUANT>, qg, dim3(64), 0, be->stream, j);
+        TTS_HIP_CHECK(hipGetLastError());
+        j.pro = PRO_COPY;
+        j.lnout = nullptr;
+    }
     const unsigned gx = (unsigned)(job_rows(j) / 16), gy = (unsigned)nct;
     auto go = [&](auto LANE) {
         constexpr bool L = decltype(LANE)::value;
