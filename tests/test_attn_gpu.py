@@ -82,10 +82,11 @@ def set_mode(hip, mode):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,hd,B", [(129, 64, 3), (460, 64, 5), (512, 64, 2), (513, 64, 2), (300, 128, 2),
-                                   (1024, 64, 2), (1309, 64, 4), (1100, 128, 2), (4096, 64, 1)])
+                                   (1024, 64, 16), (1309, 64, 16), (1100, 128, 16), (4096, 64, 16), (1309, 64, 4)])
 def test_pv_all_dims_bit_identical(hip, P, hd, B):
     """The split P.V with every dim of a (head, query, sequence) in one workgroup (k_attn_pv_mp, any context: items
-    of 512 positions; the softmax once per head) against 16 dims per workgroup (k_attn_pv): the same sums, identical bits."""
+    of 512 positions; the softmax once per head; past 512 keys only with >= 256 rows, so B = 16 there) against 16 dims per
+    workgroup (k_attn_pv): the same sums, identical bits."""
     H = 16
     rng = np.random.default_rng(P * 3 + hd + B)
     max_ctx = (P + 8 + 3) // 4 * 4  # 16-B V rows: the vector-load P.V kernels

@@ -1018,7 +1018,10 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
             const dim3 g2h((unsigned)(hd / 8), (unsigned)H, (unsigned)(n * B));  // 8 dims per workgroup
             // P <= 1024: every lane's whole V slice (16 x 16 B) is requested before the softmax
             const uint32_t pl = (uint32_t)((((P + 63) & ~63) + 64) * sizeof(float));  // s_p
-            if (vvec && be->attn_pv_mp && (hd == 64 || hd == 128)) {  // all dims of a (head, query, seq) per workgroup
+            // all dims of a (head, query, seq) per workgroup: one workgroup per row, so past 512 keys only
+            // when the rows alone fill the chip (Dia's 1024-position cross-attention has 32 rows: 8 dims
+            // per workgroup keeps 256 workgroups streaming V)
+            if (vvec && be->attn_pv_mp && (hd == 64 || hd == 128) && (P <= 512 || rows >= (size_t)be->cus)) {
                 const dim3 g3(1u, (unsigned)H, (unsigned)(n * B));
                 // TTS_HIP_OPT_ATTN_PV_MP = 2: eight waves per workgroup (half the passes; same sums)
                 if (be->attn_pv_mp == 2) {
