@@ -321,6 +321,8 @@ enum tts_hip_option {
                                     2: the same with eight waves per workgroup (hd / 32 passes); 0: 16 dims per workgroup */
     TTS_HIP_OPT_GEMM_KR_INKERNEL = 35, /* many-column (> 8) K-relay Q4_K GEMMs with at most `value` columns skip the operand
                                           pass: each (row tile, column tile) workgroup norms / quantizes its 16 columns (0 = off) */
+    TTS_HIP_OPT_GEMM_KR_CT2 = 36, /* 1: the many-column K-relay Q4_K GEMM (K = 1024 / 2048) takes two 16-column tiles per
+                                     workgroup, each weight tile loaded once for both (0 = one tile per workgroup) */
     TTS_HIP_OPT_GEMM_KR_NW = 34, /* waves per 16-row tile of the many-column (> 8) K-relay Q4_K GEMM: 4 (default) or 8 (K >= 2048) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */

@@ -96,6 +96,25 @@ def test_q4_K_prefill_gemm_eight_waves(hip, tiled, K, N, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (1024, 3072, 17), (2048, 160, 48), (1024, 4096, 64), (2048, 512, 100),
+                                   (1024, 64, 448), (4096, 1024, 32)])
+def test_q4_K_prefill_gemm_two_column_tiles(hip, tiled, K, N, M):
+    """The many-column K-relay GEMM with two 16-column tiles per workgroup (TTS_HIP_OPT_GEMM_KR_CT2, K <=
+    2048: the weight tile loaded once, both tiles' operands in LDS; K = 4096 keeps one tile): bit-identical."""
+    hip.set_option(ttship.OPT["GEMM_KR_CT2"], 1)
+    try:
+        rng = np.random.default_rng(K * 3 + N + M + tiled)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        hip.set_option(ttship.OPT["GEMM_KR_CT2"], 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [False, True])
 @pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (4096, 1024, 32), (1024, 3072, 9), (2048, 160, 17), (4096, 512, 64),
                                    (3072, 256, 40)])
 def test_q4_K_prefill_gemm_in_kernel_operands(hip, tiled, K, N, M):

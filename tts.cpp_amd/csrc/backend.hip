@@ -561,6 +561,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_ATTN_KS: be->attn_ks = value; return 0;
         case TTS_HIP_OPT_GEMV_NW_MIN: be->gemv_nw_min = value; return 0;
         case TTS_HIP_OPT_ATTN_PV8: be->attn_pv8 = value != 0; return 0;
+        case TTS_HIP_OPT_GEMM_KR_CT2: be->gemm_kr_ct2 = value != 0; return 0;
         case TTS_HIP_OPT_GEMM_KR_INKERNEL: be->gemm_kr_ink = value < 0 ? 0 : value; return 0;
         case TTS_HIP_OPT_ATTN_PV_MP: be->attn_pv_mp = value == 2 ? 2 : value != 0; return 0;
         case TTS_HIP_OPT_GEMM_KR_NW: be->gemm_kr_nw = value == 8 ? 8 : 4; return 0;

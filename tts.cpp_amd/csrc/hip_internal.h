@@ -315,6 +315,7 @@ struct tts_hip_backend {
     int gemv_q80_rw = 0;       // TTS_HIP_OPT_GEMV_Q80_RW
     int gemm_q8_staged = 2;    // TTS_HIP_OPT_GEMM_Q8_STAGED
     int64_t gemv_kr_ink = 0;   // TTS_HIP_OPT_GEMV_KR_INKERNEL (max K)
+    int gemm_kr_ct2 = 0;       // TTS_HIP_OPT_GEMM_KR_CT2: two 16-column tiles per K-relay GEMM workgroup (K <= 2048)
     int64_t gemm_kr_ink = 0;   // TTS_HIP_OPT_GEMM_KR_INKERNEL (max M of the many-column K-relay GEMM without the operand pass)
     int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
     int gemv_mf_rsplit = 1;  // matrix-core GEMV: split a tile's residues over 2 / 4 waves when tiles are few (TTS_HIP_OPT_GEMV_RSPLIT)

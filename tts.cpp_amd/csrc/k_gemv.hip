@@ -1142,26 +1142,30 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 // PRO (PRO_QUANT / PRO_LN, K <= 4096): no operand pass -- the workgroup norms / quantizes the
 // activation itself (q4k_prologue, the MFMA operand layout k_quant_mf writes), its first weight loads
 // issued between the prologue's activation loads and their use.
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY>
+// CTW = 2 (PRO_COPY, column tiles): a workgroup takes two column tiles of its row tile in turn -- the
+// tile's weights are loaded into registers once and multiplied against both tiles' operands (both in
+// LDS), instead of two workgroups streaming the same weights.
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1>
 __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
     constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
     typedef float f2v __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
-    const int ct = blockIdx.y;                 // column tile
-    const int c0 = j.bq_tile ? 16 * ct : 0;    // its first column
-    const int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;
-    const char * const bqt = j.bq + (size_t)ct * j.bq_tile;
+    const int ct0 = blockIdx.y * CTW;          // (first) column tile
+    int c0 = j.bq_tile ? 16 * ct0 : 0;         // its first column
+    int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;
+    const int ntile = CTW == 1 ? 1 : min(CTW, (int)((j.M + 15) / 16) - ct0);  // column tiles of this workgroup
+    const char * const bqt = j.bq + (size_t)ct0 * j.bq_tile;
     const int64_t bqb = j.bq_tile ? j.bq_tile : j.bq_bytes;
-    const int nslot = M * nb + 1;
+    int nslot = M * nb + 1;
     _Float16 * b16 = (_Float16 *)smem;
     _Float16 * sbs = b16 + (size_t)nslot * QK_K;
     float * xd_s = (float *)(sbs + (size_t)nslot * 16);
-    float * relay = (float *)(smem + ((bqb + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
+    float * relay = (float *)(smem + ((CTW * bqb + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
 
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
     const int r = lane & 15, kg = lane >> 4;
-    const int cc = r < M ? r : M - 1;
+    int cc = r < M ? r : M - 1;
     const int sub = SW ? wave / nwt : 0;    // SwiGLU: 0 = gate tile, 1 = up tile
     const int w = wave - sub * nwt;         // position in the relay
     const int64_t NR = SW ? j.N : job_rows(j);
@@ -1213,7 +1217,7 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     int64_t t = blockIdx.x;
     if constexpr (PRO == PRO_COPY) {
         // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
-        const int nck = (int)(bqb >> 10);
+        const int nck = (int)((ntile * bqb) >> 10);
         for (int i = wave; i < nck; i += nw)
             __builtin_amdgcn_global_load_lds(gptr(bqt + (size_t)i * 1024 + lane * 16),
                                              (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
@@ -1388,6 +1392,20 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
         TTS_TS(j, 3);
         relay_store(t);
         TTS_TS(j, 4);
+        if constexpr (CTW > 1) {
+            for (int k = 1; k < ntile; ++k) {  // the next column tile: same weight registers, its operands
+                __syncthreads();  // the relay buffer is reused
+                c0 = 16 * (ct0 + k);
+                M = min(16, (int)j.M - c0);
+                nslot = M * nb + 1;
+                b16 = (_Float16 *)(smem + (size_t)k * bqb);
+                sbs = b16 + (size_t)nslot * QK_K;
+                xd_s = (float *)(sbs + (size_t)nslot * 16);
+                cc = r < M ? r : M - 1;
+                terms(B0{});
+                relay_store(t);
+            }
+        }
     }
     TTS_TS(j, 5);
 }
@@ -2349,13 +2367,13 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 
 // ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY>
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1>
 static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
-    if constexpr (PRO == PRO_COPY) {  // in-kernel prologue (launch_q4k_kr / launch_gemm_q4k_kr decide)
+    if constexpr (PRO == PRO_COPY && CTW == 1) {  // in-kernel prologue (launch_q4k_kr / launch_gemm_q4k_kr decide)
         if (j.pro == PRO_LN) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_LN>(be, j, gx, gy);
         if (j.pro == PRO_QUANT) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_QUANT>(be, j, gx, gy);
     }
-    if constexpr (SW && !LOOP && BPW <= 3) {  // (BPW 4: the prefetch registers would spill)
+    if constexpr (SW && !LOOP && BPW <= 3 && CTW == 1) {  // (BPW 4: the prefetch registers would spill)
         // SwiGLU pairs (8 waves, ~170 VGPRs: one workgroup per CU): more pairs than CUs run as one
         // workgroup per CU walking its pairs, operands copied once, the next pair's weights prefetched
         if (be->gemv_kr_loop && gx > (unsigned)be->cus && gy == 1) {
@@ -2364,17 +2382,17 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
         }
     }
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>);
-    const size_t lds = q4k_kr_lds(j.bq_tile ? j.bq_tile : j.bq_bytes, SW);
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>);
+    const size_t lds = q4k_kr_lds(CTW * (j.bq_tile ? j.bq_tile : j.bq_bytes), SW);
     const dim3 blk(64 * NWT * (SW ? 2 : 1));
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO>), dim3(gx, gy), blk, lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>), dim3(gx, gy), blk, lds, be->stream, j);
 }
 
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
@@ -2435,8 +2453,17 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
         j.lnout = nullptr;
     }
     const unsigned gx = (unsigned)(job_rows(j) / 16), gy = (unsigned)nct;
+    // TTS_HIP_OPT_GEMM_KR_CT2: two column tiles per workgroup (weights streamed once for 32 columns) where
+    // both tiles' operands fit the LDS (K = 1024 x {1, 2})
+    const bool ct2 = be->gemm_kr_ct2 && !ink && nct >= 2 && (nb == 4 || nb == 8) && q4k_kr_lds(2 * tile, false) <= 160 * 1024;
     auto go = [&](auto LANE) {
         constexpr bool L = decltype(LANE)::value;
+        if (ct2) {
+            const unsigned gy2 = (unsigned)((nct + 1) / 2);
+            if (nb == 4) launch_q4k_kr_t<1, false, 4, L, false, PRO_COPY, 2>(be, j, gx, gy2);
+            else launch_q4k_kr_t<2, false, 4, L, false, PRO_COPY, 2>(be, j, gx, gy2);
+            return;
+        }
         // TTS_HIP_OPT_GEMM_KR_NW = 8: a tile's blocks over eight waves (K >= 2048; a longer relay, half the
         // blocks per wave)
         const bool nw8 = be->gemm_kr_nw == 8;
