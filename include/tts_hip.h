@@ -320,7 +320,8 @@ enum tts_hip_option {
                                     workgroup (hd / 16 passes of 512-position items, any P): the softmax once instead of hd / 16 times;
                                     2: the same with eight waves per workgroup (hd / 32 passes); 0: 16 dims per workgroup */
     TTS_HIP_OPT_GEMM_KR_INKERNEL = 35, /* many-column (> 8) K-relay Q4_K GEMMs with at most `value` columns skip the operand
-                                          pass: each (row tile, column tile) workgroup norms / quantizes its 16 columns (0 = off) */
+                                          pass: each (row tile, column tile) workgroup norms / quantizes its 16 columns (0 = off;
+                                          + 0x10000: only the jobs without a norm) */
     TTS_HIP_OPT_GEMM_KR_CT2 = 36, /* 1: the many-column K-relay Q4_K GEMM (K = 1024 / 2048) takes two 16-column tiles per
                                      workgroup, each weight tile loaded once for both (0 = one tile per workgroup) */
     TTS_HIP_OPT_GEMM_KR_NW = 34, /* waves per 16-row tile of the many-column (> 8) K-relay Q4_K GEMM: 4 (default) or 8 (K >= 2048) */

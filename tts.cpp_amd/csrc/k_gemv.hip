@@ -2439,8 +2439,10 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     // TTS_HIP_OPT_GEMM_KR_INKERNEL = max M: decode-sized products skip the operand pass, every (row tile,
     // column tile) workgroup norms / quantizes its 16 columns itself (q4k_prologue, its first weight
     // loads issued between the activation loads and their use); the same operand values, bit-identical
-    const bool ink = be->gemm_kr_ink > 0 && job.M <= be->gemm_kr_ink && job.K <= 4 * 1024 && !job.dbg &&
-                     (job.pro == PRO_LN || job.xcs == job.K);
+    // (bit 16 of the option: only the quantize-only jobs, whose prologue runs on every wave at once)
+    const int64_t ink_m = be->gemm_kr_ink & 0xFFFF;
+    const bool ink = ink_m > 0 && job.M <= ink_m && job.K <= 4 * 1024 && !job.dbg &&
+                     (job.pro == PRO_LN || job.xcs == job.K) && (!(be->gemm_kr_ink & 0x10000) || job.pro == PRO_QUANT);
     if (ink) {
         j.bq = nullptr;
     } else {
