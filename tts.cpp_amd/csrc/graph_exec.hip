@@ -145,6 +145,10 @@ struct Item {
     bool x_shadow = false;  // src1 = the preceding attention output: read its private copy
     const tts_tensor * snake_one = nullptr;  // SNAKE: b == nullptr, recip = snake_one[0] / alpha in the kernel
     const tts_tensor * snake_mask = nullptr;  // SNAKE: x = x * mask[t] first (the MUL node of a batched DAC decode's gap mask)
+    // EMBED, gather form (a codec quantizer's input, general_neural_audio_codec.cpp:166-172):
+    // dst [T, C] = CONT(TRANSPOSE(GET_ROWS(w [C, rows], CONT(view of I32 codes)))) in one pass
+    bool gather_t = false;
+    const tts_tensor * gt_codes = nullptr;  // the codes view (t-th id at data + t * nb[1])
     const tts_tensor * xsrc = nullptr;  // src1 is a skipped CONT of this contiguous tensor (same bytes): read its data
     bool shadow = false;    // ATTN: also write the private copy (be->shadow)
     int xattn = -1;         // GEMV: index of the short-context ATTN item whose query it produces (one launch)
@@ -339,6 +343,7 @@ struct Planner {
                 case TTS_OP_ADD: if (mask & TTS_FUSE_SNAKE) try_snake(i); break;
                 case TTS_OP_IM2COL: if (mask & TTS_FUSE_CONV) try_conv(i); break;
                 case TTS_OP_CPY: if (mask & TTS_FUSE_MCPY) try_mcpy(i); break;
+                case TTS_OP_CONT: if (mask & TTS_FUSE_EMBED) try_gather_t(i); break;
                 case TTS_OP_MUL_MAT:
                     if (!((mask & TTS_FUSE_HEADS) && try_heads(i)) && (mask & (TTS_FUSE_GROUP | TTS_FUSE_KV | TTS_FUSE_EPI))) try_gemv(i);
                     break;
@@ -1649,6 +1654,37 @@ struct Planner {
         for (int k : skip) act[k] = -1;
     }
 
+    // CONT(TRANSPOSE(GET_ROWS(W, RESHAPE(CONT(V))))) with V a strided I32 view (DAC / SNAC quantizer
+    // inputs, general_neural_audio_codec.cpp:166-172 after dac_build_audio_inputs' per-codebook view):
+    // three launches of a few hundred bytes each -> one gather writing the transposed rows.  Copies only.
+    void try_gather_t(int i) {
+        const tts_tensor * C2 = nodes[i];
+        const tts_tensor * Tv = C2->src[0];
+        if (!Tv || Tv->op != TTS_OP_TRANSPOSE || C2->type != TTS_TYPE_F32 || !contiguous(C2) || uses[Tv] != 1) return;
+        const tts_tensor * G = Tv->view_src ? Tv->view_src : Tv->src[0];
+        if (!G || G->op != TTS_OP_GET_ROWS || !index.count(G) || act[index[G]] != 0 || uses[G] != 1 || G->type != TTS_TYPE_F32 ||
+            !contiguous(G) || G->ne[2] * G->ne[3] != 1)
+            return;
+        const tts_tensor *W = G->src[0], *ix = G->src[1];
+        if (!W || W->type != TTS_TYPE_F32 || W->nb[0] != 4 || W->ne[2] * W->ne[3] != 1 || !ix || ix->type != TTS_TYPE_I32) return;
+        // ix: a RESHAPE view of C1 = CONT(V), or C1 itself
+        const tts_tensor * C1 = ix->op == TTS_OP_RESHAPE ? (ix->view_src ? ix->view_src : ix->src[0]) : ix;
+        if (ix != C1 && uses[ix] != 1) return;
+        if (!C1 || C1->op != TTS_OP_CONT || !index.count(C1) || act[index[C1]] != 0 || uses[C1] != 1) return;
+        const tts_tensor * V = C1->src[0];
+        const int64_t T = G->ne[1];
+        if (!V || V->type != TTS_TYPE_I32 || V->ne[0] != 1 || V->ne[1] * V->ne[2] * V->ne[3] != T || V->ne[2] * V->ne[3] != 1) return;
+        if (C2->ne[0] != T || C2->ne[1] != G->ne[0] || overlap(C2, V) || overlap(C2, W)) return;
+        Item it;
+        it.kind = Item::EMBED;
+        it.gather_t = true;
+        it.dst = C2;
+        it.w = W;
+        it.gt_codes = V;
+        act[index[C1]] = act[index[G]] = -1;
+        act[i] = add_item(std::move(it));
+    }
+
     void try_embed(int i) {
         const tts_tensor * R = nodes[i];
         if (!contiguous(R)) return;
@@ -2114,6 +2150,25 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
     return 0;
 }
 
+// dst[c * T + t] = W[ids[t] row, c]: GET_ROWS of an I32 view, then the transpose's CONT (try_gather_t)
+__global__ void k_gather_t(float * __restrict__ dst, const char * __restrict__ w, int64_t wnb1, const char * __restrict__ ids,
+                           int64_t inb1, int64_t T, int64_t C) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < T * C; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t c = e / T, t = e - c * T;
+        const int32_t id = *(const int32_t *)(ids + t * inb1);
+        dst[e] = *(const float *)(w + (int64_t)id * wnb1 + 4 * c);
+    }
+}
+
+static void launch_gather_t(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * w, const tts_tensor * ids) {
+    const int64_t T = dst->ne[0], C = dst->ne[1];
+    int64_t g = (T * C + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_gather_t, dim3((unsigned)g), dim3(256), 0, be->stream, (float *)dst->data, (const char *)w->data,
+                       (int64_t)w->nb[1], (const char *)ids->data, (int64_t)ids->nb[1], T, C);
+    TTS_HIP_CHECK(hipGetLastError());
+}
+
 static int run_node(tts_hip_backend * be, const tts_tensor * n) {
     if (n->op == TTS_OP_MUL_MAT) {
         const tts_tensor * a = n->src[0], * b = n->src[1];
@@ -2142,7 +2197,8 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
             return 0;
         case Item::EMBED:
-            launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
+            if (it.gather_t) launch_gather_t(be, it.dst, it.w, it.gt_codes);
+            else launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
             return 0;
         case Item::SNAKE:
             launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one, it.snake_mask);
