@@ -394,21 +394,31 @@ def dia_leg(be, args):
         d.close()
 
 
-def parler_b1_leg(args, rank, local, new_backend):
-    """TTS.cpp's serving shape (examples/server/server.cpp:316-321,885-895): one prompt per runner,
-    `b1_replicas` runners, each on its own backend (HIP stream) driven by its own host thread, all
-    prefilled to the same KV length; beside the headline's lock-step batches."""
-    R, steps = args.b1_replicas, args.b1_steps
+def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
+    """TTS.cpp's serving shape (examples/server/server.cpp:316-321,885-895): one prompt per runner, R
+    runners, each on its own backend (HIP stream) with its own model copy, driven by its own host thread
+    through TTS.cpp's own step loop (graph_compute, logits read back, host greedy sampler:
+    parler_tts_runner::decode, src/models/parler/model.cpp:648-693), all prefilled to the same KV length.
+    coalesce=True: the backend's step coalescer (coalesce.hip) runs the runners' equal steps as batched
+    launches; False: every runner alone (TTS_HIP_OPT_COALESCE = 0)."""
+    R, steps = R or args.b1_replicas, args.b1_steps
     # the same KV capacity rule as the lock-step leg: a multiple of 4 positions keeps every V row
     # 16-B aligned, so P.V takes its vector-load kernel (k_attn_pv<true, ...>)
     cfg = ttship.parler_config(batch=1, max_ctx=max(4096, args.ctx + steps + args.warmup + 64))
     bes = [new_backend() for _ in range(R)]
-    runs = [ttship.Parler(b.iface(), cfg) for b in bes]
+    for b in bes:
+        b.set_option(ttship.OPT["COALESCE"], 1 if coalesce else 0)
+    runs = [None] * R
+
+    def make(r):  # each worker loads its own model copy (runner_from_file per worker, server.cpp:316-321)
+        runs[r] = ttship.Parler(bes[r].iface(reference_flow=True), cfg)
+        runs[r].prefill(prompt_tokens(1, args.ctx, cfg.prompt_vocab, offset=rank * R + r))
+        bes[r].sync()
+
     try:
-        for r, (b, p) in enumerate(zip(bes, runs)):
-            p.prefill(prompt_tokens(1, args.ctx, cfg.prompt_vocab, offset=rank * R + r))
-            p.generate(args.warmup)
-            b.sync()
+        run_replicas(make, R)
+        run_replicas(lambda r: (runs[r].generate(args.warmup), bes[r].sync()), R)  # in step: the coalesced groups form
+        s0 = ttship.coalesce_stats(local)
 
         def one(r):
             runs[r].generate(steps)
@@ -417,13 +427,20 @@ def parler_b1_leg(args, rank, local, new_backend):
         t0 = time.perf_counter()
         run_replicas(one, R)
         dt = time.perf_counter() - t0
-        return {"workload": f"Parler-mini Q4_K AR decode, {R} runners x 1 prompt (TTS.cpp's server model), KV {args.ctx} -> "
+        s1 = ttship.coalesce_stats(local)
+        co = {k: s1[k] - s0[k] for k in ("launches", "member_steps", "alone", "refused")}
+        co["max_group"] = s1["max_group"]
+        co["wait_us_per_step"] = round((s1["wait_us"] - s0["wait_us"]) / max(1, R * steps), 1)
+        return {"workload": f"Parler-mini Q4_K AR decode, {R} runners x 1 prompt (TTS.cpp's server model: one runner, backend and "
+                            f"model copy per worker thread, graph_compute + host greedy sampler per step), KV {args.ctx} -> "
                             f"{args.ctx + steps}", "replicas": R, "batch_per_replica": 1,
+                "step_coalescer": "on" if coalesce else "off", "coalescer": co,
                 "ms_per_step": round(1000 * dt / steps, 4),
                 "ar_audio_sec_per_s": round(R * steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3)}
     finally:
         for p in runs:
-            p.close()
+            if p is not None:
+                p.close()
         for b in bes:
             b.close()
 
@@ -575,6 +592,7 @@ def main():
     ap.add_argument("--b1-replicas", type=int, default=8, help="the B=1 leg: this many runners of one prompt each, as "
                     "TTS.cpp's server workers run (0 = skip)")
     ap.add_argument("--b1-steps", type=int, default=100)
+    ap.add_argument("--b1-wide", type=int, default=32, help="the B=1 leg again with this many coalesced runners (0 = skip)")
     ap.add_argument("--p8", type=int, default=1, help="beside the headline, the AR line at 8 prompts per GPU (2 replicas x 4: "
                     "the 64-prompt batch over 8 GPUs) when the headline runs more (0 = skip)")
     ap.add_argument("--no-fusion", action="store_true")
@@ -741,11 +759,19 @@ def main():
               "ar_audio_sec_per_s": round(world * 8 * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE / d8, 3)}
     b1 = None
     if args.b1_replicas > 0:
-        barrier_sync(dist, None)
-        b1 = parler_b1_leg(args, rank, local, new_backend)
-        t = max_over_ranks(dist, local, b1["ms_per_step"])
-        b1["ms_per_step"] = t
-        b1["ar_audio_sec_per_s"] = round(world * args.b1_replicas * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
+        # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer, the same runners each
+        # alone, and b1_wide coalesced runners (the headline's prompt count per GPU)
+        b1 = {}
+        legs = [("coalesced", args.b1_replicas, True), ("alone", args.b1_replicas, False)]
+        if args.b1_wide > 0:
+            legs.append(("coalesced_wide", args.b1_wide, True))
+        for name, n_run, co in legs:
+            barrier_sync(dist, None)
+            leg = parler_b1_leg(args, rank, local, new_backend, R=n_run, coalesce=co)
+            t = max_over_ranks(dist, local, leg["ms_per_step"])
+            leg["ms_per_step"] = t
+            leg["ar_audio_sec_per_s"] = round(world * n_run * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)
+            b1[name] = leg
     kres = None
     if args.kokoro_prompts > 0:
         kb = [new_backend() for _ in range(2)]

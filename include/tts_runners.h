@@ -72,6 +72,10 @@ int32_t tts_parler_last_graph_nodes(const tts_parler * p);
 /* The last step graph's node list (valid until the next step is prepared). */
 tts_tensor * const * tts_parler_graph(const tts_parler * p, int32_t * n_nodes);
 uint64_t tts_parler_weight_bytes(const tts_parler * p);
+/* Weight introspection for tests (every weight in declaration order): name, ne[4], ggml type and the bytes
+ * as the backend stores them (F32 / F16 as ggml's); returns the byte size (dst NULL or too small: size only). */
+int32_t tts_parler_n_weights(const tts_parler * p);
+uint64_t tts_parler_weight(tts_parler * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst, uint64_t cap);
 /* Debug: copy a named node of the last graph to host (returns bytes, 0 if not found). */
 uint64_t tts_parler_get_node(tts_parler * p, const char * name, void * dst, uint64_t cap);
 /* Debug: node i of the last graph: op / type / ne; copies its bytes when contiguous (returns size). */
@@ -119,6 +123,9 @@ void tts_orpheus_set_sampling(tts_orpheus * p, const tts_sampling * cfg);
 int32_t tts_orpheus_position(const tts_orpheus * p);
 int32_t tts_orpheus_last_graph_nodes(const tts_orpheus * p);
 uint64_t tts_orpheus_weight_bytes(const tts_orpheus * p);
+/* Weight introspection for tests, as tts_parler_weight. */
+int32_t tts_orpheus_n_weights(const tts_orpheus * p);
+uint64_t tts_orpheus_weight(tts_orpheus * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst, uint64_t cap);
 tts_tensor * const * tts_orpheus_graph(const tts_orpheus * p, int32_t * n_nodes);
 
 /* Dia-1.6B config (defaults = dia_model, src/models/dia/model.h:62-85; Q8_0 weights for config 4,
@@ -194,6 +201,9 @@ void tts_dac_free(tts_dac * d);
 int tts_dac_decode(tts_dac * d, const int32_t * codes, int32_t T, float * pcm);
 int64_t tts_dac_hop(const tts_dac * d);
 int32_t tts_dac_last_graph_nodes(const tts_dac * d);
+/* Weight introspection for tests, as tts_parler_weight. */
+int32_t tts_dac_n_weights(const tts_dac * d);
+uint64_t tts_dac_weight(tts_dac * d, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst, uint64_t cap);
 /* Batched decode of nb prompts of T frames each (a serving-side layout; TTS.cpp decodes one prompt per
  * dac_runner::run): ONE graph over nb * T + (nb - 1) * gap frames, the gaps zeroed before every conv that
  * reaches across them, so each prompt's PCM is bit-identical to tts_dac_decode of that prompt.

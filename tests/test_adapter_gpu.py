@@ -144,12 +144,12 @@ def test_weight_set_failure_falls_back_to_native_bytes(hip):
     """When the backend cannot write a weight's layout (fault injected into tts_hip_weight_set), the
     adapter's set_tensor stores ggml's native Q4_K bytes with no layout flags and the graphs still
     compute the same tokens (the weight was left uninitialised before)."""
-    os.environ["TTS_HIP_FAULT_WEIGHT_SET"] = "1"
+    ttship.lib().tts_hip_test_hook(1, 1)  # TTS_HIP_HOOK_FAULT_WEIGHT_SET
     a = AdapterBackend(0)
     try:
         g = ttship.Parler(a.iface(), ttship.parler_config(batch=1, **TINY))
     finally:
-        del os.environ["TTS_HIP_FAULT_WEIGHT_SET"]
+        ttship.lib().tts_hip_test_hook(1, 0)
     d = ttship.Parler(hip.iface(), ttship.parler_config(batch=1, **TINY))
     try:
         prompt = (np.arange(7, dtype=np.int32).reshape(1, 7) * 53) % 512

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <atomic>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <thread>
 
@@ -36,9 +37,17 @@ static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tens
 // medium lane-layout Q4_K weights, keyed by device address.  A weight buffer may be allocated and
 // written through one backend and read by the graphs of another (the ggml adapter allocates through
 // a utility backend, every ggml_backend computes on its own stream), so neither is per backend.
+// Buffers are physical allocations mapped into a reserved virtual range (hipMemCreate + hipMemMap) so
+// that the step coalescer can map several backends' buffers side by side into one window
+// (coalesce.hip); TTS_HIP_COALESCE=0 falls back to plain hipMalloc.
 namespace {
 std::mutex g_reg_mu;
-std::unordered_map<const void *, size_t> g_buffers;      // base -> bytes
+struct BufRec {
+    size_t size = 0, map_size = 0;
+    hipMemGenericAllocationHandle_t h{};
+    bool vmm = false;
+};
+std::map<const char *, BufRec> g_buffers;                // base -> record (ordered: range lookups)
 std::unordered_map<const void *, uint8_t *> g_tiled;     // weight -> its tile-layout copy
 std::atomic<size_t> g_tiled_n{0};
 }  // namespace
@@ -49,7 +58,63 @@ const uint8_t * tiled_copy_find(const void * w) {
     auto it = g_tiled.find(w);
     return it == g_tiled.end() ? nullptr : it->second;
 }
+bool coalesce_enabled() {
+    static const bool on = [] {
+        const char * e = getenv("TTS_HIP_COALESCE");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size) {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_buffers.upper_bound((const char *)p);
+    if (it == g_buffers.begin()) return false;
+    --it;
+    if ((const char *)p >= it->first + it->second.size) return false;
+    if (base) *base = it->first;
+    if (size) *size = it->second.size;
+    if (vmm_handle) *vmm_handle = it->second.vmm ? (void *)it->second.h : nullptr;
+    if (map_size) *map_size = it->second.map_size;
+    return true;
+}
 }  // namespace tts
+
+// Physical allocation + reserved range + mapping (HIP virtual memory management); false = use hipMalloc.
+static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocationHandle_t * h, size_t * msz) {
+    hipMemAllocationProp prop{};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || gran == 0) {
+        (void)hipGetLastError();
+        return false;
+    }
+    const size_t n = (size + gran - 1) / gran * gran;
+    if (hipMemCreate(h, n, &prop, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    void * va = nullptr;
+    if (hipMemAddressReserve(&va, n, 0, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        hipMemRelease(*h);
+        return false;
+    }
+    hipMemAccessDesc acc{};
+    acc.location = prop.location;
+    acc.flags = hipMemAccessFlagsProtReadWrite;
+    if (hipMemMap(va, n, 0, *h, 0) != hipSuccess || hipMemSetAccess(va, n, &acc, 1) != hipSuccess) {
+        (void)hipGetLastError();
+        hipMemUnmap(va, n);
+        hipMemAddressFree(va, n);
+        hipMemRelease(*h);
+        return false;
+    }
+    *out = va;
+    *msz = n;
+    return true;
+}
 
 extern "C" {
 
@@ -68,6 +133,7 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->stream, hipStreamNonBlocking));
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->cap_stream, hipStreamNonBlocking));
     TTS_HIP_CHECK(hipStreamCreateWithFlags(&be->pf_stream, hipStreamNonBlocking));
+    TTS_HIP_CHECK(hipEventCreateWithFlags(&be->co_ev, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&be->pf_fork, hipEventDisableTiming));
     TTS_HIP_CHECK(hipEventCreateWithFlags(&be->pf_join, hipEventDisableTiming));
     hipDeviceProp_t prop;
@@ -106,6 +172,7 @@ tts_hip_backend_t tts_hip_backend_init(int device) {
 
 void tts_hip_backend_free(tts_hip_backend_t be) {
     if (!be) return;
+    tts::coalesce_backend_gone(be);
     hipSetDevice(be->device);
     hipStreamSynchronize(be->stream);
     for (auto & p : be->ev_pending) {
@@ -139,6 +206,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipStreamDestroy(be->pf_stream);
     hipEventDestroy(be->pf_fork);
     hipEventDestroy(be->pf_join);
+    hipEventDestroy(be->co_ev);
     delete be;
 }
 
@@ -198,9 +266,17 @@ void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {
     if (!be) return nullptr;
     hipSetDevice(be->device);
     void * p = nullptr;
-    if (hipMalloc(&p, size ? size : 256) != hipSuccess) return nullptr;
+    BufRec r;
+    r.size = size ? size : 256;
+    // buffers of a coalescable size (compute arenas, KV caches: 64 KiB and up) are VMM-mapped
+    if (tts::coalesce_enabled() && r.size >= ((size_t)64 << 10) && vmm_alloc(be->device, r.size, &p, &r.h, &r.map_size)) {
+        r.vmm = true;
+    } else {
+        if (hipMalloc(&p, r.size) != hipSuccess) return nullptr;
+        r.map_size = r.size;
+    }
     std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_buffers[p] = size ? size : 256;
+    g_buffers[(const char *)p] = r;
     return p;
 }
 
@@ -234,16 +310,27 @@ void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
     if (!be || !ptr) return;
     hipSetDevice(be->device);
     hipStreamSynchronize(be->stream);
-    size_t n = 0;
+    BufRec r;
+    bool known = false;
     {
         std::lock_guard<std::mutex> lk(g_reg_mu);
-        auto b = g_buffers.find(ptr);
+        auto b = g_buffers.find((const char *)ptr);
         if (b != g_buffers.end()) {
-            n = b->second;
+            r = b->second;
+            known = true;
             g_buffers.erase(b);
         }
     }
-    if (n) drop_tiled_copies(ptr, n);
+    if (known) {
+        drop_tiled_copies(ptr, r.size);
+        tts::coalesce_forget(ptr, r.size);  // coalescing windows holding this buffer are unmapped first
+    }
+    if (known && r.vmm) {
+        hipMemUnmap(ptr, r.map_size);
+        hipMemAddressFree(ptr, r.map_size);
+        hipMemRelease(r.h);
+        return;
+    }
     hipFree(ptr);
 }
 
@@ -251,6 +338,7 @@ int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
     drop_tiled_copies(dst, size);
+    tts::coalesce_written(dst, size);
     // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
     if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
     if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
@@ -264,6 +352,7 @@ int tts_hip_tensor_set_async(tts_hip_backend_t be, void * dst, const void * src,
     if (size == 0) return 0;
     hipSetDevice(be->device);
     if (size > be->pin_size / 2) return tts_hip_tensor_set(be, dst, src, size);
+    tts::coalesce_written(dst, size);
     // recycle finished regions
     while (!be->pin_pending.empty() && hipEventQuery(be->pin_pending.front().ev) == hipSuccess) {
         be->pin_events.push_back(be->pin_pending.front().ev);
@@ -327,6 +416,7 @@ int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_
 int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    tts::coalesce_written(dst, size);
     tts::launch_copy_bytes(be, dst, src, size);  // a kernel, not a blit: ~2 us less host time per step
     return hipGetLastError() == hipSuccess ? 0 : TTS_STATUS_FAILED;
 }
@@ -334,6 +424,7 @@ int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size
 int tts_hip_memset(tts_hip_backend_t be, void * dst, int value, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    tts::coalesce_written(dst, size);
     return hipMemsetAsync(dst, value, size, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
 }
 
@@ -405,14 +496,27 @@ static size_t tensor_bytes(const tts_tensor * t) {
     return n;
 }
 
+static int weight_set_impl(tts_hip_backend_t be, tts_tensor * t, const void * src);
+static std::atomic<bool> g_fault_weight_set{false};
+
+int tts_hip_test_hook(int hook, int value) {
+    if (hook == TTS_HIP_HOOK_FAULT_WEIGHT_SET) {
+        g_fault_weight_set.store(value != 0);
+        return 0;
+    }
+    return TTS_STATUS_BAD_ARG;
+}
+
 int tts_hip_weight_set(tts_hip_backend_t be, tts_tensor * t, const void * src) {
     if (!be || !t) return TTS_STATUS_BAD_ARG;
+    // fault injection for the callers' failure paths (tests/test_adapter_gpu.py, tts_hip_test_hook):
+    // no layout is written
+    if (t->type == TTS_TYPE_Q4_K && g_fault_weight_set.load(std::memory_order_relaxed)) return TTS_STATUS_ALLOC_FAILED;
+    return weight_set_impl(be, t, src);
+}
+
+static int weight_set_impl(tts_hip_backend_t be, tts_tensor * t, const void * src) {
     const size_t n = tensor_bytes(t);
-    // fault injection for the callers' failure paths (tests/test_adapter_gpu.py): no layout is written
-    if (t->type == TTS_TYPE_Q4_K) {
-        const char * f = getenv("TTS_HIP_FAULT_WEIGHT_SET");
-        if (f && f[0] == '1') return TTS_STATUS_ALLOC_FAILED;
-    }
     if (t->type == TTS_TYPE_Q4_K && t->ne[0] % 256 == 0 && t->ne[1] % 4 == 0 && t->ne[2] == 1 && t->ne[3] == 1 &&
         be->q4k_tile_bytes > 0 && (int64_t)n >= be->q4k_tile_bytes) {
         // large matrix: the matrix-core GEMV's tile layout
@@ -600,6 +704,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_GEMV_DEBUG: be->gemv_dbg = value; return 0;
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;
+        case TTS_HIP_OPT_COALESCE: be->co_member = value != 0; return 0;
         case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }

@@ -390,6 +390,12 @@ extern "C" int tts_dac_decode_batch(tts_dac * d, const int32_t * codes, int32_t 
 extern "C" int64_t tts_dac_min_gap(const tts_dac * d) { return d ? dac_min_gap(d) : 0; }
 
 extern "C" int32_t tts_dac_last_graph_nodes(const tts_dac * d) { return (int32_t)d->gctx.nodes.size(); }
+extern "C" int32_t tts_dac_n_weights(const tts_dac * d) { return d ? (int32_t)d->specs.size() : 0; }
+extern "C" uint64_t tts_dac_weight(tts_dac * d, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst,
+                                   uint64_t cap) {
+    if (!d || i < 0 || i >= (int32_t)d->specs.size()) return 0;
+    return tg::weight_out(d->be, d->specs[i].t, name, name_cap, ne, type, dst, cap);
+}
 
 extern "C" tts_tensor * const * tts_dac_graph(const tts_dac * d, int32_t * n_nodes) {
     if (n_nodes) *n_nodes = d ? (int32_t)d->gctx.nodes.size() : 0;

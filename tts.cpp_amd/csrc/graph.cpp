@@ -4,6 +4,7 @@
 #include <cassert>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <unordered_map>
 #include <unordered_set>
@@ -602,6 +603,20 @@ bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse) 
     }
     c.arena_used = fl.peak;
     return ok;
+}
+
+uint64_t weight_out(const tts_backend_iface & be, const tts_tensor * t, char * name, uint64_t name_cap, int64_t * ne, int32_t * type,
+                    void * dst, uint64_t cap) {
+    if (name && name_cap) {
+        strncpy(name, t->name, name_cap - 1);
+        name[name_cap - 1] = 0;
+    }
+    if (ne)
+        for (int k = 0; k < 4; ++k) ne[k] = t->ne[k];
+    if (type) *type = t->type;
+    const uint64_t n = nbytes(t);
+    if (dst && cap >= n && be.get(be.ctx, dst, t->data, n) != 0) return 0;
+    return n;
 }
 
 }  // namespace tg

@@ -113,4 +113,8 @@ void build_forward_expand(context & c, tts_tensor * t);
 // memory after a tensor's last use.  Returns false if the arena is too small.
 bool alloc_graph(context & c, char * arena_base, size_t arena_size, bool reuse = true);
 
+// A runner's weight i for tests and tools (tts_*_weight): name, ne, ggml type and its bytes as the
+// backend stores them (F32 / F16 as ggml's; quantized types in the backend's layout).  Returns the size.
+uint64_t weight_out(const tts_backend_iface & be, const tts_tensor * t, char * name, uint64_t name_cap, int64_t * ne, int32_t * type,
+                    void * dst, uint64_t cap);
 }  // namespace tg

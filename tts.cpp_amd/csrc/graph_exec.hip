@@ -29,7 +29,7 @@ namespace tts {
 void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int pdim, int blocks);
 void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnArgs & a);
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
-                        float * out, int hd, int P, int H, int n, int B, float * out2);
+                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs = -1, int64_t mbs = 0);
 void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
                       float eps, bool rms);
 }  // namespace tts
@@ -1935,20 +1935,19 @@ static bool ensure_scratch(tts_hip_backend * be, size_t bytes) {
 }
 
 // ---- activation preparation (cached per graph by src pointer) ----
-static int prepare_act(tts_hip_backend * be, int wtype, const tts_tensor * b, int64_t K, int64_t M, ActQuant & out) {
+static int prepare_act(tts_hip_backend * be, int wtype, const float * x, int64_t xcs, int64_t K, int64_t M, ActQuant & out) {
     ActQuant & aq = be->aq;
-    const int64_t xcs = (int64_t)(b->nb[1] / 4);
     if (wtype == TTS_TYPE_F32) {
         out = ActQuant();
         out.vtype = TTS_TYPE_F32;
         return 0;
     }
     const int vt = wtype == TTS_TYPE_Q4_K ? TTS_TYPE_Q8_K : wtype;
-    const bool hit = aq.src == b->data && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
+    const bool hit = aq.src == x && aq.K == K && aq.M == M && aq.vtype == vt && aq.graph_epoch == be->graph_epoch;
     if (!hit) {
         if (!ensure_scratch(be, act_quant_bytes(wtype, K, M))) return TTS_STATUS_ALLOC_FAILED;
-        launch_quantize_act(be, wtype, (const float *)b->data, xcs, K, M, aq);
-        aq.src = b->data;
+        launch_quantize_act(be, wtype, x, xcs, K, M, aq);
+        aq.src = x;
         aq.graph_epoch = be->graph_epoch;
     }
     out = aq;
@@ -1979,11 +1978,39 @@ static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a, bool 
     return be->repack_tmp;
 }
 
+// A coalesced step (be->bat): a one-sequence view becomes the N members' views, sequence k in member
+// k's copy (window + k * stride); a view shared by every member (stride 0) broadcasts.
+static void batch_td(const BatchCtx & bc, TD & t) {
+    const int64_t s = bc.stride(t.data);
+    t.data = bc.win(t.data);
+    if (s) {
+        t.ne[3] = bc.N;
+        t.nb[3] = s;
+    }
+}
+static int batch_n(const tts_hip_backend * be) { return be->bat ? be->bat->N : 1; }
+
 static int run_attn_item(tts_hip_backend * be, const Item & it) {
-    const TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
-    float * out2 = it.shadow && tbytes(it.out) <= be->shadow_size ? be->shadow : nullptr;
-    launch_attn_decode(be, q, k, v, it.mask ? (const float *)it.mask->data : nullptr, it.scale, (float *)it.out->data,
-                       (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], (int)it.q->ne[3], out2);
+    TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
+    float * out = (float *)it.out->data;
+    const float * mask = it.mask ? (const float *)it.mask->data : nullptr;
+    int B = (int)it.q->ne[3];
+    int64_t obs = -1, mbs = 0;
+    if (const BatchCtx * bc = be->bat) {  // (planner-checked: one sequence per member)
+        batch_td(*bc, q);
+        batch_td(*bc, k);
+        batch_td(*bc, v);
+        obs = bc->stride(out) / 4;
+        out = bc->win(out);
+        if (mask) {
+            mbs = bc->stride(mask) / 4;
+            mask = bc->win(mask);
+        }
+        B = bc->N;
+    }
+    float * out2 = it.shadow && tbytes(it.out) * (size_t)batch_n(be) <= be->shadow_size ? be->shadow : nullptr;
+    launch_attn_decode(be, q, k, v, mask, it.scale, out, (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], B, out2,
+                       obs, mbs);
     return 0;
 }
 
@@ -2005,6 +2032,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
     j.w_row_bytes = (int64_t)a0->nb[1];
     j.x = (const float *)b->data;
     j.xcs = (int64_t)(b->nb[1] / 4);
+    const BatchCtx * bc = be->bat;  // a coalesced step: M = 1 per member (planner-checked) -> N columns
+    const int64_t NB = bc ? bc->N : 1;
     j.epi = it.epi;
     j.gelu = be->gelu_table;
     if (it.res) {
@@ -2035,10 +2064,12 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             y0 = (const char *)it.tgt[k].y;
             y1 = y0 + 4 * (size_t)((Mm - 1) * it.tgt[k].ycs + (mm->ne[0] - 1) * it.tgt[k].yrs + 1);
         };
-        if (it.x_shadow && (size_t)(4 * j.K * j.M) <= be->shadow_size) {
+        const bool xs = it.x_shadow && (size_t)(4 * j.K * j.M * NB) <= be->shadow_size;
+        if (xs) {
             j.x = be->shadow;  // written by the preceding attention item (link_attn_shadow)
             j.xcs = j.K;
         }
+        // aliasing on member 0's addresses (every member's buffers share one layout; members never alias)
         const char * x0 = (const char *)j.x;
         const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
         const char * l0 = (const char *)j.lnout;
@@ -2049,6 +2080,17 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             span_y(k, y0, y1);
             x_hit |= y0 < x1 && x0 < y1;
             if (l0 && y0 < l1 && l0 < y1) j.lnout = nullptr;  // LN output already dead: its memory is an output
+        }
+        if (bc) {  // member k = column k: window addresses, member stride as the column stride
+            if (!xs) {
+                j.xcs = bc->stride(j.x) / 4;
+                j.x = bc->win(j.x);
+            }
+            if (j.lnout) {
+                j.locs = bc->stride(j.lnout) / 4;
+                j.lnout = bc->win(j.lnout);
+            }
+            j.M = NB;
         }
         // the prologue reads 16-B vectors: x 16-B aligned, columns 16-B strided (contiguous for PRO_QUANT)
         x_hit |= ((uintptr_t)j.x & 15) != 0 || (j.xcs & 3) != 0 || (j.pro == PRO_QUANT && j.xcs != j.K);
@@ -2061,18 +2103,30 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         }
     } else {
         if (it.ln) return TTS_STATUS_UNSUPPORTED;  // planner invariant: a fused LN always runs as a prologue
-        int st = prepare_act(be, j.wtype, b, j.K, j.M, j.aq);
+        if (bc) {
+            j.xcs = bc->stride(j.x) / 4;
+            j.x = bc->win(j.x);
+            j.M = NB;
+        }
+        int st = prepare_act(be, j.wtype, j.x, j.xcs, j.K, j.M, j.aq);
         if (st) return st;
+    }
+    if (bc && j.res) {
+        j.rcs = bc->stride(j.res) / 4;
+        j.res = bc->win(j.res);
     }
     // a Q4_K matrix in native layout goes through the one-matrix repack temp: launch it alone
     const bool tmp = a0->type == TTS_TYPE_Q4_K && !(a0->flags & TTS_FLAG_REPACKED);
     if (xattn) {
         const Item & A = *xattn;
-        const TD k = make_td(A.k), v = make_td(A.v);
+        TD k = make_td(A.k), v = make_td(A.v);
+        // aliasing on member 0's addresses (the x / LN-output spans of one member)
         const char * o0 = (const char *)A.out->data;
         const char * o1 = o0 + tbytes(A.out);
-        const char * x0 = (const char *)j.x;
-        const char * x1 = x0 + 4 * (size_t)((j.M - 1) * j.xcs + j.K);
+        const float * xm = bc ? (const float *)(it.ln ? it.lnx->data : b->data) : j.x;
+        const int64_t xmcs = bc ? 0 : j.xcs, mm = bc ? 1 : j.M;
+        const char * x0 = (const char *)xm;
+        const char * x1 = x0 + 4 * (size_t)((mm - 1) * xmcs + j.K);
         const bool ok = !tmp && !j.tiled && j.wtype == TTS_TYPE_Q4_K && j.K <= 1024 && j.N == 64 * A.q->ne[2] && k.nb[0] == 4 &&
                         (k.nb[1] % 16) == 0 && (k.nb[2] % 16) == 0 && (k.nb[3] % 16) == 0 && ((uintptr_t)k.data % 16) == 0 &&
                         A.k->ne[1] >= 1 && A.k->ne[1] <= 64 && !(o0 < x1 && x0 < o1) && contiguous(A.out);
@@ -2082,8 +2136,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             jj.W[0] = (const uint8_t *)weight_ptr(be, a0);
             jj.Y[0] = nullptr;
             if (jj.lnout) {  // the LN output may already be dead and its memory the attention output
-                const char * l0 = (const char *)jj.lnout;
-                const char * l1 = l0 + 4 * (size_t)((j.M - 1) * j.locs + j.K);
+                const char * l0 = it.ln ? (const char *)it.lndst->data : (const char *)jj.lnout;
+                const char * l1 = l0 + 4 * (size_t)((mm - 1) * (bc ? 0 : j.locs) + j.K);
                 if (l0 < o1 && o0 < l1) jj.lnout = nullptr;
             }
             XAttnArgs xa;
@@ -2092,10 +2146,19 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             xa.mask = A.mask ? (const float *)A.mask->data : nullptr;
             xa.scale = A.scale;
             xa.out = (float *)A.out->data;
-            xa.out2 = A.shadow && tbytes(A.out) <= be->shadow_size ? be->shadow : nullptr;
+            xa.out2 = A.shadow && tbytes(A.out) * (size_t)NB <= be->shadow_size ? be->shadow : nullptr;
             xa.P = (int)A.k->ne[1];
             xa.H = (int)A.q->ne[2];
             xa.B = (int)A.q->ne[3];
+            if (bc) {
+                batch_td(*bc, xa.k);
+                batch_td(*bc, xa.v);
+                xa.mbs = bc->stride(xa.mask) / 4;
+                xa.mask = bc->win(xa.mask);
+                xa.obs = bc->stride(xa.out) / 4;
+                xa.out = bc->win(xa.out);
+                xa.B = (int)NB;
+            }
             launch_gemv_q4K_xattn(be, jj, xa);
             return 0;
         }
@@ -2127,8 +2190,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             if (it.tgt[k].rg > 0 && jj.rep_mat >= 0) break;  // one repeat-copy target per launch
             if (jj.nmat > 0 && a->ne[1] != jj.N) jj.hetero = 1;
             jj.W[jj.nmat] = (const uint8_t *)weight_ptr(be, a, use_copy && !(a->flags & TTS_FLAG_TILED));
-            jj.Y[jj.nmat] = it.tgt[k].y;
-            jj.ycs[jj.nmat] = it.tgt[k].ycs;
+            jj.Y[jj.nmat] = bc ? bc->win(it.tgt[k].y) : it.tgt[k].y;
+            jj.ycs[jj.nmat] = bc ? bc->stride(it.tgt[k].y) / 4 : it.tgt[k].ycs;
             jj.yrs[jj.nmat] = it.tgt[k].yrs;
             if (it.tgt[k].rg > 0) {
                 jj.rep_mat = jj.nmat;
@@ -2169,7 +2232,67 @@ static void launch_gather_t(tts_hip_backend * be, const tts_tensor * dst, const 
     TTS_HIP_CHECK(hipGetLastError());
 }
 
+static int run_node(tts_hip_backend * be, const tts_tensor * n);
+
+// A tensor of member 0's graph as the N members' tensors along dim 3 (member k's copy at window + k *
+// stride); shared tensors (weights, stride 0) are left as they are and broadcast.
+static bool batch_tensor(const BatchCtx & bc, const tts_tensor * t, tts_tensor & o) {
+    o = *t;
+    const int64_t s = bc.stride(t->data);
+    o.data = bc.win(t->data);
+    if (!s) return true;
+    if (t->ne[3] != 1) return false;
+    o.ne[3] = bc.N;
+    o.nb[3] = (size_t)s;
+    return true;
+}
+
+// An unfused node of a coalesced step.  Ops that act on every dim-3 slice on its own (elementwise
+// with broadcasting, norms, copies, concat below dim 3) run once over the members' tensors; any other
+// op runs once per member on that member's own addresses.
+static int run_node_coalesced(tts_hip_backend * be, const tts_tensor * n) {
+    const BatchCtx & bc = *be->bat;
+    bool per_slice = false;
+    switch (n->op) {
+        case TTS_OP_ADD: case TTS_OP_SUB: case TTS_OP_MUL: case TTS_OP_DIV: case TTS_OP_SQR: case TTS_OP_SQRT: case TTS_OP_SIN:
+        case TTS_OP_COS: case TTS_OP_SCALE: case TTS_OP_CLAMP: case TTS_OP_LEAKY_RELU: case TTS_OP_UNARY: case TTS_OP_ROUND:
+        case TTS_OP_MOD: case TTS_OP_NORM: case TTS_OP_RMS_NORM: case TTS_OP_CONT: case TTS_OP_CPY: case TTS_OP_DUP:
+            per_slice = true;
+            break;
+        case TTS_OP_CONCAT: per_slice = n->op_params[0] < 3; break;
+        default: break;
+    }
+    tts_tensor t, srcs[TTS_MAX_SRC];
+    if (per_slice && bc.stride(n->data) && batch_tensor(bc, n, t)) {
+        for (int i = 0; i < TTS_MAX_SRC && per_slice; ++i) {
+            if (!n->src[i]) continue;
+            per_slice = batch_tensor(bc, n->src[i], srcs[i]);
+            // a copy reads as many elements as it writes: its source must be per member too
+            if ((n->op == TTS_OP_CONT || n->op == TTS_OP_CPY || n->op == TTS_OP_DUP) && !bc.stride(n->src[i]->data)) per_slice = false;
+            t.src[i] = &srcs[i];
+        }
+        if (per_slice) return launch_op(be, &t);
+    }
+    const BatchCtx * keep = be->bat;
+    be->bat = nullptr;  // member k's own graph node, run as in an uncoalesced step
+    int st = 0;
+    for (int k = 0; k < bc.N && st == 0; ++k) {
+        t = *n;
+        t.data = bc.reloc(n->data, k);
+        for (int i = 0; i < TTS_MAX_SRC; ++i) {
+            if (!n->src[i]) continue;
+            srcs[i] = *n->src[i];
+            srcs[i].data = bc.reloc(n->src[i]->data, k);
+            t.src[i] = &srcs[i];
+        }
+        st = run_node(be, &t);
+    }
+    be->bat = keep;
+    return st;
+}
+
 static int run_node(tts_hip_backend * be, const tts_tensor * n) {
+    if (be->bat) return run_node_coalesced(be, n);
     if (n->op == TTS_OP_MUL_MAT) {
         const tts_tensor * a = n->src[0], * b = n->src[1];
         if (a->ne[0] != b->ne[0] || b->ne[2] % a->ne[2] || b->ne[3] % a->ne[3]) return TTS_STATUS_UNSUPPORTED;  // ggml_can_mul_mat
@@ -2194,11 +2317,17 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             if (it.fused) return 0;  // launched with its query GEMV
             return run_attn_item(be, it);
         case Item::LN:
+            if (be->bat) {  // rows of every member (planner-checked: one-row tensors of member buffers)
+                tts_tensor d, x;
+                if (!batch_tensor(*be->bat, it.dst, d) || !batch_tensor(*be->bat, it.x, x)) return TTS_STATUS_UNSUPPORTED;
+                launch_layernorm(be, &d, &x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
+                return 0;
+            }
             launch_layernorm(be, it.dst, it.x, (const float *)it.w->data, it.b ? (const float *)it.b->data : nullptr, it.eps, it.rms);
             return 0;
         case Item::EMBED:
             if (it.gather_t) launch_gather_t(be, it.dst, it.w, it.gt_codes);
-            else launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size());
+            else launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size(), be->bat);
             return 0;
         case Item::SNAKE:
             launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one, it.snake_mask);
@@ -2242,7 +2371,57 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
     return TTS_STATUS_FAILED;
 }
 
-static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes);
+// Whether member 0's plan can run as a coalesced step: every item kind has a batched launch (or a
+// per-member one), every product and attention is one column / sequence per member, and every tensor
+// an item writes lies in a member buffer.  Checked before anything is launched: a refused step is run
+// by each member on its own instead.
+static bool coalescable(const tts_hip_backend * be, const Planner & pl, tts_tensor * const * nodes, int n_nodes,
+                        std::vector<std::pair<const void *, size_t>> & shared) {
+    const BatchCtx & bc = *be->bat;
+    auto share = [&](const tts_tensor * t) {
+        if (t && t->data) shared.emplace_back(t->data, tbytes(t));
+    };
+    for (int i = 0; i < n_nodes; ++i) {
+        const int a = pl.act[i];
+        if (a <= 0) {
+            if (a == 0 && !is_view(nodes[i]->op) && !bc.stride(nodes[i]->data)) return false;  // a shared tensor written by every member
+            continue;
+        }
+        const Item & it = pl.items[a - 1];
+        switch (it.kind) {
+            case Item::GEMV: {
+                const tts_tensor * x = it.mms[0]->src[1];
+                if (nel(x) != x->ne[0] || it.epi == EPI_SWIGLU || it.epi == EPI_SILU_MUL) return false;
+                for (const GemvTarget & t : it.tgt)
+                    if (!bc.stride(t.y)) return false;
+                if (it.ln && it.lndst && !bc.stride(it.lndst->data)) return false;
+                for (const tts_tensor * mm : it.mms) share(mm->src[0]);  // the weights
+                if (it.ln) share(it.lnw), share(it.lnb);
+                break;
+            }
+            case Item::ATTN:
+                if (it.q->ne[3] != 1 || it.k->ne[3] != 1 || it.v->ne[3] != 1 || !bc.stride(it.out->data)) return false;
+                if (it.mask && it.mask->ne[2] * it.mask->ne[3] != 1) return false;
+                break;
+            case Item::LN:
+                if (it.dst->ne[3] != 1 || it.x->ne[3] != 1 || !bc.stride(it.dst->data) || !bc.stride(it.x->data)) return false;
+                share(it.w), share(it.b);
+                break;
+            case Item::EMBED:
+                if (it.gather_t || it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3] != 1 || !bc.stride(it.dst->data)) return false;
+                for (const tts_tensor * g : it.terms) {
+                    if (g->ne[1] * g->ne[2] * g->ne[3] != 1) return false;
+                    share(g->src[0]);  // the table
+                }
+                break;
+            case Item::NODE:
+                if (!bc.stride(it.node.data)) return false;
+                break;
+            default: return false;  // LSTM / SNAKE / CONV / ADAIN / MCPY / RINT / COPY: vocoder and prefill items
+        }
+    }
+    return true;
+}
 
 // Replay through a HIP graph only for step-sized graphs: prompt-sized ones (many activation
 // columns) run once and are launched directly.
@@ -2301,6 +2480,9 @@ static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_
 extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    // a one-prompt decode step other backends on this device are also submitting: one coalesced launch
+    const int cs = coalesce_submit(be, nodes, n_nodes);
+    if (cs != kCoalesceNotTaken) return cs;
     // Recording pays off when the same graph comes back (a decode step): the first call of a
     // shape launches eagerly, so one-shot graphs (a Kokoro prompt's duration / synthesis graphs,
     // whose sizes follow the prompt) never pay for a capture and an instantiation.
@@ -2420,7 +2602,8 @@ extern "C" int tts_hip_plan_stats(tts_tensor * const * nodes, int n_nodes, int m
     return (int)pl.items.size();
 }
 
-static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
+namespace tts {
+int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     be->graph_epoch++;
     be->aq.src = nullptr;
     if (be->profile_gemv) launch_profile_spin(be, 4000.0);  // see launch_profile_spin (k_gemv.hip)
@@ -2436,7 +2619,12 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     pl.hoist_buf = (char *)be->hoist;
     pl.hoist_cap = be->hoist_size;
     if (be->fusion) pl.build(nodes, n_nodes);
+    else pl.act.assign(n_nodes, 0);
     be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
+    if (be->bat) {
+        std::vector<std::pair<const void *, size_t>> shared;
+        if (!coalescable(be, pl, nodes, n_nodes, shared) || !coalesce_check_shared(be, shared)) return TTS_STATUS_UNSUPPORTED;
+    }
     // long-context attention items in launch order: each one's K/V is prefetched into MALL on the
     // side stream right after the previous one ran (fork), and joined just before it runs
     std::vector<int> pf_items;
@@ -2508,6 +2696,7 @@ static int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nod
     if (pf_pending >= 0) TTS_HIP_CHECK(hipStreamWaitEvent(be->stream, be->pf_join, 0));  // every fork rejoins
     return 0;
 }
+}  // namespace tts
 
 extern "C" int tts_hip_gemv(tts_hip_backend_t be, int type, const void * w, const float * x, float * y, int64_t K, int64_t N,
                             int64_t M) {

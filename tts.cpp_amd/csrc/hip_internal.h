@@ -259,8 +259,57 @@ struct XAttnArgs {
     const float * mask = nullptr;  // [P] row 0 (n = 1), or null
     float scale = 1.f;
     float * out = nullptr;
-    float * out2 = nullptr;        // optional private copy (the next GEMV's input, be->shadow)
+    float * out2 = nullptr;        // optional private copy (the next GEMV's input, be->shadow), [hd, H, B] contiguous
     int P = 0, H = 0, B = 0;
+    int64_t obs = 0;               // floats between sequences of out (0: H * hd, contiguous)
+    int64_t mbs = 0;               // floats between sequences' masks (0: one mask for all)
+};
+
+// A coalesced decode step (coalesce.hip): N isomorphic one-prompt graphs of different backends
+// (TTS.cpp's server runs one runner per worker, examples/server/server.cpp:316-321) run as ONE
+// plan of member 0's graph with M = N columns.  Every buffer member 0's graph reads or writes
+// (compute arena, KV cache, inputs) has a counterpart in each member at the same offset; the N
+// counterparts are mapped into one virtual window at a fixed stride (hipMemMap of their physical
+// allocations), so member k's copy of a tensor is window + k * stride + offset: one uniform column
+// stride, which every GEMV / attention kernel already takes.  Weights are shared (member 0's copy;
+// the others hold identical bytes, checked by content hash at upload).
+struct BatchCls {
+    const char * b0 = nullptr;  // member 0's buffer
+    size_t size = 0;
+    char * win = nullptr;       // window: member k's buffer at win + k * stride
+    int64_t stride = 0;
+    std::vector<const char *> mb;  // every member's own buffer (relocated one-member launches)
+};
+struct BatchCtx {
+    int N = 0;
+    std::vector<BatchCls> cls;  // sorted by b0
+    const BatchCls * find(const void * p) const {
+        const char * c = (const char *)p;
+        size_t lo = 0, hi = cls.size();
+        while (lo < hi) {
+            const size_t m = (lo + hi) / 2;
+            if (cls[m].b0 <= c) lo = m + 1;
+            else hi = m;
+        }
+        if (lo == 0) return nullptr;
+        const BatchCls & b = cls[lo - 1];
+        return c < b.b0 + b.size ? &b : nullptr;
+    }
+    // the window address of member 0's pointer p (p itself when it is shared by every member)
+    template <typename T>
+    T * win(T * p) const {
+        const BatchCls * b = p ? find(p) : nullptr;
+        return b ? (T *)(b->win + ((const char *)p - b->b0)) : p;
+    }
+    int64_t stride(const void * p) const {  // bytes between members' copies (0: shared)
+        const BatchCls * b = p ? find(p) : nullptr;
+        return b ? b->stride : 0;
+    }
+    template <typename T>
+    T * reloc(T * p, int k) const {  // member k's own address of member 0's pointer p
+        const BatchCls * b = p ? find(p) : nullptr;
+        return b ? (T *)(b->mb[k] + ((const char *)p - b->b0)) : p;
+    }
 };
 
 }  // namespace tts
@@ -393,6 +442,11 @@ struct tts_hip_backend {
     tts_tensor * const * plan_nodes[2] = {nullptr, nullptr};
     int plan_n[2] = {0, 0};
     bool plan_eager[2] = {true, true};
+    // step coalescer (coalesce.hip): set while this (hidden, per-device) backend runs a coalesced
+    // plan; co_ev orders a member's stream with the coalesced launch
+    const tts::BatchCtx * bat = nullptr;
+    hipEvent_t co_ev = nullptr;
+    bool co_member = true;  // TTS_HIP_OPT_COALESCE: this backend's graph_compute calls may join a coalesced step
 };
 
 namespace tts {
@@ -442,7 +496,8 @@ void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int N
 int launch_sample_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, const tts_sampling * c, int64_t call,
                        int32_t * rep_state, int step, int bos, int eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
 constexpr int EMBED_MAX_TERMS = 16;
-void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n);
+struct BatchCtx;
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat = nullptr);
 // recip == nullptr: the kernel evaluates reciprocal() = one[0] / alpha[c] itself (`one` a broadcast scalar)
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
                   const tts_tensor * one = nullptr, const tts_tensor * mask = nullptr);
@@ -517,5 +572,23 @@ void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int6
 
 // ---- launchers (k_ops.hip) ----
 int launch_op(tts_hip_backend * be, const tts_tensor * node);
+
+// ---- graph execution (graph_exec.hip) and the step coalescer (coalesce.hip) ----
+// Plan and launch a node list on be->stream (be->bat set: as a coalesced step of be->bat->N members;
+// TTS_STATUS_UNSUPPORTED, before any launch, when the plan has an item without a coalesced form).
+int graph_compute_launches(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
+// graph_compute of a one-prompt decode graph while other backends on the device submit the same graph:
+// one coalesced launch for all of them.  Returns kCoalesceNotTaken when the caller runs the graph itself.
+constexpr int kCoalesceNotTaken = 1 << 20;
+int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
+// buffer registry hooks (backend.hip): a VMM-backed buffer's physical handle, and its release
+bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size);
+// a coalesced step's operands read through member 0's copy (weights, norm parameters, tables): true when
+// every member's copy holds the same bytes (checked on the device, cached until a host write)
+bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::pair<const void *, size_t>> & shared);
+void coalesce_forget(const void * base, size_t size);   // a buffer goes away: windows holding it are unmapped
+void coalesce_backend_gone(const tts_hip_backend * be); // a backend is freed: no longer awaited
+void coalesce_written(const void * p, size_t size);     // host writes: content checks over the range are dropped
+bool coalesce_enabled();
 
 }  // namespace tts

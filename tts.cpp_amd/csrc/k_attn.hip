@@ -18,9 +18,11 @@ struct AttnArgs {
     TD v;      // [P, hd, Hv, Bv] (V view of the cache, or cross_v)
     const float * mask;  // [rows >= n][P] f32, row stride P (ggml soft_max broadcast), or null
     float scale;
-    float * out;         // [hd, H, n, B] contiguous
+    float * out;         // [hd, H, n] per sequence, sequence b at out + b * obs
     int hd, P, H, n, B;
-    float * out2 = nullptr;  // optional second copy of out (the next GEMV's private input)
+    float * out2 = nullptr;  // optional second copy of out (the next GEMV's private input), [hd, H, n, B] contiguous
+    int64_t obs = 0;     // floats between sequences of out (n * H * hd when contiguous; a coalesced step's member stride)
+    int64_t mbs = 0;     // floats between sequences' masks (0: one mask for all)
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/attn_phase.hip builds only)
 };
 
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     __syncthreads();
 
     // ---- phase B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum ----
-    const float * mrow = a.mask ? a.mask + (int64_t)t * P : nullptr;
+    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)t * P : nullptr;
     float mx = -INFINITY;
     for (int i = tid; i < P; i += ATTN_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -119,7 +121,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
-    float * orow = a.out + (((int64_t)b * a.n + t) * a.H + h) * hd;
+    float * orow = a.out + (int64_t)b * a.obs + ((int64_t)t * a.H + h) * hd;
     const int waves = ATTN_THREADS / 64;
     const bool vvec = a.v.nb[0] == 4 && (a.v.nb[1] % 16) == 0 && (((uintptr_t)vbase) % 16) == 0 &&
                       a.v.nb[1] >= (int64_t)16 * ((P + 3) / 4);
@@ -280,7 +282,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     TTS_TS(a, 1);
 
     // ---- B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum; p = e * (1/sum) ----
-    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
     float mx = -INFINITY;
     for (int i = tid; i < P; i += ATTN_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     TTS_TS(a, 3);
 
     // ---- C: out[d] = sum_i (f32)(p[i] * V[d,i]) in f64 ----
-    float * orow = a.out + (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    float * orow = a.out + (int64_t)b * a.obs + ((int64_t)tq * a.H + h) * a.hd;
     float * orow2 = a.out2 ? a.out2 + (((int64_t)b * a.n + tq) * a.H + h) * a.hd : nullptr;
 #pragma unroll
     for (int ps = 0; ps < NPASS; ++ps) {
@@ -420,7 +422,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float 
 #pragma unroll
         for (int e = 0; e < 4; ++e) qv[f][e] = ((const float *)qbase)[16 * DPR * qd + 4 * f + e];
     TTS_PIN_LOADS();
-    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
     float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
     float mx = -INFINITY;
 #pragma unroll
@@ -541,9 +543,9 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
     acc += dpp_f64<DPP_HALF_MIRROR>(acc);
     acc += dpp_f64<DPP_MIRROR>(acc);
     if (t == 0 && d < a.hd) {
-        const int64_t o = (((int64_t)b * a.n + tq) * a.H + h) * a.hd + d;
-        a.out[o] = (float)acc;
-        if (a.out2) a.out2[o] = (float)acc;
+        const int64_t o = ((int64_t)tq * a.H + h) * a.hd + d;
+        a.out[(int64_t)b * a.obs + o] = (float)acc;
+        if (a.out2) a.out2[(int64_t)b * a.n * a.H * a.hd + o] = (float)acc;
     }
 }
 
@@ -625,9 +627,9 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
         acc += dpp_f64<DPP_MIRROR>(acc);
         const int d = d0 + pass * 4 * NW;
         if (t == 0 && d < a.hd) {
-            const int64_t o = (((int64_t)b * a.n + tq) * a.H + h) * a.hd + d;
-            a.out[o] = (float)acc;
-            if (a.out2) a.out2[o] = (float)acc;
+            const int64_t o = ((int64_t)tq * a.H + h) * a.hd + d;
+            a.out[(int64_t)b * a.obs + o] = (float)acc;
+            if (a.out2) a.out2[(int64_t)b * a.n * a.H * a.hd + o] = (float)acc;
         }
         acc = 0.0;
     };
@@ -745,7 +747,7 @@ __global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
     __syncthreads();
 
     // ---- B: soft_max_ext ----
-    const float * mrow = a.mask ? a.mask + (int64_t)tq * P : nullptr;
+    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
     float mx = -INFINITY;
     for (int i = tid; i < P; i += FUSED_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
     __syncthreads();
 
     // ---- C: out[d] = sum_i (f32)(p[i] * V[d,i]) in f64 ----
-    float * orow = a.out + (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    float * orow = a.out + (int64_t)b * a.obs + ((int64_t)tq * a.H + h) * a.hd;
     float * orow2 = a.out2 ? a.out2 + (((int64_t)b * a.n + tq) * a.H + h) * a.hd : nullptr;
     constexpr int kstep = 64 * UVC;
 #pragma unroll
@@ -867,7 +869,7 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
         acc += (double)__fmul_rn(kr[c].w, qv[4 * c + 3]);
     }
     float w = __fmul_rn((float)acc, a.scale);
-    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, a.mask[(int64_t)tq * P + p]));
+    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, a.mask[(int64_t)b * a.mbs + (int64_t)tq * P + p]));
     if (lane >= P) w = -INFINITY;
     float mx = w;
     mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
@@ -902,11 +904,11 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
         TTS_PIN_LOADS();
         consume(I1{}, i0 + VB);
     }
-    const int64_t orow = (((int64_t)b * a.n + tq) * a.H + h) * a.hd;
+    const int64_t orow = ((int64_t)tq * a.H + h) * a.hd;
 #pragma unroll
     for (int j = 0; j < HD / 64; ++j) {
-        a.out[orow + lane + 64 * j] = (float)o[j];
-        if (a.out2) a.out2[orow + lane + 64 * j] = (float)o[j];
+        a.out[(int64_t)b * a.obs + orow + lane + 64 * j] = (float)o[j];
+        if (a.out2) a.out2[(int64_t)b * a.n * a.H * a.hd + orow + lane + 64 * j] = (float)o[j];
     }
 }
 
@@ -954,9 +956,11 @@ void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int 
 }
 
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
-                        float * out, int hd, int P, int H, int n, int B, float * out2) {
+                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs, int64_t mbs) {
     AttnArgs a;
     a.out2 = out2;
+    a.obs = obs >= 0 ? obs : (int64_t)n * H * hd;
+    a.mbs = mbs;
     a.q = q;
     a.k = k;
     a.v = v;

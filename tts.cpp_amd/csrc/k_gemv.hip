@@ -1631,7 +1631,7 @@ __global__ __launch_bounds__(576) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
         for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
 #pragma unroll
         for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
-        mk = *(a.mask ? a.mask + p : (const float *)kbase);  // unconditional: no branch join before the barrier
+        mk = *(a.mask ? a.mask + (int64_t)b * a.mbs + p : (const float *)kbase);  // unconditional: no branch join before the barrier
     }
     __syncthreads();
     if (wave < NW) {
@@ -1680,9 +1680,9 @@ __global__ __launch_bounds__(576) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
             o += (double)__fmul_rn(pi, vv[u]);
         }
     }
-    const int64_t orow = ((int64_t)b * a.H + h) * HD;
-    a.out[orow + lane] = (float)o;
-    if (a.out2) a.out2[orow + lane] = (float)o;
+    const int64_t orow = (int64_t)h * HD + lane;
+    a.out[(int64_t)b * (a.obs ? a.obs : (int64_t)a.H * HD) + orow] = (float)o;
+    if (a.out2) a.out2[(int64_t)b * a.H * HD + orow] = (float)o;
 }
 
 // Host checks (caller): Q4_K repacked weights, one matrix of N = H * 64 rows, K <= 1024, M = B

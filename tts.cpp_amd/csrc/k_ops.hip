@@ -370,6 +370,7 @@ struct EmbedArgs {
     int n;
     float * out;
     int64_t H, M;
+    int64_t ocs;  // floats between output columns
 };
 
 __global__ void k_embed_sum(EmbedArgs a) {
@@ -385,20 +386,32 @@ __global__ void k_embed_sum(EmbedArgs a) {
                             : table_elem(T.table, T.table.data + r * T.table.nb[1], h);
         acc = t == 0 ? v : __fadd_rn(acc, v);
     }
-    a.out[m * a.H + h] = acc;
+    a.out[m * a.ocs + h] = acc;
 }
 
-void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n) {
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat) {
     EmbedArgs a{};
     a.n = n;
     a.out = (float *)out->data;
     a.H = out->ne[0];
     a.M = out->ne[1] * out->ne[2] * out->ne[3];
+    a.ocs = a.H;
     for (int i = 0; i < n; ++i) {
         a.t[i].table = make_td(gr[i]->src[0]);
         a.t[i].idx = (const int32_t *)gr[i]->src[1]->data;
         a.t[i].idx_stride = (int64_t)(gr[i]->src[1]->nb[0] / 4);
         a.t[i].rows = gr[i]->ne[1] * gr[i]->ne[2] * gr[i]->ne[3];
+    }
+    if (bat) {  // one row per member (a coalesced step's one-token graphs): column m = member m
+        a.M = bat->N;
+        a.ocs = bat->stride(a.out) / 4;
+        a.out = bat->win(a.out);
+        for (int i = 0; i < n; ++i) {
+            const int64_t s = bat->stride(a.t[i].idx);
+            a.t[i].idx_stride = s / 4;
+            a.t[i].rows = s ? bat->N : 1;
+            a.t[i].idx = bat->win(a.t[i].idx);
+        }
     }
     hipLaunchKernelGGL(k_embed_sum, dim3((unsigned)((a.H + 255) / 256), (unsigned)a.M), dim3(256), 0, be->stream, a);
     TTS_HIP_CHECK(hipGetLastError());

@@ -52,6 +52,7 @@ struct tts_orpheus {
     tts_sampling samp{};
     int64_t sample_calls = 0;
     std::vector<int32_t> rep_last, rep_count;  // [batch]
+    std::vector<tts_tensor *> wlist;  // every weight, declaration order (tts_orpheus_weight)
 };
 
 extern "C" void tts_orpheus_set_sampling(tts_orpheus * p, const tts_sampling * cfg) {
@@ -164,6 +165,7 @@ extern "C" tts_orpheus * tts_orpheus_create(const tts_backend_iface * be, const 
         L.up = wnew(p, specs, cf.weight_type, H, cf.ffn_size, 0, pre + ".up");
         L.down = wnew(p, specs, cf.weight_type, cf.ffn_size, H, 0, pre + ".down");
     }
+    for (auto & s : specs) p->wlist.push_back(s.first);
     if (!upload_weights(p, specs)) {
         fprintf(stderr, "orpheus: weight allocation/upload failed\n");
         tts_orpheus_free(p);
@@ -480,6 +482,12 @@ extern "C" int tts_orpheus_generate(tts_orpheus * p, const int32_t * first_token
 extern "C" int32_t tts_orpheus_position(const tts_orpheus * p) { return p->position; }
 extern "C" int32_t tts_orpheus_last_graph_nodes(const tts_orpheus * p) { return p->last_nodes; }
 extern "C" uint64_t tts_orpheus_weight_bytes(const tts_orpheus * p) { return p->wbytes; }
+extern "C" int32_t tts_orpheus_n_weights(const tts_orpheus * p) { return p ? (int32_t)p->wlist.size() : 0; }
+extern "C" uint64_t tts_orpheus_weight(tts_orpheus * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst,
+                                       uint64_t cap) {
+    if (!p || i < 0 || i >= (int32_t)p->wlist.size()) return 0;
+    return tg::weight_out(p->be, p->wlist[i], name, name_cap, ne, type, dst, cap);
+}
 extern "C" tts_tensor * const * tts_orpheus_graph(const tts_orpheus * p, int32_t * n_nodes) {
     if (n_nodes) *n_nodes = p ? (int32_t)p->gctx.nodes.size() : 0;
     return p ? p->gctx.nodes.data() : nullptr;

@@ -65,6 +65,7 @@ struct tts_parler {
     int64_t sample_calls = 0;                 // sampler::sample calls so far (one per step)
     std::vector<int32_t> rep_last, rep_count;  // [batch][heads] repetition-penalty state
     const tts_gguf * gguf = nullptr;  // weight source while creating from a file (else synthetic)
+    std::vector<tts_tensor *> wlist;  // every weight, declaration order (tts_parler_weight)
 };
 
 extern "C" void tts_parler_default_config(tts_parler_config * c) {
@@ -284,6 +285,7 @@ static tts_parler * parler_create(const tts_backend_iface * be, const tts_parler
     p->cfg.batch = B;
     std::vector<wspec> specs;
     declare_weights(p, specs);
+    for (auto & s : specs) p->wlist.push_back(s.t);
     if (!upload_weights(p, specs)) {
         fprintf(stderr, "parler: weight allocation/upload failed\n");
         tts_parler_free(p);
@@ -792,6 +794,12 @@ extern "C" int64_t tts_parler_host_stats(tts_parler * p, double * us5, int reset
     return n;
 }
 extern "C" int32_t tts_parler_last_graph_nodes(const tts_parler * p) { return p->last_nodes; }
+extern "C" int32_t tts_parler_n_weights(const tts_parler * p) { return p ? (int32_t)p->wlist.size() : 0; }
+extern "C" uint64_t tts_parler_weight(tts_parler * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst,
+                                      uint64_t cap) {
+    if (!p || i < 0 || i >= (int32_t)p->wlist.size()) return 0;
+    return tg::weight_out(p->be, p->wlist[i], name, name_cap, ne, type, dst, cap);
+}
 extern "C" uint64_t tts_parler_weight_bytes(const tts_parler * p) { return p->wbytes; }
 
 // The last step graph's node list (valid until the next step is prepared), e.g. for tts_hip_plan_stats.

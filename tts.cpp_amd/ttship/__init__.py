@@ -27,7 +27,7 @@ FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17, "GEMM_Q8": 18, "BGEMM_F32": 19, "CU_PARTITION": 20, "GEMV_PREQUANT": 21, "GEMV_KRELAY": 22, "ATTN_KS": 23, "ATTN_PV8": 24, "GEMV_NW_MIN": 25, "GEMV_KRELAY_LOOP": 26, "GEMV_Q80_PRO": 27, "GEMV_Q80_SLAB": 28, "GEMV_Q80_RW": 29, "GEMM_Q8_STAGED": 30, "GEMV_KR_INKERNEL": 31, "GEMV_F32_WIDE": 32, "ATTN_PV_MP": 33, "GEMM_KR_NW": 34, "GEMM_KR_INKERNEL": 35, "GEMM_KR_CT2": 36}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17, "GEMM_Q8": 18, "BGEMM_F32": 19, "CU_PARTITION": 20, "GEMV_PREQUANT": 21, "GEMV_KRELAY": 22, "ATTN_KS": 23, "ATTN_PV8": 24, "GEMV_NW_MIN": 25, "GEMV_KRELAY_LOOP": 26, "GEMV_Q80_PRO": 27, "GEMV_Q80_SLAB": 28, "GEMV_Q80_RW": 29, "GEMM_Q8_STAGED": 30, "GEMV_KR_INKERNEL": 31, "GEMV_F32_WIDE": 32, "ATTN_PV_MP": 33, "GEMM_KR_NW": 34, "GEMM_KR_INKERNEL": 35, "GEMM_KR_CT2": 36, "COALESCE": 37}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 ATTN_FUSED_ON = 128  # P >= 128 keys -> one 1024-thread launch (k_attn_fused; backend default 0 = off)
 
@@ -325,6 +325,15 @@ def lib():
         "tts_hip_gemv": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64]),
         "tts_hip_gemv_ex": (ctypes.c_int, [vp, ctypes.c_int, vp, vp, vp, i64, i64, i64, i32]),
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
+        "tts_hip_coalesce_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(i64), ctypes.c_int]),
+        "tts_hip_coalesce_set_wait": (None, [ctypes.c_int]),
+        "tts_hip_test_hook": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+        "tts_parler_n_weights": (i32, [vp]),
+        "tts_parler_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
+        "tts_orpheus_n_weights": (i32, [vp]),
+        "tts_orpheus_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
+        "tts_dac_n_weights": (i32, [vp]),
+        "tts_dac_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
         "tts_sampling_default": (None, [ctypes.POINTER(Sampling)]),
         "tts_parler_set_sampling": (None, [vp, ctypes.POINTER(Sampling)]),
         "tts_parler_set_position": (ctypes.c_int, [vp, i32]),
@@ -489,10 +498,16 @@ class HipBackend:
             raise RuntimeError("tts_hip_backend_init failed")
         self.L = L
 
-    def iface(self):
+    def iface(self, reference_flow=False):
+        """The backend vtable.  reference_flow=True keeps only what TTS.cpp's own step loop uses (graph_compute,
+        logits read back, host sampler: parler_tts_runner::decode, src/models/parler/model.cpp:648-693): no
+        prepared plans, no device sampling -- the path the step coalescer serves."""
         it = BackendIface()
         if self.L.tts_hip_backend_iface(self.ptr, ctypes.byref(it)) != 0:
             raise RuntimeError("tts_hip_backend_iface failed")
+        if reference_flow:
+            for f in ("prepare", "launch", "set_async", "copy", "greedy_step", "sample_step"):
+                setattr(it, f, None)
         return it
 
     def alloc(self, nbytes):
@@ -586,6 +601,40 @@ class HipBackend:
         if self.ptr:
             self.L.tts_hip_backend_free(self.ptr)
             self.ptr = None
+
+
+def runner_weights(n_fn, w_fn, ptr):
+    """{name: array shaped like torch (reversed ggml ne, leading 1s dropped)} of a runner's F32 / F16 weights
+    (tts_parler_weight / tts_orpheus_weight / tts_dac_weight); quantized weights are skipped."""
+    import numpy as np
+    out = {}
+    for i in range(n_fn(ptr)):
+        name = ctypes.create_string_buffer(128)
+        ne = (ctypes.c_int64 * 4)()
+        ty = ctypes.c_int32()
+        n = w_fn(ptr, i, name, 128, ne, ctypes.byref(ty), None, 0)
+        if ty.value not in (F32, F16):
+            continue
+        a = np.empty(n, dtype=np.uint8)
+        w_fn(ptr, i, name, 128, ne, ctypes.byref(ty), a.ctypes.data, n)
+        a = a.view(np.float32 if ty.value == F32 else np.float16).astype(np.float32)
+        shape = [int(v) for v in reversed(list(ne))]
+        while len(shape) > 1 and shape[0] == 1:
+            shape.pop(0)
+        out[name.value.decode()] = a.reshape(shape)
+    return out
+
+
+def coalesce_stats(device=0):
+    """Step-coalescer counters of `device` (tts_hip_coalesce_stats)."""
+    out = (ctypes.c_int64 * 6)()
+    n = lib().tts_hip_coalesce_stats(device, out, 6)
+    keys = ("launches", "member_steps", "alone", "refused", "max_group", "wait_us")
+    return {keys[i]: int(out[i]) for i in range(max(n, 0))}
+
+
+def coalesce_set_wait(us):
+    lib().tts_hip_coalesce_set_wait(int(us))
 
 
 def dia_config(**kw):
@@ -722,6 +771,9 @@ class Orpheus:
     def weight_bytes(self):
         return self.L.tts_orpheus_weight_bytes(self.ptr)
 
+    def weights(self):
+        return runner_weights(self.L.tts_orpheus_n_weights, self.L.tts_orpheus_weight, self.ptr)
+
     def plan_stats(self, mask=None):
         """Fusion coverage of the last step graph (no device needed)."""
         n = ctypes.c_int32()
@@ -835,6 +887,9 @@ class Parler:
     def weight_bytes(self):
         return self.L.tts_parler_weight_bytes(self.ptr)
 
+    def weights(self):
+        return runner_weights(self.L.tts_parler_n_weights, self.L.tts_parler_weight, self.ptr)
+
     def close(self):
         if self.ptr:
             self.L.tts_parler_free(self.ptr)
@@ -871,6 +926,9 @@ class Dac:
     @property
     def hop(self):
         return self.L.tts_dac_hop(self.ptr)
+
+    def weights(self):
+        return runner_weights(self.L.tts_dac_n_weights, self.L.tts_dac_weight, self.ptr)
 
     def decode(self, codes):
         """codes: (T, n_codebooks) int -> (T * hop,) float32 PCM."""
