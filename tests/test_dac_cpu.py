@@ -64,6 +64,21 @@ def test_dac_batch_rejects_short_gap_and_overflow():
         d.close()
 
 
+def test_dac_batch_rejects_odd_rates():
+    """An odd upsampling rate s has padding ceil(s / 2): a transposed conv then outputs T s - 1 samples,
+    which the batched layout (prompt z at z * (T + gap) * hop) cannot hold -- refused; the
+    single decode still works."""
+    cfg = ttship.dac_config(latent_dim=64, decoder_dim=64, rates=[8, 5, 4, 3], n_layers=4, max_frames=64)
+    d = ttship.Dac(py_oracle.iface(4), cfg)
+    try:
+        codes = np.zeros((2, 4, cfg.n_codebooks), np.int32)
+        with pytest.raises(RuntimeError):
+            d.decode_batch(codes)
+        assert np.all(np.isfinite(d.decode(codes[0])))
+    finally:
+        d.close()
+
+
 def test_dac_batch_masks_fused_into_snakes():
     """The batched graph's gap masks ride in the snake passes (k_snake's mask operand): the same items
     as a single decode plus the one mask product in front of the first conv."""

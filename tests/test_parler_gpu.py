@@ -192,3 +192,33 @@ def test_many_prompt_step_in_kernel_operands(hip):
         ink_be.close()
         g.close()
         c.close()
+
+
+@pytest.mark.gpu
+def test_scratch_grows_after_plans_ran():
+    """A runner that has generated (plans recorded into the backend's two slots) then runs a prompt pass
+    whose staged columns exceed the 64 MiB scratch: the scratch grows once the launched plans have run
+    and their recordings are dropped (growth used to be refused for good once any plan had been
+    recorded).  Tokens after the second prompt pass equal a fresh runner's."""
+    be = ttship.HipBackend(0)
+    be.set_option(ttship.OPT["GRAPHS"], 1)
+    cfg = ttship.parler_config(batch=16, max_ctx=512, arena_bytes=8 << 30)
+    small = (np.arange(16 * 8, dtype=np.int32).reshape(16, 8) * 37) % cfg.prompt_vocab
+    big = (np.arange(16 * 448, dtype=np.int32).reshape(16, 448) * 53) % cfg.prompt_vocab
+    p = ttship.Parler(be.iface(), cfg)
+    try:
+        p.prefill(small)
+        p.generate(4)  # plans recorded and launched
+        p.reset()
+        p.prefill(big)  # 16 x 448 columns of K = 4096: > 64 MiB of staged columns
+        got = p.generate(3)
+    finally:
+        p.close()
+    q = ttship.Parler(be.iface(), cfg)
+    try:
+        q.prefill(big)
+        ref = q.generate(3)
+    finally:
+        q.close()
+        be.close()
+    assert np.array_equal(got, ref)

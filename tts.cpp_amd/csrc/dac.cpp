@@ -332,6 +332,10 @@ static int64_t dac_min_gap(const tts_dac * d) {
 extern "C" int tts_dac_decode_batch(tts_dac * d, const int32_t * codes, int32_t nb, int32_t T, int32_t gap, float * pcm) {
     if (!d || nb <= 0 || T <= 0 || gap < 0) return TTS_STATUS_BAD_ARG;
     if (nb == 1) return tts_dac_decode(d, codes, T, pcm);
+    // the layout assumes every transposed conv outputs exactly T * stride samples per prompt:
+    // (T - 1) s - 2 ceil(s / 2) + 2 s = T s needs an even stride (an odd one gives T s - 1)
+    for (const auto & L : d->layers)
+        if (2 * L.padding != L.stride) return TTS_STATUS_BAD_ARG;
     const int64_t G = gap ? gap : dac_min_gap(d);
     if (G < dac_min_gap(d)) return TTS_STATUS_BAD_ARG;
     const int64_t span = T + G, Tt = (int64_t)nb * span - G;

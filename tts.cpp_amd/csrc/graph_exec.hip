@@ -1207,9 +1207,25 @@ struct Planner {
         Item it;
         it.kind = Item::SNAKE;
         it.x = x, it.w = alpha, it.b = R, it.dst = A;
+        // reciprocal() = DIV(broadcast view of a scalar, alpha) feeding only this snake (DAC, SNAC):
+        // the kernel divides itself (the same correctly rounded division) and the node is skipped
+        const tts_tensor * O = R->src[0];
+        const bool rfuse = R->op == TTS_OP_DIV && O && R->src[1] == alpha && sole_consumer(R) == M2 && index.count(R) && act[index[R]] == 0 &&
+                           O->type == TTS_TYPE_F32 && O->ne[0] == 1 && O->nb[1] == 0 && O->ne[2] * O->ne[3] == 1 && !overlap(A, O);
         // a time mask in front, read by this snake only (tts_dac_decode_batch zeroes the gaps between
-        // prompts): x = MUL(x0, m [ne0, 1]) -> the kernel multiplies (the same f32 product) and the node is skipped
-        if (x->op == TTS_OP_MUL && index.count(x) && act[index[x]] == 0 && uses[x] == 2) {
+        // prompts): x = MUL(x0, m [ne0, 1]) -> the kernel multiplies (the same f32 product) and the node is skipped.
+        // x0 and m are then read at the snake's position instead of the MUL's: no node still executed in
+        // between may write over them (the allocator may hand x0's memory on once the MUL has read it)
+        auto untouched_since = [&](const tts_tensor * t, int from) {
+            for (int k = from + 1; k < i; ++k) {
+                const tts_tensor * nk = nodes[k];
+                if (act[k] < 0 || is_view(nk->op) || nk == M1 || nk == S || nk == Q || nk == M2 || (rfuse && nk == R)) continue;
+                if (overlap(nk, t)) return false;
+            }
+            return true;
+        };
+        if (x->op == TTS_OP_MUL && index.count(x) && act[index[x]] == 0 && uses[x] == 2 && untouched_since(x->src[0], index[x]) &&
+            (!x->src[1] || untouched_since(x->src[1], index[x]))) {
             const tts_tensor *x0 = x->src[0], *m = x->src[1];
             const auto ci = consumers.find(x);
             bool only = ci != consumers.end() && ci->second.size() == 2;
@@ -1224,11 +1240,7 @@ struct Planner {
             }
         }
         act[index[M1]] = act[index[S]] = act[index[Q]] = act[index[M2]] = -1;
-        // reciprocal() = DIV(broadcast view of a scalar, alpha) feeding only this snake (DAC, SNAC):
-        // the kernel divides itself (the same correctly rounded division) and the node is skipped
-        const tts_tensor * O = R->src[0];
-        if (R->op == TTS_OP_DIV && O && R->src[1] == alpha && sole_consumer(R) == M2 && index.count(R) && act[index[R]] == 0 &&
-            O->type == TTS_TYPE_F32 && O->ne[0] == 1 && O->nb[1] == 0 && O->ne[2] * O->ne[3] == 1 && !overlap(A, O)) {
+        if (rfuse) {
             it.b = nullptr;
             it.snake_one = O;
             act[index[R]] = -1;
@@ -1914,12 +1926,18 @@ struct Planner {
 // while recording, the buffer cannot move and the caller's fallback applies.
 static bool ensure_scratch(tts_hip_backend * be, size_t bytes) {
     if (bytes <= be->scratch_size) return true;
-    if (be->stream == be->cap_stream || be->pexec[0] || be->pexec[1]) return false;
-    TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+    // a plan recorded but not launched yet holds the old address: the buffer cannot move
+    if (be->stream == be->cap_stream || be->plan_prepared[0] || be->plan_prepared[1]) return false;
+    TTS_HIP_CHECK(hipStreamSynchronize(be->stream));  // (every launched plan has run)
     for (int k = 0; k < tts_hip_backend::N_GSIG; ++k) {
         if (be->gsig_exec[k]) TTS_HIP_CHECK(hipGraphExecDestroy(be->gsig_exec[k]));
         be->gsig_exec[k] = nullptr;
         be->gsig[k] = 0;
+    }
+    for (int k = 0; k < 2; ++k) {  // launched plans recorded the old address: re-recorded by their next prepare
+        if (be->pexec[k]) TTS_HIP_CHECK(hipGraphExecDestroy(be->pexec[k]));
+        be->pexec[k] = nullptr;
+        be->plan_ev_pending[k] = false;
     }
     const size_t n = (bytes + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
     char * p = nullptr;
@@ -2531,7 +2549,9 @@ extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * 
     be->plan_n[slot] = n_nodes;
     be->plan_eager[slot] = !capture_worthy(be, nodes, n_nodes);
     if (be->plan_eager[slot]) return 0;
-    return capture_into(be, nodes, n_nodes, be->pexec[slot]);
+    const int st = capture_into(be, nodes, n_nodes, be->pexec[slot]);
+    be->plan_prepared[slot] = st == 0;
+    return st;
 }
 
 extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
@@ -2543,6 +2563,7 @@ extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
     } else {
         if (!be->pexec[slot]) return TTS_STATUS_BAD_ARG;
         TTS_HIP_CHECK(hipGraphLaunch(be->pexec[slot], be->stream));
+        be->plan_prepared[slot] = false;
     }
     TTS_HIP_CHECK(hipEventRecord(be->plan_ev[slot], be->stream));
     be->plan_ev_pending[slot] = true;

@@ -442,6 +442,7 @@ struct tts_hip_backend {
     tts_tensor * const * plan_nodes[2] = {nullptr, nullptr};
     int plan_n[2] = {0, 0};
     bool plan_eager[2] = {true, true};
+    bool plan_prepared[2] = {false, false};  // recorded by graph_prepare, not launched yet
     // step coalescer (coalesce.hip): set while this (hidden, per-device) backend runs a coalesced
     // plan; co_ev orders a member's stream with the coalesced launch
     const tts::BatchCtx * bat = nullptr;
