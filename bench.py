@@ -40,7 +40,9 @@ PMC_FILE = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k.json"), default=ROOT / 
 # PMC traffic of the Orpheus leg's matrix-core GEMV (scripts/gpu_pmc_orpheus.sh), newest round first
 PMC_FILE_ORPH = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k_kr_orpheus.json"), default=None)
 
-HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), token ids derived from bytes
+# examples/perf_battery/perf_battery.cpp:25-56: the reference's 29 test prompts (its list has 30 literals, but
+# "Kick the ball straight and follow through." lacks a comma, so C++ joins it with the next one)
+HARVARD = [
     "The birch canoe slid on the smooth planks.",
     "Glue the sheet to the dark blue background.",
     "It's easy to tell the depth of a well.",
@@ -49,7 +51,36 @@ HARVARD = [  # examples/perf_battery/perf_battery.cpp:25-56 (first sentences), t
     "The juice of lemons makes fine punch.",
     "The box was thrown beside the parked truck.",
     "The hogs were fed chopped corn and garbage.",
+    "Four hours of steady work faced us.",
+    "A large size in stockings is hard to sell.",
+    "The boy was there when the sun rose.",
+    "A rod is used to catch pink salmon.",
+    "The source of the huge river is the clear spring.",
+    "Kick the ball straight and follow through.Help the woman get back to her feet.",
+    "A pot of tea helps to pass the evening.",
+    "Smoky fires lack flame and heat.",
+    "The soft cushion broke the man's fall.",
+    "The salt breeze came across from the sea.",
+    "The girl at the booth sold fifty bonds.",
+    "The small pup gnawed a hole in the sock.",
+    "The fish twisted and turned on the bent hook.",
+    "Press the pants and sew a button on the vest.",
+    "The swan dive was far short of perfect.",
+    "The beauty of the view stunned the young boy.",
+    "Two blue fish swam in the tank.",
+    "Her purse was full of useless trash.",
+    "The colt reared and threw the tall rider.",
+    "It snowed, rained, and hailed the same morning.",
+    "Read verse out loud for pleasure.",
 ]
+
+
+def sentence_tokens(s, vocab):
+    """Stand-in for the T5 ids of one prompt (the tokenizer model is not available offline): one id per word
+    piece (words and punctuation) plus the closing </s> (id 1), so a prompt pass has the sentence's length."""
+    import re
+    pieces = re.findall(r"[A-Za-z']+|[^\sA-Za-z']", s)
+    return np.asarray([(sum(p.encode()) * 131 + len(p) * 7) % (vocab - 2) + 2 for p in pieces] + [1], dtype=np.int32)
 
 
 def prompt_tokens(batch, n, vocab, offset=0):
@@ -593,6 +624,9 @@ def main():
                     "TTS.cpp's server workers run (0 = skip)")
     ap.add_argument("--b1-steps", type=int, default=100)
     ap.add_argument("--b1-wide", type=int, default=32, help="the B=1 leg again with this many coalesced runners (0 = skip)")
+    ap.add_argument("--sampled-steps", type=int, default=20, help="the headline's AR decode again with seeded top-k 50 sampling "
+                    "(the reference's default sampler) for this many steps (0 = skip)")
+    ap.add_argument("--prompt-pass", type=int, default=1, help="time every prompt's own sentence prompt pass from position 0 (0 = skip)")
     ap.add_argument("--p8", type=int, default=1, help="beside the headline, the AR line at 8 prompts per GPU (2 replicas x 4: "
                     "the 64-prompt batch over 8 GPUs) when the headline runs more (0 = skip)")
     ap.add_argument("--no-fusion", action="store_true")
@@ -757,6 +791,57 @@ def main():
         close_replicas(reps8)
         p8 = {"workload": "Parler-mini Q4_K AR decode, 8 prompts per GPU (2 lock-step replicas x 4)", "ar_ms_per_step": round(1000 * d8 / args.steps, 4),
               "ar_audio_sec_per_s": round(world * 8 * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE / d8, 3)}
+    # the reference's default sampler (sampler::sample with top_k 50, temperature 1: include/common.h:45-66,
+    # src/sampler.cpp:3-69), seeded, on the device (k_sample.hip), at the headline's shape (AR only)
+    sampled = None
+    if args.sampled_steps > 0:
+        barrier_sync(dist, None)
+        reps_s, _, _ = parler_replicas(args, per_gpu, R, rank, new_backend)
+        for r, (rb, rr, _) in enumerate(reps_s):
+            rr.set_sampling(ttship.sampling(top_k=50, temperature=1.0, seed=0x5EED + rank * R + r))
+            rr.generate(2)
+        warm_concurrent(args, reps_s)
+        barrier_sync(dist, reps_s[0][0])
+        ts0 = time.perf_counter()
+        run_replicas(lambda r: (reps_s[r][1].generate(args.sampled_steps), reps_s[r][0].sync()), R)
+        ds = max_over_ranks(dist, local, time.perf_counter() - ts0)
+        close_replicas(reps_s)
+        sampled = {"workload": f"as the headline's AR decode ({R} replicas x {bl} lock-step prompts per GPU, KV {args.ctx}), with the "
+                               "reference's default sampler: seeded top-k 50, temperature 1 (device sampling, k_sample.hip)",
+                   "steps": args.sampled_steps, "ar_ms_per_step": round(1000 * ds / args.sampled_steps, 4),
+                   "ar_audio_sec_per_s": round(world * per_gpu * args.sampled_steps * SAMPLES_PER_STEP / SAMPLE_RATE / ds, 3)}
+    # the prompt pass the headline leaves out: every prompt's own sentence (perf_battery's 29, prompt g = HARVARD[g % 29])
+    # from position 0, as TTS.cpp runs it (one prompt per runner), R runners concurrently
+    prompt_pass = None
+    if args.prompt_pass:
+        barrier_sync(dist, None)
+        pcfg = ttship.parler_config(batch=1, max_ctx=256)
+        pbes = [new_backend() for _ in range(R)]
+        pruns = [ttship.Parler(b.iface(), pcfg) for b in pbes]
+        toks_pp = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], pcfg.prompt_vocab) for g in range(per_gpu)]
+        for rr, b in zip(pruns, pbes):  # warm (code objects)
+            rr.prefill(toks_pp[0].reshape(1, -1))
+            b.sync()
+
+        def pp(r):
+            for g in range(r, per_gpu, R):
+                pruns[r].reset()
+                pruns[r].prefill(toks_pp[g].reshape(1, -1))
+            pbes[r].sync()
+
+        barrier_sync(dist, pbes[0])
+        tp0 = time.perf_counter()
+        run_replicas(pp, R)
+        dtp = max_over_ranks(dist, local, time.perf_counter() - tp0)
+        for rr in pruns:
+            rr.close()
+        for b in pbes:
+            b.close()
+        prompt_pass = {"workload": f"{per_gpu} prompt passes per GPU from position 0, prompt g = perf_battery sentence g % 29 "
+                                   f"(word-piece-length synthetic ids, {min(map(len, toks_pp))}-{max(map(len, toks_pp))} tokens), "
+                                   f"{R} runners concurrently",
+                       "ms_total": round(1000 * dtp, 3), "ms_per_prompt": round(1000 * dtp * R / per_gpu, 3),
+                       "end_to_end_audio_sec_per_s_with_prompt_pass": round(audio_s / (dt + dtp), 3)}
     b1 = None
     if args.b1_replicas > 0:
         # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer, the same runners each
@@ -840,6 +925,8 @@ def main():
                 "prompts": len(gathered), "audio_sec": round(sum(len(p) for p in gathered) / SAMPLE_RATE, 3),
                 "ms": round(1000.0 * t_gather, 3), "transport": "RCCL send/recv (gatherv) to rank 0" if world > 1 else "local"},
             "parler_8_prompts_per_gpu": p8,
+            "parler_sampled_top_k": sampled,
+            "prompt_pass": prompt_pass,
             "parler_b1": b1,
             "kokoro": kres,
             "orpheus": ores,

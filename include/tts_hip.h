@@ -355,6 +355,9 @@ void tts_hip_coalesce_set_wait(int us);
  * TTS_HIP_HOOK_FAULT_WEIGHT_SET = 1: tts_hip_weight_set of a Q4_K tensor fails (the callers' fallback paths). */
 #define TTS_HIP_HOOK_FAULT_WEIGHT_SET 1
 int tts_hip_test_hook(int hook, int value);
+/* Diagnostics: on SIGSEGV / SIGBUS print the fault address, every frame as library + offset (+ symbol) and
+ * the /proc/self/maps lines near the fault, then chain to the previous handler. */
+int tts_hip_install_crash_handler(void);
 /* Sum of timed GEMV launch durations (ms), launches and algorithmic bytes since last reset, for
  * weight type `type` (-1 = all types). */
 int tts_hip_gemv_stats(tts_hip_backend_t backend, int type, double * ms, int64_t * launches, double * bytes, int reset);

@@ -11,6 +11,12 @@
 #include "hip_internal.h"
 #include <hip/hip_ext.h>
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <fcntl.h>
+#include <signal.h>
+#include <unistd.h>
+
 using namespace tts;
 
 
@@ -498,6 +504,75 @@ static size_t tensor_bytes(const tts_tensor * t) {
 
 static int weight_set_impl(tts_hip_backend_t be, tts_tensor * t, const void * src);
 static std::atomic<bool> g_fault_weight_set{false};
+
+// Crash diagnostics (tts_hip_install_crash_handler): on SIGSEGV / SIGBUS the faulting address, every
+// frame as library + offset (+ symbol when exported), and the /proc/self/maps lines around the fault
+// address go to stderr; then the previous handler (a profiler's, or the default) runs.  For hosts where
+// a fault inside the HIP runtime must be attributed from the log alone (tracer fault).
+static struct sigaction g_prev_segv, g_prev_bus;
+static void crash_write(const char * s, int n) {
+    while (n > 0) {
+        const ssize_t w = write(2, s, (size_t)n);
+        if (w <= 0) return;
+        s += w, n -= (int)w;
+    }
+}
+static void crash_handler(int sig, siginfo_t * si, void * uc) {
+    char buf[512];
+    int n = snprintf(buf, sizeof buf, "tts_hip: signal %d, fault address %p\n", sig, si ? si->si_addr : nullptr);
+    crash_write(buf, n);
+    void * fr[64];
+    const int nf = backtrace(fr, 64);
+    for (int i = 0; i < nf; ++i) {
+        Dl_info di;
+        if (dladdr(fr[i], &di) && di.dli_fname)
+            n = snprintf(buf, sizeof buf, "  #%d %p %s+0x%lx %s\n", i, fr[i], di.dli_fname, (unsigned long)((const char *)fr[i] - (const char *)di.dli_fbase),
+                         di.dli_sname ? di.dli_sname : "");
+        else
+            n = snprintf(buf, sizeof buf, "  #%d %p ?\n", i, fr[i]);
+        crash_write(buf, n);
+    }
+    // the mappings within 64 MiB of the fault address
+    const uintptr_t fa = si ? (uintptr_t)si->si_addr : 0;
+    const int fd = open("/proc/self/maps", O_RDONLY);
+    if (fd >= 0) {
+        crash_write("tts_hip: maps near the fault address:\n", 38);
+        char line[512], c;
+        int len = 0;
+        while (read(fd, &c, 1) == 1) {
+            if (c != '\n') {
+                if (len < (int)sizeof line - 2) line[len++] = c;
+                continue;
+            }
+            line[len] = 0;
+            unsigned long a = 0, b = 0;
+            if (sscanf(line, "%lx-%lx", &a, &b) == 2 && fa + (64ul << 20) >= a && fa <= b + (64ul << 20)) {
+                line[len++] = '\n';
+                crash_write(line, len);
+            }
+            len = 0;
+        }
+        close(fd);
+    }
+    const struct sigaction & prev = sig == SIGBUS ? g_prev_bus : g_prev_segv;
+    if (prev.sa_flags & SA_SIGINFO) {
+        if (prev.sa_sigaction) prev.sa_sigaction(sig, si, uc);
+    } else if (prev.sa_handler != SIG_DFL && prev.sa_handler != SIG_IGN && prev.sa_handler) {
+        prev.sa_handler(sig);
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+int tts_hip_install_crash_handler(void) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = crash_handler;
+    sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+    sigemptyset(&sa.sa_mask);
+    if (sigaction(SIGSEGV, &sa, &g_prev_segv) != 0 || sigaction(SIGBUS, &sa, &g_prev_bus) != 0) return TTS_STATUS_FAILED;
+    return 0;
+}
 
 int tts_hip_test_hook(int hook, int value) {
     if (hook == TTS_HIP_HOOK_FAULT_WEIGHT_SET) {

@@ -328,6 +328,7 @@ def lib():
         "tts_hip_coalesce_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_coalesce_set_wait": (None, [ctypes.c_int]),
         "tts_hip_test_hook": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+        "tts_hip_install_crash_handler": (ctypes.c_int, []),
         "tts_parler_n_weights": (i32, [vp]),
         "tts_parler_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
         "tts_orpheus_n_weights": (i32, [vp]),
@@ -482,6 +483,8 @@ def lib():
         fn.restype = res
         fn.argtypes = args
     _lib = L
+    if os.environ.get("TTS_HIP_CRASH_HANDLER") == "1":  # tracing / repro runs: symbolized frames + maps on a fault
+        L.tts_hip_install_crash_handler()
     return L
 
 
