@@ -173,6 +173,9 @@ void tts_dia_set_sampling(tts_dia * p, const tts_sampling * cfg);
 int32_t tts_dia_position(const tts_dia * p);
 int32_t tts_dia_last_graph_nodes(const tts_dia * p);
 uint64_t tts_dia_weight_bytes(const tts_dia * p);
+/* Weight introspection for tests, as tts_parler_weight. */
+int32_t tts_dia_n_weights(const tts_dia * p);
+uint64_t tts_dia_weight(tts_dia * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst, uint64_t cap);
 tts_tensor * const * tts_dia_graph(const tts_dia * p, int32_t * n_nodes);
 
 /* DAC decoder (codec tokens -> PCM): dac_runner::run / build_dac_graph,

@@ -38,6 +38,7 @@ struct tts_dia {
     std::vector<dia_enc_layer> enc;
     std::vector<dia_dec_layer> dec;
     std::vector<tts_tensor *> embds, heads;
+    std::vector<tts_tensor *> wlist;  // every weight, declaration order (tts_dia_weight)
     std::vector<tts_tensor *> k_l, v_l, cross_k_l, cross_v_l;
     char * arena = nullptr;
     size_t arena_size = 0;
@@ -165,6 +166,7 @@ extern "C" tts_dia * tts_dia_create(const tts_backend_iface * be, const tts_dia_
     p->dec_norm = wnew(p, specs, TTS_TYPE_F32, D, 1, 1, "decoder.norm");
     for (int i = 0; i < cf.n_output_heads; ++i)
         p->heads.push_back(wnew(p, specs, cf.head_type, D, cf.output_vocab_size, 0, "decoder.heads." + std::to_string(i)));
+    for (auto & s : specs) p->wlist.push_back(s.first);
     if (!upload_weights(p, specs)) {
         fprintf(stderr, "dia: weight allocation/upload failed\n");
         tts_dia_free(p);
@@ -536,6 +538,12 @@ extern "C" int tts_dia_generate(tts_dia * p, const int32_t * first_audio, int32_
 extern "C" int32_t tts_dia_position(const tts_dia * p) { return p->position; }
 extern "C" int32_t tts_dia_last_graph_nodes(const tts_dia * p) { return p->last_nodes; }
 extern "C" uint64_t tts_dia_weight_bytes(const tts_dia * p) { return p->wbytes; }
+extern "C" int32_t tts_dia_n_weights(const tts_dia * p) { return p ? (int32_t)p->wlist.size() : 0; }
+extern "C" uint64_t tts_dia_weight(tts_dia * p, int32_t i, char * name, uint64_t name_cap, int64_t * ne, int32_t * type, void * dst,
+                                   uint64_t cap) {
+    if (!p || i < 0 || i >= (int32_t)p->wlist.size()) return 0;
+    return tg::weight_out(p->be, p->wlist[i], name, name_cap, ne, type, dst, cap);
+}
 extern "C" tts_tensor * const * tts_dia_graph(const tts_dia * p, int32_t * n_nodes) {
     if (n_nodes) *n_nodes = p ? (int32_t)p->gctx.nodes.size() : 0;
     return p ? p->gctx.nodes.data() : nullptr;

@@ -330,6 +330,8 @@ def lib():
         "tts_hip_test_hook": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
         "tts_hip_install_crash_handler": (ctypes.c_int, []),
         "tts_parler_n_weights": (i32, [vp]),
+        "tts_dia_n_weights": (i32, [vp]),
+        "tts_dia_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
         "tts_parler_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
         "tts_orpheus_n_weights": (i32, [vp]),
         "tts_orpheus_weight": (u64, [vp, i32, ctypes.c_char_p, u64, ctypes.POINTER(i64), ctypes.POINTER(i32), vp, u64]),
@@ -702,6 +704,9 @@ class Dia:
 
     def weight_bytes(self):
         return self.L.tts_dia_weight_bytes(self.ptr)
+
+    def weights(self):
+        return runner_weights(self.L.tts_dia_n_weights, self.L.tts_dia_weight, self.ptr)
 
     def plan_stats(self, mask=None):
         n = ctypes.c_int32()
