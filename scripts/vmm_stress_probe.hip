@@ -1,7 +1,9 @@
 // Probe: churn of VMM allocations the way the op tests use buffers (several buffers made, filled from
 // pageable host memory with hipMemcpyAsync + stream sync, read by one kernel, results read back, all
 // freed), many times; variant 0 as tts_hip_buffer_alloc did it, variant 1 with a device-wide
-// synchronize after mapping, variant 2 with a stream-ordered memset of the new range.
+// synchronize after mapping, variant 2 with a stream-ordered memset of the new range, variant 3 with
+// the kernel's result written to a VMM buffer and read back from it (as the op tests read outputs),
+// variant 4 = 3 with hipMalloc / hipFree churn of other sizes in between.
 // hipcc --offload-arch=gfx950 -O2 scripts/vmm_stress_probe.hip -o /tmp/vsp
 #include <hip/hip_runtime.h>
 
@@ -60,11 +62,15 @@ int main() {
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     double * d;
     CK(hipMalloc(&d, 8));
-    for (int variant = 0; variant < 3; ++variant) {
+    for (int variant = 0; variant < 5; ++variant) {
         int bad = 0;
         for (int it = 0; it < 300; ++it) {
             const size_t n = (size_t)(200000 + 37 * it % 100000);
+            void * junk = nullptr;
+            if (variant == 4) CK(hipMalloc(&junk, (size_t)(1 + it % 7) << 20));
             V a = vmm(n * 4), b = vmm(n * 4), c = vmm(1000 * 4 > 65536 ? 4000 : 65536);
+            V o = vmm(65536);
+            double * dd = variant >= 3 ? (double *)o.va : d;
             if (variant == 1) CK(hipDeviceSynchronize());
             if (variant == 2) {
                 CK(hipMemsetAsync(a.va, 0, n * 4, st));
@@ -78,19 +84,21 @@ int main() {
             CK(hipStreamSynchronize(st));
             CK(hipMemcpyAsync(c.va, hc.data(), 4000, hipMemcpyHostToDevice, st));
             CK(hipStreamSynchronize(st));
-            CK(hipMemsetAsync(d, 0, 8, st));
-            hipLaunchKernelGGL(k_sum3, dim3(256), dim3(256), 0, st, (const float *)a.va, (const float *)b.va, (const float *)c.va, n, d);
+            CK(hipMemsetAsync(dd, 0, 8, st));
+            hipLaunchKernelGGL(k_sum3, dim3(256), dim3(256), 0, st, (const float *)a.va, (const float *)b.va, (const float *)c.va, n, dd);
             double s = 0;
-            CK(hipMemcpyAsync(&s, d, 8, hipMemcpyDeviceToHost, st));
+            CK(hipMemcpyAsync(&s, dd, 8, hipMemcpyDeviceToHost, st));
             CK(hipStreamSynchronize(st));
             const double e = 3.5 * (double)n;
             if (s != e) {
                 if (bad < 5) printf("variant %d iter %d: sum %.1f expected %.1f\n", variant, it, s, e);
                 ++bad;
             }
+            vfree(o);
             vfree(c);
             vfree(b);
             vfree(a);
+            if (junk) CK(hipFree(junk));
         }
         printf("variant %d: %d / 300 wrong\n", variant, bad);
     }

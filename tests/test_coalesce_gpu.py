@@ -176,3 +176,35 @@ def test_parler_mini_8_runners_coalesced_bit_identical():
             assert np.array_equal(got[r], alone), f"runner {r}"
     finally:
         be.close()
+
+
+@pytest.mark.gpu
+def test_adapter_runners_from_threads_coalesce_and_match_oracle():
+    """TTS.cpp's own path: one ggml backend per server worker (the adapter, reached through the ggml
+    registry and vtables, tests/ggml_stub/adapter_harness.cpp), one one-prompt Parler runner on each,
+    decoding from its own thread with logits read back every step and the host sampler.  Their step
+    graphs coalesce inside the adapter's graph_compute, and every runner's tokens are the CPU oracle's
+    at batch 1."""
+    from test_adapter_gpu import AdapterBackend
+    n, steps = 4, 12
+    cfg = ttship.parler_config(batch=1, **TINY)
+    prompts = [prompt(r) for r in range(n)]
+    ads = [AdapterBackend(0) for _ in range(n)]
+    try:
+        before = ttship.coalesce_stats(0)
+        got = serve([a.iface() for a in ads], cfg, prompts, steps)
+        after = ttship.coalesce_stats(0)
+        for a in ads:
+            s = a.stats()
+            assert s["compute_failures"] == 0 and s["refused"] == 0, (s, a.last_refused())
+    finally:
+        for a in ads:
+            a.close()
+    assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), (before, after)
+    for r in range(n):
+        c = ttship.Parler(py_oracle.iface(8), cfg)
+        try:
+            c.prefill(prompts[r])
+            assert np.array_equal(got[r], c.generate(steps)), f"runner {r}"
+        finally:
+            c.close()
