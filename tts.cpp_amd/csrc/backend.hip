@@ -85,7 +85,81 @@ bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vm
 }
 }  // namespace tts
 
-// Physical allocation + reserved range + mapping (HIP virtual memory management); false = use hipMalloc.
+// ---- virtual address arena ----
+// Every VMM range (buffers and the coalescer's windows) is carved out of ONE reservation per device,
+// made once, and a released range is not handed out again while never-used address space is left:
+// hipMemUnmap does not promise that the device's translation caches forget the range, so a new
+// physical allocation mapped at a just-released address could be read through a stale translation
+// (scripts/vmm_stress_probe.hip / vmm_alias_probe.hip: wrong sums and wrong bytes after address
+// reuse).  1 TiB of address space is half a million 2 MiB buffers; only past that are released ranges
+// reused (first fit, neighbours merged).
+namespace {
+struct VaArena {
+    std::mutex mu;
+    char * base = nullptr;
+    size_t size = 0, next = 0;
+    bool tried = false;
+    std::map<size_t, size_t> free_;  // released ranges: offset -> length
+};
+VaArena g_va[16];
+}  // namespace
+
+namespace tts {
+char * va_alloc(int device, size_t n) {
+    if (device < 0 || device >= 16 || n == 0) return nullptr;
+    VaArena & a = g_va[device];
+    std::lock_guard<std::mutex> lk(a.mu);
+    if (!a.base && !a.tried) {
+        a.tried = true;
+        // address space only (no memory behind it): as large as the runtime grants, 1 TiB first
+        for (size_t sz : {(size_t)1 << 40, (size_t)1 << 38, (size_t)1 << 36}) {
+            void * p = nullptr;
+            if (hipMemAddressReserve(&p, sz, (size_t)2 << 20, nullptr, 0) == hipSuccess && p) {
+                a.base = (char *)p;
+                a.size = sz;
+                break;
+            }
+            (void)hipGetLastError();
+        }
+    }
+    if (!a.base) return nullptr;
+    if (a.size - a.next >= n) {
+        char * p = a.base + a.next;
+        a.next += n;
+        return p;
+    }
+    for (auto it = a.free_.begin(); it != a.free_.end(); ++it) {
+        if (it->second < n) continue;
+        const size_t off = it->first, len = it->second;
+        a.free_.erase(it);
+        if (len > n) a.free_[off + n] = len - n;
+        return a.base + off;
+    }
+    return nullptr;
+}
+void va_free(int device, char * p, size_t n) {
+    if (device < 0 || device >= 16 || !p || n == 0) return;
+    VaArena & a = g_va[device];
+    std::lock_guard<std::mutex> lk(a.mu);
+    size_t off = (size_t)(p - a.base), len = n;
+    auto next = a.free_.lower_bound(off);
+    if (next != a.free_.end() && off + len == next->first) {
+        len += next->second;
+        next = a.free_.erase(next);
+    }
+    if (next != a.free_.begin()) {
+        auto prev = std::prev(next);
+        if (prev->first + prev->second == off) {
+            prev->second += len;
+            return;
+        }
+    }
+    a.free_[off] = len;
+}
+}  // namespace tts
+
+// Physical allocation + a range of the device's address arena + mapping (HIP virtual memory
+// management); false = use hipMalloc.
 static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocationHandle_t * h, size_t * msz) {
     hipMemAllocationProp prop{};
     prop.type = hipMemAllocationTypePinned;
@@ -101,19 +175,24 @@ static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocat
         (void)hipGetLastError();
         return false;
     }
-    void * va = nullptr;
-    if (hipMemAddressReserve(&va, n, 0, nullptr, 0) != hipSuccess) {
-        (void)hipGetLastError();
+    void * va = tts::va_alloc(device, n);
+    if (!va) {
         hipMemRelease(*h);
         return false;
     }
     hipMemAccessDesc acc{};
     acc.location = prop.location;
     acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (hipMemMap(va, n, 0, *h, 0) != hipSuccess || hipMemSetAccess(va, n, &acc, 1) != hipSuccess) {
+    if (hipMemMap(va, n, 0, *h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        tts::va_free(device, (char *)va, n);
+        hipMemRelease(*h);
+        return false;
+    }
+    if (hipMemSetAccess(va, n, &acc, 1) != hipSuccess) {
         (void)hipGetLastError();
         hipMemUnmap(va, n);
-        hipMemAddressFree(va, n);
+        tts::va_free(device, (char *)va, n);
         hipMemRelease(*h);
         return false;
     }
@@ -332,8 +411,11 @@ void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
         tts::coalesce_forget(ptr, r.size);  // coalescing windows holding this buffer are unmapped first
     }
     if (known && r.vmm) {
+        // hipFree waits for the whole device; an unmap does not: a stream other than this backend's (the
+        // coalescer's, another backend reading a shared buffer) may still be reading the range
+        hipDeviceSynchronize();
         hipMemUnmap(ptr, r.map_size);
-        hipMemAddressFree(ptr, r.map_size);
+        tts::va_free(be->device, (char *)ptr, r.map_size);
         hipMemRelease(r.h);
         return;
     }

@@ -58,6 +58,7 @@ struct Window {
     std::vector<const char *> bases;  // member buffers, member order
     size_t stride = 0;
     char * va = nullptr;
+    int dev = 0;
 };
 
 constexpr int kMaxDev = 16;
@@ -244,35 +245,33 @@ void copy_options(tts_hip_backend * d, const tts_hip_backend * s) {
 char * window_for(Dev & d, const std::vector<const char *> & bases, size_t stride) {
     for (const Window & w : d.windows)
         if (w.bases == bases && w.stride == stride) return w.va;
-    void * va = nullptr;
-    const size_t total = stride * bases.size();
-    if (hipMemAddressReserve(&va, total, 0, nullptr, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    size_t k = 0;
-    bool ok = true;
-    for (; k < bases.size() && ok; ++k) {
-        void * h = nullptr;
-        size_t ms = 0;
-        ok = buffer_lookup(bases[k], nullptr, nullptr, &h, &ms) && h && ms == stride &&
-             hipMemMap((char *)va + k * stride, stride, 0, (hipMemGenericAllocationHandle_t)h, 0) == hipSuccess;
-    }
-    hipMemAccessDesc acc{};
     int dev = 0;
     hipGetDevice(&dev);
+    const size_t total = stride * bases.size();
+    char * va = va_alloc(dev, total);
+    if (!va) return nullptr;
+    size_t mapped = 0;
+    bool ok = true;
+    for (; mapped < bases.size(); ++mapped) {
+        void * h = nullptr;
+        size_t ms = 0;
+        ok = buffer_lookup(bases[mapped], nullptr, nullptr, &h, &ms) && h && ms == stride &&
+             hipMemMap(va + mapped * stride, stride, 0, (hipMemGenericAllocationHandle_t)h, 0) == hipSuccess;
+        if (!ok) break;
+    }
+    hipMemAccessDesc acc{};
     acc.location.type = hipMemLocationTypeDevice;
     acc.location.id = dev;
     acc.flags = hipMemAccessFlagsProtReadWrite;
     if (ok) ok = hipMemSetAccess(va, total, &acc, 1) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
-        for (size_t u = 0; u + 1 < k; ++u) hipMemUnmap((char *)va + u * stride, stride);
-        hipMemAddressFree(va, total);
+        for (size_t u = 0; u < mapped; ++u) hipMemUnmap(va + u * stride, stride);
+        va_free(dev, va, total);
         return nullptr;
     }
-    d.windows.push_back(Window{bases, stride, (char *)va});
-    return (char *)va;
+    d.windows.push_back(Window{bases, stride, va, dev});
+    return va;
 }
 
 __global__ void k_ne_bytes(const uint4 * __restrict__ a, const uint4 * __restrict__ b, size_t n16, const uint8_t * __restrict__ ta,
@@ -527,7 +526,7 @@ void coalesce_forget(const void * base, size_t size) {
             }
             hipDeviceSynchronize();  // a coalesced step may still read the window
             for (size_t k = 0; k < w.bases.size(); ++k) hipMemUnmap(w.va + k * w.stride, w.stride);
-            hipMemAddressFree(w.va, w.stride * w.bases.size());
+            va_free(w.dev, w.va, w.stride * w.bases.size());
             d.windows.erase(d.windows.begin() + i);
         }
     }

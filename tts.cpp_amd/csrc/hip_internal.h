@@ -584,6 +584,9 @@ constexpr int kCoalesceNotTaken = 1 << 20;
 int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
 // buffer registry hooks (backend.hip): a VMM-backed buffer's physical handle, and its release
 bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size);
+// The device's virtual-address arena (one reservation, made once): ranges for VMM buffers and windows.
+char * va_alloc(int device, size_t n);
+void va_free(int device, char * p, size_t n);
 // a coalesced step's operands read through member 0's copy (weights, norm parameters, tables): true when
 // every member's copy holds the same bytes (checked on the device, cached until a host write)
 bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::pair<const void *, size_t>> & shared);
