@@ -85,81 +85,39 @@ bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vm
 }
 }  // namespace tts
 
-// ---- virtual address arena ----
-// Every VMM range (buffers and the coalescer's windows) is carved out of ONE reservation per device,
-// made once, and a released range is not handed out again while never-used address space is left:
-// hipMemUnmap does not promise that the device's translation caches forget the range, so a new
-// physical allocation mapped at a just-released address could be read through a stale translation
-// (scripts/vmm_stress_probe.hip / vmm_alias_probe.hip: wrong sums and wrong bytes after address
-// reuse).  1 TiB of address space is half a million 2 MiB buffers; only past that are released ranges
-// reused (first fit, neighbours merged).
+// ---- virtual addresses for VMM mappings ----
+// On this stack (ROCm 7.2, gfx950) an unmap does not make the device forget the old translation: new
+// physical memory mapped at an address that was mapped before is read and written through stale
+// page translations (scripts/vmm_path_probe.hip, profiles/r05/vmm_path_probe.log: with a reservation
+// per buffer freed with it, the runtime hands the freed addresses straight back and 188-200 of 200
+// churn iterations see words of other pages -- compute kernels, SDMA copies and memsets alike; with
+// the reservations never freed, 0 of 200 on every path).  Sub-ranges of one big reservation cannot be
+// given access separately (hipMemSetAccess: invalid argument).  So every mapping gets a reservation
+// of its own that is never released: a freed buffer's physical memory goes back, its addresses stay
+// reserved and unused for the life of the process (address space only: 128 TiB of it).
 namespace {
-struct VaArena {
-    std::mutex mu;
-    char * base = nullptr;
-    size_t size = 0, next = 0;
-    bool tried = false;
-    std::map<size_t, size_t> free_;  // released ranges: offset -> length
-};
-VaArena g_va[16];
+std::atomic<size_t> g_va_retired{0};  // bytes of address space retired by freed mappings
 }  // namespace
 
 namespace tts {
 char * va_alloc(int device, size_t n) {
-    if (device < 0 || device >= 16 || n == 0) return nullptr;
-    VaArena & a = g_va[device];
-    std::lock_guard<std::mutex> lk(a.mu);
-    if (!a.base && !a.tried) {
-        a.tried = true;
-        // address space only (no memory behind it): as large as the runtime grants, 1 TiB first
-        for (size_t sz : {(size_t)1 << 40, (size_t)1 << 38, (size_t)1 << 36}) {
-            void * p = nullptr;
-            if (hipMemAddressReserve(&p, sz, (size_t)2 << 20, nullptr, 0) == hipSuccess && p) {
-                a.base = (char *)p;
-                a.size = sz;
-                break;
-            }
-            (void)hipGetLastError();
-        }
+    (void)device;
+    void * p = nullptr;
+    if (hipMemAddressReserve(&p, n, 0, nullptr, 0) != hipSuccess || !p) {
+        (void)hipGetLastError();
+        return nullptr;
     }
-    if (!a.base) return nullptr;
-    if (a.size - a.next >= n) {
-        char * p = a.base + a.next;
-        a.next += n;
-        return p;
-    }
-    for (auto it = a.free_.begin(); it != a.free_.end(); ++it) {
-        if (it->second < n) continue;
-        const size_t off = it->first, len = it->second;
-        a.free_.erase(it);
-        if (len > n) a.free_[off + n] = len - n;
-        return a.base + off;
-    }
-    return nullptr;
+    return (char *)p;
 }
 void va_free(int device, char * p, size_t n) {
-    if (device < 0 || device >= 16 || !p || n == 0) return;
-    VaArena & a = g_va[device];
-    std::lock_guard<std::mutex> lk(a.mu);
-    size_t off = (size_t)(p - a.base), len = n;
-    auto next = a.free_.lower_bound(off);
-    if (next != a.free_.end() && off + len == next->first) {
-        len += next->second;
-        next = a.free_.erase(next);
-    }
-    if (next != a.free_.begin()) {
-        auto prev = std::prev(next);
-        if (prev->first + prev->second == off) {
-            prev->second += len;
-            return;
-        }
-    }
-    a.free_[off] = len;
+    (void)device;
+    (void)p;
+    g_va_retired.fetch_add(n, std::memory_order_relaxed);  // never handed back: see above
 }
 }  // namespace tts
 
-// Physical allocation + a range of the device's address arena + mapping (HIP virtual memory
-// management); false = use hipMalloc.
+// Physical allocation + a fresh reservation + mapping (HIP virtual memory management); false = use
+// hipMalloc.
 static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocationHandle_t * h, size_t * msz) {
     hipMemAllocationProp prop{};
     prop.type = hipMemAllocationTypePinned;

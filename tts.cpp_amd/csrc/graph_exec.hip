@@ -2691,6 +2691,8 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
         // The Q8_K activation cache is keyed by address and the graph reuses freed memory, so it
         // survives only launches that cannot have written over the cached source: an LN that
         // just produced it, or GEMVs whose outputs do not overlap it.
+        // (a coalesced step keys the cache by window addresses, the items below by member 0's: no reuse)
+        if (be->bat) be->aq.src = nullptr;
         if (be->aq.src) {
             const char * s0 = (const char *)be->aq.src;
             const char * s1 = s0 + (size_t)be->aq.K * (size_t)be->aq.M * 4;

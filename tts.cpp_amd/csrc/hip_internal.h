@@ -584,7 +584,8 @@ constexpr int kCoalesceNotTaken = 1 << 20;
 int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
 // buffer registry hooks (backend.hip): a VMM-backed buffer's physical handle, and its release
 bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size);
-// The device's virtual-address arena (one reservation, made once): ranges for VMM buffers and windows.
+// Address ranges for VMM mappings (buffers and windows): a fresh reservation each, retired (never
+// reused) when the mapping goes away (backend.hip).
 char * va_alloc(int device, size_t n);
 void va_free(int device, char * p, size_t n);
 // a coalesced step's operands read through member 0's copy (weights, norm parameters, tables): true when
