@@ -227,6 +227,26 @@ def cpu_baseline(args, n_threads, B):
             "codec_tokens_per_s": B * steps * HEADS / dt_ar}
 
 
+F64_MFMA_PEAK_TF = 47.0  # measured v_mfma_f64_16x16x4f64 rate on the box (scripts/mfma_f64_peak.hip)
+
+
+def dac_flops_per_frame(dcfg):
+    """Algorithmic FLOPs of the DAC-44k decoder per codec frame (2 x multiply-adds of the reference's
+    convs, general_neural_audio_codec.cpp:133-172 / dac_model.cpp:139-170): the quantizer out-projections,
+    the initial k7 conv, per layer the conv_transpose_1d (kernel 2 x rate, stride rate: 2 x Cin x Cout per
+    output sample) and three residual units (k7 + k1 convs), the final k7 conv to one channel."""
+    rates = list(dcfg.rates)[:dcfg.n_layers]
+    macs = dcfg.n_codebooks * dcfg.codebook_dim * dcfg.latent_dim + 7 * dcfg.latent_dim * dcfg.decoder_dim
+    c, s = dcfg.decoder_dim, 1
+    for r in rates:
+        co = c // 2
+        s *= r
+        macs += 2 * c * co * s + 3 * (7 + 1) * co * co * s
+        c = co
+    macs += 7 * c * s
+    return 2 * macs
+
+
 def gemv_roofline(be, runner, steps):
     """Dominant kernels of the decode step, from HIP events carried in their dispatch packets over
     profiled steps: the Q4_K dequant-GEMV / matrix-core GEMM launches (algorithmic bytes per launch =
@@ -888,6 +908,16 @@ def main():
         ts = max_over_ranks(dist, local, dres["wall_s"])
         dres["audio_sec_per_s"] = round(world * dres["audio_sec_per_gpu"] / ts, 3)
 
+    dac_roof = None
+    if dac is not None:
+        # the DAC leg as a whole (all its kernels, W concurrent decoders) against the f64 matrix-core peak:
+        # the fused convs carry ~all of its FLOPs (f16 inputs, f64 accumulation on v_mfma_f64_16x16x4f64)
+        fl = dac_flops_per_frame(dcfg) * per_gpu * args.steps
+        tf = fl / dt_dac / 1e12
+        dac_roof = {"bound": "mfma", "achieved": round(tf, 3), "peak": F64_MFMA_PEAK_TF, "unit": "TFLOP/s", "frac": round(tf / F64_MFMA_PEAK_TF, 4),
+                    "flops_per_frame": dac_flops_per_frame(dcfg), "frames": per_gpu * args.steps,
+                    "note": "algorithmic conv FLOPs of the frames decoded (gaps of batched decodes not counted) / DAC wall time per GPU; "
+                            "peak = the measured f64 MFMA rate (scripts/mfma_f64_peak.hip)"}
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -932,6 +962,7 @@ def main():
             "orpheus": ores,
             "dia": dres,
             "roofline": roof,
+            "roofline_dac": dac_roof,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
