@@ -40,11 +40,19 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
+// A buffer a graph touches, in order of first appearance (signature): graphs with equal signatures
+// touch their buffers at equal offsets, buffer j of one graph standing for buffer j of the other.
+struct BufSlot {
+    const char * base = nullptr;
+    size_t size = 0, map_size = 0;
+    bool vmm = false;
+};
 struct Req {
     tts_hip_backend * be = nullptr;
     tts_tensor * const * nodes = nullptr;
     int n = 0;
     uint64_t sig = 0;
+    std::vector<BufSlot> bufs;
     int64_t count = 0;  // the backend's coalescable submissions so far (its decode step number)
     bool taken = false, done = false;
     int status = kCoalesceNotTaken;
@@ -86,8 +94,20 @@ struct EqRec {
     size_t n;
     bool eq;  // false: known to differ (not re-checked until a write)
 };
+struct EqKey {
+    const char *a, *b;
+    size_t n;
+    bool operator==(const EqKey & o) const { return a == o.a && b == o.b && n == o.n; }
+};
+struct EqKeyHash {
+    size_t operator()(const EqKey & k) const {
+        return std::hash<const void *>()(k.a) ^ (std::hash<const void *>()(k.b) * 0x9E3779B97F4A7C15ull) ^ (k.n * 0xC2B2AE3D27D4EB4Full);
+    }
+};
 std::mutex g_eq_mu;
-std::vector<EqRec> g_eq;
+std::unordered_map<EqKey, EqRec, EqKeyHash> g_eq;
+uint64_t g_eq_epoch = 1;                            // bumped whenever a write drops records
+std::unordered_map<uint64_t, uint64_t> g_eq_group;  // group key -> epoch its shared operands were all found equal
 std::map<const char *, const char *> g_eq_cover;  // disjoint union of every checked range: start -> end
 
 void cover_add(const char * a, size_t n) {
@@ -114,9 +134,8 @@ bool cover_hits(const char * p, size_t n) {
     return it->second > p;
 }
 const EqRec * eq_known(const char * a, const char * b, size_t n) {
-    for (const EqRec & r : g_eq)
-        if (r.a == a && r.b == b && r.n == n) return &r;
-    return nullptr;
+    auto it = g_eq.find(EqKey{a, b, n});
+    return it == g_eq.end() ? nullptr : &it->second;
 }
 
 // ---- rendezvous ----
@@ -135,83 +154,72 @@ bool decode_like(tts_tensor * const * nodes, int n) {
     return any;
 }
 
-// Structure of a graph: ops, types, shapes, strides, parameters and the node each source is (leaves
-// by shape); equal signatures -> the planner builds the same items from either graph.
-uint64_t signature(tts_tensor * const * nodes, int n) {
+// Structure AND placement of a graph: ops, types, shapes, strides, parameters, layout flags, the node
+// each source is (leaves and views by description), and where every tensor lies -- (buffer j, offset)
+// with buffer j the j-th distinct buffer met, described by its size / mapping size / kind.  Two graphs
+// with equal signatures are the same step over buffers that correspond slot by slot (bufs): what
+// pairing member k's tensors with member 0's needs, computed by each runner's own thread.  Two
+// independent 64-bit hashes, folded.
+uint64_t signature(tts_tensor * const * nodes, int n, std::vector<BufSlot> & bufs) {
     std::unordered_map<const tts_tensor *, int> idx;
     idx.reserve((size_t)n * 2);
     for (int i = 0; i < n; ++i) idx[nodes[i]] = i;
-    uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)n;
-    auto mix = [&](uint64_t v) { h = (h ^ v) * 0x100000001B3ull; };
+    bufs.clear();
+    uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)n, h2 = 0x84222325CBF29CE4ull + (uint64_t)n;
+    auto mix = [&](uint64_t v) {
+        h = (h ^ v) * 0x100000001B3ull;
+        h2 = (h2 + v + 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+        h2 ^= h2 >> 31;
+    };
+    auto loc = [&](const void * p) {
+        if (!p) {
+            mix(0xD0);
+            return;
+        }
+        const char * c = (const char *)p;
+        for (size_t j = 0; j < bufs.size(); ++j)
+            if (c >= bufs[j].base && c < bufs[j].base + bufs[j].size) {
+                mix(0xB0 + j), mix((uint64_t)(c - bufs[j].base));
+                return;
+            }
+        BufSlot sl;
+        void * hd = nullptr;
+        if (!buffer_lookup(p, &sl.base, &sl.size, &hd, &sl.map_size)) {
+            mix(0xE1), mix((uint64_t)(uintptr_t)p);  // not a backend buffer: the very same address in every member
+            return;
+        }
+        sl.vmm = hd != nullptr;
+        bufs.push_back(sl);
+        mix(0xB0 + bufs.size() - 1), mix(sl.size), mix(sl.map_size), mix(sl.vmm), mix((uint64_t)(c - sl.base));
+    };
+    constexpr int kLayout = TTS_FLAG_INPUT | TTS_FLAG_OUTPUT | TTS_FLAG_REPACKED | TTS_FLAG_TILED | TTS_FLAG_TILED_COPY;
     auto tensor = [&](const tts_tensor * t) {
         mix((uint64_t)t->op << 32 | (uint32_t)t->type);
         for (int d = 0; d < 4; ++d) mix((uint64_t)t->ne[d]), mix((uint64_t)t->nb[d]);
         for (int k = 0; k < TTS_MAX_OP_PARAMS; ++k) mix((uint32_t)t->op_params[k]);
-        mix((uint64_t)(t->flags & (TTS_FLAG_INPUT | TTS_FLAG_OUTPUT)));
+        mix((uint64_t)(t->flags & kLayout));
+        loc(t->data);
+    };
+    auto ref = [&](const tts_tensor * x, int depth, auto & self) -> void {  // a source / view source
+        if (!x) {
+            mix(0x51);
+            return;
+        }
+        auto it = idx.find(x);
+        if (it != idx.end()) {
+            mix(0x1000000ull + it->second);
+            return;
+        }
+        tensor(x);
+        if (depth < 4) self(x->view_src, depth + 1, self);
     };
     for (int i = 0; i < n; ++i) {
         tensor(nodes[i]);
-        for (int s = 0; s < TTS_MAX_SRC; ++s) {
-            const tts_tensor * x = nodes[i]->src[s];
-            if (!x) {
-                mix(0x51);
-                continue;
-            }
-            auto it = idx.find(x);
-            if (it != idx.end()) mix(0x1000000ull + it->second);
-            else tensor(x);
-        }
+        ref(nodes[i]->view_src, 0, ref);
+        for (int s = 0; s < TTS_MAX_SRC; ++s) ref(nodes[i]->src[s], 0, ref);
     }
-    return h | 1;
+    return (h ^ (h2 * 0x94D049BB133111EBull)) | 1;
 }
-
-// ---- group validation: member 0's tensors against member k's ----
-struct Pairing {
-    std::unordered_map<const tts_tensor *, const tts_tensor *> seen;
-    std::map<const char *, const char *> buf;  // member 0 buffer base -> member k buffer base
-    bool ok = true;
-    void walk(const tts_tensor * a, const tts_tensor * b) {
-        if (!ok || !a || !b) {
-            if (!a != !b) ok = false;
-            return;
-        }
-        auto it = seen.find(a);
-        if (it != seen.end()) {
-            if (it->second != b) ok = false;
-            return;
-        }
-        seen[a] = b;
-        if (a->type != b->type || a->op != b->op || (a->flags ^ b->flags) & (TTS_FLAG_REPACKED | TTS_FLAG_TILED | TTS_FLAG_TILED_COPY)) {
-            ok = false;
-            return;
-        }
-        for (int d = 0; d < 4; ++d)
-            if (a->ne[d] != b->ne[d] || a->nb[d] != b->nb[d]) ok = false;
-        if (!ok) return;
-        if (a->data != b->data && a->data && b->data) {
-            const char *ba, *bb;
-            size_t sa, sb;
-            void *ha, *hb;
-            size_t ma, mb;
-            if (!buffer_lookup(a->data, &ba, &sa, &ha, &ma) || !buffer_lookup(b->data, &bb, &sb, &hb, &mb) || !ha || !hb || ma != mb ||
-                (const char *)a->data - ba != (const char *)b->data - bb) {
-                ok = false;
-                return;
-            }
-            auto bi = buf.find(ba);
-            if (bi == buf.end()) buf[ba] = bb;
-            else if (bi->second != bb) {
-                ok = false;
-                return;
-            }
-        } else if (!a->data != !b->data) {
-            ok = false;
-            return;
-        }
-        for (int s = 0; s < TTS_MAX_SRC; ++s) walk(a->src[s], b->src[s]);
-        walk(a->view_src, b->view_src);
-    }
-};
 
 void copy_options(tts_hip_backend * d, const tts_hip_backend * s) {
     d->fusion = s->fusion;
@@ -291,6 +299,9 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
     std::vector<EqRec> todo;
     {
         std::lock_guard<std::mutex> lk(g_eq_mu);
+        // the same group as a step before, with no write into a checked range since: every pair still holds
+        auto gk = g_eq_group.find(bc.key);
+        if (gk != g_eq_group.end() && gk->second == g_eq_epoch) return true;
         for (const auto & s : shared) {
             if (!bc.stride(s.first)) continue;  // the same memory for every member
             for (int k = 1; k < bc.N; ++k) {
@@ -302,7 +313,11 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
             }
         }
     }
-    if (todo.empty()) return true;
+    if (todo.empty()) {
+        std::lock_guard<std::mutex> lk(g_eq_mu);
+        g_eq_group[bc.key] = g_eq_epoch;
+        return true;
+    }
     if (d.d_flags_n < (int)todo.size()) {
         if (d.d_flags) hipFree(d.d_flags);
         d.d_flags_n = std::max((int)todo.size(), 1024);
@@ -326,10 +341,11 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
     for (size_t i = 0; i < todo.size(); ++i) {
         todo[i].eq = flags[i] == 0;
         all &= todo[i].eq;
-        g_eq.push_back(todo[i]);
+        g_eq[EqKey{todo[i].a, todo[i].b, todo[i].n}] = todo[i];
         cover_add(todo[i].a, todo[i].n);
         cover_add(todo[i].b, todo[i].n);
     }
+    if (all) g_eq_group[bc.key] = g_eq_epoch;
     return all;
 }
 
@@ -337,51 +353,45 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
 void run_group(Dev & d, std::vector<Req *> & g) {
     std::lock_guard<std::mutex> xl(d.exec_mu);
     Req * r0 = g[0];
-    // pair every member's graph with member 0's
+    // equal signatures: member k's buffer slot j stands for member 0's slot j (same sizes, same offsets)
     std::vector<Req *> mem{r0};
-    std::vector<std::map<const char *, const char *>> maps;
-    for (size_t k = 1; k < g.size(); ++k) {
-        Pairing p;
-        if (g[k]->n != r0->n) continue;
-        for (int i = 0; i < r0->n && p.ok; ++i) p.walk(r0->nodes[i], g[k]->nodes[i]);
-        if (!p.ok) continue;
-        mem.push_back(g[k]);
-        maps.push_back(std::move(p.buf));
-    }
+    for (size_t k = 1; k < g.size(); ++k)
+        if (g[k]->n == r0->n && g[k]->bufs.size() == r0->bufs.size()) mem.push_back(g[k]);
     if (mem.size() < 2) {
         d.refused++;
         return;  // statuses stay kCoalesceNotTaken: every member runs its own graph
     }
-    // classes: member 0's buffers the graph touches, with each member's counterpart
-    std::map<const char *, std::vector<const char *>> cls;
-    for (size_t k = 0; k < maps.size(); ++k)
-        for (const auto & kv : maps[k]) {
-            auto & v = cls[kv.first];
-            if (v.empty()) v.assign(mem.size(), nullptr), v[0] = kv.first;
-            v[k + 1] = kv.second;
-        }
     BatchCtx bc;
     bc.N = (int)mem.size();
-    for (auto & kv : cls) {
-        bool full = true;
-        for (const char * b : kv.second) full &= b != nullptr;
-        size_t size = 0, ms = 0;
-        void * h = nullptr;
-        if (!full || !buffer_lookup(kv.first, nullptr, &size, &h, &ms)) {
+    bc.key = r0->sig;
+    for (Req * m : mem)
+        for (const BufSlot & sl : m->bufs) bc.key = (bc.key ^ (uint64_t)(uintptr_t)sl.base) * 0x100000001B3ull;
+    for (size_t j = 0; j < r0->bufs.size(); ++j) {
+        const BufSlot & s0 = r0->bufs[j];
+        std::vector<const char *> mb(mem.size());
+        bool same = true, vmm = s0.vmm;
+        for (size_t k = 0; k < mem.size(); ++k) {
+            const BufSlot & sk = mem[k]->bufs[j];
+            mb[k] = sk.base;
+            same &= sk.base == s0.base;
+            vmm &= sk.vmm && sk.map_size == s0.map_size && sk.size == s0.size;
+        }
+        if (same) continue;  // one buffer read by every member (stride 0)
+        if (!vmm) {
             d.refused++;
             return;
         }
-        char * w = window_for(d, kv.second, ms);
+        char * w = window_for(d, mb, s0.map_size);
         if (!w) {
             d.refused++;
             return;
         }
         BatchCls c;
-        c.b0 = kv.first;
-        c.size = size;
+        c.b0 = s0.base;
+        c.size = s0.size;
         c.win = w;
-        c.stride = (int64_t)ms;
-        c.mb = kv.second;
+        c.stride = (int64_t)s0.map_size;
+        c.mb = std::move(mb);
         bc.cls.push_back(std::move(c));
     }
     std::sort(bc.cls.begin(), bc.cls.end(), [](const BatchCls & a, const BatchCls & b) { return a.b0 < b.b0; });
@@ -437,7 +447,7 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
     r.be = be;
     r.nodes = nodes;
     r.n = n;
-    r.sig = signature(nodes, n);  // outside the lock: ~700 nodes
+    r.sig = signature(nodes, n, r.bufs);  // outside the lock, in the caller's thread: ~700 nodes
     std::unique_lock<std::mutex> lk(d.mu);
     Act & me = d.seen[be];
     me.t = t0;
@@ -539,9 +549,13 @@ void coalesce_written(const void * p, size_t size) {
     if (g_eq.empty() || !cover_hits((const char *)p, size)) return;
     const char * a = (const char *)p;
     auto hits = [&](const char * x, size_t n) { return x < a + size && a < x + n; };
-    g_eq.erase(std::remove_if(g_eq.begin(), g_eq.end(), [&](const EqRec & r) { return hits(r.a, r.n) || hits(r.b, r.n); }), g_eq.end());
+    for (auto it = g_eq.begin(); it != g_eq.end();) {
+        if (hits(it->second.a, it->second.n) || hits(it->second.b, it->second.n)) it = g_eq.erase(it);
+        else ++it;
+    }
+    g_eq_epoch++;
     g_eq_cover.clear();
-    for (const EqRec & r : g_eq) cover_add(r.a, r.n), cover_add(r.b, r.n);
+    for (const auto & kv : g_eq) cover_add(kv.second.a, kv.second.n), cover_add(kv.second.b, kv.second.n);
 }
 
 }  // namespace tts

@@ -282,6 +282,7 @@ struct BatchCls {
 };
 struct BatchCtx {
     int N = 0;
+    uint64_t key = 0;  // the group: its graph signature and every member's buffers (coalesce.hip caches per key)
     std::vector<BatchCls> cls;  // sorted by b0
     const BatchCls * find(const void * p) const {
         const char * c = (const char *)p;
