@@ -240,6 +240,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     hipFree(be->gelu_table);
     if (be->sample_cand) hipFree(be->sample_cand);
     if (be->repack_tmp) hipFree(be->repack_tmp);
+    for (char * r : be->repack_retired) hipFree(r);
     for (auto & ex : be->gsig_exec)
         if (ex) hipGraphExecDestroy(ex);
     for (auto & ex : be->pexec)

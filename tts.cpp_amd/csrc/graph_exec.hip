@@ -1985,10 +1985,10 @@ static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a, bool 
     // Q4_K matrix written with plain tensor_set (native ggml layout): repack into a temp
     const size_t bytes = (size_t)a->nb[1] * (size_t)a->ne[1];
     if (be->repack_tmp_size < bytes) {
-        if (be->repack_tmp) {
-            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
-            TTS_HIP_CHECK(hipFree(be->repack_tmp));
-        }
+        // a bigger temp; the old one is retired, not freed: a recorded step graph (gsig_exec / pexec)
+        // may still repack into it on replay, and this may run under stream capture, where neither a
+        // stream synchronize nor hipFree (device-synchronizing) is allowed
+        if (be->repack_tmp) be->repack_retired.push_back(be->repack_tmp);
         TTS_HIP_CHECK(hipMalloc((void **)&be->repack_tmp, bytes));
         be->repack_tmp_size = bytes;
     }

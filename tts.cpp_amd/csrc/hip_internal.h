@@ -422,6 +422,7 @@ struct tts_hip_backend {
     std::vector<hipEvent_t> ev_free;
     char * repack_tmp = nullptr;  // device temp for Q4_K matrices not stored repacked
     size_t repack_tmp_size = 0;
+    std::vector<char *> repack_retired;  // outgrown repack temps (freed with the backend)
     // HIP graph replay of graph_compute (capture -> exec update -> one launch)
     bool use_graphs = false;
     // repeat detection for tts_hip_graph_compute: signatures of the last few graphs (node count, op
