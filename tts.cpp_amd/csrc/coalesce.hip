@@ -30,6 +30,7 @@
 #include <condition_variable>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 
@@ -60,6 +61,7 @@ struct Req {
 struct Act {
     Clock::time_point t;
     int64_t count = 0;
+    std::thread::id tid;  // the thread of its last submission
 };
 
 struct Window {
@@ -451,6 +453,7 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
     std::unique_lock<std::mutex> lk(d.mu);
     Act & me = d.seen[be];
     me.t = t0;
+    me.tid = std::this_thread::get_id();
     r.count = ++me.count;
     d.pending.push_back(&r);
     d.cv.notify_all();
@@ -473,9 +476,23 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
         }
         const auto now = Clock::now();
         int active = 0;
+        const std::thread::id tid = std::this_thread::get_id();
         for (auto it = d.seen.begin(); it != d.seen.end();) {
-            if (now - it->second.t > window && it->first != be) it = d.seen.erase(it);
-            else ++active, ++it;
+            if (now - it->second.t > window && it->first != be) {
+                it = d.seen.erase(it);
+                continue;
+            }
+            // a backend last driven from this very thread cannot submit while this thread waits here (one
+            // thread stepping several runners in turn): not waited for
+            bool here = it->first == be;
+            if (!here && it->second.tid == tid) {
+                for (Req * q : d.pending) here |= q->be == it->first && !q->taken;
+                if (!here) {
+                    ++it;
+                    continue;
+                }
+            }
+            ++active, ++it;
         }
         std::vector<Req *> open;
         for (Req * q : d.pending)
