@@ -453,6 +453,7 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
     coalesce=True: the backend's step coalescer (coalesce.hip) runs the runners' equal steps as batched
     launches; False: every runner alone (TTS_HIP_OPT_COALESCE = 0)."""
     R, steps = R or args.b1_replicas, args.b1_steps
+    prev_co = ttship.coalesce_enable(coalesce)  # (opt-in, process-wide: the runners' buffers are allocated below)
     # the same KV capacity rule as the lock-step leg: a multiple of 4 positions keeps every V row
     # 16-B aligned, so P.V takes its vector-load kernel (k_attn_pv<true, ...>)
     cfg = ttship.parler_config(batch=1, max_ctx=max(4096, args.ctx + steps + args.warmup + 64))
@@ -494,6 +495,7 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
                 p.close()
         for b in bes:
             b.close()
+        ttship.coalesce_enable(prev_co)
 
 
 def kokoro_prompt(g, vocab):

@@ -327,9 +327,9 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMM_KR_NW = 34, /* waves per 16-row tile of the many-column (> 8) K-relay Q4_K GEMM: 4 (default) or 8 (K >= 2048) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
-    TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): this backend's graph_compute of a one-prompt decode step may join the same step
-                                     of other backends on the device as one coalesced launch (tts_hip_coalesce_stats);
-                                     0 = never.  TTS_HIP_COALESCE=0 in the environment turns the coalescer off process-wide */
+    TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
+                                     backend's graph_compute of a one-prompt decode step may join the same step of other
+                                     backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */
 };
 enum tts_fuse_bits {
     TTS_FUSE_LN = 1, TTS_FUSE_GROUP = 2, TTS_FUSE_KV = 4, TTS_FUSE_EPI = 8, TTS_FUSE_HEADS = 16, TTS_FUSE_ATTN = 32,
@@ -349,8 +349,13 @@ int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
  * carried, [2] steps a member ran alone after waiting, [3] groups refused (no coalesced form / mismatched
  * members), [4] the largest group, [5] host microseconds spent waiting for members.  Returns the number written. */
 int tts_hip_coalesce_stats(int device, int64_t * out, int n);
-/* Coalescer rendezvous window (microseconds a step waits for the other active members; default 2000). */
+/* Coalescer rendezvous window (microseconds a step waits for the other active members; default 5000). */
 void tts_hip_coalesce_set_wait(int us);
+/* The step coalescer, process-wide: on = buffers allocated from now on are VMM-mapped (so members' buffers can
+ * be windowed) and one-prompt decode steps of several backends rendezvous.  Off by default; the
+ * environment variable TTS_HIP_COALESCE=1 turns it on at load.  Buffers keep the kind they were allocated with.
+ * Returns the previous setting. */
+int tts_hip_coalesce_enable(int on);
 /* Test hooks (process-wide, off by default; never read from the environment):
  * TTS_HIP_HOOK_FAULT_WEIGHT_SET = 1: tts_hip_weight_set of a Q4_K tensor fails (the callers' fallback paths). */
 #define TTS_HIP_HOOK_FAULT_WEIGHT_SET 1

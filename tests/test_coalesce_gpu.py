@@ -15,6 +15,15 @@ import pytest
 import py_oracle
 import ttship
 
+@pytest.fixture(autouse=True)
+def coalescer_on():
+    """The coalescer is opt-in (tts_hip_coalesce_enable / TTS_HIP_COALESCE=1): on for these tests, and
+    for the buffers they allocate, then back to what it was."""
+    prev = ttship.coalesce_enable(True)
+    yield
+    ttship.coalesce_enable(prev)
+
+
 TINY = dict(n_layers=2, hidden_size=256, n_attn_heads=4, ffn_size=1024, output_vocab=1088, max_ctx=128, prompt_vocab=512,
             max_positions=160)
 

@@ -64,13 +64,12 @@ const uint8_t * tiled_copy_find(const void * w) {
     auto it = g_tiled.find(w);
     return it == g_tiled.end() ? nullptr : it->second;
 }
-bool coalesce_enabled() {
-    static const bool on = [] {
-        const char * e = getenv("TTS_HIP_COALESCE");
-        return !(e && e[0] == '0');
-    }();
-    return on;
-}
+// process-wide coalescer switch (tts_hip_coalesce_enable; TTS_HIP_COALESCE=1 at load)
+static std::atomic<int> g_coalesce_on{[] {
+    const char * e = getenv("TTS_HIP_COALESCE");
+    return e && e[0] == '1' ? 1 : 0;
+}()};
+bool coalesce_enabled() { return g_coalesce_on.load(std::memory_order_relaxed) != 0; }
 bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size) {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_buffers.upper_bound((const char *)p);
@@ -160,6 +159,8 @@ static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocat
 }
 
 extern "C" {
+
+int tts_hip_coalesce_enable(int on) { return tts::g_coalesce_on.exchange(on ? 1 : 0); }
 
 int tts_hip_device_count(void) {
     int n = 0;

@@ -327,6 +327,7 @@ def lib():
         "tts_hip_counters": (ctypes.c_int, [vp, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_coalesce_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(i64), ctypes.c_int]),
         "tts_hip_coalesce_set_wait": (None, [ctypes.c_int]),
+        "tts_hip_coalesce_enable": (ctypes.c_int, [ctypes.c_int]),
         "tts_hip_test_hook": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
         "tts_hip_install_crash_handler": (ctypes.c_int, []),
         "tts_parler_n_weights": (i32, [vp]),
@@ -640,6 +641,12 @@ def coalesce_stats(device=0):
 
 def coalesce_set_wait(us):
     lib().tts_hip_coalesce_set_wait(int(us))
+
+
+def coalesce_enable(on=True):
+    """The step coalescer, process-wide (tts_hip_coalesce_enable): buffers allocated from now on are
+    VMM-mapped and one-prompt decode steps rendezvous.  Returns the previous setting."""
+    return bool(lib().tts_hip_coalesce_enable(1 if on else 0))
 
 
 def dia_config(**kw):
