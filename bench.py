@@ -646,6 +646,8 @@ def main():
                     "TTS.cpp's server workers run (0 = skip)")
     ap.add_argument("--b1-steps", type=int, default=100)
     ap.add_argument("--b1-wide", type=int, default=32, help="the B=1 leg again with this many coalesced runners (0 = skip)")
+    ap.add_argument("--b1-coalesce", type=int, default=0, help="1: also run the B=1 legs with the opt-in step coalescer "
+                    "(tts_hip_coalesce_enable; not validated on hardware this round, so off by default)")
     ap.add_argument("--sampled-steps", type=int, default=20, help="the headline's AR decode again with seeded top-k 50 sampling "
                     "(the reference's default sampler) for this many steps (0 = skip)")
     ap.add_argument("--prompt-pass", type=int, default=1, help="time every prompt's own sentence prompt pass from position 0 (0 = skip)")
@@ -869,9 +871,11 @@ def main():
         # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer, the same runners each
         # alone, and b1_wide coalesced runners (the headline's prompt count per GPU)
         b1 = {}
-        legs = [("coalesced", args.b1_replicas, True), ("alone", args.b1_replicas, False)]
-        if args.b1_wide > 0:
-            legs.append(("coalesced_wide", args.b1_wide, True))
+        legs = [("alone", args.b1_replicas, False)]
+        if args.b1_coalesce:
+            legs.insert(0, ("coalesced", args.b1_replicas, True))
+            if args.b1_wide > 0:
+                legs.append(("coalesced_wide", args.b1_wide, True))
         for name, n_run, co in legs:
             barrier_sync(dist, None)
             leg = parler_b1_leg(args, rank, local, new_backend, R=n_run, coalesce=co)
