@@ -247,6 +247,26 @@ def dac_flops_per_frame(dcfg):
     return 2 * macs
 
 
+def copy_peak(be, nbytes=1 << 30, reps=10):
+    """The measured HBM ceiling beside the 8 TB/s spec: device-to-device copies of
+    `nbytes` on the backend's stream (tts_hip_tensor_copy), read + write bytes per second over `reps`
+    copies after one warm copy."""
+    L = ttship.lib()
+    a, b = be.alloc(nbytes), be.alloc(nbytes)
+    try:
+        L.tts_hip_tensor_copy(be.ptr, b, a, nbytes)
+        be.sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            L.tts_hip_tensor_copy(be.ptr, b, a, nbytes)
+        be.sync()
+        dt = time.perf_counter() - t0
+    finally:
+        be.free(a)
+        be.free(b)
+    return round(2.0 * nbytes * reps / dt / 1e9, 1)
+
+
 def gemv_roofline(be, runner, steps):
     """Dominant kernels of the decode step, from HIP events carried in their dispatch packets over
     profiled steps: the Q4_K dequant-GEMV / matrix-core GEMM launches (algorithmic bytes per launch =
@@ -796,6 +816,7 @@ def main():
     total_prompts = per_gpu * world
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
     roof = gemv_roofline(be, runner, max(5, min(40, args.steps // 5)))
+    roof["measured_copy_peak_gbs"] = copy_peak(be)  # D2D copy rate of this GPU (read + write), beside the spec peak
     graph_nodes = runner.last_graph_nodes()
     dac_nodes = dac.last_graph_nodes() if dac is not None else None
     for xb, rd in dac_workers[R:]:
