@@ -1219,7 +1219,8 @@ struct Planner {
         auto untouched_since = [&](const tts_tensor * t, int from) {
             for (int k = from + 1; k < i; ++k) {
                 const tts_tensor * nk = nodes[k];
-                if (act[k] < 0 || is_view(nk->op) || nk == M1 || nk == S || nk == Q || nk == M2 || (rfuse && nk == R)) continue;
+                // (a node folded into another item, act -1, is still written when that item runs: checked too)
+                if (is_view(nk->op) || nk == M1 || nk == S || nk == Q || nk == M2 || (rfuse && nk == R)) continue;
                 if (overlap(nk, t)) return false;
             }
             return true;
