@@ -1361,7 +1361,8 @@ struct Planner {
         std::vector<bool> is_abs(n, false);
         for (int k : absorbed) is_abs[k] = true;
         for (int k = i + 1; k < last; ++k) {  // nodes that still run between the NORM and the item
-            if (is_abs[k] || is_view(nodes[k]->op) || act[k] < 0) continue;
+            // (a node folded into another item, act -1, is still written when that item runs: checked too)
+            if (is_abs[k] || is_view(nodes[k]->op)) continue;
             const tts_tensor * w = nodes[k];
             for (const tts_tensor * t : {X, gamma, beta, alpha, recip, one, gW, gB, bW, bB, gS})
                 if (t && t != w && overlap(w, t)) {
@@ -1891,7 +1892,7 @@ struct Planner {
             for (const auto & f : folded) {
                 if (f.second < 0) continue;
                 for (int j = f.second + 1; j < io; ++j) {
-                    if (act[j] < 0 || is_view(nodes[j]->op)) continue;
+                    if (is_view(nodes[j]->op)) continue;  // (nodes folded into other items are written when those run)
                     bool own = false;
                     for (int m : mine) own |= m == j;
                     if (!own && overlap(nodes[j], f.first)) return;
