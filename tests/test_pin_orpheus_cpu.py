@@ -67,3 +67,31 @@ def test_orpheus_graph_matches_llama(n_prompt, steps):
     err = np.abs(got - ref).max()
     assert err <= 1e-4 * scale, (err, scale)
     assert np.array_equal(got.argmax(-1), ref.argmax(-1))
+
+
+def test_orpheus_lockstep_batch_matches_llama_per_prompt():
+    """The lock-step batch (configs[4] decodes 8 prompts per GPU this way): each prompt's last prompt-pass
+    logits and decode-step logits are LlamaForCausalLM's on that prompt alone."""
+    B, n_prompt, steps = 3, 7, 3
+    cfg = ttship.orpheus_config(**dict(CFG, batch=B))
+    o = ttship.Orpheus(py_oracle.iface(4), cfg)
+    try:
+        w = o.weights()
+        rng = np.random.default_rng(123)
+        prompts = rng.integers(0, cfg.vocab_size, (B, n_prompt)).astype(np.int32)
+        toks = rng.integers(0, cfg.vocab_size, (steps, B)).astype(np.int32)
+        got = [o.prefill(prompts).reshape(B, -1)]
+        for t in toks:
+            got.append(o.decode(t).reshape(B, -1))
+        got = np.stack(got, axis=1)  # [B, 1 + steps, vocab]
+    finally:
+        o.close()
+    m = llama_from_runner(w, cfg)
+    for b in range(B):
+        ids = torch.from_numpy(np.concatenate([prompts[b], toks[:, b]]).astype(np.int64))[None]
+        with torch.no_grad():
+            ref = m(input_ids=ids).logits[0, n_prompt - 1:].numpy()
+        scale = np.abs(ref).max()
+        err = np.abs(got[b] - ref).max()
+        assert err <= 1e-4 * scale, (b, err, scale)
+        assert np.array_equal(got[b].argmax(-1), ref.argmax(-1)), b

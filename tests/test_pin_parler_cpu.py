@@ -114,3 +114,27 @@ def test_parler_graph_matches_musicgen_decoder(n_prompt, steps):
     err = np.abs(got - ref).max()
     assert err <= 1e-4 * scale, (err, scale)
     assert np.array_equal(got.argmax(-1), ref.argmax(-1))
+
+
+def test_parler_lockstep_batch_matches_musicgen_per_prompt():
+    """The lock-step batch the headline bench decodes (batch > 1: every GEMV with B columns, each prompt its
+    own KV-cache sequence): every prompt's logits are transformers' decoder run on that prompt alone."""
+    B, n_prompt, steps = 3, 6, 4
+    cfg = ttship.parler_config(**dict(CFG, batch=B))
+    p = ttship.Parler(py_oracle.iface(4), cfg)
+    try:
+        w = p.weights()
+        rng = np.random.default_rng(77)
+        prompts = rng.integers(0, cfg.prompt_vocab, (B, n_prompt)).astype(np.int32)
+        audio = rng.integers(0, cfg.audio_vocab, (steps, B, cfg.n_output_heads)).astype(np.int32)
+        p.prefill(prompts)
+        got = np.stack([p.decode(audio[s]).reshape(B, cfg.n_output_heads, cfg.output_vocab) for s in range(steps)], axis=1)
+    finally:
+        p.close()
+    m = musicgen_from_runner(w, cfg)
+    for b in range(B):
+        ref = run_musicgen(m, w, cfg, prompts[b].tolist(), audio[:, b].tolist())
+        scale = np.abs(ref).max()
+        err = np.abs(got[b] - ref).max()
+        assert err <= 1e-4 * scale, (b, err, scale)
+        assert np.array_equal(got[b].argmax(-1), ref.argmax(-1)), b
