@@ -275,9 +275,17 @@ struct PtrMap {
 struct Planner {
     tts_tensor * const * nodes;
     int n;
-    PtrMap<int> uses;
     PtrMap<int> index;
     PtrMap<SmallIdx> consumers;
+    // distinct consuming nodes of a tensor (a node listing it twice counts once): the size of its
+    // consumer list, so one map serves both
+    struct Uses {
+        PtrMap<SmallIdx> * c;
+        int operator[](const tts_tensor * t) const {
+            auto * e = c->find(t);
+            return e ? (int)e->second.size() : 0;
+        }
+    } uses{&consumers};
     std::vector<int> act;  // -1 skip, 0 run node, k>0 run items[k-1]
     std::vector<Item> items;
     std::deque<tts_tensor> derived;  // strided stand-ins for folded CONT nodes (stable addresses)
@@ -304,11 +312,11 @@ struct Planner {
     }
 
     void build(tts_tensor * const * nodes_, int n_) {
+        const auto t_build0 = std::chrono::steady_clock::now();
         nodes = nodes_;
         n = n_;
         act.assign(n, 0);
         index.reserve((size_t)n);
-        uses.reserve((size_t)n * 2);
         consumers.reserve((size_t)n * 2);
         for (int i = 0; i < n; ++i) {
             index[nodes[i]] = i;
@@ -319,17 +327,31 @@ struct Planner {
                 bool dup = false;
                 for (int s2 = 0; s2 < s; ++s2) dup |= nodes[i]->src[s2] == x;
                 if (dup) continue;
-                uses[x]++;
                 consumers[x].push_back(i);
             }
         }
+        // TTS_PLAN_TIMING=1: milliseconds per planner pass on stderr (host-cost study)
+        static const bool timing = getenv("TTS_PLAN_TIMING") != nullptr;
+        auto t_last = t_build0;
+        char tbuf[512];
+        int tlen = 0;
+        auto tmark = [&](const char * what) {
+            if (!timing) return;
+            const auto now = std::chrono::steady_clock::now();
+            tlen += snprintf(tbuf + tlen, sizeof(tbuf) - (size_t)tlen, " %s %.3f", what, std::chrono::duration<double, std::milli>(now - t_last).count());
+            t_last = now;
+        };
+        tmark("index");
         if (mask & TTS_FUSE_LSTM) try_lstm();
+        tmark("lstm");
         if (mask & TTS_FUSE_MCPY)  // roots first: a concat chain is claimed whole by its last CONCAT
             for (int i = n - 1; i >= 0; --i)
                 if (act[i] == 0 && nodes[i]->op == TTS_OP_CONCAT) try_rint(i);
+        tmark("rint");
         if (mask & TTS_FUSE_EMBED)  // roots first: a chain is claimed whole by its last ADD
             for (int i = n - 1; i >= 0; --i)
                 if (act[i] == 0 && nodes[i]->op == TTS_OP_ADD) try_embed(i);
+        tmark("embed");
         for (int i = 0; i < n; ++i) {
             if (act[i] != 0) continue;
             const tts_tensor * t = nodes[i];
@@ -350,10 +372,13 @@ struct Planner {
                 default: break;
             }
         }
+        tmark("patterns");
         if (mask & TTS_FUSE_CONTREAD) skip_cont_reads();
         if (mask & TTS_FUSE_LN) fuse_ln_into_gemv();
         link_attn_shadow();
         if (mask & TTS_FUSE_XATTN) fuse_xattn();
+        tmark("post");
+        if (timing) fprintf(stderr, "plan %d nodes ms:%s\n", n, tbuf);
     }
 
     // attention output -> [views] -> Q4_K GEMV: the attention kernel also writes a private copy

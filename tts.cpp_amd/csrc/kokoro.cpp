@@ -7,6 +7,7 @@
 // upscaled F0 it reads; its uniform draws and the window-envelope normaliser
 // (compute_window_squared_sum, util.cpp:203-217) are host inputs, as in kokoro_runner::set_inputs.
 // Weights are deterministic synthetic tensors in Kokoro-82M shapes (no checkpoints offline).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <random>
@@ -68,6 +69,7 @@ struct tts_kokoro_gen {
     tts_tensor *in_x = nullptr, *in_f0 = nullptr, *in_style = nullptr, *in_uvdata = nullptr, *in_wss = nullptr;
     bool device_draws = false;
     std::vector<float> h_uvdata, h_wss, h_window;
+    int64_t h_wss_len = -1;  // h_wss holds the window sum of squares for this output length (reused while it repeats)
 };
 
 extern "C" void tts_kokoro_gen_default_config(tts_kokoro_gen_config * c) {
@@ -409,14 +411,19 @@ int tts::kokoro_gen_set_inputs(tts_kokoro_gen * k, int64_t T, const float * rand
     float * d = k->h_uvdata.data();
     d[0] = cf.voice_threshold, d[1] = cf.noise_std, d[2] = cf.sin_amp, d[3] = cf.sin_amp / 3.0f;
     if (rand) memcpy(d + 4, rand, sizeof(float) * (size_t)(L * H));
-    const int64_t n_frames = L / cf.hop, cutoff = n_frames * cf.hop, half = cf.n_fft / 2;
-    k->h_wss.assign((size_t)L, 0.0f);
-    for (int64_t i = 0; i < n_frames + half / cf.hop; ++i)
-        for (int64_t j = 0; j < cf.n_fft; ++j) {
-            const int64_t idx = j + i * cf.hop - half;
-            if (idx < 0 || idx >= cutoff) continue;
-            k->h_wss[idx] += powf(k->h_window[j], 2);
+    if (k->h_wss_len != L) {  // a function of the length alone: built once per length
+        const int64_t n_frames = L / cf.hop, cutoff = n_frames * cf.hop, half = cf.n_fft / 2;
+        std::vector<float> w2((size_t)cf.n_fft);
+        for (int64_t j = 0; j < cf.n_fft; ++j) w2[(size_t)j] = powf(k->h_window[(size_t)j], 2);  // the same squares, once
+        k->h_wss.assign((size_t)L, 0.0f);
+        for (int64_t i = 0; i < n_frames + half / cf.hop; ++i) {
+            // the same additions in the same order (frame i, then window index j), only the bounds hoisted
+            const int64_t j0 = std::max<int64_t>(0, half - i * cf.hop), j1 = std::min<int64_t>(cf.n_fft, cutoff + half - i * cf.hop);
+            const int64_t base = i * cf.hop - half;
+            for (int64_t j = j0; j < j1; ++j) k->h_wss[(size_t)(base + j)] += w2[(size_t)j];
         }
+        k->h_wss_len = L;
+    }
     int st = k->be.set(k->be.ctx, k->in_uvdata->data, k->h_uvdata.data(), sizeof(float) * k->h_uvdata.size());
     if (st == 0) st = k->be.set(k->be.ctx, k->in_wss->data, k->h_wss.data(), sizeof(float) * k->h_wss.size());
     return st;

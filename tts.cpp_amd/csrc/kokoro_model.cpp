@@ -650,6 +650,7 @@ extern "C" int tts_kokoro_decode(tts_kokoro * k, const int32_t * tokens, int32_t
         fprintf(stderr, "kokoro: compute arena too small (%zu needed)\n", k->gctx.arena_used);
         return TTS_STATUS_ALLOC_FAILED;
     }
+    pc.mark("alloc");
     // kokoro_runner::set_inputs (model.cpp:1253-1275): duration mask row i covers frames
     // [running, running + lengths[i]) in f32, as the reference compares them
     k->h_dmask.assign((size_t)(total * n), 0.0f);
@@ -663,7 +664,7 @@ extern "C" int tts_kokoro_decode(tts_kokoro * k, const int32_t * tokens, int32_t
     if (st == 0) st = k->be.set(k->be.ctx, k->m_tokens->data, tokens, sizeof(int32_t) * (size_t)n);
     if (st == 0) st = k->be.set(k->be.ctx, k->m_dpred->data, hidden, tg::nbytes(k->m_dpred));
     if (st == 0) st = k->be.set(k->be.ctx, k->m_dmask->data, k->h_dmask.data(), sizeof(float) * k->h_dmask.size());
-    pc.mark("alloc+inputs");
+    pc.mark("inputs");
     if (st == 0) st = k->be.compute(k->be.ctx, k->gctx.nodes.data(), (int)k->gctx.nodes.size());
     pc.mark("compute");
     if (st == 0 && pcm) st = k->be.get(k->be.ctx, pcm, k->m_out->data, tg::nbytes(k->m_out));
