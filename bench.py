@@ -465,34 +465,38 @@ def dia_leg(be, args):
         d.close()
 
 
-def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
+def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True, ragged=False):
     """TTS.cpp's serving shape (examples/server/server.cpp:316-321,885-895): one prompt per runner, R
     runners, each on its own backend (HIP stream) with its own model copy, driven by its own host thread
     through TTS.cpp's own step loop (graph_compute, logits read back, host greedy sampler:
-    parler_tts_runner::decode, src/models/parler/model.cpp:648-693), all prefilled to the same KV length.
-    coalesce=True: the backend's step coalescer (coalesce.hip) runs the runners' equal steps as batched
-    launches; False: every runner alone (TTS_HIP_OPT_COALESCE = 0)."""
+    parler_tts_runner::decode, src/models/parler/model.cpp:648-693).
+    coalesce=True: the backend's step coalescer (coalesce.hip) runs the runners' steps as batched
+    launches; False: every runner alone (TTS_HIP_OPT_COALESCE = 0).  ragged=False: every runner prefilled
+    to the same KV length, started together; True: runner r's prompt is 7 r tokens longer and its thread
+    starts r ms later (the server's requests arrive at different times with different lengths)."""
     R, steps = R or args.b1_replicas, args.b1_steps
-    prev_co = ttship.coalesce_enable(coalesce)  # (opt-in, process-wide: the runners' buffers are allocated below)
     # the same KV capacity rule as the lock-step leg: a multiple of 4 positions keeps every V row
     # 16-B aligned, so P.V takes its vector-load kernel (k_attn_pv<true, ...>)
-    cfg = ttship.parler_config(batch=1, max_ctx=max(4096, args.ctx + steps + args.warmup + 64))
+    cfg = ttship.parler_config(batch=1, max_ctx=max(4096, args.ctx + 7 * R + steps + args.warmup + 64))
     bes = [new_backend() for _ in range(R)]
     for b in bes:
         b.set_option(ttship.OPT["COALESCE"], 1 if coalesce else 0)
     runs = [None] * R
+    lens = [args.ctx + (7 * r if ragged else 0) for r in range(R)]
 
     def make(r):  # each worker loads its own model copy (runner_from_file per worker, server.cpp:316-321)
         runs[r] = ttship.Parler(bes[r].iface(reference_flow=True), cfg)
-        runs[r].prefill(prompt_tokens(1, args.ctx, cfg.prompt_vocab, offset=rank * R + r))
+        runs[r].prefill(prompt_tokens(1, lens[r], cfg.prompt_vocab, offset=rank * R + r))
         bes[r].sync()
 
     try:
         run_replicas(make, R)
-        run_replicas(lambda r: (runs[r].generate(args.warmup), bes[r].sync()), R)  # in step: the coalesced groups form
+        run_replicas(lambda r: (runs[r].generate(args.warmup), bes[r].sync()), R)  # the coalesced groups form
         s0 = ttship.coalesce_stats(local)
 
         def one(r):
+            if ragged:
+                time.sleep(0.001 * r)
             runs[r].generate(steps)
             bes[r].sync()
 
@@ -500,12 +504,13 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
         run_replicas(one, R)
         dt = time.perf_counter() - t0
         s1 = ttship.coalesce_stats(local)
-        co = {k: s1[k] - s0[k] for k in ("launches", "member_steps", "alone", "refused")}
+        co = {k: s1[k] - s0[k] for k in ("launches", "member_steps", "alone", "refused", "ragged_launches")}
         co["max_group"] = s1["max_group"]
         co["wait_us_per_step"] = round((s1["wait_us"] - s0["wait_us"]) / max(1, R * steps), 1)
         return {"workload": f"Parler-mini Q4_K AR decode, {R} runners x 1 prompt (TTS.cpp's server model: one runner, backend and "
-                            f"model copy per worker thread, graph_compute + host greedy sampler per step), KV {args.ctx} -> "
-                            f"{args.ctx + steps}", "replicas": R, "batch_per_replica": 1,
+                            f"model copy per worker thread, graph_compute + host greedy sampler per step), KV "
+                            f"{min(lens)}..{max(lens)} -> +{steps}" + (", prompt lengths 7 r apart, thread r starting r ms late" if ragged else ""),
+                "replicas": R, "batch_per_replica": 1,
                 "step_coalescer": "on" if coalesce else "off", "coalescer": co,
                 "ms_per_step": round(1000 * dt / steps, 4),
                 "ar_audio_sec_per_s": round(R * steps * SAMPLES_PER_STEP / SAMPLE_RATE / dt, 3)}
@@ -515,7 +520,6 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True):
                 p.close()
         for b in bes:
             b.close()
-        ttship.coalesce_enable(prev_co)
 
 
 def kokoro_prompt(g, vocab):
@@ -665,9 +669,9 @@ def main():
     ap.add_argument("--b1-replicas", type=int, default=8, help="the B=1 leg: this many runners of one prompt each, as "
                     "TTS.cpp's server workers run (0 = skip)")
     ap.add_argument("--b1-steps", type=int, default=100)
-    ap.add_argument("--b1-wide", type=int, default=32, help="the B=1 leg again with this many coalesced runners (0 = skip)")
-    ap.add_argument("--b1-coalesce", type=int, default=0, help="1: also run the B=1 legs with the opt-in step coalescer "
-                    "(tts_hip_coalesce_enable; not validated on hardware this round, so off by default)")
+    ap.add_argument("--b1-wide", type=int, default=32, help="the ragged B=1 leg again with this many coalesced runners (0 = skip)")
+    ap.add_argument("--b1-coalesce", type=int, default=1, help="1: also run the B=1 legs with the step coalescer (equal and "
+                    "ragged KV lengths; 0 = only the runners alone)")
     ap.add_argument("--sampled-steps", type=int, default=20, help="the headline's AR decode again with seeded top-k 50 sampling "
                     "(the reference's default sampler) for this many steps (0 = skip)")
     ap.add_argument("--prompt-pass", type=int, default=1, help="time every prompt's own sentence prompt pass from position 0 (0 = skip)")
@@ -840,12 +844,16 @@ def main():
         close_replicas(reps8)
         p8 = {"workload": "Parler-mini Q4_K AR decode, 8 prompts per GPU (2 lock-step replicas x 4)", "ar_ms_per_step": round(1000 * d8 / args.steps, 4),
               "ar_audio_sec_per_s": round(world * 8 * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE / d8, 3)}
-    # The legs added in round 5 run guarded: a Python-level failure in one of them is reported in its
-    # field and does not take the headline line down with it (a device fault still would).
+    # The legs added in round 5 run guarded on one GPU: a Python-level failure in one of them is reported
+    # in its field and does not take the headline line down with it (a device fault still would).  With
+    # several ranks a failed leg re-raises: the legs run collectives, and a rank that skipped the rest of
+    # a leg's barriers / reductions would pair its next collective with another rank's different one.
     def guarded(name, fn):
         try:
             return fn()
         except Exception as e:  # noqa: BLE001
+            if dist is not None:
+                raise
             print(f"bench: leg {name} failed: {e!r}", file=sys.stderr, flush=True)
             return {"error": repr(e)}
 
@@ -854,15 +862,17 @@ def main():
     def leg_sampled():
         barrier_sync(dist, None)
         reps_s, _, _ = parler_replicas(args, per_gpu, R, rank, new_backend)
-        for r, (rb, rr, _) in enumerate(reps_s):
-            rr.set_sampling(ttship.sampling(top_k=50, temperature=1.0, seed=0x5EED + rank * R + r))
-            rr.generate(2)
-        warm_concurrent(args, reps_s)
-        barrier_sync(dist, reps_s[0][0])
-        ts0 = time.perf_counter()
-        run_replicas(lambda r: (reps_s[r][1].generate(args.sampled_steps), reps_s[r][0].sync()), R)
-        ds = max_over_ranks(dist, local, time.perf_counter() - ts0)
-        close_replicas(reps_s)
+        try:
+            for r, (rb, rr, _) in enumerate(reps_s):
+                rr.set_sampling(ttship.sampling(top_k=50, temperature=1.0, seed=0x5EED + rank * R + r))
+                rr.generate(2)
+            warm_concurrent(args, reps_s)
+            barrier_sync(dist, reps_s[0][0])
+            ts0 = time.perf_counter()
+            run_replicas(lambda r: (reps_s[r][1].generate(args.sampled_steps), reps_s[r][0].sync()), R)
+            ds = max_over_ranks(dist, local, time.perf_counter() - ts0)
+        finally:
+            close_replicas(reps_s)
         sampled = {"workload": f"as the headline's AR decode ({R} replicas x {bl} lock-step prompts per GPU, KV {args.ctx}), with the "
                                "reference's default sampler: seeded top-k 50, temperature 1 (device sampling, k_sample.hip)",
                    "steps": args.sampled_steps, "ar_ms_per_step": round(1000 * ds / args.sampled_steps, 4),
@@ -875,27 +885,30 @@ def main():
     def leg_prompt_pass():
         barrier_sync(dist, None)
         pcfg = ttship.parler_config(batch=1, max_ctx=256)
-        pbes = [new_backend() for _ in range(R)]
-        pruns = [ttship.Parler(b.iface(), pcfg) for b in pbes]
-        toks_pp = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], pcfg.prompt_vocab) for g in range(per_gpu)]
-        for rr, b in zip(pruns, pbes):  # warm (code objects)
-            rr.prefill(toks_pp[0].reshape(1, -1))
-            b.sync()
+        pbes, pruns = [], []
+        try:
+            pbes += [new_backend() for _ in range(R)]
+            pruns += [ttship.Parler(b.iface(), pcfg) for b in pbes]
+            toks_pp = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], pcfg.prompt_vocab) for g in range(per_gpu)]
+            for rr, b in zip(pruns, pbes):  # warm (code objects)
+                rr.prefill(toks_pp[0].reshape(1, -1))
+                b.sync()
 
-        def pp(r):
-            for g in range(r, per_gpu, R):
-                pruns[r].reset()
-                pruns[r].prefill(toks_pp[g].reshape(1, -1))
-            pbes[r].sync()
+            def pp(r):
+                for g in range(r, per_gpu, R):
+                    pruns[r].reset()
+                    pruns[r].prefill(toks_pp[g].reshape(1, -1))
+                pbes[r].sync()
 
-        barrier_sync(dist, pbes[0])
-        tp0 = time.perf_counter()
-        run_replicas(pp, R)
-        dtp = max_over_ranks(dist, local, time.perf_counter() - tp0)
-        for rr in pruns:
-            rr.close()
-        for b in pbes:
-            b.close()
+            barrier_sync(dist, pbes[0])
+            tp0 = time.perf_counter()
+            run_replicas(pp, R)
+            dtp = max_over_ranks(dist, local, time.perf_counter() - tp0)
+        finally:
+            for rr in pruns:
+                rr.close()
+            for b in pbes:
+                b.close()
         prompt_pass = {"workload": f"{per_gpu} prompt passes per GPU from position 0, prompt g = perf_battery sentence g % 29 "
                                    f"(word-piece-length synthetic ids, {min(map(len, toks_pp))}-{max(map(len, toks_pp))} tokens), "
                                    f"{R} runners concurrently",
@@ -906,17 +919,17 @@ def main():
     prompt_pass = guarded("prompt_pass", leg_prompt_pass) if args.prompt_pass else None
 
     def leg_b1():
-        # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer, the same runners each
-        # alone, and b1_wide coalesced runners (the headline's prompt count per GPU)
+        # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer (equal and ragged
+        # KV lengths), the same runners each alone, and b1_wide coalesced ragged runners
         b1 = {}
-        legs = [("alone", args.b1_replicas, False)]
+        legs = [("alone", args.b1_replicas, False, False)]
         if args.b1_coalesce:
-            legs.insert(0, ("coalesced", args.b1_replicas, True))
+            legs = [("coalesced", args.b1_replicas, True, False), ("coalesced_ragged", args.b1_replicas, True, True)] + legs
             if args.b1_wide > 0:
-                legs.append(("coalesced_wide", args.b1_wide, True))
-        for name, n_run, co in legs:
+                legs.append(("coalesced_ragged_wide", args.b1_wide, True, True))
+        for name, n_run, co, rg in legs:
             barrier_sync(dist, None)
-            leg = parler_b1_leg(args, rank, local, new_backend, R=n_run, coalesce=co)
+            leg = parler_b1_leg(args, rank, local, new_backend, R=n_run, coalesce=co, ragged=rg)
             t = max_over_ranks(dist, local, leg["ms_per_step"])
             leg["ms_per_step"] = t
             leg["ar_audio_sec_per_s"] = round(world * n_run * SAMPLES_PER_STEP / SAMPLE_RATE * 1000.0 / t, 3)

@@ -347,14 +347,14 @@ enum tts_fuse_bits {
 int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Step coalescer counters of `device` since process start: out[0] coalesced launches, [1] member steps they
  * carried, [2] steps a member ran alone after waiting, [3] groups refused (no coalesced form / mismatched
- * members), [4] the largest group, [5] host microseconds spent waiting for members.  Returns the number written. */
+ * members), [4] the largest group, [5] host microseconds spent waiting for members, [6] coalesced launches whose
+ * members were at different KV lengths.  Returns the number written. */
 int tts_hip_coalesce_stats(int device, int64_t * out, int n);
 /* Coalescer rendezvous window (microseconds a step waits for the other active members; default 5000). */
 void tts_hip_coalesce_set_wait(int us);
-/* The step coalescer, process-wide: on = buffers allocated from now on are VMM-mapped (so members' buffers can
- * be windowed) and one-prompt decode steps of several backends rendezvous.  Off by default; the
- * environment variable TTS_HIP_COALESCE=1 turns it on at load.  Buffers keep the kind they were allocated with.
- * Returns the previous setting. */
+/* The step coalescer, process-wide: one-prompt decode steps of several backends on one device rendezvous and run
+ * as one batched plan, also at different KV lengths.  On by default; the environment variable
+ * TTS_HIP_COALESCE=0 turns it off at load.  Returns the previous setting. */
 int tts_hip_coalesce_enable(int on);
 /* Test hooks (process-wide, off by default; never read from the environment):
  * TTS_HIP_HOOK_FAULT_WEIGHT_SET = 1: tts_hip_weight_set of a Q4_K tensor fails (the callers' fallback paths). */

@@ -16,9 +16,9 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
-    """The opt-in step coalescer's tests (test_coalesce_gpu.py) run after the parity suite: they switch the
-    process-wide coalescer on (VMM-mapped buffers) and a failure there must not stop (-x) the kernels'
-    parity tests from running."""
+    """The step coalescer's tests (test_coalesce_gpu.py) run after the parity suite: they drive many backends
+    from many threads at once, and a failure there must not stop (-x) the kernels' parity tests from
+    running."""
     items.sort(key=lambda it: it.nodeid.startswith("tests/test_coalesce_gpu.py") or "test_coalesce_gpu.py::" in it.nodeid)
 
 

@@ -7,8 +7,8 @@ runners here are driven exactly so -- one backend and one runner per host thread
 loop (graph_compute, logits read back at once, host sampler) -- and the backend coalesces their
 decode steps into batched launches.  Every runner's tokens must equal the same runner decoding
 alone and the CPU oracle's (bit-exact), with coalesced launches actually taken."""
-import os
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -16,17 +16,11 @@ import pytest
 import py_oracle
 import ttship
 
-# The coalescer's VMM mapping was reworked after the round's last GPU run (stale translations on address
-# reuse) and has not run on hardware since: these tests run when asked for
-# (TTS_HIP_COALESCE_TESTS=1), so an unvalidated path cannot fault the parity suite's GPU.
-pytestmark = pytest.mark.skipif(os.environ.get("TTS_HIP_COALESCE_TESTS") != "1",
-                                reason="opt-in step coalescer, not yet validated on hardware: TTS_HIP_COALESCE_TESTS=1 runs it")
-
 
 @pytest.fixture(autouse=True)
 def coalescer_on():
-    """The coalescer is opt-in (tts_hip_coalesce_enable / TTS_HIP_COALESCE=1): on for these tests, and
-    for the buffers they allocate, then back to what it was."""
+    """The coalescer is on by default (tts_hip_coalesce_enable); kept on for these tests whatever the
+    environment says, then back to what it was."""
     prev = ttship.coalesce_enable(True)
     yield
     ttship.coalesce_enable(prev)
@@ -58,17 +52,19 @@ def prompt(r, n=7, vocab=512):
     return ((np.arange(n, dtype=np.int32) * (31 + 2 * r) + 5 * r + 1) % vocab).reshape(1, n)
 
 
-def serve(ifaces, cfg, prompts, steps):
+def serve(ifaces, cfg, prompts, steps, stagger_s=0.0, cfgs=None):
     """One runner per iface, prefilled with its prompt, then `steps` decode steps from one thread per
-    runner (the server's workers); returns every runner's tokens."""
-    runs = [ttship.Parler(it, cfg) for it in ifaces]
+    runner (the server's workers; runner i starts i * stagger_s seconds after runner 0); returns every
+    runner's tokens."""
+    runs = [ttship.Parler(it, (cfgs[i] if cfgs else cfg)) for i, it in enumerate(ifaces)]
     try:
         for r, p in zip(runs, prompts):
-            p_ = p
-            r.prefill(p_)
+            r.prefill(p)
         out = [None] * len(runs)
 
         def go(i):
+            if stagger_s:
+                time.sleep(i * stagger_s)
             out[i] = runs[i].generate(steps)
 
         run_threads(go, len(runs))
@@ -76,6 +72,15 @@ def serve(ifaces, cfg, prompts, steps):
     finally:
         for r in runs:
             r.close()
+
+
+def oracle_tokens(cfg, p, steps):
+    c = ttship.Parler(py_oracle.iface(8), cfg)
+    try:
+        c.prefill(p)
+        return c.generate(steps)
+    finally:
+        c.close()
 
 
 @pytest.mark.gpu
@@ -112,24 +117,87 @@ def test_coalesced_runners_match_alone_and_oracle(n):
 
 
 @pytest.mark.gpu
-def test_runners_at_different_lengths_still_exact():
-    """Runners whose KV lengths differ have different step graphs: they never share a launch (only the
-    equal-length ones do), and every runner's tokens stay the oracle's."""
+def test_runners_at_different_lengths_coalesce_exact():
+    """Runners whose KV lengths differ share launches (each attention at its own key count, each KV
+    store at its own position), and every runner's tokens stay the oracle's."""
     cfg = ttship.parler_config(batch=1, **TINY)
     prompts = [prompt(0, 7), prompt(1, 7), prompt(2, 9)]
     bes = [ttship.HipBackend(0) for _ in range(3)]
     try:
+        before = ttship.coalesce_stats(0)
         got = serve([b.iface(reference_flow=True) for b in bes], cfg, prompts, 8)
+        after = ttship.coalesce_stats(0)
     finally:
         for b in bes:
             b.close()
+    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
+    assert after["member_steps"] - before["member_steps"] >= 3 * 4, (before, after)
     for r in range(3):
-        c = ttship.Parler(py_oracle.iface(8), cfg)
-        try:
-            c.prefill(prompts[r])
-            assert np.array_equal(got[r], c.generate(8)), f"runner {r}"
-        finally:
-            c.close()
+        assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], 8)), f"runner {r}"
+
+
+@pytest.mark.gpu
+def test_staggered_runners_at_four_lengths():
+    """TTS.cpp's server shape: 4 workers, 4 prompts of different lengths, decoding from 4 threads that
+    start at different times.  Most steps run coalesced (at 4 different KV lengths), and every runner's
+    tokens are its own oracle B = 1 run's."""
+    cfg = ttship.parler_config(batch=1, **TINY)
+    steps = 24
+    prompts = [prompt(r, 5 + 4 * r) for r in range(4)]
+    bes = [ttship.HipBackend(0) for _ in range(4)]
+    try:
+        before = ttship.coalesce_stats(0)
+        got = serve([b.iface(reference_flow=True) for b in bes], cfg, prompts, steps, stagger_s=0.01)
+        after = ttship.coalesce_stats(0)
+    finally:
+        for b in bes:
+            b.close()
+    carried = after["member_steps"] - before["member_steps"]
+    assert carried >= 4 * steps // 2, (before, after)  # most steps coalesced
+    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
+    for r in range(4):
+        assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], steps)), f"runner {r}"
+
+
+@pytest.mark.gpu
+def test_two_kinds_of_graphs_coalesce_separately():
+    """Two model configurations (2 and 3 layers) served at once, two runners each, at different prompt
+    lengths: each kind of step graph coalesces with its own kind (several groups per rendezvous), and
+    every runner's tokens are the oracle's."""
+    cfg2 = ttship.parler_config(batch=1, **TINY)
+    cfg3 = ttship.parler_config(batch=1, **dict(TINY, n_layers=3))
+    cfgs = [cfg2, cfg3, cfg2, cfg3]
+    prompts = [prompt(r, 6 + r) for r in range(4)]
+    bes = [ttship.HipBackend(0) for _ in range(4)]
+    try:
+        before = ttship.coalesce_stats(0)
+        got = serve([b.iface(reference_flow=True) for b in bes], None, prompts, 10, cfgs=cfgs)
+        after = ttship.coalesce_stats(0)
+    finally:
+        for b in bes:
+            b.close()
+    assert after["member_steps"] - before["member_steps"] >= 4 * 5, (before, after)
+    for r in range(4):
+        assert np.array_equal(got[r], oracle_tokens(cfgs[r], prompts[r], 10)), f"runner {r}"
+
+
+@pytest.mark.gpu
+def test_generic_head_dim_coalesced():
+    """A head dim the row / split attention kernels do not take (32): the generic decode attention
+    kernel runs the coalesced step, with its private copy of each member's output in place."""
+    cfg = ttship.parler_config(batch=1, **dict(TINY, n_attn_heads=8))
+    prompts = [prompt(r, 6 + 2 * r) for r in range(3)]
+    bes = [ttship.HipBackend(0) for _ in range(3)]
+    try:
+        before = ttship.coalesce_stats(0)
+        got = serve([b.iface(reference_flow=True) for b in bes], cfg, prompts, 8)
+        after = ttship.coalesce_stats(0)
+    finally:
+        for b in bes:
+            b.close()
+    assert after["member_steps"] - before["member_steps"] >= 3 * 4, (before, after)
+    for r in range(3):
+        assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], 8)), f"runner {r}"
 
 
 @pytest.mark.gpu
@@ -170,11 +238,11 @@ def test_weights_that_differ_are_not_shared():
 
 @pytest.mark.gpu
 def test_parler_mini_8_runners_coalesced_bit_identical():
-    """Parler-mini Q4_K (full shapes), 8 one-prompt runners on 8 backends from 8 threads: tokens and the
-    last step's logits bit-identical to each runner decoding alone."""
+    """Parler-mini Q4_K (full shapes), 8 one-prompt runners at 8 different prompt lengths on 8 backends
+    from 8 threads: tokens bit-identical to each runner decoding alone."""
     cfg = ttship.parler_config(batch=1, max_ctx=256)
     n, steps = 8, 10
-    prompts = [prompt(r, 12, cfg.prompt_vocab) for r in range(n)]
+    prompts = [prompt(r, 12 + r, cfg.prompt_vocab) for r in range(n)]
     bes = [ttship.HipBackend(0) for _ in range(n)]
     try:
         before = ttship.coalesce_stats(0)
@@ -185,6 +253,7 @@ def test_parler_mini_8_runners_coalesced_bit_identical():
             b.close()
     assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), (before, after)
     assert after["max_group"] >= 4, after
+    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
     be = ttship.HipBackend(0)
     be.set_option(ttship.OPT["COALESCE"], 0)
     try:

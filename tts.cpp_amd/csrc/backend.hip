@@ -43,15 +43,10 @@ static const size_t kPinBytes = 16u << 20;   // pinned staging ring for set_tens
 // medium lane-layout Q4_K weights, keyed by device address.  A weight buffer may be allocated and
 // written through one backend and read by the graphs of another (the ggml adapter allocates through
 // a utility backend, every ggml_backend computes on its own stream), so neither is per backend.
-// Buffers are physical allocations mapped into a reserved virtual range (hipMemCreate + hipMemMap) so
-// that the step coalescer can map several backends' buffers side by side into one window
-// (coalesce.hip); TTS_HIP_COALESCE=0 falls back to plain hipMalloc.
 namespace {
 std::mutex g_reg_mu;
 struct BufRec {
-    size_t size = 0, map_size = 0;
-    hipMemGenericAllocationHandle_t h{};
-    bool vmm = false;
+    size_t size = 0;
 };
 std::map<const char *, BufRec> g_buffers;                // base -> record (ordered: range lookups)
 std::unordered_map<const void *, uint8_t *> g_tiled;     // weight -> its tile-layout copy
@@ -64,13 +59,13 @@ const uint8_t * tiled_copy_find(const void * w) {
     auto it = g_tiled.find(w);
     return it == g_tiled.end() ? nullptr : it->second;
 }
-// process-wide coalescer switch (tts_hip_coalesce_enable; TTS_HIP_COALESCE=1 at load)
+// process-wide coalescer switch (tts_hip_coalesce_enable; TTS_HIP_COALESCE=0 at load turns it off)
 static std::atomic<int> g_coalesce_on{[] {
     const char * e = getenv("TTS_HIP_COALESCE");
-    return e && e[0] == '1' ? 1 : 0;
+    return e && e[0] == '0' ? 0 : 1;
 }()};
 bool coalesce_enabled() { return g_coalesce_on.load(std::memory_order_relaxed) != 0; }
-bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size) {
+bool buffer_lookup(const void * p, const char ** base, size_t * size) {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     auto it = g_buffers.upper_bound((const char *)p);
     if (it == g_buffers.begin()) return false;
@@ -78,85 +73,9 @@ bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vm
     if ((const char *)p >= it->first + it->second.size) return false;
     if (base) *base = it->first;
     if (size) *size = it->second.size;
-    if (vmm_handle) *vmm_handle = it->second.vmm ? (void *)it->second.h : nullptr;
-    if (map_size) *map_size = it->second.map_size;
     return true;
 }
 }  // namespace tts
-
-// ---- virtual addresses for VMM mappings ----
-// On this stack (ROCm 7.2, gfx950) an unmap does not make the device forget the old translation: new
-// physical memory mapped at an address that was mapped before is read and written through stale
-// page translations (scripts/vmm_path_probe.hip, profiles/r05/vmm_path_probe.log: with a reservation
-// per buffer freed with it, the runtime hands the freed addresses straight back and 188-200 of 200
-// churn iterations see words of other pages -- compute kernels, SDMA copies and memsets alike; with
-// the reservations never freed, 0 of 200 on every path).  Sub-ranges of one big reservation cannot be
-// given access separately (hipMemSetAccess: invalid argument).  So every mapping gets a reservation
-// of its own that is never released: a freed buffer's physical memory goes back, its addresses stay
-// reserved and unused for the life of the process (address space only: 128 TiB of it).
-namespace {
-std::atomic<size_t> g_va_retired{0};  // bytes of address space retired by freed mappings
-}  // namespace
-
-namespace tts {
-char * va_alloc(int device, size_t n) {
-    (void)device;
-    void * p = nullptr;
-    if (hipMemAddressReserve(&p, n, 0, nullptr, 0) != hipSuccess || !p) {
-        (void)hipGetLastError();
-        return nullptr;
-    }
-    return (char *)p;
-}
-void va_free(int device, char * p, size_t n) {
-    (void)device;
-    (void)p;
-    g_va_retired.fetch_add(n, std::memory_order_relaxed);  // never handed back: see above
-}
-}  // namespace tts
-
-// Physical allocation + a fresh reservation + mapping (HIP virtual memory management); false = use
-// hipMalloc.
-static bool vmm_alloc(int device, size_t size, void ** out, hipMemGenericAllocationHandle_t * h, size_t * msz) {
-    hipMemAllocationProp prop{};
-    prop.type = hipMemAllocationTypePinned;
-    prop.location.type = hipMemLocationTypeDevice;
-    prop.location.id = device;
-    size_t gran = 0;
-    if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || gran == 0) {
-        (void)hipGetLastError();
-        return false;
-    }
-    const size_t n = (size + gran - 1) / gran * gran;
-    if (hipMemCreate(h, n, &prop, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    void * va = tts::va_alloc(device, n);
-    if (!va) {
-        hipMemRelease(*h);
-        return false;
-    }
-    hipMemAccessDesc acc{};
-    acc.location = prop.location;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (hipMemMap(va, n, 0, *h, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        tts::va_free(device, (char *)va, n);
-        hipMemRelease(*h);
-        return false;
-    }
-    if (hipMemSetAccess(va, n, &acc, 1) != hipSuccess) {
-        (void)hipGetLastError();
-        hipMemUnmap(va, n);
-        tts::va_free(device, (char *)va, n);
-        hipMemRelease(*h);
-        return false;
-    }
-    *out = va;
-    *msz = n;
-    return true;
-}
 
 extern "C" {
 
@@ -313,13 +232,7 @@ void * tts_hip_buffer_alloc(tts_hip_backend_t be, size_t size) {
     void * p = nullptr;
     BufRec r;
     r.size = size ? size : 256;
-    // buffers of a coalescable size (compute arenas, KV caches: 64 KiB and up) are VMM-mapped
-    if (tts::coalesce_enabled() && r.size >= ((size_t)64 << 10) && vmm_alloc(be->device, r.size, &p, &r.h, &r.map_size)) {
-        r.vmm = true;
-    } else {
-        if (hipMalloc(&p, r.size) != hipSuccess) return nullptr;
-        r.map_size = r.size;
-    }
+    if (hipMalloc(&p, r.size) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> lk(g_reg_mu);
     g_buffers[(const char *)p] = r;
     return p;
@@ -368,16 +281,7 @@ void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
     }
     if (known) {
         drop_tiled_copies(ptr, r.size);
-        tts::coalesce_forget(ptr, r.size);  // coalescing windows holding this buffer are unmapped first
-    }
-    if (known && r.vmm) {
-        // hipFree waits for the whole device; an unmap does not: a stream other than this backend's (the
-        // coalescer's, another backend reading a shared buffer) may still be reading the range
-        hipDeviceSynchronize();
-        hipMemUnmap(ptr, r.map_size);
-        tts::va_free(be->device, (char *)ptr, r.map_size);
-        hipMemRelease(r.h);
-        return;
+        tts::coalesce_written(ptr, r.size);  // the coalescer's equal-content records over the range go
     }
     hipFree(ptr);
 }
@@ -559,42 +463,115 @@ static void crash_write(const char * s, int n) {
         s += w, n -= (int)w;
     }
 }
+// Everything below runs in the signal handler, so only async-signal-safe calls: write / read / open /
+// close, hand-rolled hex formatting, and backtrace() (libgcc is loaded at install by a first call, so
+// the handler's call does not allocate).  Frames are attributed to a mapping by reading /proc/self/maps
+// into a static buffer: "#i addr path+0xfileoffset".
+static char g_crash_maps[1 << 20];
+static int crash_hex(char * o, unsigned long v) {
+    char t[16];
+    int n = 0;
+    do t[n++] = "0123456789abcdef"[v & 15], v >>= 4; while (v);
+    o[0] = '0', o[1] = 'x';
+    for (int i = 0; i < n; ++i) o[2 + i] = t[n - 1 - i];
+    return n + 2;
+}
+static int crash_dec(char * o, int v) {
+    char t[12];
+    int n = 0;
+    do t[n++] = (char)('0' + v % 10), v /= 10; while (v);
+    for (int i = 0; i < n; ++i) o[i] = t[n - 1 - i];
+    return n;
+}
+static const char * crash_parse_hex(const char * p, unsigned long * v) {
+    unsigned long x = 0;
+    for (;; ++p) {
+        const char c = *p;
+        const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1;
+        if (d < 0) break;
+        x = x * 16 + (unsigned long)d;
+    }
+    *v = x;
+    return p;
+}
+// one maps line: start-end perms offset dev inode path
+static bool crash_map_line(const char * l, const char * e, unsigned long * a, unsigned long * b, unsigned long * off, const char ** path, int * plen) {
+    const char * p = crash_parse_hex(l, a);
+    if (*p != '-') return false;
+    p = crash_parse_hex(p + 1, b);
+    while (p < e && *p == ' ') ++p;
+    while (p < e && *p != ' ') ++p;  // perms
+    while (p < e && *p == ' ') ++p;
+    p = crash_parse_hex(p, off);
+    for (int f = 0; f < 2; ++f) {  // dev, inode
+        while (p < e && *p == ' ') ++p;
+        while (p < e && *p != ' ') ++p;
+    }
+    while (p < e && *p == ' ') ++p;
+    *path = p, *plen = (int)(e - p);
+    return true;
+}
 static void crash_handler(int sig, siginfo_t * si, void * uc) {
-    char buf[512];
-    int n = snprintf(buf, sizeof buf, "tts_hip: signal %d, fault address %p\n", sig, si ? si->si_addr : nullptr);
+    char buf[640];
+    int n = 0;
+    const char h1[] = "tts_hip: signal ";
+    for (const char * c = h1; *c; ++c) buf[n++] = *c;
+    n += crash_dec(buf + n, sig);
+    const char h2[] = ", fault address ";
+    for (const char * c = h2; *c; ++c) buf[n++] = *c;
+    const uintptr_t fa = si ? (uintptr_t)si->si_addr : 0;
+    n += crash_hex(buf + n, fa);
+    buf[n++] = '\n';
     crash_write(buf, n);
+    int mlen = 0;
+    {
+        const int fd = open("/proc/self/maps", O_RDONLY);
+        if (fd >= 0) {
+            ssize_t r;
+            while (mlen < (int)sizeof g_crash_maps - 1 && (r = read(fd, g_crash_maps + mlen, sizeof g_crash_maps - 1 - mlen)) > 0) mlen += (int)r;
+            close(fd);
+        }
+    }
     void * fr[64];
     const int nf = backtrace(fr, 64);
     for (int i = 0; i < nf; ++i) {
-        Dl_info di;
-        if (dladdr(fr[i], &di) && di.dli_fname)
-            n = snprintf(buf, sizeof buf, "  #%d %p %s+0x%lx %s\n", i, fr[i], di.dli_fname, (unsigned long)((const char *)fr[i] - (const char *)di.dli_fbase),
-                         di.dli_sname ? di.dli_sname : "");
-        else
-            n = snprintf(buf, sizeof buf, "  #%d %p ?\n", i, fr[i]);
+        n = 0;
+        buf[n++] = ' ', buf[n++] = ' ', buf[n++] = '#';
+        n += crash_dec(buf + n, i);
+        buf[n++] = ' ';
+        n += crash_hex(buf + n, (unsigned long)(uintptr_t)fr[i]);
+        buf[n++] = ' ';
+        bool found = false;
+        for (int l0 = 0; l0 < mlen && !found;) {
+            int l1 = l0;
+            while (l1 < mlen && g_crash_maps[l1] != '\n') ++l1;
+            unsigned long a = 0, b = 0, off = 0;
+            const char * path = nullptr;
+            int plen = 0;
+            if (crash_map_line(g_crash_maps + l0, g_crash_maps + l1, &a, &b, &off, &path, &plen) && (uintptr_t)fr[i] >= a &&
+                (uintptr_t)fr[i] < b && plen > 0) {
+                for (int k = 0; k < plen && n < (int)sizeof buf - 24; ++k) buf[n++] = path[k];
+                buf[n++] = '+';
+                n += crash_hex(buf + n, (unsigned long)(uintptr_t)fr[i] - a + off);
+                found = true;
+            }
+            l0 = l1 + 1;
+        }
+        if (!found) buf[n++] = '?';
+        buf[n++] = '\n';
         crash_write(buf, n);
     }
     // the mappings within 64 MiB of the fault address
-    const uintptr_t fa = si ? (uintptr_t)si->si_addr : 0;
-    const int fd = open("/proc/self/maps", O_RDONLY);
-    if (fd >= 0) {
-        crash_write("tts_hip: maps near the fault address:\n", 38);
-        char line[512], c;
-        int len = 0;
-        while (read(fd, &c, 1) == 1) {
-            if (c != '\n') {
-                if (len < (int)sizeof line - 2) line[len++] = c;
-                continue;
-            }
-            line[len] = 0;
-            unsigned long a = 0, b = 0;
-            if (sscanf(line, "%lx-%lx", &a, &b) == 2 && fa + (64ul << 20) >= a && fa <= b + (64ul << 20)) {
-                line[len++] = '\n';
-                crash_write(line, len);
-            }
-            len = 0;
-        }
-        close(fd);
+    crash_write("tts_hip: maps near the fault address:\n", 38);
+    for (int l0 = 0; l0 < mlen;) {
+        int l1 = l0;
+        while (l1 < mlen && g_crash_maps[l1] != '\n') ++l1;
+        unsigned long a = 0, b = 0, off = 0;
+        const char * path = nullptr;
+        int plen = 0;
+        if (crash_map_line(g_crash_maps + l0, g_crash_maps + l1, &a, &b, &off, &path, &plen) && fa + (64ul << 20) >= a && fa <= b + (64ul << 20))
+            crash_write(g_crash_maps + l0, l1 - l0 + (l1 < mlen ? 1 : 0));
+        l0 = l1 + 1;
     }
     const struct sigaction & prev = sig == SIGBUS ? g_prev_bus : g_prev_segv;
     if (prev.sa_flags & SA_SIGINFO) {
@@ -607,6 +584,8 @@ static void crash_handler(int sig, siginfo_t * si, void * uc) {
 }
 
 int tts_hip_install_crash_handler(void) {
+    void * warm[2];
+    (void)backtrace(warm, 2);  // loads libgcc's unwinder now, outside any signal context
     struct sigaction sa;
     memset(&sa, 0, sizeof sa);
     sa.sa_sigaction = crash_handler;

@@ -6,28 +6,31 @@
 // model.h:158-172).  Unchanged, that is N streams of M = 1 GEMVs that each re-read every weight.
 //
 // Here every backend's graph_compute of a one-prompt decode step enters a per-device rendezvous.
-// When the other recently active backends arrive with the same step graph (same ops, shapes and
-// topology: the runners are at the same KV length), the step runs ONCE as member 0's plan with M = N
-// columns (graph_exec.hip, be->bat):
-//   - every buffer member 0's graph uses has a counterpart in each member at the same offset (the
-//     runners build and allocate identical graphs); the members' physical buffers are mapped side by
-//     side into one virtual window (HIP virtual memory: tts_hip_buffer_alloc maps every buffer), so
-//     member k's tensor is window + k * stride + offset -- one uniform column / sequence stride, which
-//     the GEMV, attention, norm and embedding kernels already take;
-//   - operands read once for all members (weights, norm parameters, embedding tables) must hold equal
-//     bytes in every member (each worker loads its own copy of the model): checked on the device once
-//     and cached until a host write touches the range;
+// When the other recently active backends arrive with the same kind of step graph -- same ops, types,
+// parameters, wiring and weight shapes; their KV lengths (so their attention shapes, cache positions
+// and compute-buffer layouts) may differ -- the step runs ONCE as member 0's plan with M = N columns
+// (graph_exec.hip, be->bat):
+//   - intermediates are computed in executor memory laid out as member 0's compute buffer, member k's
+//     copy at win + k * stride: one uniform column / sequence stride, which the GEMV, attention, norm
+//     and embedding kernels take; the graph's output is copied to each member's own tensor afterwards;
+//   - member-owned operands (each member's KV-cache rows written by the K / V store epilogues, its cache
+//     and cross-attention views with its own key count, its masks and token / position inputs) are found
+//     by graph position in the member's own graph and reach the kernels as per-member offset tables;
+//   - read-only model data (weights, norm parameters, embedding tables) is read through member 0's copy
+//     after a device-side check that every member holds equal bytes (each worker loads its own copy of
+//     the model), cached until a host write touches the range;
 //   - the coalesced launches run on a hidden per-device backend's stream, after every member's stream
 //     (their input uploads), and every member's stream waits for them, so each caller's
 //     get_tensor_async sees its own logits (ggml_backend_sched_graph_compute_async is followed by an
 //     immediate read, src/tts_model.cpp:25-36).
 // Each member's results are the same sums in the same order as its own step: the kernels compute a
-// column independently of the others (tests/test_coalesce_gpu.py checks the tokens bit-exact against
-// each runner alone and against the CPU oracle).
+// column / sequence independently of the others (tests/test_coalesce_gpu.py checks the tokens bit-exact
+// against each runner alone and against the CPU oracle, also for runners at different KV lengths).
 #include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -41,19 +44,11 @@ namespace {
 
 using Clock = std::chrono::steady_clock;
 
-// A buffer a graph touches, in order of first appearance (signature): graphs with equal signatures
-// touch their buffers at equal offsets, buffer j of one graph standing for buffer j of the other.
-struct BufSlot {
-    const char * base = nullptr;
-    size_t size = 0, map_size = 0;
-    bool vmm = false;
-};
 struct Req {
     tts_hip_backend * be = nullptr;
     tts_tensor * const * nodes = nullptr;
     int n = 0;
     uint64_t sig = 0;
-    std::vector<BufSlot> bufs;
     int64_t count = 0;  // the backend's coalescable submissions so far (its decode step number)
     bool taken = false, done = false;
     int status = kCoalesceNotTaken;
@@ -62,13 +57,6 @@ struct Act {
     Clock::time_point t;
     int64_t count = 0;
     std::thread::id tid;  // the thread of its last submission
-};
-
-struct Window {
-    std::vector<const char *> bases;  // member buffers, member order
-    size_t stride = 0;
-    char * va = nullptr;
-    int dev = 0;
 };
 
 constexpr int kMaxDev = 16;
@@ -80,11 +68,13 @@ struct Dev {
     std::unordered_map<const tts_hip_backend *, Act> seen;  // active backends: last coalescable submit
     std::mutex exec_mu;                   // one coalesced step at a time (guards everything below)
     tts_hip_backend * exec = nullptr;     // hidden backend: stream + scratch of the coalesced launches
-    std::vector<Window> windows;
+    char * mem = nullptr;                 // executor memory for the members' intermediates
+    size_t mem_bytes = 0;
+    std::unordered_set<uint64_t> verified;  // group keys whose shapes and read-only operands checked out
     int * d_flags = nullptr;              // content-check mismatch flags
     int d_flags_n = 0;
     // counters (tts_hip_coalesce_stats)
-    std::atomic<int64_t> launches{0}, member_steps{0}, alone{0}, refused{0}, max_group{0}, wait_us{0};
+    std::atomic<int64_t> launches{0}, member_steps{0}, alone{0}, refused{0}, max_group{0}, wait_us{0}, ragged{0};
 };
 Dev g_dev[kMaxDev];
 std::atomic<int> g_wait_us{5000};
@@ -156,53 +146,28 @@ bool decode_like(tts_tensor * const * nodes, int n) {
     return any;
 }
 
-// Structure AND placement of a graph: ops, types, shapes, strides, parameters, layout flags, the node
-// each source is (leaves and views by description), and where every tensor lies -- (buffer j, offset)
-// with buffer j the j-th distinct buffer met, described by its size / mapping size / kind.  Two graphs
-// with equal signatures are the same step over buffers that correspond slot by slot (bufs): what
-// pairing member k's tensors with member 0's needs, computed by each runner's own thread.  Two
-// independent 64-bit hashes, folded.
-uint64_t signature(tts_tensor * const * nodes, int n, std::vector<BufSlot> & bufs) {
+// The kind of step a graph is: ops, types, parameters, layout flags and wiring (a source is the node
+// it is, or a leaf described by its type and role), plus every weight's shape -- everything but the
+// shapes and places that follow the KV length (attention over the cache, the store positions, the
+// compute-buffer layout).  Graphs with equal signatures are coalesced; co_prepare (graph_exec.hip)
+// then checks them against each other item by item.  Two independent 64-bit hashes, folded.
+uint64_t signature(tts_tensor * const * nodes, int n) {
     std::unordered_map<const tts_tensor *, int> idx;
     idx.reserve((size_t)n * 2);
     for (int i = 0; i < n; ++i) idx[nodes[i]] = i;
-    bufs.clear();
     uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)n, h2 = 0x84222325CBF29CE4ull + (uint64_t)n;
     auto mix = [&](uint64_t v) {
         h = (h ^ v) * 0x100000001B3ull;
         h2 = (h2 + v + 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
         h2 ^= h2 >> 31;
     };
-    auto loc = [&](const void * p) {
-        if (!p) {
-            mix(0xD0);
-            return;
-        }
-        const char * c = (const char *)p;
-        for (size_t j = 0; j < bufs.size(); ++j)
-            if (c >= bufs[j].base && c < bufs[j].base + bufs[j].size) {
-                mix(0xB0 + j), mix((uint64_t)(c - bufs[j].base));
-                return;
-            }
-        BufSlot sl;
-        void * hd = nullptr;
-        if (!buffer_lookup(p, &sl.base, &sl.size, &hd, &sl.map_size)) {
-            mix(0xE1), mix((uint64_t)(uintptr_t)p);  // not a backend buffer: the very same address in every member
-            return;
-        }
-        sl.vmm = hd != nullptr;
-        bufs.push_back(sl);
-        mix(0xB0 + bufs.size() - 1), mix(sl.size), mix(sl.map_size), mix(sl.vmm), mix((uint64_t)(c - sl.base));
-    };
-    constexpr int kLayout = TTS_FLAG_INPUT | TTS_FLAG_OUTPUT | TTS_FLAG_REPACKED | TTS_FLAG_TILED | TTS_FLAG_TILED_COPY;
-    auto tensor = [&](const tts_tensor * t) {
+    constexpr int kLayout = TTS_FLAG_INPUT | TTS_FLAG_OUTPUT | TTS_FLAG_REPACKED | TTS_FLAG_TILED | TTS_FLAG_TILED_COPY | TTS_FLAG_PERSIST;
+    auto kind = [&](const tts_tensor * t) {
         mix((uint64_t)t->op << 32 | (uint32_t)t->type);
-        for (int d = 0; d < 4; ++d) mix((uint64_t)t->ne[d]), mix((uint64_t)t->nb[d]);
         for (int k = 0; k < TTS_MAX_OP_PARAMS; ++k) mix((uint32_t)t->op_params[k]);
         mix((uint64_t)(t->flags & kLayout));
-        loc(t->data);
     };
-    auto ref = [&](const tts_tensor * x, int depth, auto & self) -> void {  // a source / view source
+    auto ref = [&](const tts_tensor * x) {  // a source / view source
         if (!x) {
             mix(0x51);
             return;
@@ -212,13 +177,15 @@ uint64_t signature(tts_tensor * const * nodes, int n, std::vector<BufSlot> & buf
             mix(0x1000000ull + it->second);
             return;
         }
-        tensor(x);
-        if (depth < 4) self(x->view_src, depth + 1, self);
+        kind(x);  // a leaf
     };
     for (int i = 0; i < n; ++i) {
-        tensor(nodes[i]);
-        ref(nodes[i]->view_src, 0, ref);
-        for (int s = 0; s < TTS_MAX_SRC; ++s) ref(nodes[i]->src[s], 0, ref);
+        const tts_tensor * t = nodes[i];
+        kind(t);
+        ref(t->view_src);
+        for (int s = 0; s < TTS_MAX_SRC; ++s) ref(t->src[s]);
+        if (t->op == TTS_OP_MUL_MAT && t->src[0] && t->src[0]->op == TTS_OP_NONE)  // a weight's shape
+            for (int d = 0; d < 4; ++d) mix((uint64_t)t->src[0]->ne[d]);
     }
     return (h ^ (h2 * 0x94D049BB133111EBull)) | 1;
 }
@@ -252,38 +219,6 @@ void copy_options(tts_hip_backend * d, const tts_hip_backend * s) {
     d->profile_gemv = s->profile_gemv;
 }
 
-char * window_for(Dev & d, const std::vector<const char *> & bases, size_t stride) {
-    for (const Window & w : d.windows)
-        if (w.bases == bases && w.stride == stride) return w.va;
-    int dev = 0;
-    hipGetDevice(&dev);
-    const size_t total = stride * bases.size();
-    char * va = va_alloc(dev, total);
-    if (!va) return nullptr;
-    size_t mapped = 0;
-    bool ok = true;
-    for (; mapped < bases.size(); ++mapped) {
-        void * h = nullptr;
-        size_t ms = 0;
-        ok = buffer_lookup(bases[mapped], nullptr, nullptr, &h, &ms) && h && ms == stride &&
-             hipMemMap(va + mapped * stride, stride, 0, (hipMemGenericAllocationHandle_t)h, 0) == hipSuccess;
-        if (!ok) break;
-    }
-    hipMemAccessDesc acc{};
-    acc.location.type = hipMemLocationTypeDevice;
-    acc.location.id = dev;
-    acc.flags = hipMemAccessFlagsProtReadWrite;
-    if (ok) ok = hipMemSetAccess(va, total, &acc, 1) == hipSuccess;
-    if (!ok) {
-        (void)hipGetLastError();
-        for (size_t u = 0; u < mapped; ++u) hipMemUnmap(va + u * stride, stride);
-        va_free(dev, va, total);
-        return nullptr;
-    }
-    d.windows.push_back(Window{bases, stride, va, dev});
-    return va;
-}
-
 __global__ void k_ne_bytes(const uint4 * __restrict__ a, const uint4 * __restrict__ b, size_t n16, const uint8_t * __restrict__ ta,
                            const uint8_t * __restrict__ tb, size_t tail, int * flag) {
     bool ne = false;
@@ -296,30 +231,22 @@ __global__ void k_ne_bytes(const uint4 * __restrict__ a, const uint4 * __restric
     if (ne) *flag = 1;  // any mismatch: the range is not shared
 }
 
-// Operands every member reads through member 0's copy: their bytes must be equal in each member.
-bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std::vector<std::pair<const void *, size_t>> & shared) {
+// Read-only operands every member reads through member 0's copy: (member 0's, member k's, bytes)
+// pairs whose bytes must be equal.
+bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std::vector<std::tuple<const void *, const void *, size_t>> & pairs) {
     std::vector<EqRec> todo;
     {
         std::lock_guard<std::mutex> lk(g_eq_mu);
-        // the same group as a step before, with no write into a checked range since: every pair still holds
-        auto gk = g_eq_group.find(bc.key);
-        if (gk != g_eq_group.end() && gk->second == g_eq_epoch) return true;
-        for (const auto & s : shared) {
-            if (!bc.stride(s.first)) continue;  // the same memory for every member
-            for (int k = 1; k < bc.N; ++k) {
-                const char * a = (const char *)s.first;
-                const char * b = bc.reloc(a, k);
-                const EqRec * e = eq_known(a, b, s.second);
-                if (e && !e->eq) return false;
-                if (!e) todo.push_back(EqRec{a, b, s.second, true});
-            }
+        for (const auto & pr : pairs) {
+            const char * a = (const char *)std::get<0>(pr);
+            const char * b = (const char *)std::get<1>(pr);
+            const size_t n = std::get<2>(pr);
+            const EqRec * e = eq_known(a, b, n);
+            if (e && !e->eq) return false;
+            if (!e) todo.push_back(EqRec{a, b, n, true});
         }
     }
-    if (todo.empty()) {
-        std::lock_guard<std::mutex> lk(g_eq_mu);
-        g_eq_group[bc.key] = g_eq_epoch;
-        return true;
-    }
+    if (todo.empty()) return true;
     if (d.d_flags_n < (int)todo.size()) {
         if (d.d_flags) hipFree(d.d_flags);
         d.d_flags_n = std::max((int)todo.size(), 1024);
@@ -347,62 +274,102 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
         cover_add(todo[i].a, todo[i].n);
         cover_add(todo[i].b, todo[i].n);
     }
-    if (all) g_eq_group[bc.key] = g_eq_epoch;
+    (void)bc;
     return all;
+}
+
+// Executor memory for the intermediates of member 0's graph: every compute buffer its non-leaf,
+// non-view tensors lie in, up to the last byte the graph uses there, N copies side by side.
+bool exec_layout(Dev & d, BatchCtx & bc, tts_tensor * const * nodes, int n) {
+    struct Rng {
+        const char * base;
+        size_t size, used;
+    };
+    std::vector<Rng> rs;
+    const Rng * last = nullptr;
+    for (int i = 0; i < n; ++i) {
+        const tts_tensor * t = nodes[i];
+        if (!t->data || t->view_src || t->op == TTS_OP_NONE || (t->flags & TTS_FLAG_PERSIST)) continue;
+        const char * p = (const char *)t->data;
+        size_t nb = tts_row_size(t->type, t->ne[0]) * (size_t)(t->ne[1] * t->ne[2] * t->ne[3]);
+        Rng * r = nullptr;
+        if (last && p >= last->base && p < last->base + last->size) r = const_cast<Rng *>(last);
+        for (size_t k = 0; !r && k < rs.size(); ++k)
+            if (p >= rs[k].base && p < rs[k].base + rs[k].size) r = &rs[k];
+        if (!r) {
+            const char * b = nullptr;
+            size_t sz = 0;
+            if (!buffer_lookup(p, &b, &sz)) return false;  // not a backend buffer
+            rs.push_back(Rng{b, sz, 0});
+            r = &rs.back();
+        }
+        r->used = std::max(r->used, (size_t)(p - r->base) + nb);
+        last = r;
+    }
+    size_t total = 0;
+    for (const Rng & r : rs) total += bc.N * ((r.used + 255) & ~(size_t)255);
+    if (total > d.mem_bytes) {
+        if (d.mem) {
+            TTS_HIP_CHECK(hipStreamSynchronize(d.exec->stream));  // an earlier coalesced step may still use it
+            TTS_HIP_CHECK(hipFree(d.mem));
+        }
+        d.mem_bytes = total + total / 4;
+        if (hipMalloc((void **)&d.mem, d.mem_bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            d.mem = nullptr;
+            d.mem_bytes = 0;
+            return false;
+        }
+    }
+    size_t off = 0;
+    bc.cls.clear();
+    for (const Rng & r : rs) {
+        BatchCls c;
+        c.b0 = r.base;
+        c.size = r.used;
+        c.win = d.mem + off;
+        c.stride = (int64_t)((r.used + 255) & ~(size_t)255);
+        off += bc.N * (size_t)c.stride;
+        bc.cls.push_back(c);
+    }
+    std::sort(bc.cls.begin(), bc.cls.end(), [](const BatchCls & a, const BatchCls & b) { return a.b0 < b.b0; });
+    return true;
 }
 
 // Run one group (the caller holds no lock).  Statuses are written into the requests.
 void run_group(Dev & d, std::vector<Req *> & g) {
     std::lock_guard<std::mutex> xl(d.exec_mu);
     Req * r0 = g[0];
-    // equal signatures: member k's buffer slot j stands for member 0's slot j (same sizes, same offsets)
-    std::vector<Req *> mem{r0};
-    for (size_t k = 1; k < g.size(); ++k)
-        if (g[k]->n == r0->n && g[k]->bufs.size() == r0->bufs.size()) mem.push_back(g[k]);
+    std::vector<Req *> mem;
+    for (Req * q : g)
+        if (q->n == r0->n) mem.push_back(q);
     if (mem.size() < 2) {
         d.refused++;
         return;  // statuses stay kCoalesceNotTaken: every member runs its own graph
     }
     BatchCtx bc;
     bc.N = (int)mem.size();
+    bc.n_nodes = r0->n;
     bc.key = r0->sig;
-    for (Req * m : mem)
-        for (const BufSlot & sl : m->bufs) bc.key = (bc.key ^ (uint64_t)(uintptr_t)sl.base) * 0x100000001B3ull;
-    for (size_t j = 0; j < r0->bufs.size(); ++j) {
-        const BufSlot & s0 = r0->bufs[j];
-        std::vector<const char *> mb(mem.size());
-        bool same = true, vmm = s0.vmm;
-        for (size_t k = 0; k < mem.size(); ++k) {
-            const BufSlot & sk = mem[k]->bufs[j];
-            mb[k] = sk.base;
-            same &= sk.base == s0.base;
-            vmm &= sk.vmm && sk.map_size == s0.map_size && sk.size == s0.size;
-        }
-        if (same) continue;  // one buffer read by every member (stride 0)
-        if (!vmm) {
-            d.refused++;
-            return;
-        }
-        char * w = window_for(d, mb, s0.map_size);
-        if (!w) {
-            d.refused++;
-            return;
-        }
-        BatchCls c;
-        c.b0 = s0.base;
-        c.size = s0.size;
-        c.win = w;
-        c.stride = (int64_t)s0.map_size;
-        c.mb = std::move(mb);
-        bc.cls.push_back(std::move(c));
+    for (Req * m : mem) {
+        bc.mnodes.push_back(m->nodes);
+        bc.key = (bc.key ^ (uint64_t)(uintptr_t)m->be) * 0x100000001B3ull;
     }
-    std::sort(bc.cls.begin(), bc.cls.end(), [](const BatchCls & a, const BatchCls & b) { return a.b0 < b.b0; });
     if (!d.exec) {
         d.exec = tts_hip_backend_init(r0->be->device);
         if (!d.exec) {
             d.refused++;
             return;
         }
+    }
+    if (!exec_layout(d, bc, r0->nodes, r0->n)) {
+        d.refused++;
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_eq_mu);
+        auto gk = g_eq_group.find(bc.key);
+        bc.checked = d.verified.count(bc.key) && gk != g_eq_group.end() && gk->second == g_eq_epoch;
     }
     tts_hip_backend * ex = d.exec;
     copy_options(ex, r0->be);
@@ -418,6 +385,11 @@ void run_group(Dev & d, std::vector<Req *> & g) {
         d.refused++;
         return;
     }
+    if (!bc.checked && st == 0) {
+        d.verified.insert(bc.key);
+        std::lock_guard<std::mutex> lk(g_eq_mu);
+        g_eq_group[bc.key] = g_eq_epoch;
+    }
     TTS_HIP_CHECK(hipEventRecord(ex->co_ev, ex->stream));
     for (Req * m : mem) {
         TTS_HIP_CHECK(hipStreamWaitEvent(m->be->stream, ex->co_ev, 0));
@@ -425,31 +397,39 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     }
     d.launches++;
     d.member_steps += (int64_t)mem.size();
+    if (bc.ragged) d.ragged++;
     if ((int64_t)mem.size() > d.max_group.load()) d.max_group.store((int64_t)mem.size());
 }
 
 }  // namespace
 
-bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::pair<const void *, size_t>> & shared) {
-    return check_shared(g_dev[ex->device % kMaxDev], ex, *ex->bat, shared);
+bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::tuple<const void *, const void *, size_t>> & pairs) {
+    return check_shared(g_dev[ex->device % kMaxDev], ex, *ex->bat, pairs);
 }
 
 // Rendezvous.  A request waits until every active backend (one that submitted a decode step within
-// the last 50 ms) has a request pending, then the requests of the backends furthest behind (lowest
-// step count) run, grouped by graph: runners started at different times fall into step (a backend
-// one step ahead waits for the others' next step), and an idle or finished runner drops out of the
-// active set.  A request that has waited g_wait_us runs with whatever peers it has.  A group of one,
-// or a group refused by run_group, returns kCoalesceNotTaken: each member then runs its own graph.
+// the last 50 ms and has not submitted anything else since) has a request pending, then every pending
+// request runs, grouped by kind of graph: runners that started at different times, at different
+// prompt lengths, share launches at their own KV lengths.  A backend that submits a prompt pass or a
+// codec decode leaves the active set at once (nobody waits for it), an idle or finished one after
+// 50 ms.  A request that has waited g_wait_us runs with whatever peers it has.  A group of one, or a
+// group refused by run_group, returns kCoalesceNotTaken: each member then runs its own graph.
 int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
-    if (!coalesce_enabled() || !be->co_member || be->device >= kMaxDev || !decode_like(nodes, n)) return kCoalesceNotTaken;
+    if (!coalesce_enabled() || !be->co_member || be->device < 0 || be->device >= kMaxDev) return kCoalesceNotTaken;
     Dev & d = g_dev[be->device];
+    if (!decode_like(nodes, n)) {
+        // a prompt pass, a codec decode: this backend is not stepping now -- nobody waits for it
+        std::lock_guard<std::mutex> lk(d.mu);
+        if (d.seen.erase(be)) d.cv.notify_all();
+        return kCoalesceNotTaken;
+    }
     const auto t0 = Clock::now();
     const auto window = std::chrono::milliseconds(50);
     Req r;
     r.be = be;
     r.nodes = nodes;
     r.n = n;
-    r.sig = signature(nodes, n, r.bufs);  // outside the lock, in the caller's thread: ~700 nodes
+    r.sig = signature(nodes, n);  // outside the lock, in the caller's thread: ~1200 nodes
     std::unique_lock<std::mutex> lk(d.mu);
     Act & me = d.seen[be];
     me.t = t0;
@@ -458,6 +438,9 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
     d.pending.push_back(&r);
     d.cv.notify_all();
     const auto deadline = t0 + std::chrono::microseconds(g_wait_us.load());
+    // A request leaves d.pending in the same critical section that marks it done: its owner (which
+    // returns, destroying the stack Req, once it sees done) can only observe done after re-locking, by
+    // which time no list holds it.  Callers re-read d.pending after every run, never an older snapshot.
     auto run = [&](std::vector<Req *> & g) {
         for (Req * q : g) q->taken = true;
         // the caller's own request first: its graph is the one planned (member 0)
@@ -468,6 +451,8 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
             lk.lock();
         }
         for (Req * q : g) q->done = true;
+        d.pending.erase(std::remove_if(d.pending.begin(), d.pending.end(), [](Req * q) { return q->done; }), d.pending.end());
+        d.cv.notify_all();
     };
     while (!r.done) {
         if (r.taken) {
@@ -499,17 +484,16 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
             if (!q->taken) open.push_back(q);
         bool ran = false;
         if ((int)open.size() >= active) {
-            // everyone is here: the backends furthest behind run now, one launch per distinct graph
-            int64_t cmin = INT64_MAX;
-            for (Req * q : open) cmin = std::min(cmin, q->count);
+            // everyone is here: every pending step runs now, one launch per kind of graph (members at
+            // different KV lengths share it)
             std::vector<uint64_t> sigs;
             for (Req * q : open)
-                if (q->count == cmin && std::find(sigs.begin(), sigs.end(), q->sig) == sigs.end()) sigs.push_back(q->sig);
+                if (std::find(sigs.begin(), sigs.end(), q->sig) == sigs.end()) sigs.push_back(q->sig);
             for (uint64_t sg : sigs) {
-                std::vector<Req *> g;
-                for (Req * q : open)
-                    if (q->count == cmin && q->sig == sg && !q->taken) g.push_back(q);
-                run(g);
+                std::vector<Req *> g;  // from d.pending as it is now (an earlier group's members are gone)
+                for (Req * q : d.pending)
+                    if (!q->taken && q->sig == sg) g.push_back(q);
+                if (!g.empty()) run(g);
             }
             ran = true;
         } else if (now >= deadline) {  // waited long enough: run with the peers that share this graph
@@ -519,11 +503,7 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
             run(g);
             ran = true;
         }
-        if (ran) {
-            d.pending.erase(std::remove_if(d.pending.begin(), d.pending.end(), [](Req * q) { return q->done; }), d.pending.end());
-            d.cv.notify_all();
-            continue;
-        }
+        if (ran) continue;
         d.cv.wait_until(lk, deadline);
     }
     d.wait_us += std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count();
@@ -537,27 +517,6 @@ void coalesce_backend_gone(const tts_hip_backend * be) {
     std::lock_guard<std::mutex> lk(d.mu);
     d.seen.erase(be);
     d.cv.notify_all();
-}
-
-void coalesce_forget(const void * base, size_t size) {
-    const char * a = (const char *)base;
-    for (Dev & d : g_dev) {
-        std::lock_guard<std::mutex> xl(d.exec_mu);
-        for (size_t i = 0; i < d.windows.size();) {
-            Window & w = d.windows[i];
-            bool hit = false;
-            for (const char * b : w.bases) hit |= b == a;
-            if (!hit) {
-                ++i;
-                continue;
-            }
-            hipDeviceSynchronize();  // a coalesced step may still read the window
-            for (size_t k = 0; k < w.bases.size(); ++k) hipMemUnmap(w.va + k * w.stride, w.stride);
-            va_free(w.dev, w.va, w.stride * w.bases.size());
-            d.windows.erase(d.windows.begin() + i);
-        }
-    }
-    coalesce_written(base, size);
 }
 
 void coalesce_written(const void * p, size_t size) {
@@ -581,9 +540,9 @@ extern "C" int tts_hip_coalesce_stats(int device, int64_t * out, int n) {
     if (device < 0 || device >= tts::kMaxDev || !out) return TTS_STATUS_BAD_ARG;
     tts::Dev & d = tts::g_dev[device];
     std::lock_guard<std::mutex> lk(d.mu);
-    const int64_t v[6] = {d.launches, d.member_steps, d.alone, d.refused, d.max_group, d.wait_us};
+    const int64_t v[7] = {d.launches, d.member_steps, d.alone, d.refused, d.max_group, d.wait_us, d.ragged};
     int k = 0;
-    for (; k < n && k < 6; ++k) out[k] = v[k];
+    for (; k < n && k < 7; ++k) out[k] = v[k];
     return k;
 }
 

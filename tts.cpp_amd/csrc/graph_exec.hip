@@ -20,6 +20,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include <array>
+
 #include "hip_internal.h"
 #include <chrono>
 
@@ -29,7 +31,9 @@ namespace tts {
 void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int pdim, int blocks);
 void launch_gemv_q4K_xattn(tts_hip_backend * be, const GemvJob & j, const XAttnArgs & a);
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
-                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs = -1, int64_t mbs = 0);
+                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs = -1, int64_t mbs = 0,
+                        const int64_t * koff = nullptr, const int64_t * voff = nullptr, const int64_t * moff = nullptr,
+                        const int * pseq = nullptr);
 void launch_layernorm(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const float * w, const float * b,
                       float eps, bool rms);
 }  // namespace tts
@@ -119,6 +123,7 @@ struct GemvTarget {
     int64_t ycs, yrs;
     int32_t rg = 0, nrep = 1;  // row groups of rg rows, rgs apart; nrep copies, rep apart (floats)
     int64_t rgs = 0, rep = 0;
+    const tts_tensor * yt = nullptr;  // the graph tensor y lies in (null: backend scratch); coalesced steps
 };
 
 struct Item {
@@ -565,6 +570,7 @@ struct Planner {
             return false;
         if (D0->ne[2] != 1 && D0->ne[3] != 1) return false;
         t.y = (float *)D0->data;
+        t.yt = D0;
         t.yrs = 1;
         t.rg = (int32_t)D0->ne[0];
         t.rgs = (int64_t)(D0->nb[1] / 4);
@@ -586,6 +592,7 @@ struct Planner {
             const tts_tensor * D = c;  // view of the K cache: [N] or [N, B] with row stride per sequence
             if (D->type != TTS_TYPE_F32 || D->nb[0] != 4 || D->ne[0] != N || D->ne[1] != M || D->ne[2] * D->ne[3] != 1) return false;
             t.y = (float *)D->data;
+            t.yt = D;
             t.yrs = 1;
             t.ycs = (int64_t)(D->nb[1] / 4);
             skips.push_back(index[c]);
@@ -608,6 +615,7 @@ struct Planner {
                 const tts_tensor * D = cp;
                 if (D->type != TTS_TYPE_F32 || D->ne[0] != 1 || D->ne[1] != N || D->ne[2] * D->ne[3] != M) return false;
                 t.y = (float *)D->data;
+                t.yt = D;
                 t.yrs = (int64_t)(D->nb[1] / 4);
                 t.ycs = (int64_t)(D->nb[2] / 4);
                 skips.push_back(index[C]);
@@ -650,7 +658,8 @@ struct Planner {
         it.kind = Item::GEMV;
         it.epi = EPI_SWIGLU;
         it.mms = {G, U};
-        const GemvTarget t{(float *)E->data, (int64_t)(E->nb[1] / 4), 1};
+        GemvTarget t{(float *)E->data, (int64_t)(E->nb[1] / 4), 1};
+        t.yt = E;
         it.tgt = {t, t};
         act[iS] = act[iU] = act[iE] = -1;
         act[i] = add_item(std::move(it));
@@ -688,10 +697,12 @@ struct Planner {
         g.kind = Item::GEMV;
         g.mms = {G};
         g.tgt = {GemvTarget{(float *)G->data, (int64_t)(G->nb[1] / 4), 1}};
+        g.tgt[0].yt = G;
         Item u;
         u.kind = Item::GEMV;
         u.mms = {U};
         u.tgt = {GemvTarget{(float *)E->data, (int64_t)(E->nb[1] / 4), 1}};
+        u.tgt[0].yt = E;
         u.epi = EPI_SILU_MUL;
         u.res = G;
         act[iS] = act[iE] = -1;
@@ -764,7 +775,8 @@ struct Planner {
             const bool member = j == i || (act[j] == 0 && mm->op == TTS_OP_MUL_MAT && mm->src[1] == x && is_gemv(mm) && compatible(mm));
             if (member) {
                 GemvTarget t{(float *)mm->data, (int64_t)(mm->nb[1] / 4), 1};
-                GemvTarget kt;
+                t.yt = mm;
+                GemvTarget kt{nullptr, 0, 0};
                 std::vector<int> ks;
                 if ((mask & TTS_FUSE_KV) && mm->ne[1] * mm->ne[2] * mm->ne[3] == M && kv_target(mm, M, kt, ks)) t = kt;
                 else ks.clear();
@@ -857,6 +869,7 @@ struct Planner {
                 }
                 if (it.epi != EPI_NONE && (a0->type != TTS_TYPE_F32 || !overlap(E, x))) {
                     it.tgt[0] = GemvTarget{(float *)E->data, (int64_t)(E->ne[0]), 1};  // contiguous: column stride ne0
+                    it.tgt[0].yt = E;
                     act[index[E]] = -1;
                     if (P != mm0) act[iP] = -1;
                 } else {
@@ -903,6 +916,7 @@ struct Planner {
         else return false;
         for (size_t k = 0; k < it.mms.size(); ++k)
             it.tgt.push_back(GemvTarget{(float *)((char *)last->data + k * n1 * last->nb[1]), ycs, 1});
+        for (GemvTarget & t : it.tgt) t.yt = last;
         for (int m : members) act[m] = -1;
         act[index[last]] = add_item(std::move(it));
         return true;
@@ -2023,8 +2037,48 @@ static const void * weight_ptr(tts_hip_backend * be, const tts_tensor * a, bool 
     return be->repack_tmp;
 }
 
-// A coalesced step (be->bat): a one-sequence view becomes the N members' views, sequence k in member
-// k's copy (window + k * stride); a view shared by every member (stride 0) broadcasts.
+// ---- coalesced steps (be->bat, coalesce.hip) ----
+// Member 0's tensor -> its position in the graph: node i itself, its view source, or its source s.
+// Member k's counterpart is the tensor at the same position of member k's graph (the graphs match
+// node by node: same signature, checked item by item in co_prepare).
+struct CoMap {
+    PtrMap<int64_t> pos;  // (i << 5) | slot: 31 = node i, 30 = its view source, s = its src[s]
+    void build(tts_tensor * const * nodes, int n) {
+        pos.reserve((size_t)n * 3);
+        for (int i = 0; i < n; ++i) pos[nodes[i]] = ((int64_t)i << 5) | 31;
+        for (int i = 0; i < n; ++i) {
+            const tts_tensor * t = nodes[i];
+            if (t->view_src && !pos.find(t->view_src)) pos[t->view_src] = ((int64_t)i << 5) | 30;
+            for (int s = 0; s < TTS_MAX_SRC; ++s)
+                if (t->src[s] && !pos.find(t->src[s])) pos[t->src[s]] = ((int64_t)i << 5) | s;
+        }
+    }
+    const tts_tensor * member(const BatchCtx & bc, const tts_tensor * t, int k) {
+        if (k == 0 || !t) return t;
+        auto * e = pos.find(t);
+        if (!e) return nullptr;
+        const int64_t c = e->second;
+        const tts_tensor * nd = bc.mnodes[k][c >> 5];
+        const int slot = (int)(c & 31);
+        const tts_tensor * r = slot == 31 ? nd : slot == 30 ? nd->view_src : nd->src[slot];
+        return r && r->op == t->op && r->type == t->type ? r : nullptr;
+    }
+};
+static const tts_tensor * co_member(const BatchCtx & bc, const tts_tensor * t, int k) {
+    return ((CoMap *)bc.comap)->member(bc, t, k);
+}
+// memory of an input (a leaf marked input, through views): each member's own, never shared
+static bool input_mem(const tts_tensor * t) {
+    for (int hop = 0; t && hop < 8; ++hop) {
+        if (t->op == TTS_OP_NONE) return (t->flags & TTS_FLAG_INPUT) != 0;
+        if (!is_view(t->op)) return false;
+        t = t->view_src ? t->view_src : t->src[0];
+    }
+    return false;
+}
+
+// An intermediate of member 0's graph as the N members' copies along dim 3 (member k's at executor
+// memory win + k * stride); anything else is left as it is (stride 0: read by every member).
 static void batch_td(const BatchCtx & bc, TD & t) {
     const int64_t s = bc.stride(t.data);
     t.data = bc.win(t.data);
@@ -2035,31 +2089,35 @@ static void batch_td(const BatchCtx & bc, TD & t) {
 }
 static int batch_n(const tts_hip_backend * be) { return be->bat ? be->bat->N : 1; }
 
-static int run_attn_item(tts_hip_backend * be, const Item & it) {
+static int run_attn_item(tts_hip_backend * be, const Item & it, const ItemTab * tab = nullptr) {
     TD q = make_td(it.q), k = make_td(it.k), v = make_td(it.v);
     float * out = (float *)it.out->data;
     const float * mask = it.mask ? (const float *)it.mask->data : nullptr;
-    int B = (int)it.q->ne[3];
+    int B = (int)it.q->ne[3], P = (int)it.k->ne[1];
     int64_t obs = -1, mbs = 0;
-    if (const BatchCtx * bc = be->bat) {  // (planner-checked: one sequence per member)
+    if (const BatchCtx * bc = be->bat) {  // (co_prepare-checked: one sequence per member)
         batch_td(*bc, q);
-        batch_td(*bc, k);
-        batch_td(*bc, v);
+        if (tab && tab->koff) k.ne[3] = bc->N, k.nb[3] = 0;  // each member's own cache view: koff
+        else batch_td(*bc, k);
+        if (tab && tab->voff) v.ne[3] = bc->N, v.nb[3] = 0;
+        else batch_td(*bc, v);
         obs = bc->stride(out) / 4;
         out = bc->win(out);
-        if (mask) {
+        if (mask && !(tab && tab->moff)) {
             mbs = bc->stride(mask) / 4;
             mask = bc->win(mask);
         }
         B = bc->N;
+        if (tab && tab->pseq) P = tab->pmax;
     }
     float * out2 = it.shadow && tbytes(it.out) * (size_t)batch_n(be) <= be->shadow_size ? be->shadow : nullptr;
-    launch_attn_decode(be, q, k, v, mask, it.scale, out, (int)it.q->ne[0], (int)it.k->ne[1], (int)it.q->ne[2], (int)it.q->ne[1], B, out2,
-                       obs, mbs);
+    launch_attn_decode(be, q, k, v, mask, it.scale, out, (int)it.q->ne[0], P, (int)it.q->ne[2], (int)it.q->ne[1], B, out2, obs, mbs,
+                       tab ? tab->koff : nullptr, tab ? tab->voff : nullptr, tab ? tab->moff : nullptr, tab ? tab->pseq : nullptr);
     return 0;
 }
 
-static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xattn = nullptr) {
+static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xattn = nullptr, const ItemTab * tab = nullptr,
+                         const ItemTab * xtab = nullptr) {
     const tts_tensor * mm0 = it.mms[0];
     const tts_tensor * a0 = mm0->src[0];
     // a skipped CONT (it.xsrc): its contiguous source holds the same bytes; read them in src1's shape
@@ -2196,10 +2254,19 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             xa.H = (int)A.q->ne[2];
             xa.B = (int)A.q->ne[3];
             if (bc) {
-                batch_td(*bc, xa.k);
-                batch_td(*bc, xa.v);
-                xa.mbs = bc->stride(xa.mask) / 4;
-                xa.mask = bc->win(xa.mask);
+                if (xtab && xtab->koff) xa.k.ne[3] = NB, xa.k.nb[3] = 0;  // each member's own cross K / V: offset tables
+                else batch_td(*bc, xa.k);
+                if (xtab && xtab->voff) xa.v.ne[3] = NB, xa.v.nb[3] = 0;
+                else batch_td(*bc, xa.v);
+                if (xtab && xtab->moff) {
+                    xa.moff = xtab->moff;
+                } else {
+                    xa.mbs = bc->stride(xa.mask) / 4;
+                    xa.mask = bc->win(xa.mask);
+                }
+                xa.koff = xtab ? xtab->koff : nullptr;
+                xa.voff = xtab ? xtab->voff : nullptr;
+                if (xtab && xtab->pseq) xa.pseq = xtab->pseq, xa.P = xtab->pmax;
                 xa.obs = bc->stride(xa.out) / 4;
                 xa.out = bc->win(xa.out);
                 xa.B = (int)NB;
@@ -2228,6 +2295,11 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         jj.nmat = 0;
         jj.hetero = 0;
         jj.roff[0] = 0;
+        if (bc && tab && tab->yoff) {  // members' own KV-cache rows: per-column store offsets ([target][N])
+            jj.yoff = tab->yoff + k * NB;
+            jj.yoff_ld = (int32_t)NB;
+            jj.yoff_mats = (int32_t)((uint32_t)tab->yoff_mats >> k);
+        }
         while (k < it.mms.size() && jj.nmat < GEMV_MAX_MATS) {
             const tts_tensor * a = it.mms[k]->src[0];
             // matrices of another row count share a launch only on the tile-layout kernels
@@ -2254,7 +2326,7 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
         if (jj.hetero) jj.N = 0;  // every row count comes from roff
         launch_gemv_job(be, jj);
     }
-    if (xattn) return run_attn_item(be, *xattn);  // unfused fallback: the attention right after its query
+    if (xattn) return run_attn_item(be, *xattn, xtab);  // unfused fallback: the attention right after its query
     return 0;
 }
 
@@ -2279,8 +2351,8 @@ static void launch_gather_t(tts_hip_backend * be, const tts_tensor * dst, const 
 
 static int run_node(tts_hip_backend * be, const tts_tensor * n);
 
-// A tensor of member 0's graph as the N members' tensors along dim 3 (member k's copy at window + k *
-// stride); shared tensors (weights, stride 0) are left as they are and broadcast.
+// An intermediate of member 0's graph as the N members' copies along dim 3 (member k's at executor memory
+// win + k * stride); read-only model data (stride 0) is left as it is and broadcast.
 static bool batch_tensor(const BatchCtx & bc, const tts_tensor * t, tts_tensor & o) {
     o = *t;
     const int64_t s = bc.stride(t->data);
@@ -2292,9 +2364,10 @@ static bool batch_tensor(const BatchCtx & bc, const tts_tensor * t, tts_tensor &
     return true;
 }
 
-// An unfused node of a coalesced step.  Ops that act on every dim-3 slice on its own (elementwise
-// with broadcasting, norms, copies, concat below dim 3) run once over the members' tensors; any other
-// op runs once per member on that member's own addresses.
+// An unfused node of a coalesced step (n: member 0's node).  Ops that act on every dim-3 slice on its
+// own (elementwise with broadcasting, norms, copies, concat below dim 3) run once over the members'
+// intermediates when no input or member-owned tensor is involved; any other node runs once per member,
+// on that member's own tensors (inputs, caches) and its executor copies of the intermediates.
 static int run_node_coalesced(tts_hip_backend * be, const tts_tensor * n) {
     const BatchCtx & bc = *be->bat;
     bool per_slice = false;
@@ -2308,29 +2381,42 @@ static int run_node_coalesced(tts_hip_backend * be, const tts_tensor * n) {
         default: break;
     }
     tts_tensor t, srcs[TTS_MAX_SRC];
-    if (per_slice && bc.stride(n->data) && batch_tensor(bc, n, t)) {
+    if (per_slice && !persistent_mem(n) && bc.stride(n->data) && batch_tensor(bc, n, t)) {
         for (int i = 0; i < TTS_MAX_SRC && per_slice; ++i) {
-            if (!n->src[i]) continue;
-            per_slice = batch_tensor(bc, n->src[i], srcs[i]);
+            const tts_tensor * x = n->src[i];
+            if (!x) continue;
+            // an input is each member's own; read-only model data (checked equal, co_prepare) broadcasts
+            if (input_mem(x) || (!persistent_mem(x) && !bc.stride(x->data))) {
+                per_slice = false;
+                break;
+            }
+            per_slice = batch_tensor(bc, x, srcs[i]);
             // a copy reads as many elements as it writes: its source must be per member too
-            if ((n->op == TTS_OP_CONT || n->op == TTS_OP_CPY || n->op == TTS_OP_DUP) && !bc.stride(n->src[i]->data)) per_slice = false;
+            if ((n->op == TTS_OP_CONT || n->op == TTS_OP_CPY || n->op == TTS_OP_DUP) && !bc.stride(x->data)) per_slice = false;
             t.src[i] = &srcs[i];
         }
         if (per_slice) return launch_op(be, &t);
     }
-    const BatchCtx * keep = be->bat;
-    be->bat = nullptr;  // member k's own graph node, run as in an uncoalesced step
+    BatchCtx * keep = be->bat;
+    be->bat = nullptr;  // member k's own node, run as in an uncoalesced step
     int st = 0;
+    auto addr = [&](const tts_tensor * x, int k) -> void * {  // member k's bytes of member 0's tensor x
+        if (!persistent_mem(x)) return bc.reloc(x->data, k);
+        const tts_tensor * m = co_member(bc, x, k);
+        return m ? m->data : nullptr;
+    };
     for (int k = 0; k < bc.N && st == 0; ++k) {
         t = *n;
-        t.data = bc.reloc(n->data, k);
+        t.data = addr(n, k);
         for (int i = 0; i < TTS_MAX_SRC; ++i) {
             if (!n->src[i]) continue;
             srcs[i] = *n->src[i];
-            srcs[i].data = bc.reloc(n->src[i]->data, k);
+            srcs[i].data = addr(n->src[i], k);
+            if (!srcs[i].data) st = TTS_STATUS_FAILED;
             t.src[i] = &srcs[i];
         }
-        st = run_node(be, &t);
+        if (!t.data) st = TTS_STATUS_FAILED;
+        if (st == 0) st = run_node(be, &t);
     }
     be->bat = keep;
     return st;
@@ -2346,6 +2432,7 @@ static int run_node(tts_hip_backend * be, const tts_tensor * n) {
             it.kind = Item::GEMV;
             it.mms.push_back(n);
             it.tgt.push_back(GemvTarget{(float *)n->data, (int64_t)(n->nb[1] / 4), 1});
+            it.tgt.back().yt = n;
             return run_gemv_item(be, it);
         }
         const int t = n->src[0]->type;
@@ -2356,11 +2443,15 @@ static int run_node(tts_hip_backend * be, const tts_tensor * n) {
 }
 
 static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Item> & items) {
+    // a coalesced plan's tables of member-owned operands (co_prepare), by item index
+    const ItemTab * tab = be->bat ? &be->bat->tabs[&it - items.data()] : nullptr;
     switch (it.kind) {
-        case Item::GEMV: return run_gemv_item(be, it, it.xattn >= 0 ? &items[it.xattn] : nullptr);
+        case Item::GEMV:
+            return run_gemv_item(be, it, it.xattn >= 0 ? &items[it.xattn] : nullptr, tab,
+                                 be->bat && it.xattn >= 0 ? &be->bat->tabs[it.xattn] : nullptr);
         case Item::ATTN:
             if (it.fused) return 0;  // launched with its query GEMV
-            return run_attn_item(be, it);
+            return run_attn_item(be, it, tab);
         case Item::LN:
             if (be->bat) {  // rows of every member (planner-checked: one-row tensors of member buffers)
                 tts_tensor d, x;
@@ -2372,7 +2463,7 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
             return 0;
         case Item::EMBED:
             if (it.gather_t) launch_gather_t(be, it.dst, it.w, it.gt_codes);
-            else launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size(), be->bat);
+            else launch_embed_sum(be, it.dst, it.terms.data(), (int)it.terms.size(), be->bat, tab);
             return 0;
         case Item::SNAKE:
             launch_snake(be, it.dst, it.x, it.w, it.b, it.snake_one, it.snake_mask);
@@ -2416,56 +2507,255 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
     return TTS_STATUS_FAILED;
 }
 
-// Whether member 0's plan can run as a coalesced step: every item kind has a batched launch (or a
-// per-member one), every product and attention is one column / sequence per member, and every tensor
-// an item writes lies in a member buffer.  Checked before anything is launched: a refused step is run
-// by each member on its own instead.
-static bool coalescable(const tts_hip_backend * be, const Planner & pl, tts_tensor * const * nodes, int n_nodes,
-                        std::vector<std::pair<const void *, size_t>> & shared) {
-    const BatchCtx & bc = *be->bat;
-    auto share = [&](const tts_tensor * t) {
-        if (t && t->data) shared.emplace_back(t->data, tbytes(t));
+// A node of a coalesced step launched once over every member's intermediates (run_node_coalesced's
+// rule): a per-slice op whose output and sources are intermediates or read-only model data.
+static bool co_per_slice(const BatchCtx & bc, const tts_tensor * n) {
+    switch (n->op) {
+        case TTS_OP_ADD: case TTS_OP_SUB: case TTS_OP_MUL: case TTS_OP_DIV: case TTS_OP_SQR: case TTS_OP_SQRT: case TTS_OP_SIN:
+        case TTS_OP_COS: case TTS_OP_SCALE: case TTS_OP_CLAMP: case TTS_OP_LEAKY_RELU: case TTS_OP_UNARY: case TTS_OP_ROUND:
+        case TTS_OP_MOD: case TTS_OP_NORM: case TTS_OP_RMS_NORM: case TTS_OP_CONT: case TTS_OP_CPY: case TTS_OP_DUP: break;
+        case TTS_OP_CONCAT:
+            if (n->op_params[0] < 3) break;
+            return false;
+        default: return false;
+    }
+    if (persistent_mem(n) || !bc.stride(n->data) || n->ne[3] != 1) return false;
+    for (int i = 0; i < TTS_MAX_SRC; ++i) {
+        const tts_tensor * x = n->src[i];
+        if (!x) continue;
+        if (input_mem(x) || (!persistent_mem(x) && !bc.stride(x->data))) return false;
+        if (bc.stride(x->data) && x->ne[3] != 1) return false;
+        if ((n->op == TTS_OP_CONT || n->op == TTS_OP_CPY || n->op == TTS_OP_DUP) && !bc.stride(x->data)) return false;
+    }
+    return true;
+}
+
+// Everything a coalesced step needs before its first launch, or false (nothing launched; each member
+// then runs its own graph):
+//  - every item has a batched form, with one column / sequence per member;
+//  - member k's graph matches member 0's item by item: the same shapes everywhere except each
+//    attention's key count (the members' KV lengths);
+//  - the tables of member-owned operands (ItemTab, as offsets into `tab` until uploaded): each
+//    member's KV-cache store rows, cache / cross views, masks and input indices;
+//  - the read-only operands read through member 0's copy: (member 0's, member k's, bytes) pairs whose
+//    bytes must be equal;
+//  - the output copies: the graph's output intermediates, from the executor memory to each member's
+//    own tensor (src, dst, bytes triples in `tab` at *scatter, *n_scatter of them).
+static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * nodes, int n_nodes,
+                       std::vector<std::tuple<const void *, const void *, size_t>> & shared, std::vector<int64_t> & tab,
+                       std::vector<std::array<int64_t, 5>> & offs, int64_t * scatter, int * n_scatter) {
+    BatchCtx & bc = *be->bat;
+    CoMap & cm = *(CoMap *)bc.comap;
+    const int N = bc.N;
+    auto same_ne = [](const tts_tensor * a, const tts_tensor * b) {
+        return a && b && a->ne[0] == b->ne[0] && a->ne[1] == b->ne[1] && a->ne[2] == b->ne[2] && a->ne[3] == b->ne[3];
     };
+    auto inter = [&](const tts_tensor * t) { return t && !persistent_mem(t) && bc.stride(t->data) != 0; };
+    auto equal_all = [&](const tts_tensor * t) {  // every member's counterpart has t's shape
+        if (bc.checked) return true;
+        for (int k = 1; k < N; ++k)
+            if (!same_ne(t, cm.member(bc, t, k))) return false;
+        return true;
+    };
+    auto share = [&](const tts_tensor * t) {  // read-only data read through member 0's copy
+        if (!t || bc.checked) return true;
+        for (int k = 1; k < N; ++k) {
+            const tts_tensor * m = cm.member(bc, t, k);
+            if (!same_ne(t, m) || !m->data) return false;
+            if (m->data != t->data) shared.emplace_back(t->data, m->data, tbytes(t));
+        }
+        return true;
+    };
+    auto alloc = [&](size_t n64) {
+        const int64_t o = (int64_t)tab.size();
+        tab.resize(tab.size() + n64, 0);
+        return o;
+    };
+    // per-member byte offsets of member k's counterpart of t from t (null: not resolvable)
+    auto offsets = [&](const tts_tensor * t, int64_t o, int64_t unit) {
+        for (int k = 0; k < N; ++k) {
+            const tts_tensor * m = cm.member(bc, t, k);
+            if (!m || !m->data) return false;
+            const int64_t d = (int64_t)((const char *)m->data - (const char *)t->data);
+            if (d % unit) return false;
+            tab[o + k] = d / unit;
+        }
+        return true;
+    };
+    bc.tabs.assign(pl.items.size(), ItemTab{});
+    offs.assign(pl.items.size(), std::array<int64_t, 5>{-1, -1, -1, -1, -1});
+    std::vector<std::array<int64_t, EMBED_MAX_TERMS>> ioffs(pl.items.size());
+    for (auto & r : ioffs) r.fill(-1);
     for (int i = 0; i < n_nodes; ++i) {
         const int a = pl.act[i];
-        if (a <= 0) {
-            if (a == 0 && !is_view(nodes[i]->op) && !bc.stride(nodes[i]->data)) return false;  // a shared tensor written by every member
+        const tts_tensor * nd = nodes[i];
+        if (a < 0) continue;
+        if (a == 0) {
+            if (is_view(nd->op)) continue;
+            if (!equal_all(nd)) return false;
+            for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
+                if (nd->src[s2] && !equal_all(nd->src[s2])) return false;
+            if (co_per_slice(bc, nd))
+                for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
+                    if (nd->src[s2] && persistent_mem(nd->src[s2]) && !share(nd->src[s2])) return false;
             continue;
         }
-        const Item & it = pl.items[a - 1];
+        Item & it = pl.items[a - 1];
+        ItemTab & tb = bc.tabs[a - 1];
+        auto & of = offs[a - 1];
         switch (it.kind) {
             case Item::GEMV: {
+                if (it.epi == EPI_SWIGLU || it.epi == EPI_SILU_MUL) return false;
                 const tts_tensor * x = it.mms[0]->src[1];
-                if (nel(x) != x->ne[0] || it.epi == EPI_SWIGLU || it.epi == EPI_SILU_MUL) return false;
-                for (const GemvTarget & t : it.tgt)
-                    if (!bc.stride(t.y)) return false;
-                if (it.ln && it.lndst && !bc.stride(it.lndst->data)) return false;
-                for (const tts_tensor * mm : it.mms) share(mm->src[0]);  // the weights
-                if (it.ln) share(it.lnw), share(it.lnb);
-                break;
-            }
-            case Item::ATTN:
-                if (it.q->ne[3] != 1 || it.k->ne[3] != 1 || it.v->ne[3] != 1 || !bc.stride(it.out->data)) return false;
-                if (it.mask && it.mask->ne[2] * it.mask->ne[3] != 1) return false;
-                break;
-            case Item::LN:
-                if (it.dst->ne[3] != 1 || it.x->ne[3] != 1 || !bc.stride(it.dst->data) || !bc.stride(it.x->data)) return false;
-                share(it.w), share(it.b);
-                break;
-            case Item::EMBED:
-                if (it.gather_t || it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3] != 1 || !bc.stride(it.dst->data)) return false;
-                for (const tts_tensor * g : it.terms) {
-                    if (g->ne[1] * g->ne[2] * g->ne[3] != 1) return false;
-                    share(g->src[0]);  // the table
+                if (nel(x) != x->ne[0]) return false;  // one column per member
+                const tts_tensor * xt = it.ln ? it.lnx : it.xsrc ? it.xsrc : x;
+                if (!it.x_shadow && !inter(xt)) return false;
+                if (it.res && !inter(it.res)) return false;
+                if (it.ln && it.lndst && !inter(it.lndst)) return false;
+                if (it.ln && (!share(it.lnw) || !share(it.lnb))) return false;
+                bool owned = false;
+                for (size_t k = 0; k < it.mms.size(); ++k) {
+                    if (!equal_all(it.mms[k]) || !share(it.mms[k]->src[0])) return false;
+                    const GemvTarget & t = it.tgt[k];
+                    if (!t.yt) return false;  // backend scratch (a hoisted product): no per-member form
+                    if (!persistent_mem(t.yt)) {
+                        if (!bc.stride(t.y)) return false;
+                        continue;
+                    }
+                    if (bc.stride(t.y)) return false;  // member-owned memory inside a compute buffer: no uniform form
+                    owned = true;
+                }
+                if (owned) {  // members' own cache rows (KV stores): [target][N] float offsets
+                    of[0] = alloc(it.mms.size() * (size_t)N);
+                    for (size_t k = 0; k < it.mms.size(); ++k) {
+                        const GemvTarget & t = it.tgt[k];
+                        if (!persistent_mem(t.yt)) continue;
+                        if (k >= 32 || !equal_all(t.yt) || !offsets(t.yt, of[0] + (int64_t)k * N, 4)) return false;
+                        tb.yoff_mats |= 1 << k;
+                    }
                 }
                 break;
-            case Item::NODE:
-                if (!bc.stride(it.node.data)) return false;
+            }
+            case Item::ATTN: {
+                if (it.q->ne[3] != 1 || !inter(it.q) || !inter(it.out) || !equal_all(it.q) || !equal_all(it.out)) return false;
+                if (it.mask && it.mask->ne[2] * it.mask->ne[3] != 1) return false;
+                // each member's own key count; K [hd, P, Hk], V [P, hd, Hv] with the cache's strides
+                of[3] = alloc(((size_t)N + 1) / 2);
+                int * pseq = (int *)&tab[of[3]];
+                int pmax = 0;
+                bool ragged = false;
+                for (int k = 0; k < N; ++k) {
+                    const tts_tensor * mk = cm.member(bc, it.k, k);
+                    const tts_tensor * mv = cm.member(bc, it.v, k);
+                    if (!mk || !mv || mk->ne[0] != it.k->ne[0] || mk->ne[2] != it.k->ne[2] || mk->ne[3] != 1 || mv->ne[1] != it.v->ne[1] ||
+                        mv->ne[2] != it.v->ne[2] || mv->ne[3] != 1 || mv->ne[0] != mk->ne[1] || mk->nb[1] != it.k->nb[1] ||
+                        mk->nb[2] != it.k->nb[2] || mv->nb[1] != it.v->nb[1] || mv->nb[2] != it.v->nb[2] || mk->nb[0] != it.k->nb[0] ||
+                        mv->nb[0] != it.v->nb[0])
+                        return false;
+                    pseq = (int *)&tab[of[3]];  // (tab may have moved)
+                    pseq[k] = (int)mk->ne[1];
+                    pmax = std::max(pmax, (int)mk->ne[1]);
+                    ragged |= mk->ne[1] != it.k->ne[1];
+                    if (it.mask) {
+                        const tts_tensor * mm = cm.member(bc, it.mask, k);
+                        if (!mm || mm->ne[0] != mk->ne[1] || mm->ne[1] < it.q->ne[1]) return false;
+                    }
+                }
+                tb.pmax = pmax;
+                bc.ragged |= ragged;
+                for (int w = 0; w < 2; ++w) {  // K, V: an intermediate (equal lengths only) or each member's own view
+                    const tts_tensor * kv = w ? it.v : it.k;
+                    if (inter(kv)) {
+                        if (ragged) return false;
+                        continue;
+                    }
+                    if (bc.stride(kv->data)) return false;
+                    of[1 + w] = alloc(N);
+                    if (!offsets(kv, of[1 + w], 16)) return false;  // 16-B aligned: the kernels' vector loads
+                    for (int k = 0; k < N; ++k) tab[of[1 + w] + k] *= 16;
+                }
+                if (it.mask) {
+                    if (inter(it.mask)) {
+                        if (ragged) return false;
+                    } else {
+                        of[4] = alloc(N);
+                        if (!offsets(it.mask, of[4], 4)) return false;
+                    }
+                }
                 break;
+            }
+            case Item::LN:
+                if (it.dst->ne[3] != 1 || it.x->ne[3] != 1 || !inter(it.dst) || !inter(it.x) || !equal_all(it.dst) || !equal_all(it.x)) return false;
+                if (!share(it.w) || !share(it.b)) return false;
+                break;
+            case Item::EMBED:
+                if (it.gather_t || it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3] != 1 || !inter(it.dst) || !equal_all(it.dst)) return false;
+                if (it.terms.size() > (size_t)EMBED_MAX_TERMS) return false;
+                for (size_t t = 0; t < it.terms.size(); ++t) {
+                    const tts_tensor * g = it.terms[t];
+                    if (g->ne[1] * g->ne[2] * g->ne[3] != 1 || !equal_all(g) || !share(g->src[0])) return false;
+                    const tts_tensor * idx = g->src[1];
+                    if (inter(idx)) continue;
+                    if (!input_mem(idx) || !equal_all(idx)) return false;
+                    ioffs[a - 1][t] = alloc(N);
+                    if (!offsets(idx, ioffs[a - 1][t], 4)) return false;
+                }
+                break;
+            case Item::NODE: {
+                // its node copy stands at the original's graph position (run_node_coalesced finds members' tensors by it)
+                auto * e = cm.pos.find(nd);
+                if (!e) return false;
+                cm.pos[&it.node] = e->second;
+                if (!equal_all(nd)) return false;
+                for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2) {
+                    const tts_tensor * x = it.node.src[s2];
+                    if (!x) continue;
+                    if (!cm.pos.find(x) && persistent_mem(x)) return false;  // a stand-in over member-owned memory
+                    if (cm.pos.find(x) && !equal_all(x)) return false;
+                }
+                if (co_per_slice(bc, &it.node))
+                    for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
+                        if (it.node.src[s2] && persistent_mem(it.node.src[s2]) && !share(it.node.src[s2])) return false;
+                break;
+            }
             default: return false;  // LSTM / SNAKE / CONV / ADAIN / MCPY / RINT / COPY: vocoder and prefill items
         }
     }
+    // the output intermediates back to every member: the last node and nodes marked output
+    *n_scatter = 0;
+    std::vector<const tts_tensor *> outs;
+    for (int i = 0; i < n_nodes; ++i)
+        if ((nodes[i]->flags & TTS_FLAG_OUTPUT) || i == n_nodes - 1) outs.push_back(nodes[i]);
+    std::vector<std::array<int64_t, 3>> sc;
+    for (const tts_tensor * o : outs) {
+        if (persistent_mem(o) || is_view(o->op)) continue;  // written in place per member (or a view of what is)
+        if (!inter(o) || !contiguous(o) || (tbytes(o) & 3) || !equal_all(o)) return false;
+        for (int k = 0; k < N; ++k) {
+            const tts_tensor * m = cm.member(bc, o, k);
+            if (!m || !m->data || !contiguous(m)) return false;
+            sc.push_back({(int64_t)(uintptr_t)bc.reloc(o->data, k), (int64_t)(uintptr_t)m->data, (int64_t)tbytes(o)});
+        }
+    }
+    if (!sc.empty()) {
+        *scatter = alloc(3 * sc.size());
+        for (size_t e = 0; e < sc.size(); ++e)
+            for (int c = 0; c < 3; ++c) tab[*scatter + 3 * (int64_t)e + c] = sc[e][c];
+        *n_scatter = (int)sc.size();
+    }
+    for (size_t a = 0; a < pl.items.size(); ++a)
+        for (int t = 0; t < EMBED_MAX_TERMS; ++t)
+            if (ioffs[a][t] >= 0) bc.tabs[a].ioff[t] = (const int64_t *)(intptr_t)(ioffs[a][t] + 1);  // offset + 1 until uploaded
     return true;
+}
+
+// A coalesced step's output copies: entry e = (src, dst, bytes), one workgroup row per entry.
+__global__ void k_co_scatter(const int64_t * __restrict__ tab, int n) {
+    const int e = blockIdx.y;
+    if (e >= n) return;
+    const uint32_t * src = (const uint32_t *)(uintptr_t)tab[3 * e];
+    uint32_t * dst = (uint32_t *)(uintptr_t)tab[3 * e + 1];
+    const int64_t w = tab[3 * e + 2] / 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w; i += (int64_t)gridDim.x * blockDim.x) dst[i] = src[i];
 }
 
 // Replay through a HIP graph only for step-sized graphs: prompt-sized ones (many activation
@@ -2669,9 +2959,46 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
     if (be->fusion) pl.build(nodes, n_nodes);
     else pl.act.assign(n_nodes, 0);
     be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
+    // a coalesced step: checks, the member-owned operand tables (uploaded before any launch) and the
+    // output copies (co_prepare)
+    CoMap cm;
+    int64_t sc_off = -1;
+    int n_sc = 0;
     if (be->bat) {
-        std::vector<std::pair<const void *, size_t>> shared;
-        if (!coalescable(be, pl, nodes, n_nodes, shared) || !coalesce_check_shared(be, shared)) return TTS_STATUS_UNSUPPORTED;
+        BatchCtx & bc = *be->bat;
+        cm.build(nodes, n_nodes);
+        bc.comap = &cm;
+        std::vector<std::tuple<const void *, const void *, size_t>> shared;
+        std::vector<int64_t> tab;
+        std::vector<std::array<int64_t, 5>> offs;
+        if (!co_prepare(be, pl, nodes, n_nodes, shared, tab, offs, &sc_off, &n_sc) || !coalesce_check_shared(be, shared)) {
+            bc.comap = nullptr;
+            return TTS_STATUS_UNSUPPORTED;
+        }
+        if (!tab.empty()) {
+            const size_t bytes = tab.size() * sizeof(int64_t);
+            if (bytes > be->co_tab_bytes) {
+                TTS_HIP_CHECK(hipStreamSynchronize(be->stream));  // the previous tables may still be read
+                if (be->co_tab) TTS_HIP_CHECK(hipFree(be->co_tab));
+                be->co_tab_bytes = std::max(bytes * 2, (size_t)64 << 10);
+                TTS_HIP_CHECK(hipMalloc((void **)&be->co_tab, be->co_tab_bytes));
+            }
+            if (tts_hip_tensor_set_async(be, be->co_tab, tab.data(), bytes) != 0) {
+                bc.comap = nullptr;
+                return TTS_STATUS_UNSUPPORTED;
+            }
+        }
+        for (size_t a = 0; a < pl.items.size(); ++a) {
+            ItemTab & tb = bc.tabs[a];
+            const auto & of = offs[a];
+            tb.yoff = of[0] >= 0 ? be->co_tab + of[0] : nullptr;
+            tb.koff = of[1] >= 0 ? be->co_tab + of[1] : nullptr;
+            tb.voff = of[2] >= 0 ? be->co_tab + of[2] : nullptr;
+            tb.pseq = of[3] >= 0 ? (const int *)(be->co_tab + of[3]) : nullptr;
+            tb.moff = of[4] >= 0 ? be->co_tab + of[4] : nullptr;
+            for (auto & io : tb.ioff)
+                if (io) io = be->co_tab + ((intptr_t)io - 1);
+        }
     }
     // long-context attention items in launch order: each one's K/V is prefetched into MALL on the
     // side stream right after the previous one ran (fork), and joined just before it runs
@@ -2744,6 +3071,13 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
         }
     }
     if (pf_pending >= 0) TTS_HIP_CHECK(hipStreamWaitEvent(be->stream, be->pf_join, 0));  // every fork rejoins
+    if (be->bat) {
+        if (n_sc > 0) {  // the output intermediates to every member's own tensors
+            hipLaunchKernelGGL(k_co_scatter, dim3(4, (unsigned)n_sc), dim3(256), 0, be->stream, (const int64_t *)be->co_tab + sc_off, n_sc);
+            TTS_HIP_CHECK(hipGetLastError());
+        }
+        be->bat->comap = nullptr;
+    }
     return 0;
 }
 }  // namespace tts

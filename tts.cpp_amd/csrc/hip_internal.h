@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <deque>
 #include <unordered_map>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -233,6 +234,11 @@ struct GemvJob {
     int64_t bq_bytes = 0;
     int64_t bq_tile = 0;  // > 0: columns in tiles of 16, tile c's operands at bq + c * bq_tile (its own slot layout)
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
+    // ragged columns (a coalesced step's KV-cache stores, coalesce.hip): for the matrices in yoff_mats,
+    // column m of matrix mat is stored at Y[mat] + m * ycs + yoff[mat * yoff_ld + m] (floats) -- each
+    // member's cache row at its own position
+    const int64_t * yoff = nullptr;
+    int32_t yoff_mats = 0, yoff_ld = 0;
 };
 __host__ __device__ inline int64_t job_roff(const GemvJob & j, int m) { return j.hetero ? j.roff[m] : (int64_t)m * j.N; }
 __host__ __device__ inline int64_t job_rows(const GemvJob & j) { return job_roff(j, j.nmat); }
@@ -263,27 +269,53 @@ struct XAttnArgs {
     int P = 0, H = 0, B = 0;
     int64_t obs = 0;               // floats between sequences of out (0: H * hd, contiguous)
     int64_t mbs = 0;               // floats between sequences' masks (0: one mask for all)
+    // ragged sequences (coalesce.hip): per-sequence K / V byte offsets, mask offsets (floats), key counts
+    const int64_t * koff = nullptr;
+    const int64_t * voff = nullptr;
+    const int64_t * moff = nullptr;
+    const int * pseq = nullptr;
 };
 
-// A coalesced decode step (coalesce.hip): N isomorphic one-prompt graphs of different backends
-// (TTS.cpp's server runs one runner per worker, examples/server/server.cpp:316-321) run as ONE
-// plan of member 0's graph with M = N columns.  Every buffer member 0's graph reads or writes
-// (compute arena, KV cache, inputs) has a counterpart in each member at the same offset; the N
-// counterparts are mapped into one virtual window at a fixed stride (hipMemMap of their physical
-// allocations), so member k's copy of a tensor is window + k * stride + offset: one uniform column
-// stride, which every GEMV / attention kernel already takes.  Weights are shared (member 0's copy;
-// the others hold identical bytes, checked by content hash at upload).
+// A coalesced decode step (coalesce.hip): N one-prompt decode graphs of different backends (TTS.cpp's
+// server runs one runner per worker, examples/server/server.cpp:316-321) that differ at most in their KV
+// lengths run as ONE plan of member 0's graph with M = N columns / B = N sequences.
+//  - Intermediates (every tensor the graph allocator placed, i.e. not a leaf or a view of one) are
+//    computed in executor-owned memory laid out as member 0's compute buffer, member k at win + k *
+//    stride: one uniform column / sequence stride, which the GEMV, attention, norm and embedding
+//    kernels take.  The graph's output node is copied to each member's own tensor afterwards.
+//  - Member-owned operands (KV-cache views read by attention and written by the K / V store
+//    epilogues, masks and token / position inputs) are each member's own tensors, found by node
+//    position in its graph, and reach the kernels as per-member offset tables (ItemTab), together
+//    with each member's own key count.
+//  - Read-only model data (weights, norms, tables) is read through member 0's copy, checked equal to
+//    each member's own copy on the device first.
+constexpr int EMBED_MAX_TERMS = 16;
 struct BatchCls {
     const char * b0 = nullptr;  // member 0's buffer
     size_t size = 0;
-    char * win = nullptr;       // window: member k's buffer at win + k * stride
+    char * win = nullptr;       // executor memory: member k's copy of the range at win + k * stride
     int64_t stride = 0;
-    std::vector<const char *> mb;  // every member's own buffer (relocated one-member launches)
+};
+// per-item tables of member-owned operands (device pointers, valid for the current coalesced plan)
+struct ItemTab {
+    const int64_t * yoff = nullptr;  // GEMV: [nmat][N] store offsets (floats) of the matrices in yoff_mats
+    int32_t yoff_mats = 0;
+    const int64_t *koff = nullptr, *voff = nullptr;  // ATTN: K / V view offsets per member (bytes)
+    const int64_t * moff = nullptr;                  // ATTN: mask offsets per member (floats)
+    const int * pseq = nullptr;                      // ATTN: key count per member
+    int pmax = 0;
+    const int64_t * ioff[EMBED_MAX_TERMS] = {};      // EMBED: index offsets per member (elements)
 };
 struct BatchCtx {
     int N = 0;
-    uint64_t key = 0;  // the group: its graph signature and every member's buffers (coalesce.hip caches per key)
+    uint64_t key = 0;  // the group: graph signature and member backends (coalesce.hip caches per key)
     std::vector<BatchCls> cls;  // sorted by b0
+    std::vector<tts_tensor * const *> mnodes;  // every member's node list (member 0's first; equal lengths)
+    int n_nodes = 0;
+    bool checked = false;       // this group's shapes and read-only operands were verified by an earlier step
+    bool ragged = false;        // (co_prepare) the members' KV lengths differ
+    std::vector<ItemTab> tabs;  // per plan item (graph_exec.hip)
+    void * comap = nullptr;     // graph_exec.hip: member 0's tensors -> graph positions (member k's counterparts)
     const BatchCls * find(const void * p) const {
         const char * c = (const char *)p;
         size_t lo = 0, hi = cls.size();
@@ -296,20 +328,20 @@ struct BatchCtx {
         const BatchCls & b = cls[lo - 1];
         return c < b.b0 + b.size ? &b : nullptr;
     }
-    // the window address of member 0's pointer p (p itself when it is shared by every member)
+    // the executor address of member 0's intermediate p (p itself when it is not one)
     template <typename T>
     T * win(T * p) const {
         const BatchCls * b = p ? find(p) : nullptr;
         return b ? (T *)(b->win + ((const char *)p - b->b0)) : p;
     }
-    int64_t stride(const void * p) const {  // bytes between members' copies (0: shared)
+    int64_t stride(const void * p) const {  // bytes between members' copies (0: not an intermediate)
         const BatchCls * b = p ? find(p) : nullptr;
         return b ? b->stride : 0;
     }
     template <typename T>
-    T * reloc(T * p, int k) const {  // member k's own address of member 0's pointer p
+    T * reloc(T * p, int k) const {  // member k's executor copy of member 0's intermediate p
         const BatchCls * b = p ? find(p) : nullptr;
-        return b ? (T *)(b->mb[k] + ((const char *)p - b->b0)) : p;
+        return b ? (T *)(b->win + k * b->stride + ((const char *)p - b->b0)) : p;
     }
 };
 
@@ -447,8 +479,10 @@ struct tts_hip_backend {
     bool plan_prepared[2] = {false, false};  // recorded by graph_prepare, not launched yet
     // step coalescer (coalesce.hip): set while this (hidden, per-device) backend runs a coalesced
     // plan; co_ev orders a member's stream with the coalesced launch
-    const tts::BatchCtx * bat = nullptr;
+    tts::BatchCtx * bat = nullptr;
     hipEvent_t co_ev = nullptr;
+    int64_t * co_tab = nullptr;  // device copy of a coalesced plan's per-item tables (ItemTab)
+    size_t co_tab_bytes = 0;
     bool co_member = true;  // TTS_HIP_OPT_COALESCE: this backend's graph_compute calls may join a coalesced step
 };
 
@@ -498,9 +532,9 @@ void launch_greedy_step(tts_hip_backend * be, const float * logits, int B, int N
                         int32_t * hist, int32_t * next);
 int launch_sample_step(tts_hip_backend * be, const float * logits, int B, int NH, int V, const tts_sampling * c, int64_t call,
                        int32_t * rep_state, int step, int bos, int eos, int32_t * eos_seen, int32_t * hist, int32_t * next);
-constexpr int EMBED_MAX_TERMS = 16;
 struct BatchCtx;
-void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat = nullptr);
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat = nullptr,
+                      const ItemTab * tab = nullptr);
 // recip == nullptr: the kernel evaluates reciprocal() = one[0] / alpha[c] itself (`one` a broadcast scalar)
 void launch_snake(tts_hip_backend * be, const tts_tensor * dst, const tts_tensor * x, const tts_tensor * alpha, const tts_tensor * recip,
                   const tts_tensor * one = nullptr, const tts_tensor * mask = nullptr);
@@ -584,16 +618,11 @@ int graph_compute_launches(tts_hip_backend * be, tts_tensor * const * nodes, int
 // one coalesced launch for all of them.  Returns kCoalesceNotTaken when the caller runs the graph itself.
 constexpr int kCoalesceNotTaken = 1 << 20;
 int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
-// buffer registry hooks (backend.hip): a VMM-backed buffer's physical handle, and its release
-bool buffer_lookup(const void * p, const char ** base, size_t * size, void ** vmm_handle, size_t * map_size);
-// Address ranges for VMM mappings (buffers and windows): a fresh reservation each, retired (never
-// reused) when the mapping goes away (backend.hip).
-char * va_alloc(int device, size_t n);
-void va_free(int device, char * p, size_t n);
-// a coalesced step's operands read through member 0's copy (weights, norm parameters, tables): true when
-// every member's copy holds the same bytes (checked on the device, cached until a host write)
-bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::pair<const void *, size_t>> & shared);
-void coalesce_forget(const void * base, size_t size);   // a buffer goes away: windows holding it are unmapped
+// buffer registry (backend.hip): the live tts_hip_buffer_alloc range holding p
+bool buffer_lookup(const void * p, const char ** base, size_t * size);
+// a coalesced step's read-only operands read through member 0's copy: (member 0's, member k's, bytes)
+// pairs, true when every pair holds equal bytes (checked on the device, cached until a host write)
+bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::tuple<const void *, const void *, size_t>> & pairs);
 void coalesce_backend_gone(const tts_hip_backend * be); // a backend is freed: no longer awaited
 void coalesce_written(const void * p, size_t size);     // host writes: content checks over the range are dropped
 bool coalesce_enabled();

@@ -24,7 +24,23 @@ struct AttnArgs {
     int64_t obs = 0;     // floats between sequences of out (n * H * hd when contiguous; a coalesced step's member stride)
     int64_t mbs = 0;     // floats between sequences' masks (0: one mask for all)
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/attn_phase.hip builds only)
+    // Ragged sequences (a coalesced step of runners at different KV lengths, coalesce.hip): per
+    // sequence b, the byte offsets of its K and V views from k.data / v.data (the views' own nb[3] is
+    // then 0), its mask row offset in floats (instead of b * mbs) and its key count (<= P, the grid's).
+    // The mask's row stride is the sequence's key count, as each member's own [P_b, n] mask has.
+    const int64_t * koff = nullptr;
+    const int64_t * voff = nullptr;
+    const int64_t * moff = nullptr;
+    const int * pseq = nullptr;
 };
+
+// per-sequence views of a ragged launch (AttnArgs::koff / voff / moff / pseq)
+__device__ __forceinline__ int seq_p(const AttnArgs & a, int b) { return a.pseq ? a.pseq[b] : a.P; }
+__device__ __forceinline__ int64_t seq_koff(const AttnArgs & a, int b) { return a.koff ? a.koff[b] : 0; }
+__device__ __forceinline__ int64_t seq_voff(const AttnArgs & a, int b) { return a.voff ? a.voff[b] : 0; }
+__device__ __forceinline__ const float * seq_mrow(const AttnArgs & a, int b, int tq, int P) {
+    return a.mask ? a.mask + (a.moff ? a.moff[b] : (int64_t)b * a.mbs) + (int64_t)tq * P : nullptr;
+}
 
 constexpr int ATTN_THREADS = 512;
 constexpr int ATTN_MAXP = 8192;
@@ -41,11 +57,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     __shared__ float s_redf[ATTN_THREADS / 64];
     const int h = blockIdx.x, t = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int P = a.P, hd = a.hd;
+    const int P = seq_p(a, b), hd = a.hd;
     const int hk = h / (a.H / (int)a.k.ne[2]);
     const int bk = b / (a.B / (int)a.k.ne[3]);
     const char * qbase = a.q.data + t * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
-    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
 
     // ---- phase A: kq[i] = sum_d (f32)(K[d,i] * q[d]), f64 accumulation (ggml_vec_dot_f32) ----
     // G lanes per position, each owning hd/G contiguous dims (4 when hd = 4G).
@@ -87,7 +103,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     __syncthreads();
 
     // ---- phase B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum ----
-    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)t * P : nullptr;
+    const float * mrow = seq_mrow(a, b, t, P);
     float mx = -INFINITY;
     for (int i = tid; i < P; i += ATTN_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -120,8 +136,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
     // wave's DPW dims, so DPW x chunks loads are in flight per lane before the first FMA.
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     float * orow = a.out + (int64_t)b * a.obs + ((int64_t)t * a.H + h) * hd;
+    // the shadow copy is per sequence at its contiguous place (a coalesced step's out stride is not)
+    float * orow2 = a.out2 ? a.out2 + (((int64_t)b * a.n + t) * a.H + h) * hd : nullptr;
     const int waves = ATTN_THREADS / 64;
     const bool vvec = a.v.nb[0] == 4 && (a.v.nb[1] % 16) == 0 && (((uintptr_t)vbase) % 16) == 0 &&
                       a.v.nb[1] >= (int64_t)16 * ((P + 3) / 4);
@@ -161,7 +179,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
 #pragma unroll
             for (int u = 0; u < DPW; ++u) {
                 const double s = wave_sum_d(acc[u]);
-                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+                if (lane == 0 && d0 + u < hd) {
+                    orow[d0 + u] = (float)s;
+                    if (orow2) orow2[d0 + u] = (float)s;
+                }
             }
         }
     } else {
@@ -181,7 +202,10 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode(AttnArgs a) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const double s = wave_sum_d(acc[u]);
-                if (lane == 0 && d0 + u < hd) orow[d0 + u] = (float)s;
+                if (lane == 0 && d0 + u < hd) {
+                    orow[d0 + u] = (float)s;
+                    if (orow2) orow2[d0 + u] = (float)s;
+                }
             }
         }
     }
@@ -211,14 +235,14 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane >> 4, t = lane & 15, qd = lane & 3;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hk = h / (a.H / (int)a.k.ne[2]);
     const int bk = b / (a.B / (int)a.k.ne[3]);
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
-    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int64_t knb1 = a.k.nb[1], vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
     TTS_TS(a, 0);
 
@@ -282,7 +306,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_decode_rows(AttnArgs a) {
     TTS_TS(a, 1);
 
     // ---- B: soft_max_ext: w = kq*scale + mask; max; e = expf(w - max); f64 sum; p = e * (1/sum) ----
-    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
+    const float * mrow = seq_mrow(a, b, tq, P);
     float mx = -INFINITY;
     for (int i = tid; i < P; i += ATTN_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -402,11 +426,11 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float 
     const int c = blockIdx.x, h = blockIdx.y, z = blockIdx.z;
     const int b = z / a.n, tq = z - b * a.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, qd = lane & 3;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hk = h / (a.H / (int)a.k.ne[2]);
     const int bk = b / (a.B / (int)a.k.ne[3]);
     const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
-    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
     const int64_t knb1 = a.k.nb[1];
     const int i0 = c * 128 * KS + wave * 16 + (lane >> 2);
     float4 kv[KS][F];
@@ -422,7 +446,7 @@ __global__ __launch_bounds__(ATTN_THREADS) void k_attn_scores(AttnArgs a, float 
 #pragma unroll
         for (int e = 0; e < 4; ++e) qv[f][e] = ((const float *)qbase)[16 * DPR * qd + 4 * f + e];
     TTS_PIN_LOADS();
-    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
+    const float * mrow = seq_mrow(a, b, tq, P);
     float * srow = sbuf + ((int64_t)z * a.H + h) * pstride;
     float mx = -INFINITY;
 #pragma unroll
@@ -476,10 +500,10 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv(AttnArgs a, const float * _
     const int b = z / a.n, tq = z - b * a.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane >> 4, t = lane & 15;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int64_t vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
     const int d = blockIdx.x * 4 * NW + wave * 4 + r;
     const char * vrow = vbase + (int64_t)min(d, a.hd - 1) * vnb1;
@@ -568,10 +592,10 @@ __global__ __launch_bounds__(64 * NW) void k_attn_pv_mp(AttnArgs a, const float 
     const int b = z / a.n, tq = z - b * a.n;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane >> 4, t = lane & 15;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int64_t vnb1 = a.v.nb[1];
     const int ilast = ((P - 1) >> 2) << 2;
     const int d0 = blockIdx.x * 4 * NW * NPASS + wave * 4 + r;
@@ -669,14 +693,14 @@ __global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
     const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int r = lane >> 4, t = lane & 15, qd = lane & 3;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hk = h / (a.H / (int)a.k.ne[2]);
     const int bk = b / (a.B / (int)a.k.ne[3]);
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
-    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int64_t knb1 = a.k.nb[1], vnb1 = a.v.nb[1];
     const int pos0 = wave * 16 + (lane >> 2);
 
@@ -747,7 +771,7 @@ __global__ __launch_bounds__(FUSED_THREADS) void k_attn_fused(AttnArgs a) {
     __syncthreads();
 
     // ---- B: soft_max_ext ----
-    const float * mrow = a.mask ? a.mask + (int64_t)b * a.mbs + (int64_t)tq * P : nullptr;
+    const float * mrow = seq_mrow(a, b, tq, P);
     float mx = -INFINITY;
     for (int i = tid; i < P; i += FUSED_THREADS) {
         float w = __fmul_rn(s_p[i], a.scale);
@@ -829,14 +853,14 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
     constexpr int F = HD / 4;
     const int h = blockIdx.x, tq = blockIdx.y, b = blockIdx.z;
     const int lane = threadIdx.x;
-    const int P = a.P;
+    const int P = seq_p(a, b);
     const int hk = h / (a.H / (int)a.k.ne[2]);
     const int bk = b / (a.B / (int)a.k.ne[3]);
     const int hv = h / (a.H / (int)a.v.ne[2]);
     const int bv = b / (a.B / (int)a.v.ne[3]);
     const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
-    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
-    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int p = min(lane, P - 1);
     float4 kr[F];
 #pragma unroll
@@ -869,7 +893,7 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
         acc += (double)__fmul_rn(kr[c].w, qv[4 * c + 3]);
     }
     float w = __fmul_rn((float)acc, a.scale);
-    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, a.mask[(int64_t)b * a.mbs + (int64_t)tq * P + p]));
+    if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, seq_mrow(a, b, tq, P)[p]));
     if (lane >= P) w = -INFINITY;
     float mx = w;
     mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
@@ -956,8 +980,13 @@ void launch_kv_prefetch(tts_hip_backend * be, hipStream_t st, const TD & t, int 
 }
 
 void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const TD & v, const float * mask, float scale,
-                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs, int64_t mbs) {
+                        float * out, int hd, int P, int H, int n, int B, float * out2, int64_t obs, int64_t mbs, const int64_t * koff,
+                        const int64_t * voff, const int64_t * moff, const int * pseq) {
     AttnArgs a;
+    a.koff = koff;
+    a.voff = voff;
+    a.moff = moff;
+    a.pseq = pseq;
     a.out2 = out2;
     a.obs = obs >= 0 ? obs : (int64_t)n * H * hd;
     a.mbs = mbs;
@@ -1062,8 +1091,6 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
     }
     hipLaunchKernelGGL(k_attn_decode, dim3((unsigned)H, (unsigned)n, (unsigned)B), dim3(ATTN_THREADS), 0, be->stream, a);
     TTS_HIP_CHECK(hipGetLastError());
-    if (out2)
-        launch_copy_bytes(be, out2, out, sizeof(float) * (size_t)hd * H * n * B);
 }
 
 }  // namespace tts

@@ -180,7 +180,7 @@ __device__ __forceinline__ void gemv_store(const GemvJob & j, int mat, int64_t r
     } else if (j.epi == EPI_SILU_MUL) {
         v = __fmul_rn(dev_silu(j.res[m * j.rcs + row]), v);
     }
-    float * const Y = j.Y[mat];
+    float * const Y = j.Y[mat] + ((j.yoff_mats >> mat) & 1 ? j.yoff[mat * j.yoff_ld + m] : 0);
     const int64_t ycs = j.ycs[mat], yrs = j.yrs[mat];
     if (mat == j.rep_mat) {
         const int64_t g = row / j.yrg;
@@ -1599,14 +1599,14 @@ __global__ __launch_bounds__(576) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
     const int l = lane & 7, s = lane >> 3;
     const int nb = (int)(j.K / QK_K);
     // attention operands for the attention wave (position p = lane)
-    const int P = a.P;
+    const int P = a.pseq ? a.pseq[b] : a.P;
     const int p = min(lane, P - 1);
     float4 kr[F];
     float vv[VB];
     float mk = 0.f;
     const int bk = b / (a.B / (int)a.k.ne[3]), bv = b / (a.B / (int)a.v.ne[3]);  // K/V shared across prompts or not
-    const char * kbase = a.k.data + (int64_t)h * a.k.nb[2] + (int64_t)bk * a.k.nb[3];
-    const char * vbase = a.v.data + (int64_t)h * a.v.nb[2] + (int64_t)bv * a.v.nb[3];
+    const char * kbase = a.k.data + (int64_t)h * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + (a.koff ? a.koff[b] : 0);
+    const char * vbase = a.v.data + (int64_t)h * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + (a.voff ? a.voff[b] : 0);
     u32x4 hdr[4], q[4];
     if (wave < NW) {
         const int64_t row = (int64_t)h * HD + wave * 8 + s;
@@ -1631,7 +1631,7 @@ __global__ __launch_bounds__(576) void k_gemv_q4K_xattn(GemvJob j, XAttnArgs a) 
         for (int c = 0; c < F; ++c) kr[c] = *(const float4 *)(kbase + (int64_t)p * a.k.nb[1] + 16 * c);
 #pragma unroll
         for (int u = 0; u < VB; ++u) vv[u] = *(const float *)(vbase + (int64_t)lane * a.v.nb[1] + (int64_t)min(u, P - 1) * a.v.nb[0]);
-        mk = *(a.mask ? a.mask + (int64_t)b * a.mbs + p : (const float *)kbase);  // unconditional: no branch join before the barrier
+        mk = *(a.mask ? a.mask + (a.moff ? a.moff[b] : (int64_t)b * a.mbs) + p : (const float *)kbase);  // unconditional: no branch join before the barrier
     }
     __syncthreads();
     if (wave < NW) {
@@ -2332,6 +2332,7 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
         if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
         j.x = job.x + m0 * job.xcs;
         for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+        if (job.yoff) j.yoff = job.yoff + m0;
         if (job.res) j.res = job.res + m0 * job.rcs;
         // the LN prologue holds one column's K / 256 chunks in registers (K <= 4096, as the planner's
         // LN fusion requires)
@@ -2428,6 +2429,7 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
             if (job.lnout) j.lnout = job.lnout + m0 * job.locs;
             j.x = job.x + m0 * job.xcs;
             for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+        if (job.yoff) j.yoff = job.yoff + m0;
             if (job.res) j.res = job.res + m0 * job.rcs;
             if (!launch_gemm_q4k_kr(be, j, lo)) return false;  // (the first chunk is checked before any launch below)
         }
@@ -2981,6 +2983,7 @@ void launch_gemv_job(tts_hip_backend * be, const GemvJob & job) {
         }
         if (job.x) j.x = job.x + m0 * job.xcs;
         for (int i = 0; i < job.nmat; ++i) j.Y[i] = job.Y[i] + m0 * job.ycs[i];
+        if (job.yoff) j.yoff = job.yoff + m0;
         if (job.res) j.res = job.res + m0 * job.rcs;
         switch (mc) {
             case 1: launch_gemv_mc<1>(be, j); break;

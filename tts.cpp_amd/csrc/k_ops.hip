@@ -364,6 +364,7 @@ struct EmbedTerm {
     const int32_t * idx;
     int64_t idx_stride;  // elements
     int64_t rows;        // 1 = broadcast
+    const int64_t * moff;  // column m's index at idx[moff[m]] (a coalesced step's member-owned inputs), or null
 };
 struct EmbedArgs {
     EmbedTerm t[EMBED_MAX_TERMS];
@@ -380,7 +381,7 @@ __global__ void k_embed_sum(EmbedArgs a) {
     float acc = 0.f;
     for (int t = 0; t < a.n; ++t) {
         const EmbedTerm & T = a.t[t];
-        const int64_t r = T.idx[(T.rows == 1 ? 0 : m) * T.idx_stride];
+        const int64_t r = T.moff ? T.idx[T.moff[m]] : T.idx[(T.rows == 1 ? 0 : m) * T.idx_stride];
         const float v = (T.table.type == TTS_TYPE_Q4_K && (T.table.pad & TTS_FLAG_TILED))
                             ? table_elem_q4K_tiled(T.table.data, r, T.table.ne[0] / QK_K, h)
                             : table_elem(T.table, T.table.data + r * T.table.nb[1], h);
@@ -389,7 +390,8 @@ __global__ void k_embed_sum(EmbedArgs a) {
     a.out[m * a.ocs + h] = acc;
 }
 
-void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat) {
+void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_tensor * const * gr, int n, const BatchCtx * bat,
+                      const ItemTab * tab) {
     EmbedArgs a{};
     a.n = n;
     a.out = (float *)out->data;
@@ -407,6 +409,11 @@ void launch_embed_sum(tts_hip_backend * be, const tts_tensor * out, const tts_te
         a.ocs = bat->stride(a.out) / 4;
         a.out = bat->win(a.out);
         for (int i = 0; i < n; ++i) {
+            if (tab && tab->ioff[i]) {  // each member's own index tensor (an input)
+                a.t[i].moff = tab->ioff[i];
+                a.t[i].rows = bat->N;
+                continue;
+            }
             const int64_t s = bat->stride(a.t[i].idx);
             a.t[i].idx_stride = s / 4;
             a.t[i].rows = s ? bat->N : 1;

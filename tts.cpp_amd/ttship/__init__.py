@@ -633,9 +633,9 @@ def runner_weights(n_fn, w_fn, ptr):
 
 def coalesce_stats(device=0):
     """Step-coalescer counters of `device` (tts_hip_coalesce_stats)."""
-    out = (ctypes.c_int64 * 6)()
-    n = lib().tts_hip_coalesce_stats(device, out, 6)
-    keys = ("launches", "member_steps", "alone", "refused", "max_group", "wait_us")
+    out = (ctypes.c_int64 * 7)()
+    n = lib().tts_hip_coalesce_stats(device, out, 7)
+    keys = ("launches", "member_steps", "alone", "refused", "max_group", "wait_us", "ragged_launches")
     return {keys[i]: int(out[i]) for i in range(max(n, 0))}
 
 
@@ -644,8 +644,9 @@ def coalesce_set_wait(us):
 
 
 def coalesce_enable(on=True):
-    """The step coalescer, process-wide (tts_hip_coalesce_enable): buffers allocated from now on are
-    VMM-mapped and one-prompt decode steps rendezvous.  Returns the previous setting."""
+    """The step coalescer, process-wide (tts_hip_coalesce_enable; on by default, TTS_HIP_COALESCE=0 at
+    load turns it off): one-prompt decode steps of backends on one device rendezvous and run as batched
+    launches.  Returns the previous setting."""
     return bool(lib().tts_hip_coalesce_enable(1 if on else 0))
 
 
