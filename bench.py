@@ -248,23 +248,27 @@ def dac_flops_per_frame(dcfg):
 
 
 def copy_peak(be, nbytes=1 << 30, reps=10):
-    """The measured HBM ceiling beside the 8 TB/s spec: device-to-device copies of
-    `nbytes` on the backend's stream (tts_hip_tensor_copy), read + write bytes per second over `reps`
-    copies after one warm copy."""
+    """The measured HBM ceiling beside the 8 TB/s spec: a streaming copy kernel
+    (tts_hip_copy_stream: 16-B non-temporal loads / stores per lane, the guide's float4-copy method) of
+    `nbytes` on the backend's stream, read + write bytes per second over `reps` copies after one warm
+    copy; and the runtime's device-to-device copy (tts_hip_tensor_copy) the same way."""
     L = ttship.lib()
     a, b = be.alloc(nbytes), be.alloc(nbytes)
+    out = {}
     try:
-        L.tts_hip_tensor_copy(be.ptr, b, a, nbytes)
-        be.sync()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            L.tts_hip_tensor_copy(be.ptr, b, a, nbytes)
-        be.sync()
-        dt = time.perf_counter() - t0
+        for name, fn in (("kernel", L.tts_hip_copy_stream), ("runtime", L.tts_hip_tensor_copy)):
+            if fn(be.ptr, b, a, nbytes) != 0:
+                raise RuntimeError(f"{name} copy failed")
+            be.sync()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn(be.ptr, b, a, nbytes)
+            be.sync()
+            out[name] = round(2.0 * nbytes * reps / (time.perf_counter() - t0) / 1e9, 1)
     finally:
         be.free(a)
         be.free(b)
-    return round(2.0 * nbytes * reps / dt / 1e9, 1)
+    return out
 
 
 def gemv_roofline(be, runner, steps):
@@ -701,6 +705,7 @@ def main():
     ap.add_argument("--gemv-kr-inkernel", type=int, default=None, help="TTS_HIP_OPT_GEMV_KR_INKERNEL: max K of K-relay GEMVs quantizing in-kernel (0 = operand pass)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--attn-pv-mp", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV_MP: all dims of a head per P.V workgroup (1) or 16 (0)")
+    ap.add_argument("--gemm-kr-xcd", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (1, default) or grid order (0)")
     ap.add_argument("--gemm-kr-nw", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_NW: waves per tile of the many-column K-relay GEMM (4 / 8)")
     ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")
@@ -745,7 +750,7 @@ def main():
                           ("gemv_q80_rw", "GEMV_Q80_RW"), ("gemm_q8_staged", "GEMM_Q8_STAGED"),
                           ("gemv_kr_inkernel", "GEMV_KR_INKERNEL"), ("attn_ks", "ATTN_KS"), ("attn_pv8", "ATTN_PV8"),
                           ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE"),
-                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW")):
+                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW"), ("gemm_kr_xcd", "GEMM_KR_XCD")):
             v = getattr(args, flag)
             if v is not None:
                 rb.set_option(ttship.OPT[opt], v)
@@ -821,7 +826,9 @@ def main():
     audio_s = total_prompts * args.steps * SAMPLES_PER_STEP / SAMPLE_RATE
     roof = gemv_roofline(be, runner, max(5, min(40, args.steps // 5)))
     try:
-        roof["measured_copy_peak_gbs"] = copy_peak(be)  # D2D copy rate of this GPU (read + write), beside the spec peak
+        cp = copy_peak(be)  # streaming-copy rate of this GPU (read + write), beside the spec peak
+        roof["measured_copy_peak_gbs"] = cp["kernel"]
+        roof["measured_copy_runtime_gbs"] = cp["runtime"]
     except Exception as e:  # noqa: BLE001  (a measurement beside the line, never a reason to lose it)
         roof["measured_copy_peak_gbs"] = None
         print(f"bench: copy peak failed: {e!r}", file=sys.stderr, flush=True)
@@ -881,15 +888,44 @@ def main():
 
     sampled = guarded("parler_sampled_top_k", leg_sampled) if args.sampled_steps > 0 else None
     # the prompt pass the headline leaves out: every prompt's own sentence (perf_battery's 29, prompt g = HARVARD[g % 29])
-    # from position 0, as TTS.cpp runs it (one prompt per runner), R runners concurrently
+    # from position 0 -- batched: each replica's prompts as ONE ragged prompt pass (tts_parler_prefill_ragged: every
+    # prompt at its own length, tokens equal to its own pass, tests/test_parler_gpu.py), R replicas concurrently; and
+    # as TTS.cpp runs it (one prompt per runner pass, R runners concurrently)
     def leg_prompt_pass():
         barrier_sync(dist, None)
+        toks_pp = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], cfg.prompt_vocab) for g in range(per_gpu)]
+        out = {"workload": f"{per_gpu} prompt passes per GPU from position 0, prompt g = perf_battery sentence g % 29 "
+                           f"(word-piece-length synthetic ids, {min(map(len, toks_pp))}-{max(map(len, toks_pp))} tokens)"}
+        rcfg = ttship.parler_config(batch=bl, max_ctx=256)
+        pbes, pruns = [], []
+        try:
+            pbes += [new_backend() for _ in range(R)]
+            pruns += [ttship.Parler(b.iface(), rcfg) for b in pbes]
+            for r in range(R):  # warm (code objects, the prefill's GEMM shapes)
+                pruns[r].prefill_ragged(toks_pp[r * bl:(r + 1) * bl])
+                pbes[r].sync()
+
+            def ppb(r):
+                pruns[r].reset()
+                pruns[r].prefill_ragged(toks_pp[r * bl:(r + 1) * bl])
+                pbes[r].sync()
+
+            barrier_sync(dist, pbes[0])
+            tp0 = time.perf_counter()
+            run_replicas(ppb, R)
+            dtb = max_over_ranks(dist, local, time.perf_counter() - tp0)
+        finally:
+            for rr in pruns:
+                rr.close()
+            for b in pbes:
+                b.close()
+        out.update({"batched": f"{R} replicas x one ragged prompt pass of {bl} prompts (tts_parler_prefill_ragged)",
+                    "ms_total": round(1000 * dtb, 3), "end_to_end_audio_sec_per_s_with_prompt_pass": round(audio_s / (dt + dtb), 3)})
         pcfg = ttship.parler_config(batch=1, max_ctx=256)
         pbes, pruns = [], []
         try:
             pbes += [new_backend() for _ in range(R)]
             pruns += [ttship.Parler(b.iface(), pcfg) for b in pbes]
-            toks_pp = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], pcfg.prompt_vocab) for g in range(per_gpu)]
             for rr, b in zip(pruns, pbes):  # warm (code objects)
                 rr.prefill(toks_pp[0].reshape(1, -1))
                 b.sync()
@@ -909,12 +945,10 @@ def main():
                 rr.close()
             for b in pbes:
                 b.close()
-        prompt_pass = {"workload": f"{per_gpu} prompt passes per GPU from position 0, prompt g = perf_battery sentence g % 29 "
-                                   f"(word-piece-length synthetic ids, {min(map(len, toks_pp))}-{max(map(len, toks_pp))} tokens), "
-                                   f"{R} runners concurrently",
-                       "ms_total": round(1000 * dtp, 3), "ms_per_prompt": round(1000 * dtp * R / per_gpu, 3),
-                       "end_to_end_audio_sec_per_s_with_prompt_pass": round(audio_s / (dt + dtp), 3)}
-        return prompt_pass
+        out["one_prompt_per_pass"] = {"workload": f"TTS.cpp's shape: one prompt per runner pass, {R} runners concurrently",
+                                      "ms_total": round(1000 * dtp, 3), "ms_per_prompt": round(1000 * dtp * R / per_gpu, 3),
+                                      "end_to_end_audio_sec_per_s_with_prompt_pass": round(audio_s / (dt + dtp), 3)}
+        return out
 
     prompt_pass = guarded("prompt_pass", leg_prompt_pass) if args.prompt_pass else None
 

@@ -211,6 +211,10 @@ size_t tts_hip_buffer_alignment(void);
 int tts_hip_tensor_set(tts_hip_backend_t backend, void * dst_dev, const void * src_host, size_t size);
 int tts_hip_tensor_get(tts_hip_backend_t backend, void * dst_host, const void * src_dev, size_t size);
 int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size); /* stream-ordered */
+/* Measurement helper (bench.py's measured HBM ceiling): the same copy as a streaming kernel -- 16-B loads and
+ * stores per lane, non-temporal, a grid of 8 workgroups per CU -- the guide's float4-copy method.  size % 16 == 0
+ * and both pointers 16-B aligned, else TTS_STATUS_BAD_ARG.  Stream-ordered. */
+int tts_hip_copy_stream(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size);
 /* ggml_backend_i::set_tensor_async: `src_host` is staged at once (reusable on return), the copy runs
  * in stream order after the work already queued. */
 /* Fusion coverage of a node list without a device: counts[0..14] = fused items per kind (GEMV, ATTN,
@@ -327,6 +331,8 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMM_KR_NW = 34, /* waves per 16-row tile of the many-column (> 8) K-relay Q4_K GEMM: 4 (default) or 8 (K >= 2048) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
+    TTS_HIP_OPT_GEMM_KR_XCD = 38, /* 1 (default): the many-column K-relay GEMM places a row tile's 16-column tiles on one XCD,
+                                     dispatched back to back, so the second streams the weights from that XCD's L2; 0 = grid order */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
                                      backend's graph_compute of a one-prompt decode step may join the same step of other
                                      backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */

@@ -50,6 +50,11 @@ void tts_parler_free(tts_parler * p);
 void tts_parler_reset(tts_parler * p);
 /* Text-prompt pass: tokens [batch][n] (parler batch_from_sentence path). */
 int tts_parler_prefill(tts_parler * p, const int32_t * tokens, int32_t n);
+/* One prompt pass over `batch` prompts of different lengths from an empty cache (a ragged lock-step batch):
+ * tokens [batch][n_max], prompt b = its first lens[b] ids.  Later steps decode every prompt in lockstep, each at
+ * its own position with its own mask (TTS.cpp runs one prompt per runner: parler_tts_runner::prepare_post_load /
+ * generate, src/models/parler/model.cpp:838-858; this batches them). */
+int tts_parler_prefill_ragged(tts_parler * p, const int32_t * tokens, const int32_t * lens, int32_t n_max);
 /* One AR decode step: audio tokens [batch][n_output_heads] -> logits [batch][n_output_heads][vocab]. */
 int tts_parler_decode(tts_parler * p, const int32_t * audio_tokens, float * logits);
 /* Greedy generation loop (generate_from_batch with sampler::max): runs n_steps AR steps after the

@@ -855,7 +855,7 @@ static void op_norm(tts_tensor * dst, int ith, int nth) {
 }
 
 /* ggml_compute_forward_soft_max_f32: wp = x*scale + slope*mask (mask row = i1 % ne01, row
- * stride ne00), max, expf, double sum, scale by 1/sum. */
+ * stride ne00; per-dim broadcast for 3-D / 4-D masks), max, expf, double sum, scale by 1/sum. */
 static void op_soft_max(tts_tensor * dst, int ith, int nth) {
     const tts_tensor * a = dst->src[0];
     const tts_tensor * mask = dst->src[1];
@@ -871,7 +871,14 @@ static void op_soft_max(tts_tensor * dst, int ith, int nth) {
         float * dp = (float *)((char *)dst->data + i1 * dst->nb[1]);
         for (int64_t i = 0; i < nc; ++i) wp[i] = sp[i] * scale;
         if (mask) {
-            const int64_t mr = i1 % ne01;
+            /* a 2-D mask: row i1 % ne01 (the fork's rule); a mask with ne2 / ne3 > 1 (the per-sequence masks
+             * of a ragged lock-step batch): row (i01 % ne11) of slice (i02 % ne12, i03 % ne13), as upstream
+             * ggml_compute_forward_soft_max_f32 broadcasts it */
+            int64_t mr = i1 % ne01;
+            if (mask->ne[2] * mask->ne[3] > 1) {
+                const int64_t i01 = i1 % a->ne[1], i02 = (i1 / a->ne[1]) % a->ne[2], i03 = i1 / (a->ne[1] * a->ne[2]);
+                mr = (i01 % mask->ne[1]) + mask->ne[1] * ((i02 % mask->ne[2]) + mask->ne[2] * (i03 % mask->ne[3]));
+            }
             for (int64_t i = 0; i < nc; ++i) {
                 float mv = mask->type == TTS_TYPE_F16 ? ref_fp16_to_fp32(((const ref_fp16_t *)mask->data)[mr * nc + i])
                                                       : ((const float *)mask->data)[mr * nc + i];

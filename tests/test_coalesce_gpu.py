@@ -97,7 +97,7 @@ def test_coalesced_runners_match_alone_and_oracle(n):
         for b in bes:
             b.close()
     carried = after["member_steps"] - before["member_steps"]
-    assert carried >= n * 6, (before, after)  # most steps ran coalesced
+    assert carried >= n * 6, f"{before} {after}"  # most steps ran coalesced
     # each runner alone (coalescing off) and on the oracle
     for r in range(n):
         be = ttship.HipBackend(0)
@@ -130,8 +130,8 @@ def test_runners_at_different_lengths_coalesce_exact():
     finally:
         for b in bes:
             b.close()
-    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
-    assert after["member_steps"] - before["member_steps"] >= 3 * 4, (before, after)
+    assert after["ragged_launches"] > before["ragged_launches"], f"{before} {after}"
+    assert after["member_steps"] - before["member_steps"] >= 3 * 4, f"{before} {after}"
     for r in range(3):
         assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], 8)), f"runner {r}"
 
@@ -153,8 +153,8 @@ def test_staggered_runners_at_four_lengths():
         for b in bes:
             b.close()
     carried = after["member_steps"] - before["member_steps"]
-    assert carried >= 4 * steps // 2, (before, after)  # most steps coalesced
-    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
+    assert carried >= 4 * steps // 2, f"{before} {after}"  # most steps coalesced
+    assert after["ragged_launches"] > before["ragged_launches"], f"{before} {after}"
     for r in range(4):
         assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], steps)), f"runner {r}"
 
@@ -176,7 +176,7 @@ def test_two_kinds_of_graphs_coalesce_separately():
     finally:
         for b in bes:
             b.close()
-    assert after["member_steps"] - before["member_steps"] >= 4 * 5, (before, after)
+    assert after["member_steps"] - before["member_steps"] >= 4 * 5, f"{before} {after}"
     for r in range(4):
         assert np.array_equal(got[r], oracle_tokens(cfgs[r], prompts[r], 10)), f"runner {r}"
 
@@ -195,7 +195,7 @@ def test_generic_head_dim_coalesced():
     finally:
         for b in bes:
             b.close()
-    assert after["member_steps"] - before["member_steps"] >= 3 * 4, (before, after)
+    assert after["member_steps"] - before["member_steps"] >= 3 * 4, f"{before} {after}"
     for r in range(3):
         assert np.array_equal(got[r], oracle_tokens(cfg, prompts[r], 8)), f"runner {r}"
 
@@ -226,7 +226,7 @@ def test_weights_that_differ_are_not_shared():
     finally:
         for b in bes:
             b.close()
-    assert after["launches"] == before["launches"], (before, after)
+    assert after["launches"] == before["launches"], f"{before} {after}"
     for cfg, tok in ((cfg_a, out[0]), (cfg_b, out[1])):
         c = ttship.Parler(py_oracle.iface(8), cfg)
         try:
@@ -251,9 +251,9 @@ def test_parler_mini_8_runners_coalesced_bit_identical():
     finally:
         for b in bes:
             b.close()
-    assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), (before, after)
+    assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), f"{before} {after}"
     assert after["max_group"] >= 4, after
-    assert after["ragged_launches"] > before["ragged_launches"], (before, after)
+    assert after["ragged_launches"] > before["ragged_launches"], f"{before} {after}"
     be = ttship.HipBackend(0)
     be.set_option(ttship.OPT["COALESCE"], 0)
     try:
@@ -286,7 +286,7 @@ def test_adapter_runners_from_threads_coalesce_and_match_oracle():
     finally:
         for a in ads:
             a.close()
-    assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), (before, after)
+    assert after["member_steps"] - before["member_steps"] >= n * (steps // 2), f"{before} {after}"
     for r in range(n):
         c = ttship.Parler(py_oracle.iface(8), cfg)
         try:

@@ -47,3 +47,38 @@ def test_parler_node_order_is_the_reference_order():
         assert "TRANSPOSE" in first_layer and first_layer.count("CPY") == 2
     finally:
         c.close()
+
+
+def _ragged_prompts(lens, vocab=512):
+    return [((np.arange(L, dtype=np.int32) * (31 + 2 * r) + 5 * r + 1) % vocab).astype(np.int32) for r, L in enumerate(lens)]
+
+
+def test_ragged_batch_equals_each_prompt_alone():
+    """A ragged lock-step batch (tts_parler_prefill_ragged: prompts of 5, 9 and 7 tokens in one prompt
+    pass, then decoded in lockstep at their own positions, each with its own mask over the padding
+    slots) gives every prompt the tokens of its own B = 1 run, on the oracle."""
+    lens = [5, 9, 7]
+    prompts = _ragged_prompts(lens)
+    c = ttship.Parler(py_oracle.iface(4), ttship.parler_config(batch=3, **TINY))
+    c.prefill_ragged(prompts)
+    got = c.generate(8)
+    c.close()
+    for r, p in enumerate(prompts):
+        a = ttship.Parler(py_oracle.iface(4), ttship.parler_config(batch=1, **TINY))
+        a.prefill(p.reshape(1, -1))
+        ref = a.generate(8)
+        a.close()
+        assert np.array_equal(got[r], ref[0]), f"prompt {r}"
+
+
+def test_ragged_batch_rejects_bad_lengths():
+    c = ttship.Parler(py_oracle.iface(2), ttship.parler_config(batch=2, **TINY))
+    try:
+        import pytest
+        with pytest.raises(RuntimeError):
+            c.prefill_ragged([np.zeros(0, np.int32), np.ones(3, np.int32)])  # an empty prompt
+        c.prefill_ragged(_ragged_prompts([3, 4]))
+        with pytest.raises(RuntimeError):
+            c.prefill_ragged(_ragged_prompts([3, 4]))  # only from an empty cache
+    finally:
+        c.close()

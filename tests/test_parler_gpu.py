@@ -222,3 +222,64 @@ def test_scratch_grows_after_plans_ran():
         q.close()
         be.close()
     assert np.array_equal(got, ref)
+
+
+def _ragged_prompts(lens, vocab):
+    return [((np.arange(L, dtype=np.int32) * (31 + 2 * r) + 5 * r + 1) % vocab).astype(np.int32) for r, L in enumerate(lens)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_sampling", [True, False])
+def test_ragged_batch_tiny(hip, device_sampling):
+    """Prompts of 5, 9, 7 and 12 tokens in ONE prompt pass (tts_parler_prefill_ragged), then decoded in
+    lockstep, each at its own position with its own mask: tokens equal the oracle's ragged batch and each
+    prompt's own B = 1 run on the GPU."""
+    lens = [5, 9, 7, 12]
+    prompts = _ragged_prompts(lens, 512)
+    g, c = make_pair(hip, batch=4, **TINY)
+    try:
+        g.set_device_sampling(device_sampling)
+        g.prefill_ragged(prompts)
+        c.prefill_ragged(prompts)
+        tg = g.generate(12)
+        tc = c.generate(12)
+        assert np.array_equal(tg, tc), f"token mismatch\n{tg}\n{tc}"
+    finally:
+        g.close()
+        c.close()
+    one = ttship.Parler(hip.iface(), ttship.parler_config(batch=1, **TINY))
+    try:
+        for r, p in enumerate(prompts):
+            one.reset()
+            one.prefill(p.reshape(1, -1))
+            assert np.array_equal(one.generate(12)[0], tg[r]), f"prompt {r}"
+    finally:
+        one.close()
+
+
+@pytest.mark.gpu
+def test_ragged_prompt_pass_parler_mini(hip):
+    """Parler-mini Q4_K (full shapes): the perf_battery sentences' word-piece lengths (bench.py
+    sentence_tokens) as one ragged prompt pass of 8 prompts, 16 decode steps: every prompt's tokens equal
+    its own prompt pass and decode alone (TTS.cpp's one-prompt generate, model.cpp:838-858)."""
+    import sys
+    import pathlib
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
+    import bench
+    cfg = ttship.parler_config(batch=8, max_ctx=256)
+    prompts = [bench.sentence_tokens(bench.HARVARD[g], cfg.prompt_vocab) for g in range(8)]
+    assert len({len(p) for p in prompts}) > 3  # ragged
+    g = ttship.Parler(hip.iface(), cfg)
+    try:
+        g.prefill_ragged(prompts)
+        tg = g.generate(16)
+    finally:
+        g.close()
+    one = ttship.Parler(hip.iface(), ttship.parler_config(batch=1, max_ctx=256))
+    try:
+        for r, p in enumerate(prompts):
+            one.reset()
+            one.prefill(p.reshape(1, -1))
+            assert np.array_equal(one.generate(16)[0], tg[r]), f"prompt {r}"
+    finally:
+        one.close()

@@ -365,6 +365,14 @@ int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_
     return 0;
 }
 
+int tts_hip_copy_stream(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
+    if (!be || !dst || !src || size % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16) return TTS_STATUS_BAD_ARG;
+    if (size == 0) return 0;
+    hipSetDevice(be->device);
+    tts::launch_copy_stream(be, dst, src, (int64_t)(size / 16));
+    return hipGetLastError() == hipSuccess ? 0 : TTS_STATUS_FAILED;
+}
+
 int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
@@ -801,6 +809,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_GEMV_UNIQUE: be->gemv_unique = value != 0; return 0;
         case TTS_HIP_OPT_GEMV_KS: be->gemv_ks_tiles = value > 0 ? value : 0; return 0;
         case TTS_HIP_OPT_COALESCE: be->co_member = value != 0; return 0;
+        case TTS_HIP_OPT_GEMM_KR_XCD: be->gemm_kr_xcd = value != 0; return 0;
         case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }

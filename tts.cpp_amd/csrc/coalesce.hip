@@ -213,6 +213,7 @@ void copy_options(tts_hip_backend * d, const tts_hip_backend * s) {
     d->gemm_q8_staged = s->gemm_q8_staged;
     d->gemv_kr_ink = s->gemv_kr_ink;
     d->gemm_kr_ct2 = s->gemm_kr_ct2;
+    d->gemm_kr_xcd = s->gemm_kr_xcd;
     d->gemm_kr_ink = s->gemm_kr_ink;
     d->gemv_nw_min = s->gemv_nw_min;
     d->gemv_mf_rsplit = s->gemv_mf_rsplit;
@@ -247,6 +248,7 @@ bool check_shared(Dev & d, tts_hip_backend * ex, const BatchCtx & bc, const std:
         }
     }
     if (todo.empty()) return true;
+    if (co_debug()) fprintf(stderr, "coalesce: content check of %zu ranges\n", todo.size());
     if (d.d_flags_n < (int)todo.size()) {
         if (d.d_flags) hipFree(d.d_flags);
         d.d_flags_n = std::max((int)todo.size(), 1024);
@@ -344,6 +346,7 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     for (Req * q : g)
         if (q->n == r0->n) mem.push_back(q);
     if (mem.size() < 2) {
+        if (co_debug()) fprintf(stderr, "coalesce: group refused: node counts differ\n");
         d.refused++;
         return;  // statuses stay kCoalesceNotTaken: every member runs its own graph
     }
@@ -363,6 +366,7 @@ void run_group(Dev & d, std::vector<Req *> & g) {
         }
     }
     if (!exec_layout(d, bc, r0->nodes, r0->n)) {
+        if (co_debug()) fprintf(stderr, "coalesce: group refused: executor layout\n");
         d.refused++;
         return;
     }
@@ -382,6 +386,7 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     const int st = graph_compute_launches(ex, r0->nodes, r0->n);
     ex->bat = nullptr;
     if (st == TTS_STATUS_UNSUPPORTED) {  // refused before any launch: each member runs its own graph
+        if (co_debug()) fprintf(stderr, "coalesce: group of %d refused by the plan\n", bc.N);
         d.refused++;
         return;
     }

@@ -1914,6 +1914,8 @@ struct Planner {
         if (V->ne[2] != H || V->ne[3] != B) return;  // kqv = mul_mat(kq, V): V carries the batch dims
         if (mask && (mask->type != TTS_TYPE_F32 || !contiguous(mask) || mask->ne[0] < P)) return;
         if (mask && mask->ne[0] != P) return;  // ggml reads mask rows with stride ne00 == P
+        // a 2-D mask serves every head and sequence; [P, rows, 1, B]: one per sequence (a ragged lock-step batch)
+        if (mask && (mask->ne[1] < nq || mask->ne[2] != 1 || (mask->ne[3] != 1 && mask->ne[3] != B))) return;
         if (nq * H * B * hd != O->ne[0] * O->ne[1] * O->ne[2] * O->ne[3]) return;
         // aliasing: O may coincide exactly with Q's storage (read-before-write per workgroup), nothing else
         const tts_tensor * Qbase = Q->view_src ? Q->view_src : Q;
@@ -2067,14 +2069,18 @@ struct CoMap {
 static const tts_tensor * co_member(const BatchCtx & bc, const tts_tensor * t, int k) {
     return ((CoMap *)bc.comap)->member(bc, t, k);
 }
+// The tensor whose memory t is (a view's -- CPY included -- is its view source's, ggml's view_src).
+static const tts_tensor * mem_root(const tts_tensor * t) { return t && t->view_src ? t->view_src : t; }
+// memory that is each member's own and outlives the step: a leaf's (weights, caches, inputs) or a
+// PERSIST tensor's, through any view (a KV-store CPY writes its cache's memory)
+static bool owned_mem(const tts_tensor * t) {
+    const tts_tensor * r = mem_root(t);
+    return r && (r->op == TTS_OP_NONE || (r->flags & TTS_FLAG_PERSIST) || persistent_mem(r));
+}
 // memory of an input (a leaf marked input, through views): each member's own, never shared
 static bool input_mem(const tts_tensor * t) {
-    for (int hop = 0; t && hop < 8; ++hop) {
-        if (t->op == TTS_OP_NONE) return (t->flags & TTS_FLAG_INPUT) != 0;
-        if (!is_view(t->op)) return false;
-        t = t->view_src ? t->view_src : t->src[0];
-    }
-    return false;
+    const tts_tensor * r = mem_root(t);
+    return r && r->op == TTS_OP_NONE && (r->flags & TTS_FLAG_INPUT) != 0;
 }
 
 // An intermediate of member 0's graph as the N members' copies along dim 3 (member k's at executor
@@ -2094,7 +2100,7 @@ static int run_attn_item(tts_hip_backend * be, const Item & it, const ItemTab * 
     float * out = (float *)it.out->data;
     const float * mask = it.mask ? (const float *)it.mask->data : nullptr;
     int B = (int)it.q->ne[3], P = (int)it.k->ne[1];
-    int64_t obs = -1, mbs = 0;
+    int64_t obs = -1, mbs = it.mask && it.mask->ne[3] > 1 ? (int64_t)(it.mask->nb[3] / 4) : 0;  // per-sequence masks
     if (const BatchCtx * bc = be->bat) {  // (co_prepare-checked: one sequence per member)
         batch_td(*bc, q);
         if (tab && tab->koff) k.ne[3] = bc->N, k.nb[3] = 0;  // each member's own cache view: koff
@@ -2381,12 +2387,12 @@ static int run_node_coalesced(tts_hip_backend * be, const tts_tensor * n) {
         default: break;
     }
     tts_tensor t, srcs[TTS_MAX_SRC];
-    if (per_slice && !persistent_mem(n) && bc.stride(n->data) && batch_tensor(bc, n, t)) {
+    if (per_slice && !owned_mem(n) && bc.stride(n->data) && batch_tensor(bc, n, t)) {
         for (int i = 0; i < TTS_MAX_SRC && per_slice; ++i) {
             const tts_tensor * x = n->src[i];
             if (!x) continue;
             // an input is each member's own; read-only model data (checked equal, co_prepare) broadcasts
-            if (input_mem(x) || (!persistent_mem(x) && !bc.stride(x->data))) {
+            if (input_mem(x) || (!owned_mem(x) && !bc.stride(x->data))) {
                 per_slice = false;
                 break;
             }
@@ -2401,7 +2407,7 @@ static int run_node_coalesced(tts_hip_backend * be, const tts_tensor * n) {
     be->bat = nullptr;  // member k's own node, run as in an uncoalesced step
     int st = 0;
     auto addr = [&](const tts_tensor * x, int k) -> void * {  // member k's bytes of member 0's tensor x
-        if (!persistent_mem(x)) return bc.reloc(x->data, k);
+        if (!owned_mem(x)) return bc.reloc(x->data, k);
         const tts_tensor * m = co_member(bc, x, k);
         return m ? m->data : nullptr;
     };
@@ -2507,6 +2513,20 @@ static int run_item(tts_hip_backend * be, const Item & it, const std::vector<Ite
     return TTS_STATUS_FAILED;
 }
 
+// TTS_HIP_COALESCE_DEBUG=1: why a coalesced step was refused (stderr), for diagnosing a group that never forms
+bool tts::co_debug() {
+    static const bool on = [] {
+        const char * e = getenv("TTS_HIP_COALESCE_DEBUG");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+#define CO_NO()                                                                                   \
+    do {                                                                                          \
+        if (tts::co_debug()) fprintf(stderr, "coalesce: step refused at graph_exec.hip:%d\n", __LINE__); \
+        return false;                                                                             \
+    } while (0)
+
 // A node of a coalesced step launched once over every member's intermediates (run_node_coalesced's
 // rule): a per-slice op whose output and sources are intermediates or read-only model data.
 static bool co_per_slice(const BatchCtx & bc, const tts_tensor * n) {
@@ -2519,11 +2539,11 @@ static bool co_per_slice(const BatchCtx & bc, const tts_tensor * n) {
             return false;
         default: return false;
     }
-    if (persistent_mem(n) || !bc.stride(n->data) || n->ne[3] != 1) return false;
+    if (owned_mem(n) || !bc.stride(n->data) || n->ne[3] != 1) return false;
     for (int i = 0; i < TTS_MAX_SRC; ++i) {
         const tts_tensor * x = n->src[i];
         if (!x) continue;
-        if (input_mem(x) || (!persistent_mem(x) && !bc.stride(x->data))) return false;
+        if (input_mem(x) || (!owned_mem(x) && !bc.stride(x->data))) return false;
         if (bc.stride(x->data) && x->ne[3] != 1) return false;
         if ((n->op == TTS_OP_CONT || n->op == TTS_OP_CPY || n->op == TTS_OP_DUP) && !bc.stride(x->data)) return false;
     }
@@ -2550,7 +2570,7 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
     auto same_ne = [](const tts_tensor * a, const tts_tensor * b) {
         return a && b && a->ne[0] == b->ne[0] && a->ne[1] == b->ne[1] && a->ne[2] == b->ne[2] && a->ne[3] == b->ne[3];
     };
-    auto inter = [&](const tts_tensor * t) { return t && !persistent_mem(t) && bc.stride(t->data) != 0; };
+    auto inter = [&](const tts_tensor * t) { return t && !owned_mem(t) && bc.stride(t->data) != 0; };
     auto equal_all = [&](const tts_tensor * t) {  // every member's counterpart has t's shape
         if (bc.checked) return true;
         for (int k = 1; k < N; ++k)
@@ -2592,12 +2612,12 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
         if (a < 0) continue;
         if (a == 0) {
             if (is_view(nd->op)) continue;
-            if (!equal_all(nd)) return false;
+            if (!equal_all(nd)) CO_NO();
             for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
-                if (nd->src[s2] && !equal_all(nd->src[s2])) return false;
+                if (nd->src[s2] && !equal_all(nd->src[s2])) CO_NO();
             if (co_per_slice(bc, nd))
                 for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
-                    if (nd->src[s2] && persistent_mem(nd->src[s2]) && !share(nd->src[s2])) return false;
+                    if (nd->src[s2] && owned_mem(nd->src[s2]) && !share(nd->src[s2])) CO_NO();
             continue;
         }
         Item & it = pl.items[a - 1];
@@ -2605,40 +2625,40 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
         auto & of = offs[a - 1];
         switch (it.kind) {
             case Item::GEMV: {
-                if (it.epi == EPI_SWIGLU || it.epi == EPI_SILU_MUL) return false;
+                if (it.epi == EPI_SWIGLU || it.epi == EPI_SILU_MUL) CO_NO();
                 const tts_tensor * x = it.mms[0]->src[1];
-                if (nel(x) != x->ne[0]) return false;  // one column per member
+                if (nel(x) != x->ne[0]) CO_NO();  // one column per member
                 const tts_tensor * xt = it.ln ? it.lnx : it.xsrc ? it.xsrc : x;
-                if (!it.x_shadow && !inter(xt)) return false;
-                if (it.res && !inter(it.res)) return false;
-                if (it.ln && it.lndst && !inter(it.lndst)) return false;
-                if (it.ln && (!share(it.lnw) || !share(it.lnb))) return false;
+                if (!it.x_shadow && !inter(xt)) CO_NO();
+                if (it.res && !inter(it.res)) CO_NO();
+                if (it.ln && it.lndst && !inter(it.lndst)) CO_NO();
+                if (it.ln && (!share(it.lnw) || !share(it.lnb))) CO_NO();
                 bool owned = false;
                 for (size_t k = 0; k < it.mms.size(); ++k) {
-                    if (!equal_all(it.mms[k]) || !share(it.mms[k]->src[0])) return false;
+                    if (!equal_all(it.mms[k]) || !share(it.mms[k]->src[0])) CO_NO();
                     const GemvTarget & t = it.tgt[k];
-                    if (!t.yt) return false;  // backend scratch (a hoisted product): no per-member form
-                    if (!persistent_mem(t.yt)) {
-                        if (!bc.stride(t.y)) return false;
+                    if (!t.yt) CO_NO();  // backend scratch (a hoisted product): no per-member form
+                    if (!owned_mem(t.yt)) {
+                        if (!bc.stride(t.y)) CO_NO();
                         continue;
                     }
-                    if (bc.stride(t.y)) return false;  // member-owned memory inside a compute buffer: no uniform form
+                    if (bc.stride(t.y)) CO_NO();  // member-owned memory inside a compute buffer: no uniform form
                     owned = true;
                 }
                 if (owned) {  // members' own cache rows (KV stores): [target][N] float offsets
                     of[0] = alloc(it.mms.size() * (size_t)N);
                     for (size_t k = 0; k < it.mms.size(); ++k) {
                         const GemvTarget & t = it.tgt[k];
-                        if (!persistent_mem(t.yt)) continue;
-                        if (k >= 32 || !equal_all(t.yt) || !offsets(t.yt, of[0] + (int64_t)k * N, 4)) return false;
+                        if (!owned_mem(t.yt)) continue;
+                        if (k >= 32 || !equal_all(t.yt) || !offsets(t.yt, of[0] + (int64_t)k * N, 4)) CO_NO();
                         tb.yoff_mats |= 1 << k;
                     }
                 }
                 break;
             }
             case Item::ATTN: {
-                if (it.q->ne[3] != 1 || !inter(it.q) || !inter(it.out) || !equal_all(it.q) || !equal_all(it.out)) return false;
-                if (it.mask && it.mask->ne[2] * it.mask->ne[3] != 1) return false;
+                if (it.q->ne[3] != 1 || !inter(it.q) || !inter(it.out) || !equal_all(it.q) || !equal_all(it.out)) CO_NO();
+                if (it.mask && it.mask->ne[2] * it.mask->ne[3] != 1) CO_NO();
                 // each member's own key count; K [hd, P, Hk], V [P, hd, Hv] with the cache's strides
                 of[3] = alloc(((size_t)N + 1) / 2);
                 int * pseq = (int *)&tab[of[3]];
@@ -2651,14 +2671,14 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
                         mv->ne[2] != it.v->ne[2] || mv->ne[3] != 1 || mv->ne[0] != mk->ne[1] || mk->nb[1] != it.k->nb[1] ||
                         mk->nb[2] != it.k->nb[2] || mv->nb[1] != it.v->nb[1] || mv->nb[2] != it.v->nb[2] || mk->nb[0] != it.k->nb[0] ||
                         mv->nb[0] != it.v->nb[0])
-                        return false;
+                        CO_NO();
                     pseq = (int *)&tab[of[3]];  // (tab may have moved)
                     pseq[k] = (int)mk->ne[1];
                     pmax = std::max(pmax, (int)mk->ne[1]);
                     ragged |= mk->ne[1] != it.k->ne[1];
                     if (it.mask) {
                         const tts_tensor * mm = cm.member(bc, it.mask, k);
-                        if (!mm || mm->ne[0] != mk->ne[1] || mm->ne[1] < it.q->ne[1]) return false;
+                        if (!mm || mm->ne[0] != mk->ne[1] || mm->ne[1] < it.q->ne[1]) CO_NO();
                     }
                 }
                 tb.pmax = pmax;
@@ -2666,59 +2686,59 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
                 for (int w = 0; w < 2; ++w) {  // K, V: an intermediate (equal lengths only) or each member's own view
                     const tts_tensor * kv = w ? it.v : it.k;
                     if (inter(kv)) {
-                        if (ragged) return false;
+                        if (ragged) CO_NO();
                         continue;
                     }
-                    if (bc.stride(kv->data)) return false;
+                    if (bc.stride(kv->data)) CO_NO();
                     of[1 + w] = alloc(N);
-                    if (!offsets(kv, of[1 + w], 16)) return false;  // 16-B aligned: the kernels' vector loads
+                    if (!offsets(kv, of[1 + w], 16)) CO_NO();  // 16-B aligned: the kernels' vector loads
                     for (int k = 0; k < N; ++k) tab[of[1 + w] + k] *= 16;
                 }
                 if (it.mask) {
                     if (inter(it.mask)) {
-                        if (ragged) return false;
+                        if (ragged) CO_NO();
                     } else {
                         of[4] = alloc(N);
-                        if (!offsets(it.mask, of[4], 4)) return false;
+                        if (!offsets(it.mask, of[4], 4)) CO_NO();
                     }
                 }
                 break;
             }
             case Item::LN:
-                if (it.dst->ne[3] != 1 || it.x->ne[3] != 1 || !inter(it.dst) || !inter(it.x) || !equal_all(it.dst) || !equal_all(it.x)) return false;
-                if (!share(it.w) || !share(it.b)) return false;
+                if (it.dst->ne[3] != 1 || it.x->ne[3] != 1 || !inter(it.dst) || !inter(it.x) || !equal_all(it.dst) || !equal_all(it.x)) CO_NO();
+                if (!share(it.w) || !share(it.b)) CO_NO();
                 break;
             case Item::EMBED:
-                if (it.gather_t || it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3] != 1 || !inter(it.dst) || !equal_all(it.dst)) return false;
-                if (it.terms.size() > (size_t)EMBED_MAX_TERMS) return false;
+                if (it.gather_t || it.dst->ne[1] * it.dst->ne[2] * it.dst->ne[3] != 1 || !inter(it.dst) || !equal_all(it.dst)) CO_NO();
+                if (it.terms.size() > (size_t)EMBED_MAX_TERMS) CO_NO();
                 for (size_t t = 0; t < it.terms.size(); ++t) {
                     const tts_tensor * g = it.terms[t];
-                    if (g->ne[1] * g->ne[2] * g->ne[3] != 1 || !equal_all(g) || !share(g->src[0])) return false;
+                    if (g->ne[1] * g->ne[2] * g->ne[3] != 1 || !equal_all(g) || !share(g->src[0])) CO_NO();
                     const tts_tensor * idx = g->src[1];
                     if (inter(idx)) continue;
-                    if (!input_mem(idx) || !equal_all(idx)) return false;
+                    if (!input_mem(idx) || !equal_all(idx)) CO_NO();
                     ioffs[a - 1][t] = alloc(N);
-                    if (!offsets(idx, ioffs[a - 1][t], 4)) return false;
+                    if (!offsets(idx, ioffs[a - 1][t], 4)) CO_NO();
                 }
                 break;
             case Item::NODE: {
                 // its node copy stands at the original's graph position (run_node_coalesced finds members' tensors by it)
                 auto * e = cm.pos.find(nd);
-                if (!e) return false;
+                if (!e) CO_NO();
                 cm.pos[&it.node] = e->second;
-                if (!equal_all(nd)) return false;
+                if (!equal_all(nd)) CO_NO();
                 for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2) {
                     const tts_tensor * x = it.node.src[s2];
                     if (!x) continue;
-                    if (!cm.pos.find(x) && persistent_mem(x)) return false;  // a stand-in over member-owned memory
-                    if (cm.pos.find(x) && !equal_all(x)) return false;
+                    if (!cm.pos.find(x) && owned_mem(x)) CO_NO();  // a stand-in over member-owned memory
+                    if (cm.pos.find(x) && !equal_all(x)) CO_NO();
                 }
                 if (co_per_slice(bc, &it.node))
                     for (int s2 = 0; s2 < TTS_MAX_SRC; ++s2)
-                        if (it.node.src[s2] && persistent_mem(it.node.src[s2]) && !share(it.node.src[s2])) return false;
+                        if (it.node.src[s2] && owned_mem(it.node.src[s2]) && !share(it.node.src[s2])) CO_NO();
                 break;
             }
-            default: return false;  // LSTM / SNAKE / CONV / ADAIN / MCPY / RINT / COPY: vocoder and prefill items
+            default: CO_NO();  // LSTM / SNAKE / CONV / ADAIN / MCPY / RINT / COPY: vocoder and prefill items
         }
     }
     // the output intermediates back to every member: the last node and nodes marked output
@@ -2728,11 +2748,11 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
         if ((nodes[i]->flags & TTS_FLAG_OUTPUT) || i == n_nodes - 1) outs.push_back(nodes[i]);
     std::vector<std::array<int64_t, 3>> sc;
     for (const tts_tensor * o : outs) {
-        if (persistent_mem(o) || is_view(o->op)) continue;  // written in place per member (or a view of what is)
-        if (!inter(o) || !contiguous(o) || (tbytes(o) & 3) || !equal_all(o)) return false;
+        if (owned_mem(o) || is_view(o->op)) continue;  // written in place per member (or a view of what is)
+        if (!inter(o) || !contiguous(o) || (tbytes(o) & 3) || !equal_all(o)) CO_NO();
         for (int k = 0; k < N; ++k) {
             const tts_tensor * m = cm.member(bc, o, k);
-            if (!m || !m->data || !contiguous(m)) return false;
+            if (!m || !m->data || !contiguous(m)) CO_NO();
             sc.push_back({(int64_t)(uintptr_t)bc.reloc(o->data, k), (int64_t)(uintptr_t)m->data, (int64_t)tbytes(o)});
         }
     }

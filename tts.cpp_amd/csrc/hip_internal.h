@@ -239,6 +239,7 @@ struct GemvJob {
     // member's cache row at its own position
     const int64_t * yoff = nullptr;
     int32_t yoff_mats = 0, yoff_ld = 0;
+    int32_t xcd_cols = 0;  // many-column K-relay GEMM: a row tile's column tiles on one XCD (TTS_HIP_OPT_GEMM_KR_XCD)
 };
 __host__ __device__ inline int64_t job_roff(const GemvJob & j, int m) { return j.hetero ? j.roff[m] : (int64_t)m * j.N; }
 __host__ __device__ inline int64_t job_rows(const GemvJob & j) { return job_roff(j, j.nmat); }
@@ -397,6 +398,7 @@ struct tts_hip_backend {
     int gemv_q80_rw = 0;       // TTS_HIP_OPT_GEMV_Q80_RW
     int gemm_q8_staged = 2;    // TTS_HIP_OPT_GEMM_Q8_STAGED
     int64_t gemv_kr_ink = 0;   // TTS_HIP_OPT_GEMV_KR_INKERNEL (max K)
+    int gemm_kr_xcd = 1;       // TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (its L2 serves the second)
     int gemm_kr_ct2 = 0;       // TTS_HIP_OPT_GEMM_KR_CT2: two 16-column tiles per K-relay GEMM workgroup (K <= 2048)
     int64_t gemm_kr_ink = 0;   // TTS_HIP_OPT_GEMM_KR_INKERNEL (max M of the many-column K-relay GEMM without the operand pass)
     int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
@@ -609,6 +611,7 @@ void launch_repack_q4_K(tts_hip_backend * be, const void * src, void * dst, int6
 
 // ---- launchers (k_ops.hip) ----
 int launch_op(tts_hip_backend * be, const tts_tensor * node);
+void launch_copy_stream(tts_hip_backend * be, void * dst, const void * src, int64_t n16);  // tts_hip_copy_stream
 
 // ---- graph execution (graph_exec.hip) and the step coalescer (coalesce.hip) ----
 // Plan and launch a node list on be->stream (be->bat set: as a coalesced step of be->bat->N members;
@@ -626,5 +629,6 @@ bool coalesce_check_shared(tts_hip_backend * ex, const std::vector<std::tuple<co
 void coalesce_backend_gone(const tts_hip_backend * be); // a backend is freed: no longer awaited
 void coalesce_written(const void * p, size_t size);     // host writes: content checks over the range are dropped
 bool coalesce_enabled();
+bool co_debug();  // TTS_HIP_COALESCE_DEBUG=1 (graph_exec.hip)
 
 }  // namespace tts

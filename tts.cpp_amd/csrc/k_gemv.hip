@@ -1151,7 +1151,19 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     typedef float f2v __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int nb = (int)(j.K / QK_K);
-    const int ct0 = blockIdx.y * CTW;          // (first) column tile
+    int tx = blockIdx.x, ty = blockIdx.y;
+    if constexpr (!LOOP && CTW == 1) {
+        // j.xcd_cols: the column tiles of one row tile on one XCD, dispatched back to back (the dispatcher
+        // puts workgroup b on XCD b % 8): the second streams the tile's weights out of that XCD's L2
+        // instead of HBM.  The work per (row tile, column tile) is unchanged.
+        if (j.xcd_cols && gridDim.y > 1) {
+            const int n = gridDim.x * gridDim.y;
+            const int w = xcd_contiguous(blockIdx.x + gridDim.x * blockIdx.y, n);
+            tx = w / gridDim.y;
+            ty = w - tx * gridDim.y;
+        }
+    }
+    const int ct0 = ty * CTW;                  // (first) column tile
     int c0 = j.bq_tile ? 16 * ct0 : 0;         // its first column
     int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;
     const int ntile = CTW == 1 ? 1 : min(CTW, (int)((j.M + 15) / 16) - ct0);  // column tiles of this workgroup
@@ -1214,7 +1226,7 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, LOOP ? 1 : 0>;
-    int64_t t = blockIdx.x;
+    int64_t t = tx;
     if constexpr (PRO == PRO_COPY) {
         // operands by LDS-DMA, then this wave's weights (unconditional, clamped)
         const int nck = (int)((ntile * bqb) >> 10);
@@ -2457,6 +2469,7 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
         j.lnout = nullptr;
     }
     const unsigned gx = (unsigned)(job_rows(j) / 16), gy = (unsigned)nct;
+    j.xcd_cols = be->gemm_kr_xcd && nct > 1 ? 1 : 0;
     // TTS_HIP_OPT_GEMM_KR_CT2: two column tiles per workgroup (weights streamed once for 32 columns) where
     // both tiles' operands fit the LDS (K = 1024 x {1, 2})
     const bool ct2 = be->gemm_kr_ct2 && !ink && nct >= 2 && (nb == 4 || nb == 8) && q4k_kr_lds(2 * tile, false) <= 160 * 1024;

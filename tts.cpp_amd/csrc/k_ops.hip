@@ -254,20 +254,23 @@ __global__ __launch_bounds__(256) void k_norm(TD dst, TD a, float eps) {
     }
 }
 
-// ---- SOFT_MAX ext (scale, optional mask row i1 % ne01 with row stride ne00) ----
-__global__ __launch_bounds__(256) void k_soft_max(TD dst, TD a, const char * mask, int mask_f16, float scale) {
+// ---- SOFT_MAX ext (scale, optional mask: a 2-D mask's row i01 for every head and sequence, row stride
+// ne00; a mask with ne2 / ne3 > 1 broadcast per dim as upstream ggml does, i02 % ne12, i03 % ne13 --
+// the per-sequence masks of a ragged lock-step batch) ----
+__global__ __launch_bounds__(256) void k_soft_max(TD dst, TD a, TD m, int mask_f16, float scale) {
     __shared__ double shd[8];
     __shared__ float shf[8];
     const int64_t r = blockIdx.x;
     const int64_t nc = a.ne[0];
     const float * sp = (const float *)(a.data + r * a.nb[1]);
     float * dp = (float *)(dst.data + r * dst.nb[1]);
-    const int64_t mr = r % a.ne[1];
+    const int64_t i01 = r % a.ne[1], i02 = (r / a.ne[1]) % a.ne[2], i03 = r / (a.ne[1] * a.ne[2]);
+    const char * mask = m.data ? m.data + (i01 % m.ne[1]) * m.nb[1] + (i02 % m.ne[2]) * m.nb[2] + (i03 % m.ne[3]) * m.nb[3] : nullptr;
     float mx = -INFINITY;
     for (int64_t i = threadIdx.x; i < nc; i += blockDim.x) {
         float w = __fmul_rn(sp[i], scale);
         if (mask) {
-            const float mv = mask_f16 ? __half2float(((const __half *)mask)[mr * nc + i]) : ((const float *)mask)[mr * nc + i];
+            const float mv = mask_f16 ? __half2float(((const __half *)mask)[i]) : ((const float *)mask)[i];
             w = __fadd_rn(w, __fmul_rn(1.0f, mv));
         }
         dp[i] = w;
@@ -674,8 +677,17 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
         case TTS_OP_SOFT_MAX: {
             const int64_t nr = s0->ne[1] * s0->ne[2] * s0->ne[3];
             const tts_tensor * m = node->src[1];
-            hipLaunchKernelGGL(k_soft_max, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), m ? (const char *)m->data : nullptr,
-                               m ? (m->type == TTS_TYPE_F16) : 0, op_f(node, 0));
+            TD md{};
+            if (m) {
+                md = make_td(m);
+                // rows of ne00 elements (ggml reads mask rows with stride ne00)
+                md.nb[1] = (size_t)tts_type_size(m->type) * (size_t)s0->ne[0];
+                if (m->ne[2] * m->ne[3] == 1) md.nb[2] = md.nb[3] = 0, md.ne[2] = md.ne[3] = 1;
+            } else {
+                md.ne[1] = md.ne[2] = md.ne[3] = 1;
+            }
+            hipLaunchKernelGGL(k_soft_max, dim3((unsigned)nr), dim3(256), 0, st, d, make_td(s0), md, m ? (m->type == TTS_TYPE_F16) : 0,
+                               op_f(node, 0));
         } break;
         case TTS_OP_GET_ROWS: {
             const int64_t nr = s1->ne[0] * s1->ne[1] * s1->ne[2];
@@ -736,6 +748,31 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
     }
     TTS_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+}  // namespace tts
+
+namespace tts {
+
+// ---- streaming copy (tts_hip_copy_stream): the HBM ceiling the bench reports beside the 8 TB/s spec ----
+__global__ __launch_bounds__(256) void k_copy_stream(uint4 * __restrict__ dst, const uint4 * __restrict__ src, int64_t n16) {
+    typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+    u4v * d = (u4v *)dst;
+    const u4v * s = (const u4v *)src;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * gs < n16; i += 4 * gs) {  // four 16-B loads in flight per lane
+        u4v v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(s + i + u * gs);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], d + i + u * gs);
+    }
+    for (; i < n16; i += gs) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+void launch_copy_stream(tts_hip_backend * be, void * dst, const void * src, int64_t n16) {
+    hipLaunchKernelGGL(k_copy_stream, dim3((unsigned)(8 * be->cu_total)), dim3(256), 0, be->stream, (uint4 *)dst, (const uint4 *)src, n16);
 }
 
 }  // namespace tts

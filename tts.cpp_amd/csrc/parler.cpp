@@ -6,6 +6,10 @@
 //
 // Extension (batch > 1): B independent prompts stepped in lockstep share every weight GEMV
 // (M = B columns) while each keeps its own KV cache (attention gets a 4th "sequence" dim).
+// Prompts of different lengths (tts_parler_prefill_ragged) share one prompt pass: sequence b's
+// prompt holds KV slots [0, len_b), slots [len_b, n_max) are padding its own mask hides, and from
+// slot n_max on every sequence's decode tokens share slots; position ids and masks are per
+// sequence.  Each sequence then sees exactly its own prompt's keys, in order.
 // With batch == 1 the node list is exactly the reference's.
 #include <chrono>
 #include <cmath>
@@ -45,8 +49,14 @@ struct tts_parler {
     tg::context gctx;
     tts_tensor * res = nullptr;
     tts_tensor *in_tokens = nullptr, *in_positions = nullptr, *in_mask = nullptr, *in_mask_cross = nullptr;
-    int32_t position = 0;
+    int32_t position = 0;  // KV slots in use (every sequence)
     int32_t current_step = 0;
+    // ragged lock-step batch (tts_parler_prefill_ragged): sequence b's prompt is seq_len[b] tokens,
+    // slots [seq_len[b], hole_end) are never attended, slot s >= hole_end has position id
+    // seq_len[b] + s - hole_end
+    bool ragged = false;
+    std::vector<int32_t> seq_len;
+    int32_t hole_end = 0;
     int32_t last_nodes = 0;
     double host_us[5] = {0, 0, 0, 0, 0};  // build, alloc, set_inputs, compute (record + launch), get (wait)
     bool prepared = false;  // a step is built and recorded, waiting for launch_step
@@ -352,6 +362,9 @@ extern "C" void tts_parler_free(tts_parler * p) {
 
 extern "C" void tts_parler_reset(tts_parler * p) {
     p->position = 0;
+    p->ragged = false;
+    p->seq_len.clear();
+    p->hole_end = 0;
     p->current_step = 0;
     p->prepared = false;
     p->output_tokens.assign(p->cfg.batch, {});
@@ -378,8 +391,9 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
     tg::context & c = p->gctx;
     c.reset();
 
-    // parler_build_inp_embd (model.cpp:387-410)
-    p->in_positions = tg::new_tensor_1d(c, TTS_TYPE_I32, n);
+    // parler_build_inp_embd (model.cpp:387-410); a ragged batch: positions per sequence ([B][n])
+    const bool rg = p->ragged && B > 1;
+    p->in_positions = tg::new_tensor_1d(c, TTS_TYPE_I32, rg ? (int64_t)n * B : n);
     tg::set_input(p->in_positions);
     tts_tensor * inp = nullptr;
     if (audio) {
@@ -412,11 +426,13 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
             inp = tg::reshape_3d(c, tg::get_rows(c, p->prompt_embd, p->in_tokens), H, n, B);  // [H, n, B]
         }
     }
-    tts_tensor * inpL = tg::add(c, inp, tg::get_rows(c, p->pos_embd, p->in_positions));
+    tts_tensor * pe = tg::get_rows(c, p->pos_embd, p->in_positions);
+    if (rg && !audio) pe = tg::reshape_3d(c, pe, H, n, B);
+    tts_tensor * inpL = tg::add(c, inp, pe);
     if (B > 1 && audio) inpL = tg::reshape_3d(c, inpL, H, 1, B);
 
-    // build_attn_mask / build_attn_mask_cross (model.cpp:459-471)
-    p->in_mask = tg::new_tensor_2d(c, TTS_TYPE_F32, full, full);
+    // build_attn_mask / build_attn_mask_cross (model.cpp:459-471); a ragged batch: one per sequence
+    p->in_mask = rg ? tg::new_tensor_4d(c, TTS_TYPE_F32, full, n, 1, B) : tg::new_tensor_2d(c, TTS_TYPE_F32, full, full);
     tg::set_input(p->in_mask);
     p->in_mask_cross = tg::new_tensor_2d(c, TTS_TYPE_F32, cf.n_encode, n);
     tg::set_input(p->in_mask_cross);
@@ -534,14 +550,31 @@ static int set_inputs(tts_parler * p, const int32_t * tokens, bool audio, int n,
     } else {
         st |= be.set(be.ctx, p->in_tokens->data, tokens, sizeof(int32_t) * n * B);
     }
-    std::vector<int32_t> pos(n);
-    for (int i = 0; i < n; ++i) pos[i] = p->position + i;
-    st |= be.set(be.ctx, p->in_positions->data, pos.data(), sizeof(int32_t) * n);
     const int64_t full = p->position + n;
-    std::vector<float> mask((size_t)n * full);
-    for (int i = 0; i < n; ++i)
-        for (int64_t j = 0; j < full; ++j) mask[(size_t)i * full + j] = j > pos[i] ? -INFINITY : 0.0f;
-    st |= be.set(be.ctx, p->in_mask->data, mask.data(), mask.size() * sizeof(float));
+    if (p->ragged && B > 1) {
+        // per sequence: slot s's position id, and a mask hiding later slots and the padding slots
+        std::vector<int32_t> pos((size_t)n * B);
+        std::vector<float> mask((size_t)B * n * full);
+        for (int b = 0; b < B; ++b) {
+            const int32_t L = p->seq_len[b];
+            for (int i = 0; i < n; ++i) {
+                const int32_t s = p->position + i;
+                pos[(size_t)b * n + i] = s < p->hole_end ? s : L + (s - p->hole_end);
+                for (int64_t j = 0; j < full; ++j)
+                    mask[((size_t)b * n + i) * full + j] = j > s || (j >= L && j < p->hole_end) ? -INFINITY : 0.0f;
+            }
+        }
+        st |= be.set(be.ctx, p->in_positions->data, pos.data(), sizeof(int32_t) * pos.size());
+        st |= be.set(be.ctx, p->in_mask->data, mask.data(), mask.size() * sizeof(float));
+    } else {
+        std::vector<int32_t> pos(n);
+        for (int i = 0; i < n; ++i) pos[i] = p->position + i;
+        st |= be.set(be.ctx, p->in_positions->data, pos.data(), sizeof(int32_t) * n);
+        std::vector<float> mask((size_t)n * full);
+        for (int i = 0; i < n; ++i)
+            for (int64_t j = 0; j < full; ++j) mask[(size_t)i * full + j] = j > pos[i] ? -INFINITY : 0.0f;
+        st |= be.set(be.ctx, p->in_mask->data, mask.data(), mask.size() * sizeof(float));
+    }
     std::vector<float> mc((size_t)cf.n_encode * n, 0.0f);
     st |= be.set(be.ctx, p->in_mask_cross->data, mc.data(), mc.size() * sizeof(float));
     return st;
@@ -618,6 +651,25 @@ static int decode(tts_parler * p, const int32_t * tokens, bool audio, int n, flo
 
 extern "C" int tts_parler_prefill(tts_parler * p, const int32_t * tokens, int32_t n) {
     int st = decode(p, tokens, false, n, nullptr);
+    if (st == 0) p->be.synchronize(p->be.ctx);
+    return st;
+}
+
+// One prompt pass over B prompts of different lengths (lens[b] <= n_max tokens each, row b of
+// `tokens` holding n_max ids, the tail past lens[b] ignored) from an empty cache: a ragged lock-step
+// batch (see the top of the file).  Every sequence's later tokens equal its own prompt's alone.
+extern "C" int tts_parler_prefill_ragged(tts_parler * p, const int32_t * tokens, const int32_t * lens, int32_t n_max) {
+    if (!p || !tokens || !lens || n_max < 1 || p->position != 0 || p->current_step != 0) return TTS_STATUS_BAD_ARG;
+    const int B = p->cfg.batch;
+    for (int b = 0; b < B; ++b)
+        if (lens[b] < 1 || lens[b] > n_max) return TTS_STATUS_BAD_ARG;
+    p->seq_len.assign(lens, lens + B);
+    p->hole_end = n_max;
+    p->ragged = B > 1;
+    std::vector<int32_t> tok((size_t)B * n_max);
+    for (int b = 0; b < B; ++b)
+        for (int i = 0; i < n_max; ++i) tok[(size_t)b * n_max + i] = i < lens[b] ? tokens[(size_t)b * n_max + i] : 0;  // padding: never attended
+    int st = decode(p, tok.data(), false, n_max, nullptr);
     if (st == 0) p->be.synchronize(p->be.ctx);
     return st;
 }
