@@ -598,7 +598,11 @@ def parler_replicas(args, per_gpu, R, rank, new_backend, dac_cfg=None):
     for r, (rb, rr, rd) in enumerate(reps):
         rb.sync()
         tp0 = time.perf_counter()
-        rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * per_gpu + r * bl))
+        if getattr(args, "no_prefill", False):  # (counter runs: the decode step's work at KV ctx without the long prompt pass)
+            rr.prefill(prompt_tokens(bl, 8, cfg.prompt_vocab, offset=rank * per_gpu + r * bl))
+            rr.set_position(args.ctx)
+        else:
+            rr.prefill(prompt_tokens(bl, args.ctx, cfg.prompt_vocab, offset=rank * per_gpu + r * bl))
         rb.sync()
         prefill_ms.append(1000.0 * (time.perf_counter() - tp0))
         rr.generate(min(2, args.warmup))  # the step graph recorded (first sighting eager, then captured)
@@ -668,6 +672,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="prompts per GPU instead of --prompts / world (weak scaling)")
     ap.add_argument("--ctx", type=int, default=448, help="KV length when timing starts (prompt prefill)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true", help="counter / trace runs: an 8-token prompt pass, then the KV length "
+                    "set to --ctx (tts_parler_set_position: the decode steps do the work of KV ctx without its prompt pass)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--cpu-steps", type=int, default=400)
     ap.add_argument("--b1-replicas", type=int, default=8, help="the B=1 leg: this many runners of one prompt each, as "

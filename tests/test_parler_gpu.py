@@ -268,7 +268,7 @@ def test_ragged_prompt_pass_parler_mini(hip):
     import bench
     cfg = ttship.parler_config(batch=8, max_ctx=256)
     prompts = [bench.sentence_tokens(bench.HARVARD[g], cfg.prompt_vocab) for g in range(8)]
-    assert len({len(p) for p in prompts}) > 3  # ragged
+    assert len({len(p) for p in prompts}) >= 3  # ragged
     g = ttship.Parler(hip.iface(), cfg)
     try:
         g.prefill_ragged(prompts)
