@@ -497,6 +497,7 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True, ragged=
         run_replicas(make, R)
         run_replicas(lambda r: (runs[r].generate(args.warmup), bes[r].sync()), R)  # the coalesced groups form
         s0 = ttship.coalesce_stats(local)
+        runs[0].host_stats(reset=True)
 
         def one(r):
             if ragged:
@@ -511,6 +512,9 @@ def parler_b1_leg(args, rank, local, new_backend, R=None, coalesce=True, ragged=
         co = {k: s1[k] - s0[k] for k in ("launches", "member_steps", "alone", "refused", "ragged_launches")}
         co["max_group"] = s1["max_group"]
         co["wait_us_per_step"] = round((s1["wait_us"] - s0["wait_us"]) / max(1, R * steps), 1)
+        co["runner0_host_us_per_step"] = runs[0].host_stats(reset=True)  # build / alloc / set_inputs / compute (incl. the rendezvous) / get
+        nl = max(1, co["launches"])  # host time per coalesced launch: the whole run_group, its layout / plan / tables parts
+        co["host_us_per_launch"] = {k: round((s1[k] - s0[k]) / nl, 1) for k in ("exec_us", "layout_us", "plan_us", "tables_us")}
         return {"workload": f"Parler-mini Q4_K AR decode, {R} runners x 1 prompt (TTS.cpp's server model: one runner, backend and "
                             f"model copy per worker thread, graph_compute + host greedy sampler per step), KV "
                             f"{min(lens)}..{max(lens)} -> +{steps}" + (", prompt lengths 7 r apart, thread r starting r ms late" if ragged else ""),
@@ -711,6 +715,7 @@ def main():
     ap.add_argument("--gemv-kr-inkernel", type=int, default=None, help="TTS_HIP_OPT_GEMV_KR_INKERNEL: max K of K-relay GEMVs quantizing in-kernel (0 = operand pass)")
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--attn-pv-mp", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV_MP: all dims of a head per P.V workgroup (1) or 16 (0)")
+    ap.add_argument("--gemm-kr-cp", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_CP: two column tiles per K-relay workgroup on parallel wave halves (1) or not (0)")
     ap.add_argument("--gemm-kr-xcd", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (1, default) or grid order (0)")
     ap.add_argument("--gemm-kr-nw", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_NW: waves per tile of the many-column K-relay GEMM (4 / 8)")
     ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
@@ -756,7 +761,7 @@ def main():
                           ("gemv_q80_rw", "GEMV_Q80_RW"), ("gemm_q8_staged", "GEMM_Q8_STAGED"),
                           ("gemv_kr_inkernel", "GEMV_KR_INKERNEL"), ("attn_ks", "ATTN_KS"), ("attn_pv8", "ATTN_PV8"),
                           ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE"),
-                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW"), ("gemm_kr_xcd", "GEMM_KR_XCD")):
+                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW"), ("gemm_kr_xcd", "GEMM_KR_XCD"), ("gemm_kr_cp", "GEMM_KR_CP")):
             v = getattr(args, flag)
             if v is not None:
                 rb.set_option(ttship.OPT[opt], v)

@@ -333,6 +333,8 @@ enum tts_hip_option {
                                      0 = default geometry, about one row group per wave over every CU) */
     TTS_HIP_OPT_GEMM_KR_XCD = 38, /* 1 (default): the many-column K-relay GEMM places a row tile's 16-column tiles on one XCD,
                                      dispatched back to back, so the second streams the weights from that XCD's L2; 0 = grid order */
+    TTS_HIP_OPT_GEMM_KR_CP = 39,  /* 1: the many-column K-relay GEMM (K = 1024 / 2048) gives a workgroup two 16-column tiles on two
+                                     parallel wave halves (the weight tile streamed from HBM once for both; 0 = one tile each) */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
                                      backend's graph_compute of a one-prompt decode step may join the same step of other
                                      backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */
@@ -354,7 +356,9 @@ int tts_hip_set_option(tts_hip_backend_t backend, int option, int value);
 /* Step coalescer counters of `device` since process start: out[0] coalesced launches, [1] member steps they
  * carried, [2] steps a member ran alone after waiting, [3] groups refused (no coalesced form / mismatched
  * members), [4] the largest group, [5] host microseconds spent waiting for members, [6] coalesced launches whose
- * members were at different KV lengths.  Returns the number written. */
+ * members were at different KV lengths, [7] host microseconds in the coalesced steps' execution (grouping,
+ * layout, plan, tables, launches), [8] of it in the executor layout, [9] planning, [10] tables (co_prepare + upload).
+ * Returns the number written. */
 int tts_hip_coalesce_stats(int device, int64_t * out, int n);
 /* Coalescer rendezvous window (microseconds a step waits for the other active members; default 5000). */
 void tts_hip_coalesce_set_wait(int us);

@@ -115,6 +115,29 @@ def test_q4_K_prefill_gemm_two_column_tiles(hip, tiled, K, N, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("opt,val", [("GEMM_KR_CP", 1), ("GEMM_KR_XCD", 0)])
+@pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (2048, 1024, 32), (1024, 3072, 48), (2048, 160, 17), (1024, 512, 64),
+                                   (4096, 1024, 32)])
+def test_q4_K_prefill_gemm_column_pairs(hip, tiled, opt, val, K, N, M):
+    """The many-column K-relay GEMM with a row tile's two column tiles on one workgroup's two wave halves
+    (TTS_HIP_OPT_GEMM_KR_CP; K = 4096 keeps one tile per workgroup), and without the XCD-contiguous
+    column-tile order (TTS_HIP_OPT_GEMM_KR_XCD = 0; on by default): the same sums, bit-identical (odd
+    tile counts leave the last pair's second half idle)."""
+    dflt = {"GEMM_KR_CP": 0, "GEMM_KR_XCD": 1}[opt]
+    hip.set_option(ttship.OPT[opt], val)
+    try:
+        rng = np.random.default_rng(K * 5 + N + M + tiled)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        hip.set_option(ttship.OPT[opt], dflt)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [False, True])
 @pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (4096, 1024, 32), (1024, 3072, 9), (2048, 160, 17), (4096, 512, 64),
                                    (3072, 256, 40)])
 def test_q4_K_prefill_gemm_in_kernel_operands(hip, tiled, K, N, M):

@@ -165,8 +165,8 @@ def test_graph_replay_across_kernel_switches(hip, batch):
 def test_many_prompt_step_in_kernel_operands(hip):
     """Parler-mini Q4_K at 32 lock-step prompts (every decode product has M = 32 > 8 columns: the K-relay
     GEMM over two column tiles) with the LN / quantize prologues inside the GEMM workgroups
-    (TTS_HIP_OPT_GEMM_KR_INKERNEL), and with both column tiles in one workgroup (TTS_HIP_OPT_GEMM_KR_CT2),
-    against the default: tokens and logits bit-identical, tokens equal to the oracle's."""
+    (TTS_HIP_OPT_GEMM_KR_INKERNEL), with both column tiles in one workgroup in turn (TTS_HIP_OPT_GEMM_KR_CT2)
+    and on parallel wave halves (TTS_HIP_OPT_GEMM_KR_CP), against the default: tokens and logits bit-identical, tokens equal to the oracle's."""
     B = 32
     prompt = (np.arange(7 * B, dtype=np.int32).reshape(B, 7) * 41 + 3) % 1000
     ink_be = ttship.HipBackend(0)
@@ -174,18 +174,23 @@ def test_many_prompt_step_in_kernel_operands(hip):
     ct2_be = ttship.HipBackend(0)
     ct2_be.set_option(ttship.OPT["GEMM_KR_CT2"], 1)
     k2 = ttship.Parler(ct2_be.iface(), ttship.parler_config(batch=B))
+    cp_be = ttship.HipBackend(0)
+    cp_be.set_option(ttship.OPT["GEMM_KR_CP"], 1)
+    k3 = ttship.Parler(cp_be.iface(), ttship.parler_config(batch=B))
     g, c = make_pair(hip, batch=B)
     k = ttship.Parler(ink_be.iface(), ttship.parler_config(batch=B))
     try:
-        for r in (g, c, k, k2):
+        for r in (g, c, k, k2, k3):
             r.prefill(prompt)
-        tg, tc, tk, t2 = g.generate(4), c.generate(4), k.generate(4), k2.generate(4)
+        tg, tc, tk, t2, t3 = g.generate(4), c.generate(4), k.generate(4), k2.generate(4), k3.generate(4)
         assert np.array_equal(tg, tc), f"token mismatch vs oracle\n{tg}\n{tc}"
-        assert np.array_equal(tk, tg) and np.array_equal(t2, tg)
+        assert np.array_equal(tk, tg) and np.array_equal(t2, tg) and np.array_equal(t3, tg)
         toks = np.full((B, 9), 5, dtype=np.int32)
         lg = g.decode(toks)
-        assert np.array_equal(lg, k.decode(toks)) and np.array_equal(lg, k2.decode(toks))
+        assert np.array_equal(lg, k.decode(toks)) and np.array_equal(lg, k2.decode(toks)) and np.array_equal(lg, k3.decode(toks))
     finally:
+        k3.close()
+        cp_be.close()
         k2.close()
         ct2_be.close()
         k.close()

@@ -75,6 +75,7 @@ struct Dev {
     int d_flags_n = 0;
     // counters (tts_hip_coalesce_stats)
     std::atomic<int64_t> launches{0}, member_steps{0}, alone{0}, refused{0}, max_group{0}, wait_us{0}, ragged{0};
+    std::atomic<int64_t> exec_ns{0}, layout_ns{0};  // host time of run_group, of exec_layout
 };
 Dev g_dev[kMaxDev];
 std::atomic<int> g_wait_us{5000};
@@ -152,9 +153,18 @@ bool decode_like(tts_tensor * const * nodes, int n) {
 // compute-buffer layout).  Graphs with equal signatures are coalesced; co_prepare (graph_exec.hip)
 // then checks them against each other item by item.  Two independent 64-bit hashes, folded.
 uint64_t signature(tts_tensor * const * nodes, int n) {
-    std::unordered_map<const tts_tensor *, int> idx;
-    idx.reserve((size_t)n * 2);
-    for (int i = 0; i < n; ++i) idx[nodes[i]] = i;
+    // node -> index: an open-addressing table per thread (every decode step of every runner hashes its graph)
+    thread_local std::vector<std::pair<const tts_tensor *, int>> tab;
+    size_t cap = 64;
+    while (cap < 2 * (size_t)n) cap <<= 1;
+    tab.assign(cap, {nullptr, -1});
+    const size_t mask = cap - 1;
+    auto slot = [&](const tts_tensor * t) {
+        size_t i = (size_t)(((uint64_t)(uintptr_t)t * 0x9E3779B97F4A7C15ull) >> 32) & mask;
+        while (tab[i].first && tab[i].first != t) i = (i + 1) & mask;
+        return i;
+    };
+    for (int i = 0; i < n; ++i) tab[slot(nodes[i])] = {nodes[i], i};
     uint64_t h = 0xCBF29CE484222325ull ^ (uint64_t)n, h2 = 0x84222325CBF29CE4ull + (uint64_t)n;
     auto mix = [&](uint64_t v) {
         h = (h ^ v) * 0x100000001B3ull;
@@ -172,12 +182,12 @@ uint64_t signature(tts_tensor * const * nodes, int n) {
             mix(0x51);
             return;
         }
-        auto it = idx.find(x);
-        if (it != idx.end()) {
-            mix(0x1000000ull + it->second);
+        const auto & e = tab[slot(x)];
+        if (e.first) {
+            mix(0x1000000ull + e.second);
             return;
         }
-        kind(x);  // a leaf
+        mix(0x4C00000000ull | (uint64_t)(uint32_t)x->type << 8 | (uint64_t)(x->flags & kLayout));  // a leaf: no parameters
     };
     for (int i = 0; i < n; ++i) {
         const tts_tensor * t = nodes[i];
@@ -214,6 +224,7 @@ void copy_options(tts_hip_backend * d, const tts_hip_backend * s) {
     d->gemv_kr_ink = s->gemv_kr_ink;
     d->gemm_kr_ct2 = s->gemm_kr_ct2;
     d->gemm_kr_xcd = s->gemm_kr_xcd;
+    d->gemm_kr_cp = s->gemm_kr_cp;
     d->gemm_kr_ink = s->gemm_kr_ink;
     d->gemv_nw_min = s->gemv_nw_min;
     d->gemv_mf_rsplit = s->gemv_mf_rsplit;
@@ -341,6 +352,12 @@ bool exec_layout(Dev & d, BatchCtx & bc, tts_tensor * const * nodes, int n) {
 // Run one group (the caller holds no lock).  Statuses are written into the requests.
 void run_group(Dev & d, std::vector<Req *> & g) {
     std::lock_guard<std::mutex> xl(d.exec_mu);
+    const auto tg0 = Clock::now();
+    struct Acc {  // run_group's host time, whatever the exit
+        Dev & d;
+        Clock::time_point t0;
+        ~Acc() { d.exec_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count(); }
+    } acc{d, tg0};
     Req * r0 = g[0];
     std::vector<Req *> mem;
     for (Req * q : g)
@@ -365,7 +382,10 @@ void run_group(Dev & d, std::vector<Req *> & g) {
             return;
         }
     }
-    if (!exec_layout(d, bc, r0->nodes, r0->n)) {
+    const auto tl0 = Clock::now();
+    const bool lay = exec_layout(d, bc, r0->nodes, r0->n);
+    d.layout_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - tl0).count();
+    if (!lay) {
         if (co_debug()) fprintf(stderr, "coalesce: group refused: executor layout\n");
         d.refused++;
         return;
@@ -545,9 +565,11 @@ extern "C" int tts_hip_coalesce_stats(int device, int64_t * out, int n) {
     if (device < 0 || device >= tts::kMaxDev || !out) return TTS_STATUS_BAD_ARG;
     tts::Dev & d = tts::g_dev[device];
     std::lock_guard<std::mutex> lk(d.mu);
-    const int64_t v[7] = {d.launches, d.member_steps, d.alone, d.refused, d.max_group, d.wait_us, d.ragged};
+    const tts_hip_backend * ex = d.exec;
+    const int64_t v[11] = {d.launches, d.member_steps, d.alone, d.refused, d.max_group, d.wait_us, d.ragged, d.exec_ns / 1000,
+                           d.layout_ns / 1000, ex ? ex->cap_plan_ns / 1000 : 0, ex ? ex->co_prep_ns / 1000 : 0};
     int k = 0;
-    for (; k < n && k < 7; ++k) out[k] = v[k];
+    for (; k < n && k < 11; ++k) out[k] = v[k];
     return k;
 }
 

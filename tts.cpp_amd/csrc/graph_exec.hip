@@ -2985,6 +2985,12 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
     int64_t sc_off = -1;
     int n_sc = 0;
     if (be->bat) {
+        const auto tq0 = std::chrono::steady_clock::now();
+        struct Acc {
+            tts_hip_backend * be;
+            std::chrono::steady_clock::time_point t0;
+            ~Acc() { be->co_prep_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count(); }
+        } acc{be, tq0};
         BatchCtx & bc = *be->bat;
         cm.build(nodes, n_nodes);
         bc.comap = &cm;

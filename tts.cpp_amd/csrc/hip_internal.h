@@ -398,6 +398,7 @@ struct tts_hip_backend {
     int gemv_q80_rw = 0;       // TTS_HIP_OPT_GEMV_Q80_RW
     int gemm_q8_staged = 2;    // TTS_HIP_OPT_GEMM_Q8_STAGED
     int64_t gemv_kr_ink = 0;   // TTS_HIP_OPT_GEMV_KR_INKERNEL (max K)
+    int gemm_kr_cp = 0;        // TTS_HIP_OPT_GEMM_KR_CP: two column tiles per workgroup on parallel wave halves
     int gemm_kr_xcd = 1;       // TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (its L2 serves the second)
     int gemm_kr_ct2 = 0;       // TTS_HIP_OPT_GEMM_KR_CT2: two 16-column tiles per K-relay GEMM workgroup (K <= 2048)
     int64_t gemm_kr_ink = 0;   // TTS_HIP_OPT_GEMM_KR_INKERNEL (max M of the many-column K-relay GEMM without the operand pass)
@@ -485,6 +486,7 @@ struct tts_hip_backend {
     hipEvent_t co_ev = nullptr;
     int64_t * co_tab = nullptr;  // device copy of a coalesced plan's per-item tables (ItemTab)
     size_t co_tab_bytes = 0;
+    int64_t co_prep_ns = 0;      // host time of co_prepare + the tables' upload (coalesced steps)
     bool co_member = true;  // TTS_HIP_OPT_COALESCE: this backend's graph_compute calls may join a coalesced step
 };
 

@@ -1145,8 +1145,12 @@ __global__ __launch_bounds__(512) void k_gemv_q4K_mf(GemvJob j) {
 // CTW = 2 (PRO_COPY, column tiles): a workgroup takes two column tiles of its row tile in turn -- the
 // tile's weights are loaded into registers once and multiplied against both tiles' operands (both in
 // LDS), instead of two workgroups streaming the same weights.
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1>
-__global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
+// CP (PRO_COPY, column tiles): the workgroup's two wave halves take column tiles 2y and 2y + 1 of the
+// same row tile at once -- both halves request the same weight bytes, the second half's requests are
+// served by the CU's caches, so each weight tile is streamed from HBM once for 32 columns while every
+// tile keeps its own NWT-wave relay (same additions, same order as CTW = 1: bit-identical).
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1, bool CP = false>
+__global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr(GemvJob j) {
     constexpr int nwt = NWT;  // waves per tile: blocks w*BPW .. of a K = 256 * NWT * BPW row
     typedef float f2v __attribute__((ext_vector_type(2)));
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1163,22 +1167,24 @@ __global__ __launch_bounds__(64 * NWT * (SW ? 2 : 1)) void k_gemv_q4K_kr(GemvJob
             ty = w - tx * gridDim.y;
         }
     }
-    const int ct0 = ty * CTW;                  // (first) column tile
-    int c0 = j.bq_tile ? 16 * ct0 : 0;         // its first column
-    int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;
-    const int ntile = CTW == 1 ? 1 : min(CTW, (int)((j.M + 15) / 16) - ct0);  // column tiles of this workgroup
+    constexpr int CT = CP ? 2 : CTW;            // column tiles per workgroup
+    const int ct0 = ty * CT;                   // (first) column tile
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+    const int sub = (SW || CP) ? wave / nwt : 0;  // SwiGLU: 0 = gate tile, 1 = up tile; CP: the column tile ct0 + sub
+    int c0 = j.bq_tile ? 16 * (ct0 + (CP ? sub : 0)) : 0;  // the first column
+    int M = j.bq_tile ? min(16, (int)j.M - c0) : (int)j.M;  // (CP: <= 0 for the idle half of an odd last pair)
+    const int ntile = CT == 1 ? 1 : min(CT, (int)((j.M + 15) / 16) - ct0);  // column tiles of this workgroup
     const char * const bqt = j.bq + (size_t)ct0 * j.bq_tile;
     const int64_t bqb = j.bq_tile ? j.bq_tile : j.bq_bytes;
-    int nslot = M * nb + 1;
-    _Float16 * b16 = (_Float16 *)smem;
+    const int Ma = M > 0 ? M : 1;              // slot addressing of an idle half (it stores nothing)
+    int nslot = Ma * nb + 1;
+    _Float16 * b16 = (_Float16 *)(smem + (CP ? (size_t)sub * bqb : 0));
     _Float16 * sbs = b16 + (size_t)nslot * QK_K;
     float * xd_s = (float *)(sbs + (size_t)nslot * 16);
-    float * relay = (float *)(smem + ((CTW * bqb + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
+    float * relay = (float *)(smem + ((CT * bqb + 15) & ~(int64_t)15));  // [1 or 2 sub-tiles][64 lanes][36]
 
-    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
     const int r = lane & 15, kg = lane >> 4;
-    int cc = r < M ? r : M - 1;
-    const int sub = SW ? wave / nwt : 0;    // SwiGLU: 0 = gate tile, 1 = up tile
+    int cc = r < Ma ? r : Ma - 1;
     const int w = wave - sub * nwt;         // position in the relay
     const int64_t NR = SW ? j.N : job_rows(j);
     const int64_t T = NR / 16;              // launcher: whole tiles
@@ -2380,9 +2386,9 @@ static void launch_q4k_mf(tts_hip_backend * be, const GemvJob & job) {
 
 // ---- K-relay matrix-core path (k_gemv_q4K_kr) ----
 static size_t q4k_kr_lds(int64_t bq_bytes, bool sw) { return (size_t)((bq_bytes + 15) & ~15) + (sw ? 2 * 64 * 36 * 4 + 64 * 16 : 64 * 36 * 4); }
-template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1>
+template <int BPW, bool SW, int NWT, bool LANE = false, bool LOOP = false, int PRO = PRO_COPY, int CTW = 1, bool CP = false>
 static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx, unsigned gy = 1) {
-    if constexpr (PRO == PRO_COPY && CTW == 1) {  // in-kernel prologue (launch_q4k_kr / launch_gemm_q4k_kr decide)
+    if constexpr (PRO == PRO_COPY && CTW == 1 && !CP) {  // in-kernel prologue (launch_q4k_kr / launch_gemm_q4k_kr decide)
         if (j.pro == PRO_LN) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_LN>(be, j, gx, gy);
         if (j.pro == PRO_QUANT) return launch_q4k_kr_t<BPW, SW, NWT, LANE, LOOP, PRO_QUANT>(be, j, gx, gy);
     }
@@ -2395,17 +2401,17 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
         }
     }
     static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>);
-    const size_t lds = q4k_kr_lds(CTW * (j.bq_tile ? j.bq_tile : j.bq_bytes), SW);
-    const dim3 blk(64 * NWT * (SW ? 2 : 1));
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW, CP>);
+    const size_t lds = q4k_kr_lds((CP ? 2 : CTW) * (j.bq_tile ? j.bq_tile : j.bq_bytes), SW || CP);
+    const dim3 blk(64 * NWT * ((SW || CP) ? 2 : 1));
     if (be->profile_gemv) {
         hipEvent_t e0, e1;
         profile_pair(be, e0, e1);
-        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
+        hipExtLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW, CP>), dim3(gx, gy), blk, (uint32_t)lds, be->stream, e0, e1, 0u, j);
         profile_push(be, e0, e1, gemv_bytes(j), TTS_TYPE_Q4_K);
         return;
     }
-    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW>), dim3(gx, gy), blk, lds, be->stream, j);
+    hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW, CP>), dim3(gx, gy), blk, lds, be->stream, j);
 }
 
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
@@ -2473,8 +2479,16 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     // TTS_HIP_OPT_GEMM_KR_CT2: two column tiles per workgroup (weights streamed once for 32 columns) where
     // both tiles' operands fit the LDS (K = 1024 x {1, 2})
     const bool ct2 = be->gemm_kr_ct2 && !ink && nct >= 2 && (nb == 4 || nb == 8) && q4k_kr_lds(2 * tile, false) <= 160 * 1024;
+    // TTS_HIP_OPT_GEMM_KR_CP: two column tiles per workgroup on parallel wave halves (weights from HBM once)
+    const bool cp = be->gemm_kr_cp && !ink && nct >= 2 && (nb == 4 || nb == 8) && q4k_kr_lds(2 * tile, true) <= 160 * 1024;
     auto go = [&](auto LANE) {
         constexpr bool L = decltype(LANE)::value;
+        if (cp) {
+            const unsigned gy2 = (unsigned)((nct + 1) / 2);
+            if (nb == 4) launch_q4k_kr_t<1, false, 4, L, false, PRO_COPY, 1, true>(be, j, gx, gy2);
+            else launch_q4k_kr_t<2, false, 4, L, false, PRO_COPY, 1, true>(be, j, gx, gy2);
+            return;
+        }
         if (ct2) {
             const unsigned gy2 = (unsigned)((nct + 1) / 2);
             if (nb == 4) launch_q4k_kr_t<1, false, 4, L, false, PRO_COPY, 2>(be, j, gx, gy2);
