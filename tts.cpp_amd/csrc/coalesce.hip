@@ -71,6 +71,7 @@ struct Dev {
     char * mem = nullptr;                 // executor memory for the members' intermediates
     size_t mem_bytes = 0;
     std::unordered_set<uint64_t> verified;  // group keys whose shapes and read-only operands checked out
+    std::unordered_set<uint64_t> no_form;   // kinds of graph whose plan has no coalesced form (never waited for again)
     int * d_flags = nullptr;              // content-check mismatch flags
     int d_flags_n = 0;
     // counters (tts_hip_coalesce_stats)
@@ -408,6 +409,12 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     if (st == TTS_STATUS_UNSUPPORTED) {  // refused before any launch: each member runs its own graph
         if (co_debug()) fprintf(stderr, "coalesce: group of %d refused by the plan\n", bc.N);
         d.refused++;
+        // a graph kind whose members cannot share a step (an item with no batched form, weights that differ):
+        // later steps of that kind run at once instead of waiting for peers again
+        if (!bc.differs) {
+            std::lock_guard<std::mutex> lk(d.mu);
+            d.no_form.insert(r0->sig);
+        }
         return;
     }
     if (!bc.checked && st == 0) {
@@ -456,6 +463,10 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
     r.n = n;
     r.sig = signature(nodes, n);  // outside the lock, in the caller's thread: ~1200 nodes
     std::unique_lock<std::mutex> lk(d.mu);
+    if (d.no_form.count(r.sig)) {  // known to have no coalesced form: no rendezvous, and not waited for
+        if (d.seen.erase(be)) d.cv.notify_all();
+        return kCoalesceNotTaken;
+    }
     Act & me = d.seen[be];
     me.t = t0;
     me.tid = std::this_thread::get_id();

@@ -2997,7 +2997,12 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
         std::vector<std::tuple<const void *, const void *, size_t>> shared;
         std::vector<int64_t> tab;
         std::vector<std::array<int64_t, 5>> offs;
-        if (!co_prepare(be, pl, nodes, n_nodes, shared, tab, offs, &sc_off, &n_sc) || !coalesce_check_shared(be, shared)) {
+        if (!co_prepare(be, pl, nodes, n_nodes, shared, tab, offs, &sc_off, &n_sc)) {
+            bc.comap = nullptr;
+            return TTS_STATUS_UNSUPPORTED;
+        }
+        if (!coalesce_check_shared(be, shared)) {
+            bc.differs = true;
             bc.comap = nullptr;
             return TTS_STATUS_UNSUPPORTED;
         }

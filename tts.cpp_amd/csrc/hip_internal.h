@@ -315,6 +315,7 @@ struct BatchCtx {
     int n_nodes = 0;
     bool checked = false;       // this group's shapes and read-only operands were verified by an earlier step
     bool ragged = false;        // (co_prepare) the members' KV lengths differ
+    bool differs = false;       // refused because a member's read-only data differs (not for lack of a batched form)
     std::vector<ItemTab> tabs;  // per plan item (graph_exec.hip)
     void * comap = nullptr;     // graph_exec.hip: member 0's tensors -> graph positions (member k's counterparts)
     const BatchCls * find(const void * p) const {

@@ -506,6 +506,14 @@ static tts_tensor * build_graph(tts_parler * p, bool audio, int n) {
         cur = tg::add(c, cur, residualffn);
         inpL = cur;
     }
+    if (!audio && B > 1) {
+        // a batched prompt pass (our extension; B = 1 keeps the reference's node list): its logits are
+        // never read (tts_parler_prefill / _ragged pass no output), so the final norm and the nine heads
+        // over every prompt token (9 x 1088 rows x n * B columns of F32 products) are not built
+        tg::set_output(cur);
+        tg::build_forward_expand(c, cur);
+        return cur;
+    }
     cur = layer_norm(c, cur, p->norm, p->norm_b);
     // parler_build_head_outputs (model.cpp:441-457)
     tts_tensor * out = nullptr;
