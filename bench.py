@@ -39,6 +39,10 @@ HBM_PEAK_GBS = 8000.0           # MI355X spec (MI355X_MICROARCH.md chip table)
 PMC_FILE = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k.json"), default=ROOT / "profiles" / "r01" / "pmc_gemv_q4k.json")
 # PMC traffic of the Orpheus leg's matrix-core GEMV (scripts/gpu_pmc_orpheus.sh), newest round first
 PMC_FILE_ORPH = max((ROOT / "profiles").glob("r*/pmc_gemv_q4k_kr_orpheus.json"), default=None)
+# PMC traffic of the Dia leg's slab Q8_0 GEMV (scripts/gpu_pmc_r6.sh)
+PMC_FILE_DIA = max((ROOT / "profiles").glob("r*/pmc_gemv_q8_0s_dia.json"), default=None)
+# PMC traffic of the decode attention pair at the headline's KV length (scripts/gpu_pmc_r6.sh)
+PMC_FILE_ATTN = max((ROOT / "profiles").glob("r*/pmc_attn_kv448.json"), default=None)
 
 # examples/perf_battery/perf_battery.cpp:25-56: the reference's 29 test prompts (its list has 30 literals, but
 # "Kick the ball straight and follow through." lacks a comma, so C++ joins it with the next one)
@@ -290,6 +294,7 @@ def gemv_roofline(be, runner, steps):
     if PMC_FILE.exists():
         pmc = json.loads(PMC_FILE.read_text())
         traffic, src, mode = pmc.get("hbm_bytes_per_launch"), str(PMC_FILE.relative_to(ROOT)), pmc.get("command")
+    pa = json.loads(PMC_FILE_ATTN.read_text()) if PMC_FILE_ATTN else {}
     a_us = 1000.0 * ams / max(alaunches, 1)
     a_bpl = abytes / max(alaunches, 1)
     a_gbs = a_bpl / (a_us * 1e-6) / 1e9 if alaunches else 0.0
@@ -299,7 +304,8 @@ def gemv_roofline(be, runner, steps):
             "avg_launch_us": round(avg_us, 3), "bytes_per_launch": round(bpl, 1), "launches_sampled": launches,
             "attention": {"kernel": "k_attn_scores + k_attn_pv (one decode attention)", "achieved": round(a_gbs, 1),
                           "frac": round(a_gbs / HBM_PEAK_GBS, 4), "avg_us": round(a_us, 3), "bytes_per_call": round(a_bpl, 1),
-                          "calls_sampled": alaunches}}
+                          "calls_sampled": alaunches, "traffic": pa.get("pair_hbm_bytes_per_call"),
+                          "traffic_source": str(PMC_FILE_ATTN.relative_to(ROOT)) if PMC_FILE_ATTN else None}}
 
 
 def run_replicas(fn, n):
@@ -451,6 +457,7 @@ def dia_leg(be, args):
         d.generate(toks[-1], 8)
         ms, launches, nbytes = be.gemv_stats(ttship.Q8_0, reset=True)
         be.set_option(ttship.OPT["PROFILE_GEMV"], 0)
+        pmc = json.loads(PMC_FILE_DIA.read_text()) if PMC_FILE_DIA else {}
         avg_us = 1000.0 * ms / max(launches, 1)
         gbs = nbytes / max(launches, 1) / (avg_us * 1e-6) / 1e9 if launches else 0.0
         return {"workload": f"Dia-1.6B Q8_0 CFG decode (BASELINE configs[3]), 1 prompt = a {len(text)}-byte two-speaker dialogue, "
@@ -463,7 +470,10 @@ def dia_leg(be, args):
                 "encoder_step_ms": round(1000 * t_enc, 1), "weight_bytes": d.weight_bytes(),
                 "roofline": {"bound": "hbm", "kernel": "k_gemv_q8_0s (slab Q8_0 GEMV, <= 8 columns)", "achieved": round(gbs, 1),
                              "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_us, 3),
-                             "bytes_per_launch": round(nbytes / max(launches, 1), 1), "launches_sampled": launches, "traffic": None}}
+                             "bytes_per_launch": round(nbytes / max(launches, 1), 1), "launches_sampled": launches,
+                             "traffic": pmc.get("hbm_bytes_per_launch"),
+                             "traffic_source": str(PMC_FILE_DIA.relative_to(ROOT)) if PMC_FILE_DIA else None,
+                             "traffic_mode": pmc.get("command")}}
     finally:
         dac.close()
         d.close()
@@ -716,7 +726,7 @@ def main():
     ap.add_argument("--gemv-nw-min", type=int, default=None, help="TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup")
     ap.add_argument("--attn-pv-mp", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV_MP: all dims of a head per P.V workgroup (1) or 16 (0)")
     ap.add_argument("--gemm-kr-cp", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_CP: two column tiles per K-relay workgroup on parallel wave halves (1) or not (0)")
-    ap.add_argument("--gemm-kr-xcd", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (1, default) or grid order (0)")
+    ap.add_argument("--gemm-kr-xcd", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (1) or grid order (0, default)")
     ap.add_argument("--gemm-kr-nw", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_NW: waves per tile of the many-column K-relay GEMM (4 / 8)")
     ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
     ap.add_argument("--graphs", type=int, default=1, help="replay each step as a HIP graph (1) or launch eagerly (0)")

@@ -331,8 +331,9 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMM_KR_NW = 34, /* waves per 16-row tile of the many-column (> 8) K-relay Q4_K GEMM: 4 (default) or 8 (K >= 2048) */
     TTS_HIP_OPT_GEMV_NW_MIN = 25, /* lane-layout Q4_K GEMVs: at least `value` waves per workgroup (fewer, fuller workgroups;
                                      0 = default geometry, about one row group per wave over every CU) */
-    TTS_HIP_OPT_GEMM_KR_XCD = 38, /* 1 (default): the many-column K-relay GEMM places a row tile's 16-column tiles on one XCD,
-                                     dispatched back to back, so the second streams the weights from that XCD's L2; 0 = grid order */
+    TTS_HIP_OPT_GEMM_KR_XCD = 38, /* 1: the many-column K-relay GEMM places a row tile's 16-column tiles on one XCD, dispatched
+                                     back to back (for the second to stream the weights from that XCD's L2); 0 (default) = grid
+                                     order (no gain in HBM bytes or step time) */
     TTS_HIP_OPT_GEMM_KR_CP = 39,  /* 1: the many-column K-relay GEMM (K = 1024 / 2048) gives a workgroup two 16-column tiles on two
                                      parallel wave halves (the weight tile streamed from HBM once for both; 0 = one tile each) */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this

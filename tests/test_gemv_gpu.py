@@ -115,15 +115,15 @@ def test_q4_K_prefill_gemm_two_column_tiles(hip, tiled, K, N, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiled", [False, True])
-@pytest.mark.parametrize("opt,val", [("GEMM_KR_CP", 1), ("GEMM_KR_XCD", 0)])
+@pytest.mark.parametrize("opt,val", [("GEMM_KR_CP", 1), ("GEMM_KR_XCD", 1)])
 @pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (2048, 1024, 32), (1024, 3072, 48), (2048, 160, 17), (1024, 512, 64),
                                    (4096, 1024, 32)])
 def test_q4_K_prefill_gemm_column_pairs(hip, tiled, opt, val, K, N, M):
     """The many-column K-relay GEMM with a row tile's two column tiles on one workgroup's two wave halves
-    (TTS_HIP_OPT_GEMM_KR_CP; K = 4096 keeps one tile per workgroup), and without the XCD-contiguous
-    column-tile order (TTS_HIP_OPT_GEMM_KR_XCD = 0; on by default): the same sums, bit-identical (odd
+    (TTS_HIP_OPT_GEMM_KR_CP; K = 4096 keeps one tile per workgroup), and with the XCD-contiguous
+    column-tile order (TTS_HIP_OPT_GEMM_KR_XCD = 1; off by default): the same sums, bit-identical (odd
     tile counts leave the last pair's second half idle)."""
-    dflt = {"GEMM_KR_CP": 0, "GEMM_KR_XCD": 1}[opt]
+    dflt = {"GEMM_KR_CP": 0, "GEMM_KR_XCD": 0}[opt]
     hip.set_option(ttship.OPT[opt], val)
     try:
         rng = np.random.default_rng(K * 5 + N + M + tiled)

@@ -371,11 +371,18 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     BatchCtx bc;
     bc.N = (int)mem.size();
     bc.n_nodes = r0->n;
-    bc.key = r0->sig;
+    // the group key: the graph kind and the member backends as a set (whichever member arrived last and
+    // plans its graph as member 0, the verified structure and shared-data checks hold for the set)
+    std::vector<uintptr_t> bes;
     for (Req * m : mem) {
         bc.mnodes.push_back(m->nodes);
-        bc.key = (bc.key ^ (uint64_t)(uintptr_t)m->be) * 0x100000001B3ull;
+        bes.push_back((uintptr_t)m->be);
     }
+    for (size_t k = 1; k < bes.size(); ++k)
+        if (bes[k] < bes[bc.canon]) bc.canon = (int)k;
+    std::sort(bes.begin(), bes.end());
+    bc.key = r0->sig;
+    for (uintptr_t b : bes) bc.key = (bc.key ^ (uint64_t)b) * 0x100000001B3ull;
     if (!d.exec) {
         d.exec = tts_hip_backend_init(r0->be->device);
         if (!d.exec) {

@@ -2577,12 +2577,17 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
             if (!same_ne(t, cm.member(bc, t, k))) return false;
         return true;
     };
-    auto share = [&](const tts_tensor * t) {  // read-only data read through member 0's copy
+    // read-only data read through member 0's copy: every member's copy equal to the set's canonical
+    // member's (equality is transitive; the pairs stay the same whichever member plans, so they cache)
+    auto share = [&](const tts_tensor * t) {
         if (!t || bc.checked) return true;
-        for (int k = 1; k < N; ++k) {
+        const tts_tensor * tc = cm.member(bc, t, bc.canon);
+        if (!same_ne(t, tc) || !tc->data) return false;
+        for (int k = 0; k < N; ++k) {
+            if (k == bc.canon) continue;
             const tts_tensor * m = cm.member(bc, t, k);
             if (!same_ne(t, m) || !m->data) return false;
-            if (m->data != t->data) shared.emplace_back(t->data, m->data, tbytes(t));
+            if (m->data != tc->data) shared.emplace_back(tc->data, m->data, tbytes(t));
         }
         return true;
     };

@@ -314,6 +314,7 @@ struct BatchCtx {
     std::vector<tts_tensor * const *> mnodes;  // every member's node list (member 0's first; equal lengths)
     int n_nodes = 0;
     bool checked = false;       // this group's shapes and read-only operands were verified by an earlier step
+    int canon = 0;              // the member whose read-only data every other member's is compared with (stable per set)
     bool ragged = false;        // (co_prepare) the members' KV lengths differ
     bool differs = false;       // refused because a member's read-only data differs (not for lack of a batched form)
     std::vector<ItemTab> tabs;  // per plan item (graph_exec.hip)
@@ -400,7 +401,7 @@ struct tts_hip_backend {
     int gemm_q8_staged = 2;    // TTS_HIP_OPT_GEMM_Q8_STAGED
     int64_t gemv_kr_ink = 0;   // TTS_HIP_OPT_GEMV_KR_INKERNEL (max K)
     int gemm_kr_cp = 0;        // TTS_HIP_OPT_GEMM_KR_CP: two column tiles per workgroup on parallel wave halves
-    int gemm_kr_xcd = 1;       // TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (its L2 serves the second)
+    int gemm_kr_xcd = 0;       // TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (measured no gain: off)
     int gemm_kr_ct2 = 0;       // TTS_HIP_OPT_GEMM_KR_CT2: two 16-column tiles per K-relay GEMM workgroup (K <= 2048)
     int64_t gemm_kr_ink = 0;   // TTS_HIP_OPT_GEMM_KR_INKERNEL (max M of the many-column K-relay GEMM without the operand pass)
     int gemv_nw_min = 0;       // TTS_HIP_OPT_GEMV_NW_MIN: minimum waves per lane-layout Q4_K GEMV workgroup
