@@ -973,6 +973,72 @@ def main():
 
     prompt_pass = guarded("prompt_pass", leg_prompt_pass) if args.prompt_pass else None
 
+    # TTS.cpp's generate() shape (parler_tts_runner::generate, src/models/parler/model.cpp:838-858) for the whole
+    # prompt set: every prompt's own perf_battery sentence as the prompt pass (one ragged pass per replica,
+    # tts_parler_prefill_ragged), the AR decode from there (each prompt at its own position), and the DAC decode --
+    # all inside the timed region, on the headline's replicas / DAC workers layout
+    def leg_generate_shape():
+        barrier_sync(dist, None)
+        gcfg = ttship.parler_config(batch=bl, max_ctx=256 + args.steps + 64, arena_bytes=max(4, (bl + 7) // 8 * 4) << 30)
+        sents = [sentence_tokens(HARVARD[(rank * per_gpu + g) % len(HARVARD)], gcfg.prompt_vocab) for g in range(per_gpu)]
+        gbes, gruns, gdecs = [], [], []
+        try:
+            for r in range(R):
+                gbes.append(new_backend())
+                gruns.append(ttship.Parler(gbes[-1].iface(), gcfg))
+            while len(gdecs) < W:
+                if len(gbes) <= len(gdecs):
+                    gbes.append(new_backend())
+                gdecs.append(new_dac_for(args, gbes[len(gdecs)], dcfg))
+            toks_g = [None] * R
+            pcm_g = [None] * per_gpu
+
+            def ar(r):
+                gruns[r].reset()
+                gruns[r].prefill_ragged(sents[r * bl:(r + 1) * bl])
+                toks_g[r] = gruns[r].generate(args.steps)
+                gbes[r].sync()
+
+            def dac_w(w):
+                xb, rd = gbes[w], gdecs[w]
+                for bt in range(w, n_dac_batches, W):
+                    gs = list(range(bt * NBD, min(per_gpu, (bt + 1) * NBD)))
+                    if len(gs) == 1 or NBD == 1:
+                        for g in gs:
+                            pcm_g[g] = rd.decode(dac_codes(toks_g[g // bl][g % bl], dcfg.codebook_size))
+                    else:
+                        out = rd.decode_batch(np.stack([dac_codes(toks_g[g // bl][g % bl], dcfg.codebook_size) for g in gs]))
+                        for i, g in enumerate(gs):
+                            pcm_g[g] = out[i]
+                xb.sync()
+
+            run_replicas(ar, R)  # warm: code objects, step graphs, the prompt pass's shapes
+            run_replicas(dac_w, W)
+            barrier_sync(dist, gbes[0])
+            tg0 = time.perf_counter()
+            run_replicas(ar, R)
+            tg1 = time.perf_counter()
+            run_replicas(dac_w, W)
+            barrier_sync(dist, gbes[0])
+            tg2 = time.perf_counter()
+            dtg = max_over_ranks(dist, local, tg2 - tg0)
+            dtg_ar = max_over_ranks(dist, local, tg1 - tg0)
+        finally:
+            for d_ in gdecs:
+                d_.close()
+            for rr in gruns:
+                rr.close()
+            for b in gbes:
+                b.close()
+        return {"workload": f"TTS.cpp's generate() per prompt, for the whole set: prompt g = perf_battery sentence g % 29 "
+                            f"({min(map(len, sents))}-{max(map(len, sents))} word-piece ids) as one ragged prompt pass per replica, "
+                            f"then {args.steps} AR steps from each prompt's own position, then DAC-44k, all timed "
+                            f"({R} replicas x {bl} prompts, {W} DAC decoders)",
+                "audio_sec_per_s": round(audio_s / dtg, 3), "ms_total": round(1000 * dtg, 3),
+                "prompt_pass_and_ar_ms": round(1000 * dtg_ar, 3)}
+
+    generate_shape = guarded("parler_generate_shape", leg_generate_shape) if args.prompt_pass and not args.no_dac else None
+
     def leg_b1():
         # TTS.cpp's serving shape: b1_replicas one-prompt runners with the step coalescer (equal and ragged
         # KV lengths), the same runners each alone, and b1_wide coalesced ragged runners
@@ -1072,6 +1138,7 @@ def main():
             "parler_8_prompts_per_gpu": p8,
             "parler_sampled_top_k": sampled,
             "prompt_pass": prompt_pass,
+            "parler_generate_shape": generate_shape,
             "parler_b1": b1,
             "kokoro": kres,
             "orpheus": ores,

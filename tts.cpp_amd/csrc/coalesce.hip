@@ -70,7 +70,11 @@ struct Dev {
     tts_hip_backend * exec = nullptr;     // hidden backend: stream + scratch of the coalesced launches
     char * mem = nullptr;                 // executor memory for the members' intermediates
     size_t mem_bytes = 0;
-    std::unordered_set<uint64_t> verified;  // group keys whose shapes and read-only operands checked out
+    // Backends whose graphs of one kind (signature) were verified against each other (same shapes, equal
+    // read-only data), as classes of a union-find per kind: a set whose members all lie in one class skips
+    // the checks.  Dropped whenever a host write invalidates content records (g_eq_epoch).
+    std::unordered_map<uint64_t, std::unordered_map<uintptr_t, uintptr_t>> equal;
+    uint64_t equal_epoch = 0;
     std::unordered_set<uint64_t> no_form;   // kinds of graph whose plan has no coalesced form (never waited for again)
     int * d_flags = nullptr;              // content-check mismatch flags
     int d_flags_n = 0;
@@ -101,7 +105,6 @@ struct EqKeyHash {
 std::mutex g_eq_mu;
 std::unordered_map<EqKey, EqRec, EqKeyHash> g_eq;
 uint64_t g_eq_epoch = 1;                            // bumped whenever a write drops records
-std::unordered_map<uint64_t, uint64_t> g_eq_group;  // group key -> epoch its shared operands were all found equal
 std::map<const char *, const char *> g_eq_cover;  // disjoint union of every checked range: start -> end
 
 void cover_add(const char * a, size_t n) {
@@ -398,10 +401,29 @@ void run_group(Dev & d, std::vector<Req *> & g) {
         d.refused++;
         return;
     }
+    uint64_t epoch;
     {
         std::lock_guard<std::mutex> lk(g_eq_mu);
-        auto gk = g_eq_group.find(bc.key);
-        bc.checked = d.verified.count(bc.key) && gk != g_eq_group.end() && gk->second == g_eq_epoch;
+        epoch = g_eq_epoch;
+    }
+    if (d.equal_epoch != epoch) {
+        d.equal.clear();
+        d.equal_epoch = epoch;
+    }
+    auto & uf = d.equal[r0->sig];
+    auto root = [&](uintptr_t x) {
+        auto it = uf.find(x);
+        if (it == uf.end()) return x;
+        while (it->second != x) {
+            x = it->second;
+            it = uf.find(x);
+        }
+        return x;
+    };
+    {
+        const uintptr_t r = uf.count((uintptr_t)mem[0]->be) ? root((uintptr_t)mem[0]->be) : 0;
+        bc.checked = r != 0;
+        for (size_t k = 1; k < mem.size() && bc.checked; ++k) bc.checked = uf.count((uintptr_t)mem[k]->be) && root((uintptr_t)mem[k]->be) == r;
     }
     tts_hip_backend * ex = d.exec;
     copy_options(ex, r0->be);
@@ -424,10 +446,16 @@ void run_group(Dev & d, std::vector<Req *> & g) {
         }
         return;
     }
-    if (!bc.checked && st == 0) {
-        d.verified.insert(bc.key);
-        std::lock_guard<std::mutex> lk(g_eq_mu);
-        g_eq_group[bc.key] = g_eq_epoch;
+    if (!bc.checked && st == 0) {  // every member verified against the canonical one: one class
+        const uintptr_t c = (uintptr_t)mem[bc.canon]->be;
+        if (!uf.count(c)) uf[c] = c;
+        const uintptr_t rc = root(c);
+        for (Req * m : mem) {
+            const uintptr_t b = (uintptr_t)m->be;
+            if (!uf.count(b)) uf[b] = b;
+            const uintptr_t rb = root(b);
+            if (rb != rc) uf[rb] = rc;
+        }
     }
     TTS_HIP_CHECK(hipEventRecord(ex->co_ev, ex->stream));
     for (Req * m : mem) {
@@ -557,6 +585,11 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
 void coalesce_backend_gone(const tts_hip_backend * be) {
     if (be->device < 0 || be->device >= kMaxDev) return;
     Dev & d = g_dev[be->device];
+    {
+        // a later backend may reuse this address with other weights: no verified class survives it
+        std::lock_guard<std::mutex> xl(d.exec_mu);
+        d.equal.clear();
+    }
     std::lock_guard<std::mutex> lk(d.mu);
     d.seen.erase(be);
     d.cv.notify_all();
