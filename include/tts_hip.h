@@ -212,7 +212,8 @@ int tts_hip_tensor_set(tts_hip_backend_t backend, void * dst_dev, const void * s
 int tts_hip_tensor_get(tts_hip_backend_t backend, void * dst_host, const void * src_dev, size_t size);
 int tts_hip_tensor_copy(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size); /* stream-ordered */
 /* Measurement helper (bench.py's measured HBM ceiling): the same copy as a streaming kernel -- 16-B loads and
- * stores per lane, non-temporal, a grid of 8 workgroups per CU -- the guide's float4-copy method.  size % 16 == 0
+ * stores per lane, non-temporal, 16 workgroups per CU each copying one contiguous chunk -- the guide's float4-copy
+ * method.  size % 16 == 0
  * and both pointers 16-B aligned, else TTS_STATUS_BAD_ARG.  Stream-ordered. */
 int tts_hip_copy_stream(tts_hip_backend_t backend, void * dst_dev, const void * src_dev, size_t size);
 /* ggml_backend_i::set_tensor_async: `src_host` is staged at once (reusable on return), the copy runs
@@ -336,6 +337,10 @@ enum tts_hip_option {
                                      order (no gain in HBM bytes or step time) */
     TTS_HIP_OPT_GEMM_KR_CP = 39,  /* 1: the many-column K-relay GEMM (K = 1024 / 2048) gives a workgroup two 16-column tiles on two
                                      parallel wave halves (the weight tile streamed from HBM once for both; 0 = one tile each) */
+    TTS_HIP_OPT_GEMM_KR_WALK = 40, /* many-column K-relay GEMMs of more than 4 16-column tiles (prompt passes):
+                                      `value` workgroups per column tile, each copying its operand tile once and walking every
+                                      `value`-th row tile (the next tile's weights requested before the current tile's relay);
+                                      0 = one workgroup per (row tile, column tile) */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
                                      backend's graph_compute of a one-prompt decode step may join the same step of other
                                      backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */

@@ -15,4 +15,13 @@ grep -A80 "tts_hip: signal" $O/run.log | grep -E "^  #" | while read -r n addr w
 done > $O/frames.txt
 grep -B2 -A40 "tts_hip: signal" $O/run.log | head -80
 cat $O/frames.txt
+# keep what is judged: the stats, a per-kernel summary and the line; the per-dispatch CSV is too big to bring back
+f=$(find $O/run -name "*kernel_trace.csv" | head -1)
+if [ -n "$f" ]; then
+  python3 $R/scripts/prof_summary.py "$f" k_gemv_q4K_kr k_attn_scores k_attn_pv_mp k_gemv_q8_0s > $O/summary.txt
+  head -30 $O/summary.txt
+  find $O/run -name "*kernel_stats.csv" -exec cp {} $O/kernel_stats.csv \;
+  rm -f "$f"
+fi
+grep '^{"metric"' $O/run.log > $O/line.json; tail -c 300 $O/line.json
 exit 0

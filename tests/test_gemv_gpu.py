@@ -138,6 +138,26 @@ def test_q4_K_prefill_gemm_column_pairs(hip, tiled, opt, val, K, N, M):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("tiled", [False, True])
+@pytest.mark.parametrize("walk", [3, 8])
+@pytest.mark.parametrize("K,N,M", [(1024, 1024, 96), (4096, 1024, 80), (2048, 512, 100), (3072, 256, 77), (1024, 3072, 576)])
+def test_q4_K_prefill_gemm_row_walk(hip, tiled, walk, K, N, M):
+    """The prompt pass's many-column K-relay GEMM with `walk` workgroups per column tile, each copying its
+    operand tile once and walking every walk-th row tile (TTS_HIP_OPT_GEMM_KR_WALK; more than 4 column
+    tiles): the same sums, bit-identical."""
+    hip.set_option(ttship.OPT["GEMM_KR_WALK"], walk)
+    try:
+        rng = np.random.default_rng(K * 3 + N + M + tiled + walk)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        hip.set_option(ttship.OPT["GEMM_KR_WALK"], 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tiled", [False, True])
 @pytest.mark.parametrize("K,N,M", [(1024, 1024, 32), (4096, 1024, 32), (1024, 3072, 9), (2048, 160, 17), (4096, 512, 64),
                                    (3072, 256, 40)])
 def test_q4_K_prefill_gemm_in_kernel_operands(hip, tiled, K, N, M):

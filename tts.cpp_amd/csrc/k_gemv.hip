@@ -1198,8 +1198,16 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 
     TTS_TS(j, 0);
     u32x4 hd[LOOP ? 2 : 1][BPW], qa[LOOP ? 2 : 1][BPW], qb[LOOP ? 2 : 1][BPW];
-    auto load_w = [&](auto BUF, int64_t t) __attribute__((always_inline)) {
+    // j.xcd_cols: the weights are loaded with the default (L2-allocating) policy, so the row tile's
+    // other column tile, dispatched on the same XCD right after, reads them from that XCD's L2; a
+    // non-temporal load would not leave them there
+    auto load_w_pol = [&](auto BUF, auto PLAIN, int64_t t) __attribute__((always_inline)) {
         constexpr int bf = decltype(BUF)::value;
+        constexpr bool plain = decltype(PLAIN)::value;
+        auto ld = [](const auto * p) __attribute__((always_inline)) {
+            if constexpr (plain) return *gptr(p);
+            else return TTS_WLOAD(p);
+        };
         t = t < T ? t : T - 1;
         const int mat = tile_mat(t);
         int64_t row = tile_row0(t, mat) + r;
@@ -1210,11 +1218,11 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 #pragma unroll
             for (int u = 0; u < BPW; ++u) {
                 const uint8_t * bp = wr + (int64_t)min(w * BPW + u, nb - 1) * 144;
-                hd[bf][u] = TTS_WLOAD((const u32x4 *)bp);
+                hd[bf][u] = ld((const u32x4 *)bp);
 #pragma unroll
                 for (int l = 0; l < 4; ++l) {
-                    qa[bf][u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
-                    qb[bf][u][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
+                    qa[bf][u][l] = ld((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
+                    qb[bf][u][l] = ld((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
                 }
             }
         } else {
@@ -1223,12 +1231,16 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 #pragma unroll
             for (int u = 0; u < BPW; ++u) {
                 const uint8_t * bp = wt + (int64_t)min(w * BPW + u, nb - 1) * 576;
-                hd[bf][u] = TTS_WLOAD((const u32x4 *)(bp + ri * 16));
-                qa[bf][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
-                qb[bf][u] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
+                hd[bf][u] = ld((const u32x4 *)(bp + ri * 16));
+                qa[bf][u] = ld((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri) * 16));
+                qb[bf][u] = ld((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri) * 16));
             }
         }
         TTS_PIN_LOADS();
+    };
+    auto load_w = [&](auto BUF, int64_t t) __attribute__((always_inline)) {
+        if (!LOOP && CTW == 1 && j.xcd_cols && gridDim.y > 1) load_w_pol(BUF, std::true_type{}, t);
+        else load_w_pol(BUF, std::false_type{}, t);
     };
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, LOOP ? 1 : 0>;
@@ -2493,6 +2505,20 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
             const unsigned gy2 = (unsigned)((nct + 1) / 2);
             if (nb == 4) launch_q4k_kr_t<1, false, 4, L, false, PRO_COPY, 2>(be, j, gx, gy2);
             else launch_q4k_kr_t<2, false, 4, L, false, PRO_COPY, 2>(be, j, gx, gy2);
+            return;
+        }
+        // TTS_HIP_OPT_GEMM_KR_WALK = G: G workgroups per column tile, each copying its column tile's operands
+        // into LDS once and walking row tiles tx, tx + G, ... (the next tile's weights requested before the
+        // current tile's relay): the operand tile crosses L2 -> LDS G times instead of once per row tile.
+        // Same (row, column) arithmetic: bit-identical.
+        const int walk = be->gemm_kr_walk;
+        if (walk > 0 && nct > 4 && gx > (unsigned)walk) {
+            switch (nb) {
+                case 4: launch_q4k_kr_t<1, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
+                case 8: launch_q4k_kr_t<2, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
+                case 12: launch_q4k_kr_t<3, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
+                default: launch_q4k_kr_t<4, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
+            }
             return;
         }
         // TTS_HIP_OPT_GEMM_KR_NW = 8: a tile's blocks over eight waves (K >= 2048; a longer relay, half the

@@ -755,24 +755,29 @@ int launch_op(tts_hip_backend * be, const tts_tensor * node) {
 namespace tts {
 
 // ---- streaming copy (tts_hip_copy_stream): the HBM ceiling the bench reports beside the 8 TB/s spec ----
+// Each workgroup copies one contiguous chunk, four consecutive 4 KB pieces in flight per iteration
+// (16-B non-temporal loads / stores per lane).  Measured on MI355X (scripts/copy_peak.hip,
+// profiles/r06/copy_peak_variants.txt): 5.5-5.7 TB/s read + write at 16 workgroups per CU, against
+// 4.4-5.1 for the grid-stride form of the same loads.
 __global__ __launch_bounds__(256) void k_copy_stream(uint4 * __restrict__ dst, const uint4 * __restrict__ src, int64_t n16) {
     typedef unsigned int u4v __attribute__((ext_vector_type(4)));
     u4v * d = (u4v *)dst;
     const u4v * s = (const u4v *)src;
-    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * gs < n16; i += 4 * gs) {  // four 16-B loads in flight per lane
+    const int64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = (int64_t)blockIdx.x * per, b1 = b0 + per < n16 ? b0 + per : n16;
+    int64_t i = b0 + threadIdx.x;
+    for (; i + 3 * 256 < b1; i += 4 * 256) {
         u4v v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(s + i + u * gs);
+        for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(s + i + u * 256);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], d + i + u * gs);
+        for (int u = 0; u < 4; ++u) __builtin_nontemporal_store(v[u], d + i + u * 256);
     }
-    for (; i < n16; i += gs) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+    for (; i < b1; i += 256) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
 }
 
 void launch_copy_stream(tts_hip_backend * be, void * dst, const void * src, int64_t n16) {
-    hipLaunchKernelGGL(k_copy_stream, dim3((unsigned)(8 * be->cu_total)), dim3(256), 0, be->stream, (uint4 *)dst, (const uint4 *)src, n16);
+    hipLaunchKernelGGL(k_copy_stream, dim3((unsigned)(16 * be->cu_total)), dim3(256), 0, be->stream, (uint4 *)dst, (const uint4 *)src, n16);
 }
 
 }  // namespace tts
