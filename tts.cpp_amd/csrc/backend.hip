@@ -147,6 +147,7 @@ void tts_hip_backend_free(tts_hip_backend_t be) {
     for (auto e : be->pin_events) hipEventDestroy(e);
     for (auto e : be->plan_ev) hipEventDestroy(e);
     hipHostFree(be->pin);
+    if (be->rb_host) hipHostFree(be->rb_host);
     hipFree(be->scratch);
     hipFree(be->shadow);
     hipFree(be->argmax_keys);
@@ -289,10 +290,19 @@ void tts_hip_buffer_free(tts_hip_backend_t be, void * ptr) {
 int tts_hip_tensor_set(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     drop_tiled_copies(dst, size);
     tts::coalesce_written(dst, size);
-    // synchronous w.r.t. the host buffer (the caller may reuse it immediately)
-    if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+    // synchronous (the copy has landed on return, as ggml_backend_tensor_set promises).  Small inputs (a
+    // step's tokens, positions, masks) are staged through this backend's own pinned ring: a pageable
+    // copy goes through the runtime's staging buffer, which many runners' threads (the step
+    // coalescer's one-prompt runners) take in turn
+    if (size > 0 && size <= be->pin_size / 4) {
+        const int st = tts_hip_tensor_set_async(be, dst, src, size);
+        if (st != 0) return st;
+    } else if (hipMemcpyAsync(dst, src, size, hipMemcpyHostToDevice, be->stream) != hipSuccess) {
+        return TTS_STATUS_FAILED;
+    }
     if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
     return 0;
 }
@@ -303,8 +313,10 @@ int tts_hip_tensor_set_async(tts_hip_backend_t be, void * dst, const void * src,
     if (!be) return TTS_STATUS_BAD_ARG;
     if (size == 0) return 0;
     hipSetDevice(be->device);
+    be->rb_clear();
     if (size > be->pin_size / 2) return tts_hip_tensor_set(be, dst, src, size);
     tts::coalesce_written(dst, size);
+    std::lock_guard<std::mutex> pl(be->pin_mu);
     // recycle finished regions
     while (!be->pin_pending.empty() && hipEventQuery(be->pin_pending.front().ev) == hipSuccess) {
         be->pin_events.push_back(be->pin_pending.front().ev);
@@ -344,6 +356,7 @@ int tts_hip_greedy_step(tts_hip_backend_t be, const float * logits, int32_t B, i
                         int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next) {
     if (!be || !logits || B <= 0 || NH <= 0 || V <= 0) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     launch_greedy_step(be, logits, B, NH, V, step, bos, eos, eos_seen, hist, next);
     return 0;
 }
@@ -352,12 +365,26 @@ int tts_hip_sample_step(tts_hip_backend_t be, const float * logits, int32_t B, i
                         int32_t * rep_state, int32_t step, int32_t bos, int32_t eos, int32_t * eos_seen, int32_t * hist, int32_t * next) {
     if (!be || !logits || !cfg || B <= 0 || NH <= 0 || V <= 0) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     return launch_sample_step(be, logits, B, NH, V, cfg, call, rep_state, step, bos, eos, eos_seen, hist, next);
 }
 
 int tts_hip_tensor_get(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    // an output of this backend's last coalesced step: the executor already copied it to host memory
+    // in stream order (co_readback)
+    if (be->rb_any.load(std::memory_order_acquire)) {
+        std::lock_guard<std::mutex> l(be->rb_mu);
+        for (const auto & r : be->rb) {
+            const char * s = (const char *)src;
+            if (s >= r.dev && s + size <= r.dev + r.bytes) {
+                if (hipStreamSynchronize(be->stream) != hipSuccess) return TTS_STATUS_FAILED;
+                memcpy(dst, be->rb_host + r.off + (s - r.dev), size);
+                return 0;
+            }
+        }
+    }
     // The reference reads the host copy right after get_tensor_async with no synchronize
     // (src/tts_model.cpp:25-36), so this call completes the stream first.
     if (hipMemcpyAsync(dst, src, size, hipMemcpyDeviceToHost, be->stream) != hipSuccess) return TTS_STATUS_FAILED;
@@ -369,6 +396,7 @@ int tts_hip_copy_stream(tts_hip_backend_t be, void * dst, const void * src, size
     if (!be || !dst || !src || size % 16 || ((uintptr_t)dst | (uintptr_t)src) % 16) return TTS_STATUS_BAD_ARG;
     if (size == 0) return 0;
     hipSetDevice(be->device);
+    be->rb_clear();
     tts::launch_copy_stream(be, dst, src, (int64_t)(size / 16));
     return hipGetLastError() == hipSuccess ? 0 : TTS_STATUS_FAILED;
 }
@@ -376,6 +404,7 @@ int tts_hip_copy_stream(tts_hip_backend_t be, void * dst, const void * src, size
 int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     tts::coalesce_written(dst, size);
     tts::launch_copy_bytes(be, dst, src, size);  // a kernel, not a blit: ~2 us less host time per step
     return hipGetLastError() == hipSuccess ? 0 : TTS_STATUS_FAILED;
@@ -384,6 +413,7 @@ int tts_hip_tensor_copy(tts_hip_backend_t be, void * dst, const void * src, size
 int tts_hip_memset(tts_hip_backend_t be, void * dst, int value, size_t size) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     tts::coalesce_written(dst, size);
     return hipMemsetAsync(dst, value, size, be->stream) == hipSuccess ? 0 : TTS_STATUS_FAILED;
 }

@@ -379,6 +379,7 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     std::vector<uintptr_t> bes;
     for (Req * m : mem) {
         bc.mnodes.push_back(m->nodes);
+        bc.mbe.push_back(m->be);
         bes.push_back((uintptr_t)m->be);
     }
     for (size_t k = 1; k < bes.size(); ++k)

@@ -2201,8 +2201,8 @@ static int run_gemv_item(tts_hip_backend * be, const Item & it, const Item * xat
             }
             j.M = NB;
         }
-        // the prologue reads 16-B vectors: x 16-B aligned, columns 16-B strided (contiguous for PRO_QUANT)
-        x_hit |= ((uintptr_t)j.x & 15) != 0 || (j.xcs & 3) != 0 || (j.pro == PRO_QUANT && j.xcs != j.K);
+        // the prologue reads 16-B vectors: x 16-B aligned, columns 16-B strided
+        x_hit |= ((uintptr_t)j.x & 15) != 0 || (j.xcs & 3) != 0;
         if (x_hit) {
             if (!ensure_scratch(be, (size_t)(4 * j.K * j.M))) return TTS_STATUS_ALLOC_FAILED;
             launch_copy_cols(be, (float *)be->scratch, j.x, j.K, j.xcs, j.M);
@@ -2773,6 +2773,46 @@ static bool co_prepare(tts_hip_backend * be, Planner & pl, tts_tensor * const * 
     return true;
 }
 
+// A coalesced step's outputs also go to each member's pinned read-back buffer, in this stream's order
+// after the step (member k's entries are k, k + N, ... of the output copies): the member's
+// tts_hip_tensor_get of its logits is then a stream synchronize and a host memcpy, instead of N
+// device-to-host copies issued by N threads one after another.
+static void co_readback(tts_hip_backend * be, const std::vector<int64_t> & sc, int n_sc) {
+    BatchCtx & bc = *be->bat;
+    const int N = bc.N;
+    if ((int)bc.mbe.size() != N) return;
+    std::vector<size_t> need(N, 0), off(N, 0);
+    for (int e = 0; e < n_sc; ++e) need[e % N] += ((size_t)sc[3 * e + 2] + 255) & ~(size_t)255;
+    for (int k = 0; k < N; ++k) {
+        tts_hip_backend * m = bc.mbe[k];
+        m->rb_clear();
+        if (need[k] <= m->rb_cap) continue;
+        if (m->rb_host) {  // an earlier step's copy into it is ordered before this point of this stream
+            TTS_HIP_CHECK(hipStreamSynchronize(be->stream));
+            TTS_HIP_CHECK(hipHostFree(m->rb_host));
+            m->rb_host = nullptr;
+            m->rb_cap = 0;
+        }
+        if (hipHostMalloc((void **)&m->rb_host, need[k], hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            m->rb_host = nullptr;
+            continue;
+        }
+        m->rb_cap = need[k];
+    }
+    for (int e = 0; e < n_sc; ++e) {
+        const int k = e % N;
+        tts_hip_backend * m = bc.mbe[k];
+        if (!m->rb_host) continue;
+        const size_t bytes = (size_t)sc[3 * e + 2];
+        TTS_HIP_CHECK(hipMemcpyAsync(m->rb_host + off[k], (const void *)(uintptr_t)sc[3 * e], bytes, hipMemcpyDeviceToHost, be->stream));
+        std::lock_guard<std::mutex> l(m->rb_mu);
+        m->rb.push_back({(const char *)(uintptr_t)sc[3 * e + 1], bytes, off[k]});
+        m->rb_any.store(true, std::memory_order_release);
+        off[k] += (bytes + 255) & ~(size_t)255;
+    }
+}
+
 // A coalesced step's output copies: entry e = (src, dst, bytes), one workgroup row per entry.
 __global__ void k_co_scatter(const int64_t * __restrict__ tab, int n) {
     const int e = blockIdx.y;
@@ -2840,6 +2880,7 @@ static int capture_into(tts_hip_backend * be, tts_tensor * const * nodes, int n_
 extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     if (!be) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();  // this step may write what the last coalesced step's read-back holds
     // a one-prompt decode step other backends on this device are also submitting: one coalesced launch
     const int cs = coalesce_submit(be, nodes, n_nodes);
     if (cs != kCoalesceNotTaken) return cs;
@@ -2881,6 +2922,7 @@ extern "C" int tts_hip_graph_compute(tts_hip_backend_t be, tts_tensor * const * 
 extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes, int slot) {
     if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     if (be->plan_ev_pending[slot]) {  // the slot's previous launch must have run before it is re-recorded
         const auto t0 = std::chrono::steady_clock::now();
         TTS_HIP_CHECK(hipEventSynchronize(be->plan_ev[slot]));
@@ -2899,6 +2941,7 @@ extern "C" int tts_hip_graph_prepare(tts_hip_backend_t be, tts_tensor * const * 
 extern "C" int tts_hip_graph_launch(tts_hip_backend_t be, int slot) {
     if (!be || slot < 0 || slot > 1) return TTS_STATUS_BAD_ARG;
     hipSetDevice(be->device);
+    be->rb_clear();
     if (be->plan_eager[slot]) {
         const int st = graph_compute_launches(be, be->plan_nodes[slot], be->plan_n[slot]);
         if (st != 0) return st;
@@ -2989,6 +3032,7 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
     CoMap cm;
     int64_t sc_off = -1;
     int n_sc = 0;
+    std::vector<int64_t> sc_host;  // the output copies (src, dst, bytes), member k's at entries k, k + N, ...
     if (be->bat) {
         const auto tq0 = std::chrono::steady_clock::now();
         struct Acc {
@@ -3011,6 +3055,7 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
             bc.comap = nullptr;
             return TTS_STATUS_UNSUPPORTED;
         }
+        if (n_sc > 0) sc_host.assign(tab.begin() + sc_off, tab.begin() + sc_off + 3 * (int64_t)n_sc);
         if (!tab.empty()) {
             const size_t bytes = tab.size() * sizeof(int64_t);
             if (bytes > be->co_tab_bytes) {
@@ -3111,6 +3156,7 @@ int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int
         if (n_sc > 0) {  // the output intermediates to every member's own tensors
             hipLaunchKernelGGL(k_co_scatter, dim3(4, (unsigned)n_sc), dim3(256), 0, be->stream, (const int64_t *)be->co_tab + sc_off, n_sc);
             TTS_HIP_CHECK(hipGetLastError());
+            co_readback(be, sc_host, n_sc);
         }
         be->bat->comap = nullptr;
     }

@@ -6,7 +6,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <atomic>
 #include <deque>
+#include <mutex>
 #include <unordered_map>
 #include <tuple>
 #include <vector>
@@ -312,6 +314,7 @@ struct BatchCtx {
     uint64_t key = 0;  // the group: graph signature and member backends (coalesce.hip caches per key)
     std::vector<BatchCls> cls;  // sorted by b0
     std::vector<tts_tensor * const *> mnodes;  // every member's node list (member 0's first; equal lengths)
+    std::vector<tts_hip_backend *> mbe;         // every member's backend (the read-back of its outputs)
     int n_nodes = 0;
     bool checked = false;       // this group's shapes and read-only operands were verified by an earlier step
     int canon = 0;              // the member whose read-only data every other member's is compared with (stable per set)
@@ -432,6 +435,7 @@ struct tts_hip_backend {
     };
     std::deque<PinRec> pin_pending;
     std::vector<hipEvent_t> pin_events;
+    std::mutex pin_mu;  // the ring is shared by every thread that uploads through this backend
     // completion of each plan slot's last launch: a slot is re-recorded only after it ran
     hipEvent_t plan_ev[2] = {nullptr, nullptr};
     bool plan_ev_pending[2] = {false, false};
@@ -491,6 +495,25 @@ struct tts_hip_backend {
     size_t co_tab_bytes = 0;
     int64_t co_prep_ns = 0;      // host time of co_prepare + the tables' upload (coalesced steps)
     bool co_member = true;  // TTS_HIP_OPT_COALESCE: this backend's graph_compute calls may join a coalesced step
+    // read-back of a coalesced step's outputs: the executor copies this member's output tensors into
+    // rb_host (pinned) in the step's own stream order, so tts_hip_tensor_get of such a range is served
+    // from host memory after a stream synchronize instead of one device-to-host copy per member.
+    // Entries are valid until this backend's next write or compute call (rb_clear).
+    struct RbEnt {
+        const char * dev;
+        size_t bytes, off;
+    };
+    char * rb_host = nullptr;
+    size_t rb_cap = 0;
+    std::vector<RbEnt> rb;
+    std::mutex rb_mu;                  // rb: the executor's thread writes it, this backend's callers read / drop it
+    std::atomic<bool> rb_any{false};   // rb non-empty (checked before taking rb_mu)
+    void rb_clear() {
+        if (!rb_any.load(std::memory_order_acquire)) return;
+        std::lock_guard<std::mutex> l(rb_mu);
+        rb.clear();
+        rb_any.store(false, std::memory_order_release);
+    }
 };
 
 namespace tts {

@@ -292,7 +292,7 @@ __device__ __forceinline__ void q80_row_block(const float (&v)[16], int lane, in
 // Loads are unconditional (addresses clamped into range) so that a wave issues all of them before
 // the first use: a load under a guard is sunk next to its use, and every block then pays a full
 // L2 round trip (measured: 0.4 us per block).  The launcher guarantees 16-B aligned x / lnw / lnb
-// and, for PRO_QUANT, contiguous columns (xcs == K).
+// and 16-B aligned column strides.
 __device__ __forceinline__ void ld4(const float * p, float (&v)[4]) {
     const f32x4 t = *gptr((const f32x4 *)p);
     v[0] = t.x, v[1] = t.y, v[2] = t.z, v[3] = t.w;
@@ -333,7 +333,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nwaves ? nwaves : blockDim.x >> 6;
     const int r = lane >> 4, t = lane & 15;
     const int M = xcol ? 1 : ov.mcols > 0 ? ov.mcols : (int)j.M;
-    const float * const X = xcol ? xcol : j.x + (int64_t)ov.col0 * j.xcs;  // (PRO_QUANT: xcs == K, launcher-checked)
+    const float * const X = xcol ? xcol : j.x + (int64_t)ov.col0 * j.xcs;
+    const int64_t xcs = xcol ? 0 : j.xcs;  // (one column: xcol)
     const int trash = M * nb;  // LDS slot that absorbs the writes of padding rows
     auto put = [&](const float (&v)[16], int lane, int slot) {
         slot = slot == trash ? (ov.trash >= 0 ? ov.trash : slot) : ov.slot0 + slot;
@@ -342,7 +343,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
         else q8k_row_block(v, lane, xq_s + (int64_t)slot * QK_K, xd_s + slot, xs_s + slot * 8);
     };
     if (PRO == PRO_QUANT) {
-        // pass p quantizes blocks 4p..4p+3 (block qb = column m, chunk b at x + qb*256)
+        // pass p quantizes blocks 4p..4p+3 (block qb = column qb / nb, chunk qb % nb at x + column * xcs +
+        // chunk * 256; columns contiguous or strided, e.g. a coalesced step's members)
         constexpr int QP = NCH <= 4 ? 2 : 4;  // passes whose loads a wave keeps in flight
         const int nq = M * nb, npass = (nq + 3) / 4;
         auto batch = [&](int p0, bool first) {
@@ -350,7 +352,8 @@ __device__ __forceinline__ void q4k_prologue(const GemvJob & j, int nb, int8_t *
 #pragma unroll
             for (int u = 0; u < QP; ++u) {
                 const int qb = min(4 * min(p0 + u * nw, npass - 1) + r, nq - 1);
-                const float * src = X + (int64_t)qb * QK_K + 16 * t;
+                const int mc = qb / nb;
+                const float * src = X + (int64_t)mc * xcs + (int64_t)(qb - mc * nb) * QK_K + 16 * t;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) ld4(src + 4 * k, *(float (*)[4]) & v[u][4 * k]);
             }
