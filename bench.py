@@ -728,6 +728,7 @@ def main():
     ap.add_argument("--attn-pv-mp", type=int, default=None, help="TTS_HIP_OPT_ATTN_PV_MP: all dims of a head per P.V workgroup (1) or 16 (0)")
     ap.add_argument("--gemm-kr-cp", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_CP: two column tiles per K-relay workgroup on parallel wave halves (1) or not (0)")
     ap.add_argument("--gemm-kr-walk", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_WALK: row-tile walkers per column tile of the prompt pass's many-column K-relay GEMM (0 = one workgroup per tile pair)")
+    ap.add_argument("--gemm-pf", type=int, default=None, help="TTS_HIP_OPT_GEMM_PF: min columns of a Q4_K product on the prefill GEMM (0 = K-relay GEMM)")
     ap.add_argument("--gemm-kr-xcd", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (1) or grid order (0, default)")
     ap.add_argument("--gemm-kr-nw", type=int, default=None, help="TTS_HIP_OPT_GEMM_KR_NW: waves per tile of the many-column K-relay GEMM (4 / 8)")
     ap.add_argument("--gemv-f32-wide", type=int, default=None, help="TTS_HIP_OPT_GEMV_F32_WIDE: wide GEMV for the F32 heads at 9..64 columns (1) or the tiled GEMM (0)")
@@ -773,7 +774,7 @@ def main():
                           ("gemv_q80_rw", "GEMV_Q80_RW"), ("gemm_q8_staged", "GEMM_Q8_STAGED"),
                           ("gemv_kr_inkernel", "GEMV_KR_INKERNEL"), ("attn_ks", "ATTN_KS"), ("attn_pv8", "ATTN_PV8"),
                           ("kv_prefetch_blocks", "KV_PREFETCH_BLOCKS"), ("gemv_f32_wide", "GEMV_F32_WIDE"),
-                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW"), ("gemm_kr_xcd", "GEMM_KR_XCD"), ("gemm_kr_cp", "GEMM_KR_CP"), ("gemm_kr_walk", "GEMM_KR_WALK")):
+                          ("attn_pv_mp", "ATTN_PV_MP"), ("gemm_kr_nw", "GEMM_KR_NW"), ("gemm_kr_xcd", "GEMM_KR_XCD"), ("gemm_kr_cp", "GEMM_KR_CP"), ("gemm_kr_walk", "GEMM_KR_WALK"), ("gemm_pf", "GEMM_PF")):
             v = getattr(args, flag)
             if v is not None:
                 rb.set_option(ttship.OPT[opt], v)

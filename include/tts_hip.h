@@ -341,6 +341,9 @@ enum tts_hip_option {
                                       `value` workgroups per column tile, each copying its operand tile once and walking every
                                       `value`-th row tile (the next tile's weights requested before the current tile's relay);
                                       0 = one workgroup per (row tile, column tile) */
+    TTS_HIP_OPT_GEMM_PF = 41,     /* many-column Q4_K products (prompt passes) of at least `value` columns (default 64) on the
+                                     prefill GEMM: a wave per two 16-row tiles of one 16-column tile over the whole row, ggml's
+                                     block chain in registers (no relay); 0 = the K-relay GEMM for every column count */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
                                      backend's graph_compute of a one-prompt decode step may join the same step of other
                                      backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */

@@ -1444,6 +1444,179 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 }
 
 // ------------------------------------------------------------------------------------------
+// Many-column Q4_K GEMM for prompt passes (k_gemm_q4K_pf): the K-relay kernel's per-block arithmetic
+// (the same exact-integer f16 MFMA dots, the same rounded f32 terms) with the work cut the other way.
+// At prefill sizes a K-relay workgroup computes one 16 x 16 (row tile, column tile) pair and copies
+// its column tile's whole operand (16 columns x K) into LDS for it: a 1024 x 1024 matrix at 576
+// columns moves 64 x 36 such copies of 35 KB through L2.  Here the operand tile is copied into LDS
+// once for PF_RT row tiles: each wave owns two row tiles of the column tile for the WHOLE row, every
+// block in ascending order, so ggml's chain (sums[l] += p_l, sumf -= q, then sumf + sums[0..7]) runs
+// in the wave's registers with no relay and no barrier; a block's operand fragments (from LDS) serve
+// both row tiles.  The next block's weights are requested before the current block's MFMAs.  Same additions in the same order as vec_dot_q4_K_q8_K:
+// bit-identical.  Operands: k_quant_mf's layout, one bq_tile per 16-column tile (j.bq, j.bq_tile).
+constexpr int PF_RS = 2;                 // row tiles per wave
+constexpr int PF_RT = 4 * PF_RS;         // row tiles per workgroup (four waves)
+template <int NB, bool LANE>
+__global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    constexpr int RS = PF_RS;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 15, kg = lane >> 4;
+    const int ct = blockIdx.y;
+    const int c0 = 16 * ct;
+    const int M = min(16, (int)j.M - c0);
+    const int cc = r < M ? r : M - 1;
+    const int nslot = M * NB + 1;
+    // the column tile's operands into LDS (the same bytes the K-relay kernel DMAs)
+    {
+        const char * src = j.bq + (size_t)ct * j.bq_tile;
+        const int nck = (int)(((size_t)nslot * (2 * QK_K + 32 + 4) + 1023) >> 10);
+        for (int i = wave; i < nck; i += 4)
+            __builtin_amdgcn_global_load_lds(gptr(src + (size_t)i * 1024 + lane * 16),
+                                             (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
+    }
+    const _Float16 * const b16 = (const _Float16 *)smem;
+    const _Float16 * const sbs = b16 + (size_t)nslot * QK_K;
+    const float * const xd = (const float *)(sbs + (size_t)nslot * 16);
+    const int64_t T = job_rows(j) / 16;  // launcher: whole row tiles
+    const int64_t tw = ((int64_t)blockIdx.x * 4 + wave) * RS;  // this wave's first row tile
+    auto mat_of = [&](int64_t flat) {
+        int mt = 0;
+        while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
+        return mt;
+    };
+    const uint8_t * wp[RS];  // LANE: this lane's row; tiled: its 4-row group (row & 3 in ri[])
+    int ri[RS];
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs) {
+        const int64_t t = tw + rs < T ? tw + rs : T - 1;
+        const int mat = __builtin_amdgcn_readfirstlane(mat_of(t * 16));
+        const int64_t row = t * 16 - job_roff(j, mat) + r;
+        if constexpr (LANE) wp[rs] = j.W[mat] + row * j.w_row_bytes;
+        else wp[rs] = j.W[mat] + (row >> 2) * NB * 576;
+        ri[rs] = (int)(row & 3);
+    }
+    u32x4 hd[2][RS], qa[2][RS], qb[2][RS];
+    auto load_w = [&](auto BUF, int b) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
+#pragma unroll
+        for (int rs = 0; rs < RS; ++rs) {
+            if constexpr (LANE) {
+                const uint8_t * bp = wp[rs] + (int64_t)b * 144;
+                hd[bf][rs] = TTS_WLOAD((const u32x4 *)bp);
+#pragma unroll
+                for (int l = 0; l < 4; ++l) {
+                    qa[bf][rs][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + l * 16 + kg * 4));
+                    qb[bf][rs][l] = TTS_WLOAD((const uint32_t *)(bp + 16 + (l + 4) * 16 + kg * 4));
+                }
+            } else {
+                const uint8_t * bp = wp[rs] + (int64_t)b * 576;
+                hd[bf][rs] = TTS_WLOAD((const u32x4 *)(bp + ri[rs] * 16));
+                qa[bf][rs] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2) * 4 + ri[rs]) * 16));
+                qb[bf][rs] = TTS_WLOAD((const u32x4 *)(bp + 64 + ((kg * 2 + 1) * 4 + ri[rs]) * 16));
+            }
+        }
+        TTS_PIN_LOADS();
+    };
+    using B0 = std::integral_constant<int, 0>;
+    using B1 = std::integral_constant<int, 1>;
+    load_w(B0{}, 0);
+    __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
+    f2v sums[RS][8][2], sumf[RS][2];
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs)
+#pragma unroll
+        for (int hq = 0; hq < 2; ++hq) {
+            sumf[rs][hq] = f2v{0.f, 0.f};
+#pragma unroll
+            for (int l = 0; l < 8; ++l) sums[rs][l][hq] = f2v{0.f, 0.f};
+        }
+    // one block: the integer dots of k_gemv_q4K_kr's terms, folded into the chain at once
+    auto block = [&](auto BUF, int b) __attribute__((always_inline)) {
+        constexpr int bf = decltype(BUF)::value;
+        const size_t slot = (size_t)cc * NB + b;
+        const _Float16 * bsl = b16 + slot * QK_K + kg * 8;
+        f16x8 B[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) B[l] = *(const f16x8 *)(bsl + l * 32);
+        const f16x8 Bs = *(const f16x8 *)(sbs + slot * 16 + (kg & 1) * 8);
+        const float yd = xd[slot];
+#pragma unroll
+        for (int rs = 0; rs < RS; ++rs) {
+            const u32x4 h = hd[bf][rs];
+            const uint32_t sc_lo = h.y & 0x3F3F3F3Fu, mn_lo = h.z & 0x3F3F3F3Fu;
+            const uint32_t sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+            const uint32_t mn_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+            const uint32_t sw = (kg < 2 ? sc_lo : sc_hi) >> ((kg & 1) * 16);
+            const _Float16 s0 = (_Float16)(float)(sw & 0xFF), s1 = (_Float16)(float)((sw >> 8) & 0xFF);
+            const f16x2 S0 = {s0, s0}, S1 = {s1, s1};
+            const _Float16 o0 = (_Float16)(-1024.f * (float)(sw & 0xFF)), o1 = (_Float16)(-1024.f * (float)((sw >> 8) & 0xFF));
+            const f16x2 O0 = {o0, o0}, O1 = {o1, o1};
+            f32x4 acc[8];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) {
+                const uint32_t D = l < 4 ? qa[bf][rs][l & 3] : qb[bf][rs][l & 3];
+                const uint32_t lo = D & 0x0F0F0F0Fu, hi = (D >> 4) & 0x0F0F0F0Fu;
+                const f16x2 a0 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C010C00u), S0, O0);
+                const f16x2 a1 = __builtin_elementwise_fma(byte2_f16_biased(lo, 0x0C030C02u), S0, O0);
+                const f16x2 a2 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C010C00u), S1, O1);
+                const f16x2 a3 = __builtin_elementwise_fma(byte2_f16_biased(hi, 0x0C030C02u), S1, O1);
+                const f16x8 A = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y, a3.x, a3.y};
+                acc[l] = __builtin_amdgcn_mfma_f32_16x16x32_f16(A, B[l], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            }
+            const _Float16 mm = (_Float16)(kg == 0 ? 1.f : kg == 1 ? 64.f : 0.f);
+            const f16x2 MM = {mm, mm}, OFF = {(_Float16)-1024.f, (_Float16)-1024.f};
+            const f16x2 m0 = (byte2_f16_biased(mn_lo, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m1 = (byte2_f16_biased(mn_lo, 0x0C030C02u) + OFF) * MM;
+            const f16x2 m2 = (byte2_f16_biased(mn_hi, 0x0C010C00u) + OFF) * MM;
+            const f16x2 m3 = (byte2_f16_biased(mn_hi, 0x0C030C02u) + OFF) * MM;
+            const f16x8 As = {m0.x, m0.y, m1.x, m1.y, m2.x, m2.y, m3.x, m3.y};
+            const f32x4 si = __builtin_amdgcn_mfma_f32_16x16x32_f16(As, Bs, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            float dy[4], dmy[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t hx = (uint32_t)__shfl((int)h.x, 4 * kg + q);  // d | dmin of row 4kg + q
+                dy[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx & 0xFFFF)), yd);
+                dmy[q] = __fmul_rn(dev_fp16_to_fp32((uint16_t)(hx >> 16)), yd);
+            }
+#pragma unroll
+            for (int hq = 0; hq < 2; ++hq) {
+                const f2v d2 = {dy[2 * hq], dy[2 * hq + 1]}, dm2 = {dmy[2 * hq], dmy[2 * hq + 1]};
+#pragma unroll
+                for (int l = 0; l < 8; ++l) sums[rs][l][hq] = sums[rs][l][hq] + d2 * f2v{acc[l][2 * hq], acc[l][2 * hq + 1]};
+                sumf[rs][hq] = sumf[rs][hq] - dm2 * f2v{si[2 * hq], si[2 * hq + 1]};
+            }
+        }
+    };
+    // pairs of blocks, not unrolled (an unrolled chain lets the compiler hoist every block's operand
+    // reads and spill); NB is even: each pair's second block's weights are requested before its
+    // first block's MFMAs, the next pair's first block's before its second's
+#pragma unroll 1
+    for (int b = 0; b < NB; b += 2) {
+        load_w(B1{}, b + 1);
+        block(B0{}, b);
+        if (b + 2 < NB) load_w(B0{}, b + 2);
+        block(B1{}, b + 1);
+    }
+#pragma unroll
+    for (int rs = 0; rs < RS; ++rs) {
+        if (tw + rs >= T) break;  // (wave-uniform)
+        const int64_t t = tw + rs;
+        const int mat = __builtin_amdgcn_readfirstlane(mat_of(t * 16));
+        const int64_t row0 = t * 16 - job_roff(j, mat);
+        const int64_t rows_m = job_roff(j, mat + 1) - job_roff(j, mat);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float tot = sumf[rs][q >> 1][q & 1];
+#pragma unroll
+            for (int l = 0; l < 8; ++l) tot = __fadd_rn(tot, sums[rs][l][q >> 1][q & 1]);
+            const int64_t rr = row0 + 4 * kg + q;
+            if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, c0 + r, tot);
+        }
+    }
+}
+// ------------------------------------------------------------------------------------------
 // Matrix-core Q4_K GEMV for latency-bound decode matrices (k_gemv_q4K_ks).  Parler's matrices are
 // 0.6-2.4 MB: the row phase of the VALU kernels is ~1.2-2.5 us of dependent integer dots at one wave
 // per SIMD, and k_gemv_q4K_mf streams a tile's blocks through ONE wave.  Here a workgroup owns one
@@ -2429,6 +2602,16 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
     hipLaunchKernelGGL((k_gemv_q4K_kr<BPW, SW, NWT, LANE, LOOP, PRO, CTW, CP>), dim3(gx, gy), blk, lds, be->stream, j);
 }
 
+// LDS of one column tile's operands (k_quant_mf's slot layout, whole 1 KB DMA chunks)
+static size_t q4k_pf_lds(int64_t nb) { return (size_t)((((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023); }
+template <int NB, bool LANE>
+static void launch_q4k_pf_t(tts_hip_backend * be, const GemvJob & j, unsigned gy) {
+    static std::atomic<uint32_t> attr_done{0};
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemm_q4K_pf<NB, LANE>);
+    const unsigned gx = (unsigned)((job_rows(j) / 16 + PF_RT - 1) / PF_RT);
+    hipLaunchKernelGGL((k_gemm_q4K_pf<NB, LANE>), dim3(gx, gy), dim3(256), (uint32_t)q4k_pf_lds(NB), be->stream, j);
+}
+
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns
 // (16-column tiles), then the K-relay kernel over (row tile, column tile) -- the same per-(row,
 // column) arithmetic as the GEMV, so bit-identical to ggml's order, in two launches instead of one
@@ -2515,12 +2698,23 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
         // current tile's relay): the operand tile crosses L2 -> LDS G times instead of once per row tile.
         // Same (row, column) arithmetic: bit-identical.
         const int walk = be->gemm_kr_walk;
-        if (walk > 0 && nct > 4 && gx > (unsigned)walk) {
+        if (walk > 0 && nct > 4 && gx > (unsigned)walk && !ink) {
             switch (nb) {
                 case 4: launch_q4k_kr_t<1, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
                 case 8: launch_q4k_kr_t<2, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
                 case 12: launch_q4k_kr_t<3, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
                 default: launch_q4k_kr_t<4, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
+            }
+            return;
+        }
+        // TTS_HIP_OPT_GEMM_PF = min columns: prompt-pass products on k_gemm_q4K_pf (a wave per RS row tiles x one
+        // column tile over the whole row, no relay)
+        if (be->gemm_pf > 0 && j.M >= be->gemm_pf && !ink && j.bq) {  // (operands from the operand pass only)
+            switch (nb) {
+                case 4: launch_q4k_pf_t<4, L>(be, j, gy); break;
+                case 8: launch_q4k_pf_t<8, L>(be, j, gy); break;
+                case 12: launch_q4k_pf_t<12, L>(be, j, gy); break;
+                default: launch_q4k_pf_t<16, L>(be, j, gy); break;
             }
             return;
         }
