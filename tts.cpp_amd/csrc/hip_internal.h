@@ -235,6 +235,8 @@ struct GemvJob {
     const char * bq = nullptr;
     int64_t bq_bytes = 0;
     int64_t bq_tile = 0;  // > 0: columns in tiles of 16, tile c's operands at bq + c * bq_tile (its own slot layout)
+    int32_t bq_slot = 0;  // halves per operand slot (0 = QK_K; the prefill GEMM pads slots to QK_K + 8 so a block's
+                          // 16 columns sit on different LDS banks)
     unsigned long long * ts = nullptr;  // phase timestamps (scripts/gemv_phase.hip builds only)
     // ragged columns (a coalesced step's KV-cache stores, coalesce.hip): for the matrices in yoff_mats,
     // column m of matrix mat is stored at Y[mat] + m * ycs + yoff[mat * yoff_ld + m] (floats) -- each

@@ -1456,6 +1456,7 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 // bit-identical.  Operands: k_quant_mf's layout, one bq_tile per 16-column tile (j.bq, j.bq_tile).
 constexpr int PF_RS = 2;                 // row tiles per wave
 constexpr int PF_RT = 4 * PF_RS;         // row tiles per workgroup (four waves)
+constexpr int PF_SLOT = QK_K + 8;        // halves per operand slot: columns 528 B apart, 16 B off the LDS bank period
 template <int NB, bool LANE>
 __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     typedef float f2v __attribute__((ext_vector_type(2)));
@@ -1471,13 +1472,13 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     // the column tile's operands into LDS (the same bytes the K-relay kernel DMAs)
     {
         const char * src = j.bq + (size_t)ct * j.bq_tile;
-        const int nck = (int)(((size_t)nslot * (2 * QK_K + 32 + 4) + 1023) >> 10);
+        const int nck = (int)(((size_t)nslot * (2 * PF_SLOT + 32 + 4) + 1023) >> 10);
         for (int i = wave; i < nck; i += 4)
             __builtin_amdgcn_global_load_lds(gptr(src + (size_t)i * 1024 + lane * 16),
                                              (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
     }
     const _Float16 * const b16 = (const _Float16 *)smem;
-    const _Float16 * const sbs = b16 + (size_t)nslot * QK_K;
+    const _Float16 * const sbs = b16 + (size_t)nslot * PF_SLOT;
     const float * const xd = (const float *)(sbs + (size_t)nslot * 16);
     const int64_t T = job_rows(j) / 16;  // launcher: whole row tiles
     const int64_t tw = ((int64_t)blockIdx.x * 4 + wave) * RS;  // this wave's first row tile
@@ -1536,7 +1537,7 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     auto block = [&](auto BUF, int b) __attribute__((always_inline)) {
         constexpr int bf = decltype(BUF)::value;
         const size_t slot = (size_t)cc * NB + b;
-        const _Float16 * bsl = b16 + slot * QK_K + kg * 8;
+        const _Float16 * bsl = b16 + slot * PF_SLOT + kg * 8;
         f16x8 B[8];
 #pragma unroll
         for (int l = 0; l < 8; ++l) B[l] = *(const f16x8 *)(bsl + l * 32);
@@ -2415,8 +2416,9 @@ __global__ __launch_bounds__(64) void k_quant_mf(GemvJob j) {
     const int ct = j.bq_tile ? m >> 4 : 0, lm = j.bq_tile ? m & 15 : m;
     const int Mt = j.bq_tile ? min(16, (int)j.M - 16 * ct) : (int)j.M;
     const int nslot = Mt * nb + 1;
+    const int sh = j.bq_slot ? j.bq_slot : QK_K;  // halves per slot
     _Float16 * b16 = (_Float16 *)(j.bq + (size_t)ct * j.bq_tile);
-    _Float16 * sb = b16 + (size_t)nslot * QK_K;
+    _Float16 * sb = b16 + (size_t)nslot * sh;
     float * xd = (float *)(sb + (size_t)nslot * 16);
     const float * x = j.x + (int64_t)m * j.xcs;
     const int b = blockIdx.x * 4 + r;
@@ -2485,7 +2487,7 @@ __global__ __launch_bounds__(64) void k_quant_mf(GemvJob j) {
         }
     }
     const int slot = b < nb ? lm * nb + b : nslot - 1;
-    q8k_row_block_mf(v, lane, b16 + (size_t)slot * QK_K, sb + (size_t)slot * 16, xd + slot);
+    q8k_row_block_mf(v, lane, b16 + (size_t)slot * sh, sb + (size_t)slot * 16, xd + slot);
 }
 
 static bool q4k_mf_eligible(const tts_hip_backend * be, const GemvJob & j) {
@@ -2603,7 +2605,7 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
 }
 
 // LDS of one column tile's operands (k_quant_mf's slot layout, whole 1 KB DMA chunks)
-static size_t q4k_pf_lds(int64_t nb) { return (size_t)((((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023); }
+static size_t q4k_pf_lds(int64_t nb) { return (size_t)((((16 * nb + 1) * (2 * PF_SLOT + 32 + 4)) + 1023) & ~(int64_t)1023); }
 template <int NB, bool LANE>
 static void launch_q4k_pf_t(tts_hip_backend * be, const GemvJob & j, unsigned gy) {
     static std::atomic<uint32_t> attr_done{0};
@@ -2624,7 +2626,17 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     if (nb != 4 && nb != 8 && nb != 12 && nb != 16) return false;
     for (int m = 0; m <= job.nmat; ++m)
         if (job_roff(job, m) % 16) return false;
-    const int64_t tile = (((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
+    // TTS_HIP_OPT_GEMM_KR_INKERNEL = max M: decode-sized products skip the operand pass, every (row tile,
+    // column tile) workgroup norms / quantizes its 16 columns itself (q4k_prologue, its first weight
+    // loads issued between the activation loads and their use); the same operand values, bit-identical
+    // (bit 16 of the option: only the quantize-only jobs, whose prologue runs on every wave at once)
+    const int64_t ink_m = be->gemm_kr_ink & 0xFFFF;
+    const bool ink = ink_m > 0 && job.M <= ink_m && job.K <= 4 * 1024 && !job.dbg &&
+                     (job.pro == PRO_LN || job.xcs == job.K) && (!(be->gemm_kr_ink & 0x10000) || job.pro == PRO_QUANT);
+    // TTS_HIP_OPT_GEMM_PF = min columns: prompt-pass products on the prefill GEMM (k_gemm_q4K_pf), whose
+    // operand slots are padded (PF_SLOT halves)
+    const bool pf = be->gemm_pf > 0 && job.M >= be->gemm_pf && !ink;
+    const int64_t tile = pf ? (int64_t)q4k_pf_lds(nb) : (((16 * nb + 1) * (2 * QK_K + 32 + 4)) + 1023) & ~(int64_t)1023;
     const int64_t nct = (job.M + 15) / 16;
     if (q4k_kr_lds(tile, false) > 160 * 1024) return false;
     // the operands go to the top of scratch; its bottom may hold this job's staged input columns
@@ -2654,13 +2666,7 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     GemvJob j = job;
     j.bq_tile = tile;
     j.bq_bytes = tile * nct;
-    // TTS_HIP_OPT_GEMM_KR_INKERNEL = max M: decode-sized products skip the operand pass, every (row tile,
-    // column tile) workgroup norms / quantizes its 16 columns itself (q4k_prologue, its first weight
-    // loads issued between the activation loads and their use); the same operand values, bit-identical
-    // (bit 16 of the option: only the quantize-only jobs, whose prologue runs on every wave at once)
-    const int64_t ink_m = be->gemm_kr_ink & 0xFFFF;
-    const bool ink = ink_m > 0 && job.M <= ink_m && job.K <= 4 * 1024 && !job.dbg &&
-                     (job.pro == PRO_LN || job.xcs == job.K) && (!(be->gemm_kr_ink & 0x10000) || job.pro == PRO_QUANT);
+    j.bq_slot = pf ? PF_SLOT : 0;
     if (ink) {
         j.bq = nullptr;
     } else {
@@ -2681,6 +2687,16 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
     const bool cp = be->gemm_kr_cp && !ink && nct >= 2 && (nb == 4 || nb == 8) && q4k_kr_lds(2 * tile, true) <= 160 * 1024;
     auto go = [&](auto LANE) {
         constexpr bool L = decltype(LANE)::value;
+        // the prefill GEMM: a wave per two 16-row tiles of one 16-column tile over the whole row, no relay
+        if (pf) {
+            switch (nb) {
+                case 4: launch_q4k_pf_t<4, L>(be, j, gy); break;
+                case 8: launch_q4k_pf_t<8, L>(be, j, gy); break;
+                case 12: launch_q4k_pf_t<12, L>(be, j, gy); break;
+                default: launch_q4k_pf_t<16, L>(be, j, gy); break;
+            }
+            return;
+        }
         if (cp) {
             const unsigned gy2 = (unsigned)((nct + 1) / 2);
             if (nb == 4) launch_q4k_kr_t<1, false, 4, L, false, PRO_COPY, 1, true>(be, j, gx, gy2);
@@ -2704,17 +2720,6 @@ static bool launch_gemm_q4k_kr(tts_hip_backend * be, const GemvJob & job, size_t
                 case 8: launch_q4k_kr_t<2, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
                 case 12: launch_q4k_kr_t<3, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
                 default: launch_q4k_kr_t<4, false, 4, L, true>(be, j, (unsigned)walk, gy); break;
-            }
-            return;
-        }
-        // TTS_HIP_OPT_GEMM_PF = min columns: prompt-pass products on k_gemm_q4K_pf (a wave per RS row tiles x one
-        // column tile over the whole row, no relay)
-        if (be->gemm_pf > 0 && j.M >= be->gemm_pf && !ink && j.bq) {  // (operands from the operand pass only)
-            switch (nb) {
-                case 4: launch_q4k_pf_t<4, L>(be, j, gy); break;
-                case 8: launch_q4k_pf_t<8, L>(be, j, gy); break;
-                case 12: launch_q4k_pf_t<12, L>(be, j, gy); break;
-                default: launch_q4k_pf_t<16, L>(be, j, gy); break;
             }
             return;
         }
