@@ -127,3 +127,44 @@ def test_fused_attention_bit_identical_to_row_kernel(hip, P, hd, B):
         outs.append(g.node_array(o))
     set_mode(hip, "default")
     assert np.array_equal(outs[0], outs[1])
+
+
+def build_multi(g, q, kc, vc, mask, P, n, hd, H, Hk, B, max_ctx):
+    """n queries per sequence (a prompt pass): q (B, n, H, hd), mask [n, P]; otherwise as build()."""
+    ql = g.leaf(q)                                            # ne [hd, H, n, B]
+    qp = g.permute(ql, (0, 2, 1, 3))                          # [hd, n, H, B]
+    qc = g.node("CONT", F32, [hd, n, H, B], [qp])
+    kl = g.leaf(kc)
+    k = g.view(kl, [hd, P, Hk, B], [4, Hk * hd * 4, hd * 4, kl.nb[2]])
+    kcont = g.node("CONT", F32, [hd, P, Hk, B], [k])
+    kq = g.node("MUL_MAT", F32, [P, n, H, B], [kcont, qc])
+    ml = g.leaf(mask)                                         # ne [P, n]
+    sm = g.node("SOFT_MAX", F32, [P, n, H, B], [kq, ml], fparams={0: float(1.0 / np.sqrt(hd)), 1: 0.0})
+    vl = g.leaf(vc)
+    v = g.view(vl, [P, hd, Hk, B], [4, max_ctx * 4, max_ctx * hd * 4, vl.nb[2]])
+    kqv = g.node("MUL_MAT", F32, [n, hd, H, B], [sm, v])
+    merged = g.permute(kqv, (2, 0, 1, 3))                     # [hd, H, n, B]
+    return g.node("CONT", F32, [hd, H, n, B], [merged])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,n,hd,H,Hk,B", [(18, 18, 64, 16, 16, 4), (3, 18, 64, 16, 16, 2), (64, 64, 64, 4, 4, 2),
+                                           (37, 5, 128, 8, 8, 2), (9, 4, 64, 16, 4, 3), (1, 4, 64, 4, 4, 1)])
+def test_short_context_many_queries_bit_exact(hip, P, n, hd, H, Hk, B):
+    """A prompt pass's short-context attention (n >= 4 queries, P <= 64: k_attn_small_q, K / V staged in LDS
+    once per head and sequence): bit-identical to the oracle's unfused chain, causal mask included."""
+    rng = np.random.default_rng(P * 13 + n + hd)
+    max_ctx = P + 24
+    q = rng.standard_normal((B, n, H, hd)).astype(np.float32)
+    kc = rng.standard_normal((B, max_ctx, Hk * hd)).astype(np.float32)
+    vc = rng.standard_normal((B, Hk * hd, max_ctx)).astype(np.float32)
+    mask = np.zeros((n, P), np.float32)
+    for i in range(n):  # causal over the last n positions (the prompt's own rows)
+        mask[i, max(0, P - n) + i + 1:] = -np.inf
+    g1, g2 = nd.Graph(), nd.Graph()
+    o1 = build_multi(g1, q, kc, vc, mask, P, n, hd, H, Hk, B, max_ctx)
+    o2 = build_multi(g2, q, kc, vc, mask, P, n, hd, H, Hk, B, max_ctx)
+    g1.run_hip(hip)
+    g2.run_oracle(n_threads=8)
+    gpu, ref = g1.node_array(o1), g2.node_array(o2)
+    assert np.array_equal(gpu, ref)

@@ -937,6 +937,75 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Short contexts with many queries (a prompt pass: Parler's self-attention over the prompt and its
+// cross-attention over the T5 encoding, n = 8-18 queries per sequence): k_attn_small's arithmetic
+// per (head, query, sequence), but one workgroup per (head, sequence) stages K and V into LDS once
+// (rows padded off the bank period) and its four waves take the queries in turn.  k_attn_small
+// gives every query its own wave, which re-reads the (head, sequence)'s V with one scalar load per
+// (dim, position) across 64 rows.  The sums are k_attn_small's, in its order: bit-identical.
+template <int HD>
+__global__ __launch_bounds__(256) void k_attn_small_q(AttnArgs a) {
+    constexpr int KP = HD + 1;  // floats per K row in LDS
+    constexpr int VP = 65;      // floats per V row (dim) in LDS: positions 0..63
+    __shared__ float sk[64 * KP];
+    __shared__ float sv[HD * VP];
+    const int h = blockIdx.x, b = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int P = seq_p(a, b);
+    const int hk = h / (a.H / (int)a.k.ne[2]);
+    const int bk = b / (a.B / (int)a.k.ne[3]);
+    const int hv = h / (a.H / (int)a.v.ne[2]);
+    const int bv = b / (a.B / (int)a.v.ne[3]);
+    const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
+    const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
+    const int64_t knb1 = a.k.nb[1], vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
+    for (int i = tid; i < P * HD; i += 256) {  // K [p][d] (d contiguous in memory)
+        const int p = i / HD, d = i - p * HD;
+        sk[p * KP + d] = *(const float *)(kbase + (int64_t)p * knb1 + 4 * d);
+    }
+    for (int i = tid; i < P * HD; i += 256) {  // V [d][p]
+        const int d = i / P, p = i - d * P;
+        sv[d * VP + p] = *(const float *)(vbase + (int64_t)d * vnb1 + (int64_t)p * vnb0);
+    }
+    __syncthreads();
+    const int p = min(lane, P - 1);
+    for (int tq = wave; tq < a.n; tq += 4) {
+        const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
+        double acc = 0.0;
+#pragma unroll 16
+        for (int d = 0; d < HD; ++d) acc += (double)__fmul_rn(sk[p * KP + d], *(const float *)(qbase + (int64_t)d * a.q.nb[0]));
+        float w = __fmul_rn((float)acc, a.scale);
+        if (a.mask) w = __fadd_rn(w, __fmul_rn(1.0f, seq_mrow(a, b, tq, P)[p]));
+        if (lane >= P) w = -INFINITY;
+        float mx = w;
+        mx = fmaxf(mx, dpp_f32<DPP_XOR1>(mx));
+        mx = fmaxf(mx, dpp_f32<DPP_XOR2>(mx));
+        mx = fmaxf(mx, dpp_f32<DPP_HALF_MIRROR>(mx));
+        mx = fmaxf(mx, dpp_f32<DPP_MIRROR>(mx));
+        mx = fmaxf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16))),
+                   fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32)), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48))));
+        const float e = lane < P ? cr_expf(__fsub_rn(w, mx)) : 0.f;
+        double sum = 0.0;
+        for (int i = 0; i < P; ++i) sum += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), i));
+        const float pr = __fmul_rn(e, (float)(1.0 / sum));
+        double o[HD / 64];
+#pragma unroll
+        for (int j = 0; j < HD / 64; ++j) o[j] = 0.0;
+        for (int i = 0; i < P; ++i) {
+            const float pi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pr), i));
+#pragma unroll
+            for (int j = 0; j < HD / 64; ++j) o[j] += (double)__fmul_rn(pi, sv[(lane + 64 * j) * VP + i]);
+        }
+        const int64_t orow = ((int64_t)tq * a.H + h) * a.hd;
+#pragma unroll
+        for (int j = 0; j < HD / 64; ++j) {
+            a.out[(int64_t)b * a.obs + orow + lane + 64 * j] = (float)o[j];
+            if (a.out2) a.out2[(int64_t)b * a.n * a.H * a.hd + orow + lane + 64 * j] = (float)o[j];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // KV prefetch into the memory-side Infinity Cache (MALL).  Decode attention streams the whole KV
 // cache of a layer once per step (Parler B = 8, P = 900: 59 MB); cold from HBM the row kernel
 // reaches about half the bandwidth it gets from MALL-resident data, while the GEMVs between two
@@ -1005,6 +1074,13 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
     const bool krows = (hd == 64 || hd == 128) && k.nb[0] == 4 && (k.nb[1] % 16) == 0 &&
                        (((uintptr_t)k.data) % 16) == 0 && (k.nb[2] % 16) == 0 &&
                        (k.nb[3] % 16) == 0 && q.nb[0] == 4 && P > 0;
+    if (krows && P <= 64 && n >= 4) {  // a prompt pass: K / V staged once per (head, sequence)
+        const dim3 grid((unsigned)H, (unsigned)B);
+        if (hd == 64) hipLaunchKernelGGL(k_attn_small_q<64>, grid, dim3(256), 0, be->stream, a);
+        else hipLaunchKernelGGL(k_attn_small_q<128>, grid, dim3(256), 0, be->stream, a);
+        TTS_HIP_CHECK(hipGetLastError());
+        return;
+    }
     if (krows && P <= 64) {
         const dim3 grid((unsigned)H, (unsigned)n, (unsigned)B);
         if (hd == 64) hipLaunchKernelGGL(k_attn_small<64>, grid, dim3(64), 0, be->stream, a);
