@@ -149,7 +149,7 @@ def build_multi(g, q, kc, vc, mask, P, n, hd, H, Hk, B, max_ctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("P,n,hd,H,Hk,B", [(18, 18, 64, 16, 16, 4), (3, 18, 64, 16, 16, 2), (64, 64, 64, 4, 4, 2),
-                                           (37, 5, 128, 8, 8, 2), (9, 4, 64, 16, 4, 3), (1, 4, 64, 4, 4, 1)])
+                                           (37, 5, 128, 8, 8, 2), (9, 4, 64, 16, 16, 3), (1, 4, 64, 4, 4, 1)])
 def test_short_context_many_queries_bit_exact(hip, P, n, hd, H, Hk, B):
     """A prompt pass's short-context attention (n >= 4 queries, P <= 64: k_attn_small_q, K / V staged in LDS
     once per head and sequence): bit-identical to the oracle's unfused chain, causal mask included."""
