@@ -52,8 +52,6 @@ struct Req {
     int64_t count = 0;  // the backend's coalescable submissions so far (its decode step number)
     bool taken = false, done = false;
     int status = kCoalesceNotTaken;
-    void * pre = nullptr;     // its plan (graph_exec.hip), made while it waited; set and read under Dev::mu
-    bool pre_tried = false;
 };
 struct Act {
     Clock::time_point t;
@@ -356,7 +354,7 @@ bool exec_layout(Dev & d, BatchCtx & bc, tts_tensor * const * nodes, int n) {
 }
 
 // Run one group (the caller holds no lock).  Statuses are written into the requests.
-void run_group(Dev & d, std::vector<Req *> & g, void * pre) {
+void run_group(Dev & d, std::vector<Req *> & g) {
     std::lock_guard<std::mutex> xl(d.exec_mu);
     const auto tg0 = Clock::now();
     struct Acc {  // run_group's host time, whatever the exit
@@ -436,7 +434,6 @@ void run_group(Dev & d, std::vector<Req *> & g, void * pre) {
         TTS_HIP_CHECK(hipStreamWaitEvent(ex->stream, m->be->co_ev, 0));
     }
     ex->bat = &bc;
-    bc.preplan = pre;
     const int st = graph_compute_launches(ex, r0->nodes, r0->n);
     ex->bat = nullptr;
     if (st == TTS_STATUS_UNSUPPORTED) {  // refused before any launch: each member runs its own graph
@@ -518,14 +515,11 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
     // which time no list holds it.  Callers re-read d.pending after every run, never an older snapshot.
     auto run = [&](std::vector<Req *> & g) {
         for (Req * q : g) q->taken = true;
-        // member 0 (the graph that is planned): a request whose own thread already planned it while it
-        // waited, else the caller's own
+        // the caller's own request first: its graph is the one planned (member 0)
         std::stable_partition(g.begin(), g.end(), [&](Req * q) { return q == &r; });
-        std::stable_partition(g.begin(), g.end(), [&](Req * q) { return q->pre != nullptr; });
         if (g.size() >= 2) {
-            void * pre = g[0]->pre;  // (read under the lock; its owner frees it only once g[0] is done)
             lk.unlock();
-            run_group(d, g, pre);
+            run_group(d, g);
             lk.lock();
         }
         for (Req * q : g) q->done = true;
@@ -582,25 +576,10 @@ int coalesce_submit(tts_hip_backend * be, tts_tensor * const * nodes, int n) {
             ran = true;
         }
         if (ran) continue;
-        if (!r.pre_tried && d.exec) {
-            // peers still missing: plan this graph for the executor meanwhile (whoever runs the group
-            // then skips the planner), and look again
-            r.pre_tried = true;
-            const tts_hip_backend * ex = d.exec;
-            lk.unlock();
-            void * p = coalesce_preplan(ex, nodes, n);
-            lk.lock();
-            r.pre = p;
-            continue;
-        }
         d.cv.wait_until(lk, deadline);
     }
     d.wait_us += std::chrono::duration_cast<std::chrono::microseconds>(Clock::now() - t0).count();
     if (r.status == kCoalesceNotTaken) d.alone++;
-    void * pre = r.pre;
-    r.pre = nullptr;
-    lk.unlock();
-    if (pre) coalesce_preplan_free(pre);  // (its group, if any, has finished with it: r is done)
     return r.status;
 }
 

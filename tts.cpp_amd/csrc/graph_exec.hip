@@ -3022,40 +3022,15 @@ static void plan_setup(Planner & pl, const tts_hip_backend * be) {
     pl.hoist_cap = be->hoist_size;
 }
 
-// A coalescer member's plan of its own graph, built by its thread while the rendezvous still waits
-// for the other members (coalesce.hip), for the executor `ex` that will run it.
-struct PrePlan {
-    Planner pl;
-    int mask = 0;
-    bool q80pro = false;
-};
-void * coalesce_preplan(const tts_hip_backend * ex, tts_tensor * const * nodes, int n_nodes) {
-    if (!ex || !ex->fusion) return nullptr;
-    auto * p = new PrePlan;
-    plan_setup(p->pl, ex);
-    p->pl.build(nodes, n_nodes);
-    p->mask = ex->fusion;
-    p->q80pro = ex->gemv_q80_pro != 0;
-    return p;
-}
-void coalesce_preplan_free(void * p) { delete (PrePlan *)p; }
-
 int graph_compute_launches(tts_hip_backend_t be, tts_tensor * const * nodes, int n_nodes) {
     be->graph_epoch++;
     be->aq.src = nullptr;
     if (be->profile_gemv) launch_profile_spin(be, 4000.0);  // see launch_profile_spin (k_gemv.hip)
     const auto tp0 = std::chrono::steady_clock::now();
-    Planner pl_own;
-    Planner * plp = &pl_own;
-    PrePlan * pre = be->bat ? (PrePlan *)be->bat->preplan : nullptr;
-    if (pre && pre->mask == be->fusion && pre->q80pro == (be->gemv_q80_pro != 0)) {
-        plp = &pre->pl;  // member 0's plan, made while the group was gathering
-    } else {
-        plan_setup(pl_own, be);
-        if (be->fusion) pl_own.build(nodes, n_nodes);
-        else pl_own.act.assign(n_nodes, 0);
-    }
-    Planner & pl = *plp;
+    Planner pl;
+    plan_setup(pl, be);
+    if (be->fusion) pl.build(nodes, n_nodes);
+    else pl.act.assign(n_nodes, 0);
     be->cap_plan_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - tp0).count();
     // a coalesced step: checks, the member-owned operand tables (uploaded before any launch) and the
     // output copies (co_prepare)

@@ -317,7 +317,6 @@ struct BatchCtx {
     std::vector<BatchCls> cls;  // sorted by b0
     std::vector<tts_tensor * const *> mnodes;  // every member's node list (member 0's first; equal lengths)
     std::vector<tts_hip_backend *> mbe;         // every member's backend (the read-back of its outputs)
-    void * preplan = nullptr;                   // member 0's plan, made by its thread while the group gathered
     int n_nodes = 0;
     bool checked = false;       // this group's shapes and read-only operands were verified by an earlier step
     int canon = 0;              // the member whose read-only data every other member's is compared with (stable per set)
@@ -649,9 +648,6 @@ void launch_copy_stream(tts_hip_backend * be, void * dst, const void * src, int6
 // Plan and launch a node list on be->stream (be->bat set: as a coalesced step of be->bat->N members;
 // TTS_STATUS_UNSUPPORTED, before any launch, when the plan has an item without a coalesced form).
 int graph_compute_launches(tts_hip_backend * be, tts_tensor * const * nodes, int n_nodes);
-// coalescer: a member's plan of its own graph for the executor `ex` (null: none), and its release
-void * coalesce_preplan(const tts_hip_backend * ex, tts_tensor * const * nodes, int n_nodes);
-void coalesce_preplan_free(void * p);
 // graph_compute of a one-prompt decode graph while other backends on the device submit the same graph:
 // one coalesced launch for all of them.  Returns kCoalesceNotTaken when the caller runs the graph itself.
 constexpr int kCoalesceNotTaken = 1 << 20;
