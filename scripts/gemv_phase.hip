@@ -39,9 +39,17 @@ int main() {
         {"orph_gateup_ln_m8", 3072, 8192, 8, PRO_LN, 2},   {"orph_down_quant_m8", 8192, 3072, 8, PRO_QUANT, 1},
         {"orph_qkv_ln_m8", 3072, 5120, 8, PRO_LN, 1},
     };
+    // GEMV_PHASE_PREFILL: the batched prompt pass's products (576 columns: 32 prompts x 18 tokens) on the
+    // prefill GEMM (k_gemm_q4K_pf; ts 0 entry, 1 loads issued, 2 operands landed, 3 first block pair, 4 last, 5 exit)
+    const Shape prefill[] = {
+        {"pf_oproj_576", 1024, 1024, 576, PRO_QUANT, 1}, {"pf_fc1_576", 1024, 4096, 576, PRO_QUANT, 1},
+        {"pf_fc2_576", 4096, 1024, 576, PRO_QUANT, 1},
+    };
     const bool orph = getenv("GEMV_PHASE_ORPHEUS") != nullptr;
-    const std::vector<Shape> shapes = orph ? std::vector<Shape>(std::begin(orpheus), std::end(orpheus))
-                                           : std::vector<Shape>(std::begin(parler), std::end(parler));
+    const bool pfs = getenv("GEMV_PHASE_PREFILL") != nullptr;
+    const std::vector<Shape> shapes = pfs ? std::vector<Shape>(std::begin(prefill), std::end(prefill))
+                                      : orph ? std::vector<Shape>(std::begin(orpheus), std::end(orpheus))
+                                             : std::vector<Shape>(std::begin(parler), std::end(parler));
     tts_hip_backend be;
     be.gemv_unique = getenv("GEMV_UNIQUE") ? atoi(getenv("GEMV_UNIQUE")) : 1;
     if (getenv("GEMV_KS")) be.gemv_ks_tiles = atoi(getenv("GEMV_KS"));
@@ -64,12 +72,12 @@ int main() {
     const size_t nts = 1 << 20;
     TTS_HIP_CHECK(hipMalloc(&W, wbytes));
     TTS_HIP_CHECK(hipMemcpy(W, hw.data(), wbytes, hipMemcpyHostToDevice));
-    std::vector<float> hx(8 * 8192);
+    std::vector<float> hx(576 * 4096);
     std::normal_distribution<float> nd(0.f, 1.f);
     for (auto & v : hx) v = nd(rng);
     TTS_HIP_CHECK(hipMalloc(&x, hx.size() * 4));
     TTS_HIP_CHECK(hipMemcpy(x, hx.data(), hx.size() * 4, hipMemcpyHostToDevice));
-    TTS_HIP_CHECK(hipMalloc(&y, 4 * 8 * 8192 * 4));
+    TTS_HIP_CHECK(hipMalloc(&y, (size_t)4 * 576 * 8192 * 4));
     TTS_HIP_CHECK(hipMalloc(&lnw, 4096 * 4));
     TTS_HIP_CHECK(hipMalloc(&lnb, 4096 * 4));
     TTS_HIP_CHECK(hipMalloc(&lno, 8 * 4096 * 4));
@@ -96,7 +104,7 @@ int main() {
         j.w_row_bytes = s.K / 256 * 144;
         for (int i = 0; i < s.nmat; ++i) {
             j.W[i] = W + (size_t)i * s.N * j.w_row_bytes;
-            j.Y[i] = y + (size_t)i * 8 * s.N;  // y holds 4 x 8 x 8192
+            j.Y[i] = y + (size_t)i * s.M * s.N;  // y holds 4 x 576 x 8192
             j.ycs[i] = s.N;
             j.yrs[i] = 1;
         }

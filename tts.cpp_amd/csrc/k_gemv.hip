@@ -1469,6 +1469,7 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     const int M = min(16, (int)j.M - c0);
     const int cc = r < M ? r : M - 1;
     const int nslot = M * NB + 1;
+    TTS_TS(j, 0);
     // the column tile's operands into LDS (the same bytes the K-relay kernel DMAs)
     {
         const char * src = j.bq + (size_t)ct * j.bq_tile;
@@ -1523,7 +1524,9 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     using B0 = std::integral_constant<int, 0>;
     using B1 = std::integral_constant<int, 1>;
     load_w(B0{}, 0);
+    TTS_TS(j, 1);
     __syncthreads();  // the operand DMA has landed (the compiler waits for all of it here)
+    TTS_TS(j, 2);
     f2v sums[RS][8][2], sumf[RS][2];
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs)
@@ -1599,7 +1602,9 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
         block(B0{}, b);
         if (b + 2 < NB) load_w(B0{}, b + 2);
         block(B1{}, b + 1);
+        if (b == 0) TTS_TS(j, 3);
     }
+    TTS_TS(j, 4);
 #pragma unroll
     for (int rs = 0; rs < RS; ++rs) {
         if (tw + rs >= T) break;  // (wave-uniform)
@@ -1616,6 +1621,7 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
             if (r < M && rr < rows_m) gemv_store<8>(j, mat, rr, c0 + r, tot);
         }
     }
+    TTS_TS(j, 5);
 }
 // ------------------------------------------------------------------------------------------
 // Matrix-core Q4_K GEMV for latency-bound decode matrices (k_gemv_q4K_ks).  Parler's matrices are
