@@ -344,6 +344,7 @@ enum tts_hip_option {
     TTS_HIP_OPT_GEMM_PF = 41,     /* many-column Q4_K products (prompt passes) of at least `value` columns (default 64) on the
                                      prefill GEMM: a wave per two 16-row tiles of one 16-column tile over the whole row, ggml's
                                      block chain in registers (no relay); 0 = the K-relay GEMM for every column count */
+    TTS_HIP_OPT_GEMM_PF_NW = 42,  /* waves per prefill-GEMM workgroup: 4 (default; 8 row tiles share one operand copy) or 8 (16) */
     TTS_HIP_OPT_COALESCE = 37,    /* 1 (default): while the process-wide coalescer is on (tts_hip_coalesce_enable), this
                                      backend's graph_compute of a one-prompt decode step may join the same step of other
                                      backends on the device as one coalesced launch (tts_hip_coalesce_stats); 0 = never */

@@ -140,18 +140,23 @@ def test_q4_K_prefill_gemm_column_pairs(hip, tiled, opt, val, K, N, M):
 @pytest.mark.parametrize("tiled", [False, True])
 @pytest.mark.parametrize("K,N,M", [(1024, 1024, 64), (4096, 1024, 80), (2048, 512, 100), (3072, 256, 77), (1024, 3072, 576),
                                    (1024, 48, 65), (4096, 16, 130)])
-def test_q4_K_prefill_gemm_pf(hip, tiled, K, N, M):
+@pytest.mark.parametrize("nw", [4, 8])
+def test_q4_K_prefill_gemm_pf(hip, tiled, K, N, M, nw):
     """The prompt pass's Q4_K GEMM (k_gemm_q4K_pf, TTS_HIP_OPT_GEMM_PF: >= 64 columns by default): a wave per
     two 16-row tiles of one 16-column tile over the whole row, ggml's block chain in registers -- the same
     sums in the same order as the oracle, bit-identical (ragged last column tiles, row counts that leave
     a workgroup's last waves without a tile)."""
     hip.set_option(ttship.OPT["GEMM_PF"], 64)
-    rng = np.random.default_rng(K * 11 + N + M + tiled)
-    w = helpers.rand_q4_K(rng, N, K)
-    x = rng.standard_normal((M, K)).astype(np.float32)
-    ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
-    got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
-    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    hip.set_option(ttship.OPT["GEMM_PF_NW"], nw)
+    try:
+        rng = np.random.default_rng(K * 11 + N + M + tiled)
+        w = helpers.rand_q4_K(rng, N, K)
+        x = rng.standard_normal((M, K)).astype(np.float32)
+        ref = py_oracle.gemv(ttship.Q4_K, w, x, N)
+        got = run_gpu_tiled(hip, w, x, N) if tiled else run_gpu(hip, ttship.Q4_K, w, x, N)
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), np.abs(got - ref).max()
+    finally:
+        hip.set_option(ttship.OPT["GEMM_PF_NW"], 4)
 
 
 @pytest.mark.gpu

@@ -843,6 +843,7 @@ extern "C" int tts_hip_set_option(tts_hip_backend_t be, int option, int value) {
         case TTS_HIP_OPT_GEMM_KR_CP: be->gemm_kr_cp = value != 0; return 0;
         case TTS_HIP_OPT_GEMM_KR_WALK: be->gemm_kr_walk = value < 0 ? 0 : value; return 0;
         case TTS_HIP_OPT_GEMM_PF: be->gemm_pf = value < 0 ? 0 : value; return 0;
+        case TTS_HIP_OPT_GEMM_PF_NW: be->gemm_pf_nw = value == 8 ? 8 : 4; return 0;
         case TTS_HIP_OPT_KV_PREFETCH_BLOCKS: be->kv_prefetch_blocks = value > 0 ? value : 1; return 0;
         default: return TTS_STATUS_BAD_ARG;
     }

@@ -407,6 +407,7 @@ struct tts_hip_backend {
     int64_t gemv_kr_ink = 0;   // TTS_HIP_OPT_GEMV_KR_INKERNEL (max K)
     int gemm_kr_walk = 0;      // TTS_HIP_OPT_GEMM_KR_WALK: row-tile walkers per column tile of a many-column GEMM
     int gemm_pf = 64;          // TTS_HIP_OPT_GEMM_PF: many-column Q4_K products of >= value columns on k_gemm_q4K_pf (0 = off)
+    int gemm_pf_nw = 4;        // TTS_HIP_OPT_GEMM_PF_NW: waves per prefill-GEMM workgroup (4 or 8)
     int gemm_kr_cp = 0;        // TTS_HIP_OPT_GEMM_KR_CP: two column tiles per workgroup on parallel wave halves
     int gemm_kr_xcd = 0;       // TTS_HIP_OPT_GEMM_KR_XCD: a row tile's column tiles on one XCD (measured no gain: off)
     int gemm_kr_ct2 = 0;       // TTS_HIP_OPT_GEMM_KR_CT2: two 16-column tiles per K-relay GEMM workgroup (K <= 2048)

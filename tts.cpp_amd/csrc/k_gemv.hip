@@ -1449,16 +1449,15 @@ __global__ __launch_bounds__(64 * NWT * ((SW || CP) ? 2 : 1)) void k_gemv_q4K_kr
 // At prefill sizes a K-relay workgroup computes one 16 x 16 (row tile, column tile) pair and copies
 // its column tile's whole operand (16 columns x K) into LDS for it: a 1024 x 1024 matrix at 576
 // columns moves 64 x 36 such copies of 35 KB through L2.  Here the operand tile is copied into LDS
-// once for PF_RT row tiles: each wave owns two row tiles of the column tile for the WHOLE row, every
+// once for 4 x 2 row tiles (8 x 2 with TTS_HIP_OPT_GEMM_PF_NW = 8): each wave owns two row tiles of the column tile for the WHOLE row, every
 // block in ascending order, so ggml's chain (sums[l] += p_l, sumf -= q, then sumf + sums[0..7]) runs
 // in the wave's registers with no relay and no barrier; a block's operand fragments (from LDS) serve
 // both row tiles.  The next block's weights are requested before the current block's MFMAs.  Same additions in the same order as vec_dot_q4_K_q8_K:
 // bit-identical.  Operands: k_quant_mf's layout, one bq_tile per 16-column tile (j.bq, j.bq_tile).
 constexpr int PF_RS = 2;                 // row tiles per wave
-constexpr int PF_RT = 4 * PF_RS;         // row tiles per workgroup (four waves)
 constexpr int PF_SLOT = QK_K + 8;        // halves per operand slot: columns 528 B apart, 16 B off the LDS bank period
-template <int NB, bool LANE>
-__global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
+template <int NB, bool LANE, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void k_gemm_q4K_pf(GemvJob j) {
     typedef float f2v __attribute__((ext_vector_type(2)));
     constexpr int RS = PF_RS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1474,7 +1473,7 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     {
         const char * src = j.bq + (size_t)ct * j.bq_tile;
         const int nck = (int)(((size_t)nslot * (2 * PF_SLOT + 32 + 4) + 1023) >> 10);
-        for (int i = wave; i < nck; i += 4)
+        for (int i = wave; i < nck; i += NW)
             __builtin_amdgcn_global_load_lds(gptr(src + (size_t)i * 1024 + lane * 16),
                                              (__attribute__((address_space(3))) void *)(smem + (size_t)i * 1024), 16, 0, 0);
     }
@@ -1482,7 +1481,7 @@ __global__ __launch_bounds__(256) void k_gemm_q4K_pf(GemvJob j) {
     const _Float16 * const sbs = b16 + (size_t)nslot * PF_SLOT;
     const float * const xd = (const float *)(sbs + (size_t)nslot * 16);
     const int64_t T = job_rows(j) / 16;  // launcher: whole row tiles
-    const int64_t tw = ((int64_t)blockIdx.x * 4 + wave) * RS;  // this wave's first row tile
+    const int64_t tw = ((int64_t)blockIdx.x * NW + wave) * RS;  // this wave's first row tile
     auto mat_of = [&](int64_t flat) {
         int mt = 0;
         while (mt + 1 < j.nmat && flat >= job_roff(j, mt + 1)) ++mt;
@@ -2612,12 +2611,18 @@ static void launch_q4k_kr_t(tts_hip_backend * be, const GemvJob & j, unsigned gx
 
 // LDS of one column tile's operands (k_quant_mf's slot layout, whole 1 KB DMA chunks)
 static size_t q4k_pf_lds(int64_t nb) { return (size_t)((((16 * nb + 1) * (2 * PF_SLOT + 32 + 4)) + 1023) & ~(int64_t)1023); }
+template <int NB, bool LANE, int NW>
+static void launch_q4k_pf_nw(tts_hip_backend * be, const GemvJob & j, unsigned gy) {
+    static std::atomic<uint32_t> attr_done{0};
+    set_lds_attr_once(attr_done, be->device, (const void *)k_gemm_q4K_pf<NB, LANE, NW>);
+    const unsigned gx = (unsigned)((job_rows(j) / 16 + NW * PF_RS - 1) / (NW * PF_RS));
+    hipLaunchKernelGGL((k_gemm_q4K_pf<NB, LANE, NW>), dim3(gx, gy), dim3(64 * NW), (uint32_t)q4k_pf_lds(NB), be->stream, j);
+}
+// TTS_HIP_OPT_GEMM_PF_NW: waves per workgroup (4: 8 row tiles per operand copy; 8: 16)
 template <int NB, bool LANE>
 static void launch_q4k_pf_t(tts_hip_backend * be, const GemvJob & j, unsigned gy) {
-    static std::atomic<uint32_t> attr_done{0};
-    set_lds_attr_once(attr_done, be->device, (const void *)k_gemm_q4K_pf<NB, LANE>);
-    const unsigned gx = (unsigned)((job_rows(j) / 16 + PF_RT - 1) / PF_RT);
-    hipLaunchKernelGGL((k_gemm_q4K_pf<NB, LANE>), dim3(gx, gy), dim3(256), (uint32_t)q4k_pf_lds(NB), be->stream, j);
+    if (be->gemm_pf_nw == 8) launch_q4k_pf_nw<NB, LANE, 8>(be, j, gy);
+    else launch_q4k_pf_nw<NB, LANE, 4>(be, j, gy);
 }
 
 // Many-column Q4_K MUL_MAT (prompt prefill) on the matrix cores: the operand pass over all M columns

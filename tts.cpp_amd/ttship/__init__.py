@@ -27,7 +27,7 @@ FUSE_ALL = sum(FUSE.values())
 UNARY = {"ABS": 0, "NEG": 1, "TANH": 2, "RELU": 3, "SIGMOID": 4, "GELU": 5, "SILU": 6, "EXP": 7}
 
 # tts_hip_option ids (include/tts_hip.h)
-OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17, "GEMM_Q8": 18, "BGEMM_F32": 19, "CU_PARTITION": 20, "GEMV_PREQUANT": 21, "GEMV_KRELAY": 22, "ATTN_KS": 23, "ATTN_PV8": 24, "GEMV_NW_MIN": 25, "GEMV_KRELAY_LOOP": 26, "GEMV_Q80_PRO": 27, "GEMV_Q80_SLAB": 28, "GEMV_Q80_RW": 29, "GEMM_Q8_STAGED": 30, "GEMV_KR_INKERNEL": 31, "GEMV_F32_WIDE": 32, "ATTN_PV_MP": 33, "GEMM_KR_NW": 34, "GEMM_KR_INKERNEL": 35, "GEMM_KR_CT2": 36, "COALESCE": 37, "GEMM_KR_XCD": 38, "GEMM_KR_CP": 39, "GEMM_KR_WALK": 40, "GEMM_PF": 41}
+OPT = {"FUSION": 0, "PROFILE_GEMV": 1, "GRAPHS": 2, "CONV_F32ACC": 3, "CONVT_LDS": 4, "ATTN_SPLIT": 5, "KV_PREFETCH": 6, "KV_PREFETCH_BLOCKS": 7, "Q4K_TILE_BYTES": 8, "GEMV_DEBUG": 10, "GEMV_UNIQUE": 11, "CONV_SPLIT": 12, "GEMV_KS": 13, "ATTN_FUSED": 14, "ATTN_PV16": 15, "Q4K_DUAL_BYTES": 16, "GEMV_RSPLIT": 17, "GEMM_Q8": 18, "BGEMM_F32": 19, "CU_PARTITION": 20, "GEMV_PREQUANT": 21, "GEMV_KRELAY": 22, "ATTN_KS": 23, "ATTN_PV8": 24, "GEMV_NW_MIN": 25, "GEMV_KRELAY_LOOP": 26, "GEMV_Q80_PRO": 27, "GEMV_Q80_SLAB": 28, "GEMV_Q80_RW": 29, "GEMM_Q8_STAGED": 30, "GEMV_KR_INKERNEL": 31, "GEMV_F32_WIDE": 32, "ATTN_PV_MP": 33, "GEMM_KR_NW": 34, "GEMM_KR_INKERNEL": 35, "GEMM_KR_CT2": 36, "COALESCE": 37, "GEMM_KR_XCD": 38, "GEMM_KR_CP": 39, "GEMM_KR_WALK": 40, "GEMM_PF": 41, "GEMM_PF_NW": 42}
 ATTN_SPLIT_DEFAULT = 128  # backend default: P >= 128 keys -> split (scores + softmax/P.V) kernels
 ATTN_FUSED_ON = 128  # P >= 128 keys -> one 1024-thread launch (k_attn_fused; backend default 0 = off)
 
