@@ -302,6 +302,7 @@ struct Planner {
     size_t conv_stage_cap = 0;
     char * hoist_buf = nullptr;  // backend scratch for hoisted products whose own memory is still in use (try_gemv)
     size_t hoist_cap = 0, hoist_used = 0;
+    int hoist_live = -1;  // the last node position whose COPY item still reads the hoist buffer
     size_t lstm_cap = 0, lstm_used = 0;
 
     const tts_tensor * sole_consumer(const tts_tensor * t) {
@@ -714,6 +715,9 @@ struct Planner {
     void try_gemv(int i) {
         const tts_tensor * mm0 = nodes[i];
         if (!is_gemv(mm0)) return;
+        // every earlier hoisted product has been copied to its tensor before position i runs: the hoist
+        // buffer is free again (a step hoists K and V over Q once per layer)
+        if (i > hoist_live) hoist_used = 0;
         const tts_tensor * a0 = mm0->src[0];
         const tts_tensor * x = mm0->src[1];
         const int64_t M = x->ne[1] * x->ne[2] * x->ne[3];
@@ -806,6 +810,7 @@ struct Planner {
                         t = ht;
                         copy_back = j;
                         hoist_used += (obytes + 255) & ~(size_t)255;
+                        hoist_live = std::max(hoist_live, j);
                         ok = true;
                     }
                 }
