@@ -940,11 +940,13 @@ __global__ __launch_bounds__(64) void k_attn_small(AttnArgs a) {
 // Short contexts with many queries (a prompt pass: Parler's self-attention over the prompt and its
 // cross-attention over the T5 encoding, n = 8-18 queries per sequence): k_attn_small's arithmetic
 // per (head, query, sequence), but one workgroup per (head, sequence) stages K and V into LDS once
-// (rows padded off the bank period) and its four waves take the queries in turn.  k_attn_small
+// (rows padded off the bank period) and its 16 waves take the queries in turn.  k_attn_small
 // gives every query its own wave, which re-reads the (head, sequence)'s V with one scalar load per
 // (dim, position) across 64 rows.  The sums are k_attn_small's, in its order: bit-identical.
+constexpr int ATTN_SQ_WAVES = 16;  // waves per (head, sequence) workgroup of k_attn_small_q: one or two queries each
 template <int HD>
-__global__ __launch_bounds__(256) void k_attn_small_q(AttnArgs a) {
+__global__ __launch_bounds__(64 * ATTN_SQ_WAVES) void k_attn_small_q(AttnArgs a) {
+    constexpr int NW = ATTN_SQ_WAVES;
     constexpr int KP = HD + 1;  // floats per K row in LDS
     constexpr int VP = 65;      // floats per V row (dim) in LDS: positions 0..63
     __shared__ float sk[64 * KP];
@@ -959,17 +961,17 @@ __global__ __launch_bounds__(256) void k_attn_small_q(AttnArgs a) {
     const char * kbase = a.k.data + (int64_t)hk * a.k.nb[2] + (int64_t)bk * a.k.nb[3] + seq_koff(a, b);
     const char * vbase = a.v.data + (int64_t)hv * a.v.nb[2] + (int64_t)bv * a.v.nb[3] + seq_voff(a, b);
     const int64_t knb1 = a.k.nb[1], vnb0 = a.v.nb[0], vnb1 = a.v.nb[1];
-    for (int i = tid; i < P * HD; i += 256) {  // K [p][d] (d contiguous in memory)
+    for (int i = tid; i < P * HD; i += 64 * NW) {  // K [p][d] (d contiguous in memory)
         const int p = i / HD, d = i - p * HD;
         sk[p * KP + d] = *(const float *)(kbase + (int64_t)p * knb1 + 4 * d);
     }
-    for (int i = tid; i < P * HD; i += 256) {  // V [d][p]
+    for (int i = tid; i < P * HD; i += 64 * NW) {  // V [d][p]
         const int d = i / P, p = i - d * P;
         sv[d * VP + p] = *(const float *)(vbase + (int64_t)d * vnb1 + (int64_t)p * vnb0);
     }
     __syncthreads();
     const int p = min(lane, P - 1);
-    for (int tq = wave; tq < a.n; tq += 4) {
+    for (int tq = wave; tq < a.n; tq += NW) {
         const char * qbase = a.q.data + tq * a.q.nb[1] + (int64_t)h * a.q.nb[2] + (int64_t)b * a.q.nb[3];
         double acc = 0.0;
 #pragma unroll 16
@@ -1076,8 +1078,8 @@ void launch_attn_decode(tts_hip_backend * be, const TD & q, const TD & k, const 
                        (k.nb[3] % 16) == 0 && q.nb[0] == 4 && P > 0;
     if (krows && P <= 64 && n >= 4) {  // a prompt pass: K / V staged once per (head, sequence)
         const dim3 grid((unsigned)H, (unsigned)B);
-        if (hd == 64) hipLaunchKernelGGL(k_attn_small_q<64>, grid, dim3(256), 0, be->stream, a);
-        else hipLaunchKernelGGL(k_attn_small_q<128>, grid, dim3(256), 0, be->stream, a);
+        if (hd == 64) hipLaunchKernelGGL(k_attn_small_q<64>, grid, dim3(64 * ATTN_SQ_WAVES), 0, be->stream, a);
+        else hipLaunchKernelGGL(k_attn_small_q<128>, grid, dim3(64 * ATTN_SQ_WAVES), 0, be->stream, a);
         TTS_HIP_CHECK(hipGetLastError());
         return;
     }
