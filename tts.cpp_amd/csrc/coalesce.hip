@@ -428,8 +428,15 @@ void run_group(Dev & d, std::vector<Req *> & g) {
     }
     tts_hip_backend * ex = d.exec;
     copy_options(ex, r0->be);
-    // the members' queued work (their input uploads) first
+    // the members' queued work (their input uploads) first.  A member whose stream has drained (its
+    // synchronous tensor_set uploads have, the usual case) has nothing to order behind: no fence.
+    static const bool fence_all = getenv("TTS_CO_FENCE_ALL") != nullptr;
     for (Req * m : mem) {
+        if (!fence_all) {
+            const hipError_t q = hipStreamQuery(m->be->stream);
+            if (q == hipSuccess) continue;
+            if (q != hipErrorNotReady) TTS_HIP_CHECK(q);
+        }
         TTS_HIP_CHECK(hipEventRecord(m->be->co_ev, m->be->stream));
         TTS_HIP_CHECK(hipStreamWaitEvent(ex->stream, m->be->co_ev, 0));
     }
